@@ -1,0 +1,14 @@
+"""etcd_amd -- MI355X-native engine for etcd's WAL replay-and-verify path.
+
+Product layout:
+  csrc/        HIP kernels (gfx950) + host C++ behind the C ABI in include/ewal.h
+  libewal.so   built in-tree by build.sh
+  wal.py       mirror of the reference `wal` package (OpenAtIndex/ReadAll/Create/...)
+  snap.py      mirror of `snap.Snapshotter` (Load / batch verify)
+  raft.py      batched `raft.maybeCommit`
+  crc.py       `pkg/crc` digest (chained CRC-32C) over host or device buffers
+"""
+from . import _lib  # noqa: F401  (fails loudly if libewal.so is missing)
+from .wal import Context, OpenAtIndex, Create, Encoder, readall_bytes, synth_wal  # noqa: F401
+
+__all__ = ["Context", "OpenAtIndex", "Create", "Encoder", "readall_bytes", "synth_wal"]

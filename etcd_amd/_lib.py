@@ -1,0 +1,163 @@
+"""ctypes binding of libewal.so (include/ewal.h).
+
+The shared library is built in-tree by etcd_amd/build.sh (hipcc, gfx950).
+There is no CPU fallback: if the library is missing this module raises at
+import, and every compute call on a machine without a GPU returns
+EWAL_E_NODEVICE, which the wrappers raise as NoDeviceError.
+"""
+import ctypes as C
+import os
+import re
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libewal.so")
+HEADER = os.path.join(os.path.dirname(_HERE), "include", "ewal.h")
+
+if not os.path.exists(LIB_PATH):
+    raise ImportError("etcd_amd: %s is missing -- run etcd_amd/build.sh (hipcc --offload-arch=gfx950)" % LIB_PATH)
+
+lib = C.CDLL(LIB_PATH)
+
+# ---- status codes (include/ewal.h) --------------------------------------
+OK = 0
+EOF = 1
+ERR_UNEXPECTED_EOF = 2
+ERR_RECORD_CRC = 3
+ERR_WAL_CRC = 4
+ERR_METADATA_CONFLICT = 5
+ERR_INDEX_NOT_FOUND = 6
+ERR_WRONG_TYPE = 7
+ERR_UNEXPECTED_TYPE = 8
+ERR_FILE_NOT_FOUND = 9
+ERR_SNAP_CRC = 10
+ERR_NO_SNAPSHOT = 11
+PANIC_NEG_LENGTH = 32
+PANIC_BOUNDS = 33
+PANIC_ENTRY = 34
+PANIC_STATE = 35
+PANIC_INDEX_GAP = 36
+NONTERMINATING = 37
+UNSUPPORTED_ENCODING = 48
+E_HIP, E_INVAL, E_NOMEM, E_NODEVICE, E_TIMEOUT, E_IO = -1, -2, -3, -4, -5, -6
+
+CASTAGNOLI, IEEE, KOOPMAN = 0x82F63B78, 0xEDB88320, 0xEB31D82E
+
+
+class Result(C.Structure):
+    _fields_ = [("status", C.c_int32), ("flags", C.c_int32), ("detail", C.c_int64), ("fail_record", C.c_int64),
+                ("fail_offset", C.c_int64), ("n_records", C.c_int64), ("last_crc", C.c_uint32),
+                ("reserved0", C.c_uint32), ("enti", C.c_uint64), ("metadata_off", C.c_int64),
+                ("metadata_len", C.c_int64), ("has_state", C.c_int32), ("reserved1", C.c_int32),
+                ("state_term", C.c_uint64), ("state_vote", C.c_uint64), ("state_commit", C.c_uint64),
+                ("n_ents", C.c_int64), ("n_candidates", C.c_int64), ("n_runs", C.c_int64), ("device_ms", C.c_double),
+                ("stream_ms", C.c_double)]
+
+
+class EntryDesc(C.Structure):
+    _fields_ = [("term", C.c_uint64), ("index", C.c_uint64), ("data_off", C.c_uint64), ("data_len", C.c_uint64),
+                ("type", C.c_int32), ("data_nil", C.c_int32)]
+
+
+class RecordDesc(C.Structure):
+    _fields_ = [("offset", C.c_uint64), ("data_off", C.c_uint64), ("data_len", C.c_uint64), ("type", C.c_int64),
+                ("crc", C.c_uint32), ("chained_crc", C.c_uint32)]
+
+
+class SnapshotDesc(C.Structure):
+    _fields_ = [("index", C.c_uint64), ("term", C.c_uint64), ("data_off", C.c_uint64), ("data_len", C.c_uint64),
+                ("n_nodes", C.c_int64), ("n_removed", C.c_int64), ("nodes", C.c_uint64 * 64),
+                ("removed", C.c_uint64 * 64)]
+
+
+vp = C.c_void_p
+u8p = C.POINTER(C.c_uint8)
+_SIGS = {
+    "ewal_ctx_create": (C.c_int, [C.c_int, C.POINTER(vp)]),
+    "ewal_ctx_destroy": (None, [vp]),
+    "ewal_ctx_set_stream": (C.c_int, [vp, vp]),
+    "ewal_status_string": (C.c_char_p, [C.c_int]),
+    "ewal_last_device_ms": (C.c_float, [vp]),
+    "ewal_device_count": (C.c_int, []),
+    "ewal_readall_device": (C.c_int, [vp, vp, C.c_uint64, C.c_uint64, C.POINTER(Result)]),
+    "ewal_device_alloc": (C.c_int, [vp, C.c_uint64, C.POINTER(vp)]),
+    "ewal_device_free": (C.c_int, [vp, vp]),
+    "ewal_upload": (C.c_int, [vp, vp, vp, C.c_uint64]),
+    "ewal_download": (C.c_int, [vp, vp, vp, C.c_uint64]),
+    "ewal_stage_to_device": (C.c_int, [vp, vp, C.c_uint64, C.POINTER(vp)]),
+    "ewal_readall_host": (C.c_int, [vp, vp, C.c_uint64, C.c_uint64, C.POINTER(Result)]),
+    "ewal_copy_entries": (C.c_int64, [vp, C.POINTER(EntryDesc), C.c_int64]),
+    "ewal_copy_records": (C.c_int64, [vp, C.POINTER(RecordDesc), C.c_int64]),
+    "ewal_open_at_index": (C.c_int, [C.c_char_p, C.c_uint64, C.POINTER(vp)]),
+    "ewal_wal_readall": (C.c_int, [vp, vp, C.POINTER(Result)]),
+    "ewal_wal_bytes": (u8p, [vp, C.POINTER(C.c_uint64)]),
+    "ewal_wal_seq": (C.c_uint64, [vp]),
+    "ewal_wal_close": (None, [vp]),
+    "ewal_create": (C.c_int, [C.c_char_p, C.c_char_p, C.c_uint64, C.c_int, C.POINTER(vp)]),
+    "ewal_writer_save_entry": (C.c_int, [vp, C.c_int32, C.c_uint64, C.c_uint64, C.c_char_p, C.c_uint64]),
+    "ewal_writer_save_state": (C.c_int, [vp, C.c_uint64, C.c_uint64, C.c_uint64]),
+    "ewal_writer_cut": (C.c_int, [vp]),
+    "ewal_writer_sync": (C.c_int, [vp]),
+    "ewal_writer_close": (None, [vp]),
+    "ewal_encoder_new": (vp, [C.c_uint32, C.c_uint64]),
+    "ewal_encoder_encode": (C.c_int, [vp, C.c_int64, C.c_char_p, C.c_uint64, C.c_int]),
+    "ewal_encoder_save_entry": (C.c_int, [vp, C.c_int32, C.c_uint64, C.c_uint64, C.c_char_p, C.c_uint64]),
+    "ewal_encoder_save_state": (C.c_int, [vp, C.c_uint64, C.c_uint64, C.c_uint64]),
+    "ewal_encoder_bytes": (u8p, [vp, C.POINTER(C.c_uint64)]),
+    "ewal_encoder_crc": (C.c_uint32, [vp]),
+    "ewal_encoder_free": (None, [vp]),
+    "ewal_synth_wal": (C.c_int64, [C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint32, C.c_int64, vp, C.c_uint64,
+                                   C.POINTER(C.c_int64)]),
+    "ewal_crc32_update_device": (C.c_int, [vp, C.c_uint32, C.c_uint32, vp, C.c_uint64, C.POINTER(C.c_uint32)]),
+    "ewal_crc32_update_host": (C.c_uint32, [C.c_uint32, C.c_uint32, C.c_char_p, C.c_uint64]),
+    "ewal_crc32_combine": (C.c_uint32, [C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint64]),
+    "esnap_verify_packed": (C.c_int, [vp, vp, C.c_uint64, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.c_uint32,
+                                      C.c_uint32, C.POINTER(C.c_int32), C.POINTER(C.c_uint32),
+                                      C.POINTER(C.c_uint32)]),
+    "esnap_copy_snapshot": (C.c_int, [vp, C.c_uint32, C.POINTER(SnapshotDesc)]),
+    "esnap_load_dir": (C.c_int, [vp, C.c_char_p, C.c_uint32, C.POINTER(SnapshotDesc), C.POINTER(C.c_char_p)]),
+    "ecommit_batch_device": (C.c_int, [vp, C.c_uint64, vp, vp, vp, vp, vp, vp, vp, vp, vp, C.POINTER(C.c_double)]),
+}
+for _name, (_res, _args) in _SIGS.items():
+    _f = getattr(lib, _name)
+    _f.restype = _res
+    _f.argtypes = _args
+
+
+def header_symbols(path=HEADER):
+    """Every function declared in include/ewal.h."""
+    txt = open(path).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(e(?:wal|snap|commit)_[a-z0-9_]+)\s*\(", txt)))
+
+
+def status_string(st):
+    return lib.ewal_status_string(st).decode()
+
+
+class EwalError(Exception):
+    """An EWAL_* status: the Go sentinel or panic class of the reference."""
+
+    def __init__(self, status, detail=0, record=-1, offset=-1):
+        self.status, self.detail, self.record, self.offset = status, detail, record, offset
+        msg = status_string(status)
+        if status == ERR_UNEXPECTED_TYPE:
+            msg = "unexpected block type %d" % detail
+        super().__init__(msg)
+
+
+class NoDeviceError(EwalError):
+    pass
+
+
+class GoPanic(EwalError):
+    """The reference panics here (make/slice bounds/mustUnmarshal*)."""
+
+
+def check(st, detail=0, record=-1, offset=-1):
+    if st == OK:
+        return
+    if st == E_NODEVICE:
+        raise NoDeviceError(st)
+    if 32 <= st <= 37:
+        raise GoPanic(st, detail, record, offset)
+    raise EwalError(st, detail, record, offset)

@@ -1,0 +1,89 @@
+// crc_math.h -- reflected CRC-32 arithmetic used by the engine (host side).
+//
+// Restates Go hash/crc32 (Update(crc, tab, p) = ^update(^crc, tab, p); the
+// call sites are pkg/crc/crc.go:32, snap/snapshotter.go:53,98, wal/wal.go:49)
+// in the affine form the GPU pipeline needs:
+//
+//   raw(c, D)        register after feeding D from register c (no inversion)
+//   lin(D)           raw(0, D)                       -- GF(2)-linear in D
+//   S_n(c)           raw(c, n zero bytes)            -- GF(2)-linear in c
+//   raw(c, A||B)   = S_|B|(raw(c, A)) ^ lin(B)
+//   Update(c, D)   = S_n(c ^ ~0) ^ lin(D) ^ ~0 = S_n(c) ^ Update(0, D)
+//
+// Tables built here (per polynomial) and uploaded to the device:
+//   slice[4][256]      slicing-by-4 tables (slice[0] = MakeTable(poly))
+//   shift[m][4][256]   byte tables of S_{2^m}, m = 0..EW_SHIFT_LEVELS-1:
+//                      S_{2^m}(x) = ^_k shift[m][k][(x >> 8k) & 0xff]
+#pragma once
+#include <cstdint>
+#include <cstring>
+#include <vector>
+
+#define EW_SHIFT_LEVELS 48  // S_{2^m} for m < 48: lengths up to 256 TiB
+
+namespace ewal {
+
+struct CrcTables {
+  uint32_t poly = 0;
+  uint32_t slice[4][256];
+  std::vector<uint32_t> shift;  // EW_SHIFT_LEVELS * 4 * 256
+
+  explicit CrcTables(uint32_t p) : poly(p), shift((size_t)EW_SHIFT_LEVELS * 1024) {
+    for (uint32_t i = 0; i < 256; i++) {
+      uint32_t c = i;
+      for (int j = 0; j < 8; j++) c = (c & 1) ? (c >> 1) ^ poly : (c >> 1);
+      slice[0][i] = c;
+    }
+    for (int t = 1; t < 4; t++)
+      for (uint32_t i = 0; i < 256; i++)
+        slice[t][i] = (slice[t - 1][i] >> 8) ^ slice[0][slice[t - 1][i] & 0xff];
+    // S_1 as a GF(2) matrix (column j = S_1(1 << j)), then repeated squaring.
+    uint32_t m[32], sq[32];
+    for (int j = 0; j < 32; j++) {
+      uint32_t x = 1u << j;
+      m[j] = slice[0][x & 0xff] ^ (x >> 8);
+    }
+    for (int lvl = 0; lvl < EW_SHIFT_LEVELS; lvl++) {
+      uint32_t *tb = &shift[(size_t)lvl * 1024];
+      for (int k = 0; k < 4; k++)
+        for (uint32_t b = 0; b < 256; b++) tb[k * 256 + b] = matvec(m, b << (8 * k));
+      for (int j = 0; j < 32; j++) sq[j] = matvec(m, m[j]);
+      std::memcpy(m, sq, sizeof(m));
+    }
+  }
+
+  static uint32_t matvec(const uint32_t *m, uint32_t x) {
+    uint32_t r = 0;
+    for (int j = 0; x; j++, x >>= 1)
+      if (x & 1) r ^= m[j];
+    return r;
+  }
+
+  uint32_t shift_pow2(int lvl, uint32_t x) const {
+    const uint32_t *tb = &shift[(size_t)lvl * 1024];
+    return tb[x & 0xff] ^ tb[256 + ((x >> 8) & 0xff)] ^ tb[512 + ((x >> 16) & 0xff)] ^ tb[768 + (x >> 24)];
+  }
+  // S_n(x) for any n < 2^48.
+  uint32_t shift_n(uint64_t n, uint32_t x) const {
+    for (int lvl = 0; n; lvl++, n >>= 1)
+      if (n & 1) x = shift_pow2(lvl, x);
+    return x;
+  }
+  uint32_t raw(uint32_t c, const uint8_t *p, size_t n) const {
+    while (n >= 4) {
+      uint32_t w;
+      std::memcpy(&w, p, 4);
+      c ^= w;
+      c = slice[3][c & 0xff] ^ slice[2][(c >> 8) & 0xff] ^ slice[1][(c >> 16) & 0xff] ^ slice[0][c >> 24];
+      p += 4;
+      n -= 4;
+    }
+    while (n--) c = slice[0][(c ^ *p++) & 0xff] ^ (c >> 8);
+    return c;
+  }
+  uint32_t update(uint32_t crc, const uint8_t *p, size_t n) const { return ~raw(~crc, p, n); }
+  // Update(crc_a, B) given crc_b = Update(0, B): S_n(crc_a) ^ crc_b.
+  uint32_t combine(uint32_t crc_a, uint32_t crc_b, uint64_t len_b) const { return shift_n(len_b, crc_a) ^ crc_b; }
+};
+
+}  // namespace ewal

@@ -1,0 +1,627 @@
+// ewal_api.hip -- C ABI + host driver for the device pipeline (single TU).
+//
+// Implements include/ewal.h's compute entry points.  The pipeline for
+// (*WAL).ReadAll (wal/wal.go:164-216) is:
+//   k_stream (one HBM pass) -> framing (k_link, runs, pointer jumping) ->
+//   k_decode -> k_verify -> k_meta -> entry ops (k_opflag, k_gap, k_ents)
+// and the host only classifies the chain's terminal frame and assembles the
+// ewal_result from a few device reductions.  No CPU decoding or CRC happens
+// on this path; without a GPU every call returns EWAL_E_NODEVICE.
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <vector>
+
+#include "crc_math.h"
+#include "wal_kernels.hip"
+#include "aux_kernels.hip"
+
+#define EW_CHECK(x)                                                          \
+  do {                                                                       \
+    hipError_t e_ = (x);                                                     \
+    if (e_ != hipSuccess) {                                                  \
+      std::fprintf(stderr, "ewal: HIP error %s at %s:%d\n", hipGetErrorString(e_), __FILE__, __LINE__); \
+      return EWAL_E_HIP;                                                     \
+    }                                                                        \
+  } while (0)
+
+namespace {
+
+struct DevTables {
+  uint32_t *slice = nullptr;  // [4][256]
+  uint32_t *shift = nullptr;  // [48][4][256]
+};
+
+struct DevBuf {
+  void *p = nullptr;
+  size_t cap = 0;
+  // grow-only device buffer
+  hipError_t ensure(size_t n) {
+    if (n <= cap) return hipSuccess;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+    size_t want = std::max<size_t>(n, 256);
+    hipError_t e = hipMalloc(&p, want);
+    if (e == hipSuccess) cap = want;
+    return e;
+  }
+  template <typename T> T *as() { return static_cast<T *>(p); }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+};
+
+struct Small {  // per-call device scratch (zeroed / initialised each call)
+  uint32_t ticket;
+  uint32_t errflag;
+  ChainInfo ci;
+  ReadAllAgg agg;
+  uint32_t nsel;      // hipcub select counts
+  uint32_t nsel2;
+  uint32_t nsel3;
+  uint32_t pad;
+};
+
+}  // namespace
+
+struct ewal_ctx {
+  int device = 0;
+  int num_cu = 256;
+  hipStream_t stream = nullptr;
+  bool own_stream = false;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr, evs0 = nullptr, evs1 = nullptr;
+  std::map<uint32_t, DevTables> tables;
+  std::map<uint32_t, std::unique_ptr<ewal::CrcTables>> host_tables;
+  DevBuf v, pwave, desc, cpos, clen, nxt, exc, E, rs, jl, vis, entry, on, rec_cand, rd, opf, ops, kk, kkrev, suf,
+      ents, recs, tmp, small, sdesc, snaps, hbuf_dev;
+  Small *h_small = nullptr;  // pinned mirror
+  // results of the last readall
+  uint64_t last_n = 0, last_nents = 0;
+  bool last_ok = false;
+};
+
+static int get_tables(ewal_ctx *c, uint32_t poly, DevTables **out) {
+  auto it = c->tables.find(poly);
+  if (it != c->tables.end()) {
+    *out = &it->second;
+    return 0;
+  }
+  auto ht = std::make_unique<ewal::CrcTables>(poly);
+  DevTables t;
+  EW_CHECK(hipMalloc(&t.slice, sizeof(ht->slice)));
+  EW_CHECK(hipMalloc(&t.shift, ht->shift.size() * sizeof(uint32_t)));
+  EW_CHECK(hipMemcpy(t.slice, ht->slice, sizeof(ht->slice), hipMemcpyHostToDevice));
+  EW_CHECK(hipMemcpy(t.shift, ht->shift.data(), ht->shift.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+  c->host_tables[poly] = std::move(ht);
+  c->tables[poly] = t;
+  *out = &c->tables[poly];
+  return 0;
+}
+
+static inline unsigned grid_for(uint64_t n, unsigned bs) { return (unsigned)((n + bs - 1) / bs); }
+
+// hipcub DeviceSelect::Flagged(counting 0.., flags) -> out, count in *d_count
+static int select_flagged(ewal_ctx *c, const uint8_t *flags, uint32_t n, uint32_t *out, uint32_t *d_count) {
+  hipcub::CountingInputIterator<uint32_t> it(0);
+  size_t bytes = 0;
+  EW_CHECK(hipcub::DeviceSelect::Flagged(nullptr, bytes, it, flags, out, d_count, (int)n, c->stream));
+  EW_CHECK(c->tmp.ensure(bytes));
+  EW_CHECK(hipcub::DeviceSelect::Flagged(c->tmp.p, bytes, it, flags, out, d_count, (int)n, c->stream));
+  return 0;
+}
+
+// Run k_stream over d_buf[0..B): fills c->v, c->pwave (and candidates when
+// find_cand).  Returns the candidate count via *K (synchronises).
+static int run_stream(ewal_ctx *c, DevTables *tb, const uint8_t *d_buf, uint64_t B, int find_cand, uint64_t ccap,
+                      uint64_t *K) {
+  const uint64_t ntiles64 = (B + EW_TILE - 1) / EW_TILE;
+  if (ntiles64 >= 0xffffffffull) return EWAL_E_INVAL;
+  const uint32_t ntiles = (uint32_t)std::max<uint64_t>(ntiles64, 1);
+  EW_CHECK(c->v.ensure((size_t)ntiles * EW_THREADS * 4));
+  EW_CHECK(c->pwave.ensure((size_t)ntiles * EW_WAVES * 4));
+  EW_CHECK(c->desc.ensure((size_t)ntiles * sizeof(TileDesc)));
+  EW_CHECK(hipMemsetAsync(c->desc.p, 0, (size_t)ntiles * sizeof(TileDesc), c->stream));
+  EW_CHECK(hipMemsetAsync(c->small.p, 0, sizeof(Small), c->stream));
+  StreamArgs a;
+  a.buf = d_buf;
+  a.B = B;
+  a.ntiles = ntiles;
+  a.find_cand = find_cand;
+  a.g_slice = tb->slice;
+  a.g_shift = tb->shift;
+  a.v = c->v.as<uint32_t>();
+  a.pwave = c->pwave.as<uint32_t>();
+  a.cpos = c->cpos.as<uint64_t>();
+  a.clen = c->clen.as<uint64_t>();
+  a.ccap = ccap;
+  a.desc = c->desc.as<TileDesc>();
+  a.ticket = &c->small.as<Small>()->ticket;
+  a.errflag = &c->small.as<Small>()->errflag;
+  const unsigned grid = (unsigned)std::min<uint64_t>(ntiles, (uint64_t)c->num_cu);
+  EW_CHECK(hipEventRecord(c->evs0, c->stream));
+  hipLaunchKernelGGL(k_stream, dim3(grid), dim3(EW_THREADS), 0, c->stream, a);
+  EW_CHECK(hipGetLastError());
+  EW_CHECK(hipEventRecord(c->evs1, c->stream));
+  if (K) {
+    unsigned long long tot = 0;
+    EW_CHECK(hipMemcpyAsync(&tot, &a.desc[ntiles - 1].inc_cnt, 8, hipMemcpyDeviceToHost, c->stream));
+    EW_CHECK(hipMemcpyAsync(c->h_small, c->small.p, sizeof(Small), hipMemcpyDeviceToHost, c->stream));
+    EW_CHECK(hipStreamSynchronize(c->stream));
+    if (c->h_small->errflag) return EWAL_E_TIMEOUT;
+    *K = tot;
+  }
+  return 0;
+}
+
+static int classify_terminal(ewal_ctx *c, const uint8_t *d_buf, uint64_t B, uint64_t q, int *st) {
+  // decoder.decode at frame start q when q is not a candidate frame
+  // (wal/decoder.go:28-39 + io.ReadFull's EOF/ErrUnexpectedEOF rule).
+  if (q == B) { *st = EWAL_OK; return 0; }
+  if (B - q < 8) { *st = EWAL_ERR_UNEXPECTED_EOF; return 0; }
+  int64_t L = 0;
+  EW_CHECK(hipMemcpyAsync(&L, d_buf + q, 8, hipMemcpyDeviceToHost, c->stream));
+  EW_CHECK(hipStreamSynchronize(c->stream));
+  const uint64_t rem = B - q - 8;
+  if (L < 0) *st = EWAL_PANIC_NEG_LENGTH;
+  else if ((uint64_t)L > rem) *st = rem == 0 ? EWAL_OK : EWAL_ERR_UNEXPECTED_EOF;
+  else *st = EWAL_UNSUPPORTED_ENCODING;   // a frame that fits but is not canonical
+  return 0;
+}
+
+static int readall_impl(ewal_ctx *c, const uint8_t *d_buf, uint64_t B, uint64_t ri, ewal_result *out) {
+  std::memset(out, 0, sizeof(*out));
+  out->fail_record = -1;
+  out->fail_offset = -1;
+  out->metadata_off = -1;
+  c->last_ok = false;
+  c->last_n = 0;
+  c->last_nents = 0;
+  if (((uintptr_t)d_buf & 15) != 0 && B) return EWAL_E_INVAL;
+  DevTables *tb;
+  int rc = get_tables(c, 0x82F63B78u, &tb);
+  if (rc) return rc;
+  EW_CHECK(c->small.ensure(sizeof(Small)));
+  EW_CHECK(hipEventRecord(c->ev0, c->stream));
+
+  uint64_t n = 0;          // frames on the chain
+  uint64_t q = 0;          // terminal frame offset
+  uint64_t K = 0;
+  if (B > 0) {
+    uint64_t ccap = std::min<uint64_t>(B / 128 + 65536, 0xfffffff0ull);
+    for (;;) {
+      EW_CHECK(c->cpos.ensure(ccap * 8));
+      EW_CHECK(c->clen.ensure(ccap * 8));
+      rc = run_stream(c, tb, d_buf, B, 1, ccap, &K);
+      if (rc) return rc;
+      if (K <= ccap) break;
+      if (K >= 0xfffffff0ull) return EWAL_E_NOMEM;
+      ccap = K + 1024;
+    }
+  }
+  out->n_candidates = (int64_t)K;
+  uint64_t pos0 = ~0ull;
+  if (K) {
+    EW_CHECK(hipMemcpyAsync(&pos0, c->cpos.p, 8, hipMemcpyDeviceToHost, c->stream));
+    EW_CHECK(hipStreamSynchronize(c->stream));
+  }
+  Small *ds = c->small.as<Small>();
+  if (K && pos0 == 0) {
+    const uint32_t K32 = (uint32_t)K;
+    EW_CHECK(c->nxt.ensure((size_t)K * 4));
+    EW_CHECK(c->exc.ensure((size_t)K));
+    EW_CHECK(c->E.ensure((size_t)K * 4));
+    hipLaunchKernelGGL(k_link, dim3(grid_for(K, 256)), dim3(256), 0, c->stream, c->cpos.as<uint64_t>(),
+                       c->clen.as<uint64_t>(), K32, c->nxt.as<uint32_t>(), c->exc.as<uint8_t>());
+    rc = select_flagged(c, c->exc.as<uint8_t>(), K32, c->E.as<uint32_t>(), &ds->nsel);
+    if (rc) return rc;
+    EW_CHECK(hipMemcpyAsync(c->h_small, ds, sizeof(Small), hipMemcpyDeviceToHost, c->stream));
+    EW_CHECK(hipStreamSynchronize(c->stream));
+    const uint32_t R = c->h_small->nsel;
+    out->n_runs = R;
+    int top = 0;
+    while ((1ull << top) < R) ++top;
+    EW_CHECK(c->jl.ensure((size_t)R * 4 * (top + 1)));
+    EW_CHECK(c->vis.ensure(R));
+    EW_CHECK(c->entry.ensure((size_t)R * 4));
+    uint32_t *J = c->jl.as<uint32_t>();
+    hipLaunchKernelGGL(k_runs, dim3(grid_for(R, 256)), dim3(256), 0, c->stream, c->E.as<uint32_t>(), R,
+                       c->nxt.as<uint32_t>(), J);
+    for (int k = 1; k <= top; ++k)
+      hipLaunchKernelGGL(k_jump, dim3(grid_for(R, 256)), dim3(256), 0, c->stream, J + (size_t)(k - 1) * R,
+                         J + (size_t)k * R, R);
+    EW_CHECK(hipMemsetAsync(c->vis.p, 0, R, c->stream));
+    EW_CHECK(hipMemsetAsync(c->vis.p, 1, 1, c->stream));
+    for (int k = top; k >= 0; --k)
+      hipLaunchKernelGGL(k_mark, dim3(grid_for(R, 256)), dim3(256), 0, c->stream, J + (size_t)k * R,
+                         c->vis.as<uint8_t>(), R);
+    EW_CHECK(hipMemsetAsync(c->entry.p, 0xff, (size_t)R * 4, c->stream));
+    hipLaunchKernelGGL(k_entry, dim3(grid_for(R, 256)), dim3(256), 0, c->stream, c->E.as<uint32_t>(),
+                       c->nxt.as<uint32_t>(), J, c->vis.as<uint8_t>(), R, c->entry.as<uint32_t>(), &ds->ci);
+    EW_CHECK(c->on.ensure(K));
+    EW_CHECK(c->rec_cand.ensure((size_t)K * 4));
+    hipLaunchKernelGGL(k_member, dim3(grid_for(K, 256)), dim3(256), 0, c->stream, c->E.as<uint32_t>(), R,
+                       c->vis.as<uint8_t>(), c->entry.as<uint32_t>(), K32, c->on.as<uint8_t>());
+    rc = select_flagged(c, c->on.as<uint8_t>(), K32, c->rec_cand.as<uint32_t>(), &ds->nsel2);
+    if (rc) return rc;
+    EW_CHECK(hipMemcpyAsync(c->h_small, ds, sizeof(Small), hipMemcpyDeviceToHost, c->stream));
+    EW_CHECK(hipStreamSynchronize(c->stream));
+    n = c->h_small->nsel2;
+    const uint32_t lc = c->h_small->ci.last_cand;
+    uint64_t pl[2];
+    EW_CHECK(hipMemcpyAsync(&pl[0], c->cpos.as<uint64_t>() + lc, 8, hipMemcpyDeviceToHost, c->stream));
+    EW_CHECK(hipMemcpyAsync(&pl[1], c->clen.as<uint64_t>() + lc, 8, hipMemcpyDeviceToHost, c->stream));
+    EW_CHECK(hipStreamSynchronize(c->stream));
+    q = pl[0] + 8 + pl[1];
+  }
+  int tst = EWAL_OK;
+  rc = classify_terminal(c, d_buf, B, q, &tst);
+  if (rc) return rc;
+
+  ReadAllAgg hagg;
+  hagg.first_fail = ~0ull;
+  hagg.last_entry = -1;
+  hagg.last_state = -1;
+  hagg.first_meta = ~0ull;
+  uint32_t nops = 0;
+  if (n) {
+    const uint32_t n32 = (uint32_t)n;
+    EW_CHECK(c->rd.ensure((size_t)n * sizeof(RecDesc)));
+    EW_CHECK(hipMemcpyAsync(&ds->agg, &hagg, sizeof(hagg), hipMemcpyHostToDevice, c->stream));
+    RecDesc *rd = c->rd.as<RecDesc>();
+    hipLaunchKernelGGL(k_decode, dim3(grid_for(n, 256)), dim3(256), 0, c->stream, d_buf, c->cpos.as<uint64_t>(),
+                       c->clen.as<uint64_t>(), c->rec_cand.as<uint32_t>(), n32, rd);
+    hipLaunchKernelGGL(k_verify, dim3(grid_for(n, 256)), dim3(256), 0, c->stream, d_buf, c->pwave.as<uint32_t>(),
+                       c->v.as<uint32_t>(), tb->slice, tb->shift, rd, n32, &ds->agg);
+    hipLaunchKernelGGL(k_meta, dim3(grid_for(n, 256)), dim3(256), 0, c->stream, d_buf, rd, n32, &ds->agg);
+    EW_CHECK(c->opf.ensure(n));
+    EW_CHECK(c->ops.ensure((size_t)n * 4));
+    hipLaunchKernelGGL(k_opflag, dim3(grid_for(n, 256)), dim3(256), 0, c->stream, rd, n32, ri, c->opf.as<uint8_t>());
+    rc = select_flagged(c, c->opf.as<uint8_t>(), n32, c->ops.as<uint32_t>(), &ds->nsel3);
+    if (rc) return rc;
+    EW_CHECK(hipMemcpyAsync(c->h_small, ds, sizeof(Small), hipMemcpyDeviceToHost, c->stream));
+    EW_CHECK(hipStreamSynchronize(c->stream));
+    nops = c->h_small->nsel3;
+    if (nops) {
+      EW_CHECK(c->kk.ensure((size_t)nops * 8));
+      hipLaunchKernelGGL(k_gap, dim3(grid_for(nops, 256)), dim3(256), 0, c->stream, rd, c->ops.as<uint32_t>(),
+                         nops, ri, c->kk.as<uint64_t>(), &ds->agg);
+    }
+    EW_CHECK(hipMemcpyAsync(c->h_small, ds, sizeof(Small), hipMemcpyDeviceToHost, c->stream));
+    EW_CHECK(hipStreamSynchronize(c->stream));
+    hagg = c->h_small->agg;
+  }
+  out->n_records = (int64_t)n;
+
+  if (hagg.first_fail < n) {
+    RecDesc f;
+    EW_CHECK(hipMemcpyAsync(&f, c->rd.as<RecDesc>() + hagg.first_fail, sizeof(f), hipMemcpyDeviceToHost, c->stream));
+    EW_CHECK(hipStreamSynchronize(c->stream));
+    out->status = f.st;
+    out->fail_record = (int64_t)hagg.first_fail;
+    out->fail_offset = (int64_t)f.off;
+    out->n_records = (int64_t)hagg.first_fail;
+    if (f.st == EWAL_ERR_UNEXPECTED_TYPE) out->detail = f.type;
+    if (f.st == EWAL_PANIC_INDEX_GAP) out->detail = (int64_t)f.f1;
+  } else if (tst != EWAL_OK) {
+    out->status = tst;
+    out->fail_record = (int64_t)n;
+    out->fail_offset = (int64_t)q;
+  } else {
+    uint64_t enti = 0;
+    if (hagg.last_entry >= 0) {
+      RecDesc e;
+      EW_CHECK(hipMemcpyAsync(&e, c->rd.as<RecDesc>() + hagg.last_entry, sizeof(e), hipMemcpyDeviceToHost, c->stream));
+      EW_CHECK(hipStreamSynchronize(c->stream));
+      enti = e.f1;
+    }
+    out->enti = enti;
+    if (enti < ri) {
+      out->status = EWAL_ERR_INDEX_NOT_FOUND;
+    } else {
+      out->status = EWAL_OK;
+      if (n) {
+        RecDesc last;
+        EW_CHECK(hipMemcpyAsync(&last, c->rd.as<RecDesc>() + (n - 1), sizeof(last), hipMemcpyDeviceToHost, c->stream));
+        RecDesc md, sd;
+        if (hagg.first_meta != ~0ull)
+          EW_CHECK(hipMemcpyAsync(&md, c->rd.as<RecDesc>() + hagg.first_meta, sizeof(md), hipMemcpyDeviceToHost, c->stream));
+        if (hagg.last_state >= 0)
+          EW_CHECK(hipMemcpyAsync(&sd, c->rd.as<RecDesc>() + hagg.last_state, sizeof(sd), hipMemcpyDeviceToHost, c->stream));
+        uint64_t klast = 0;
+        if (nops) EW_CHECK(hipMemcpyAsync(&klast, c->kk.as<uint64_t>() + (nops - 1), 8, hipMemcpyDeviceToHost, c->stream));
+        EW_CHECK(hipStreamSynchronize(c->stream));
+        out->last_crc = last.chained;
+        if (hagg.first_meta != ~0ull) {
+          out->metadata_off = (int64_t)md.doff;
+          out->metadata_len = (int64_t)md.dlen;
+        }
+        if (hagg.last_state >= 0) {
+          out->has_state = 1;
+          out->state_term = sd.f0;
+          out->state_vote = sd.f1;
+          out->state_commit = sd.f2;
+        }
+        const uint64_t nents = nops ? klast + 1 : 0;
+        out->n_ents = (int64_t)nents;
+        if (nents) {
+          // suffix-min over kk via a reversed inclusive min-scan
+          EW_CHECK(c->kkrev.ensure((size_t)nops * 8));
+          EW_CHECK(c->suf.ensure((size_t)nops * 8));
+          EW_CHECK(c->ents.ensure((size_t)nents * sizeof(ewal_entry)));
+          uint64_t *kk = c->kk.as<uint64_t>();
+          uint64_t *kr = c->kkrev.as<uint64_t>();
+          uint64_t *sf = c->suf.as<uint64_t>();
+          hipLaunchKernelGGL(k_reverse_u64, dim3(grid_for(nops, 256)), dim3(256), 0, c->stream, kk, kr, nops);
+          size_t bytes = 0;
+          EW_CHECK(hipcub::DeviceScan::InclusiveScan(nullptr, bytes, kr, sf, hipcub::Min(), (int)nops, c->stream));
+          EW_CHECK(c->tmp.ensure(bytes));
+          EW_CHECK(hipcub::DeviceScan::InclusiveScan(c->tmp.p, bytes, kr, sf, hipcub::Min(), (int)nops, c->stream));
+          hipLaunchKernelGGL(k_reverse_u64, dim3(grid_for(nops, 256)), dim3(256), 0, c->stream, sf, kr, nops);
+          hipLaunchKernelGGL(k_ents, dim3(grid_for(nops, 256)), dim3(256), 0, c->stream, c->rd.as<RecDesc>(),
+                             c->ops.as<uint32_t>(), nops, kk, kr, c->ents.as<ewal_entry>(), nents);
+        }
+        c->last_nents = nents;
+      }
+      c->last_ok = true;
+    }
+  }
+  c->last_n = n;
+  EW_CHECK(hipEventRecord(c->ev1, c->stream));
+  EW_CHECK(hipEventSynchronize(c->ev1));
+  float ms = 0;
+  EW_CHECK(hipEventElapsedTime(&ms, c->ev0, c->ev1));
+  out->device_ms = ms;
+  if (B) {
+    EW_CHECK(hipEventElapsedTime(&ms, c->evs0, c->evs1));
+    out->stream_ms = ms;
+  }
+  return out->status;
+}
+
+extern "C" {
+
+int ewal_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+int ewal_ctx_create(int device, ewal_ctx **out) {
+  *out = nullptr;
+  int n = ewal_device_count();
+  if (n <= 0) return EWAL_E_NODEVICE;
+  if (device < 0 || device >= n) return EWAL_E_INVAL;
+  EW_CHECK(hipSetDevice(device));
+  auto *c = new ewal_ctx();
+  c->device = device;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
+    c->num_cu = prop.multiProcessorCount;
+  EW_CHECK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+  c->own_stream = true;
+  EW_CHECK(hipEventCreate(&c->ev0));
+  EW_CHECK(hipEventCreate(&c->ev1));
+  EW_CHECK(hipEventCreate(&c->evs0));
+  EW_CHECK(hipEventCreate(&c->evs1));
+  EW_CHECK(hipHostMalloc((void **)&c->h_small, sizeof(Small), hipHostMallocDefault));
+  EW_CHECK(c->small.ensure(sizeof(Small)));
+  *out = c;
+  return EWAL_OK;
+}
+
+void ewal_ctx_destroy(ewal_ctx *c) {
+  if (!c) return;
+  (void)hipSetDevice(c->device);
+  (void)hipStreamSynchronize(c->stream);
+  DevBuf *bufs[] = {&c->v, &c->pwave, &c->desc, &c->cpos, &c->clen, &c->nxt, &c->exc, &c->E, &c->rs, &c->jl,
+                    &c->vis, &c->entry, &c->on, &c->rec_cand, &c->rd, &c->opf, &c->ops, &c->kk, &c->kkrev,
+                    &c->suf, &c->ents, &c->recs, &c->tmp, &c->small, &c->sdesc, &c->snaps, &c->hbuf_dev};
+  for (DevBuf *b : bufs) b->release();
+  for (auto &kv : c->tables) {
+    (void)hipFree(kv.second.slice);
+    (void)hipFree(kv.second.shift);
+  }
+  if (c->h_small) (void)hipHostFree(c->h_small);
+  (void)hipEventDestroy(c->ev0);
+  (void)hipEventDestroy(c->ev1);
+  (void)hipEventDestroy(c->evs0);
+  (void)hipEventDestroy(c->evs1);
+  if (c->own_stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+}
+
+int ewal_ctx_set_stream(ewal_ctx *c, void *s) {
+  if (!c) return EWAL_E_INVAL;
+  (void)hipSetDevice(c->device);
+  if (c->own_stream) (void)hipStreamDestroy(c->stream);
+  if (s) {
+    c->stream = (hipStream_t)s;
+    c->own_stream = false;
+  } else {
+    EW_CHECK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    c->own_stream = true;
+  }
+  return EWAL_OK;
+}
+
+int ewal_readall_device(ewal_ctx *c, const void *d_buf, uint64_t len, uint64_t ri, ewal_result *out) {
+  if (!c || !out || (!d_buf && len)) return EWAL_E_INVAL;
+  EW_CHECK(hipSetDevice(c->device));
+  return readall_impl(c, (const uint8_t *)d_buf, len, ri, out);
+}
+
+int ewal_device_alloc(ewal_ctx *c, uint64_t len, void **d_out) {
+  if (!c || !d_out) return EWAL_E_INVAL;
+  EW_CHECK(hipSetDevice(c->device));
+  if (hipMalloc(d_out, std::max<uint64_t>(len, 16)) != hipSuccess) return EWAL_E_NOMEM;
+  return EWAL_OK;
+}
+int ewal_device_free(ewal_ctx *c, void *d) {
+  if (!c) return EWAL_E_INVAL;
+  EW_CHECK(hipSetDevice(c->device));
+  if (d) EW_CHECK(hipFree(d));
+  return EWAL_OK;
+}
+int ewal_upload(ewal_ctx *c, void *d, const void *h, uint64_t len) {
+  if (!c || (len && (!d || !h))) return EWAL_E_INVAL;
+  EW_CHECK(hipSetDevice(c->device));
+  if (len) EW_CHECK(hipMemcpyAsync(d, h, len, hipMemcpyHostToDevice, c->stream));
+  EW_CHECK(hipStreamSynchronize(c->stream));
+  return EWAL_OK;
+}
+int ewal_download(ewal_ctx *c, void *h, const void *d, uint64_t len) {
+  if (!c || (len && (!d || !h))) return EWAL_E_INVAL;
+  EW_CHECK(hipSetDevice(c->device));
+  if (len) EW_CHECK(hipMemcpyAsync(h, d, len, hipMemcpyDeviceToHost, c->stream));
+  EW_CHECK(hipStreamSynchronize(c->stream));
+  return EWAL_OK;
+}
+
+int ewal_stage_to_device(ewal_ctx *c, const void *h_buf, uint64_t len, void **d_out) {
+  if (!c || !d_out || (!h_buf && len)) return EWAL_E_INVAL;
+  EW_CHECK(hipSetDevice(c->device));
+  EW_CHECK(c->hbuf_dev.ensure(len + 16));
+  if (len) EW_CHECK(hipMemcpyAsync(c->hbuf_dev.p, h_buf, len, hipMemcpyHostToDevice, c->stream));
+  EW_CHECK(hipStreamSynchronize(c->stream));
+  *d_out = c->hbuf_dev.p;
+  return EWAL_OK;
+}
+
+int ewal_readall_host(ewal_ctx *c, const void *h_buf, uint64_t len, uint64_t ri, ewal_result *out) {
+  if (!c || !out || (!h_buf && len)) return EWAL_E_INVAL;
+  EW_CHECK(hipSetDevice(c->device));
+  EW_CHECK(c->hbuf_dev.ensure(len + 16));
+  if (len) EW_CHECK(hipMemcpyAsync(c->hbuf_dev.p, h_buf, len, hipMemcpyHostToDevice, c->stream));
+  return readall_impl(c, c->hbuf_dev.as<uint8_t>(), len, ri, out);
+}
+
+int64_t ewal_copy_entries(ewal_ctx *c, ewal_entry *out, int64_t cap) {
+  if (!c || (!out && cap)) return EWAL_E_INVAL;
+  if (!c->last_ok) return 0;
+  int64_t n = std::min<int64_t>(cap, (int64_t)c->last_nents);
+  if (n > 0) {
+    EW_CHECK(hipMemcpyAsync(out, c->ents.p, (size_t)n * sizeof(ewal_entry), hipMemcpyDeviceToHost, c->stream));
+    EW_CHECK(hipStreamSynchronize(c->stream));
+  }
+  return n;
+}
+
+int64_t ewal_copy_records(ewal_ctx *c, ewal_record *out, int64_t cap) {
+  if (!c || (!out && cap)) return EWAL_E_INVAL;
+  int64_t n = std::min<int64_t>(cap, (int64_t)c->last_n);
+  if (n > 0) {
+    EW_CHECK(c->recs.ensure((size_t)n * sizeof(ewal_record)));
+    hipLaunchKernelGGL(k_records_out, dim3(grid_for(n, 256)), dim3(256), 0, c->stream, c->rd.as<RecDesc>(),
+                       (uint32_t)n, c->recs.as<ewal_record>());
+    EW_CHECK(hipMemcpyAsync(out, c->recs.p, (size_t)n * sizeof(ewal_record), hipMemcpyDeviceToHost, c->stream));
+    EW_CHECK(hipStreamSynchronize(c->stream));
+  }
+  return n;
+}
+
+int ewal_crc32_update_device(ewal_ctx *c, uint32_t crc, uint32_t poly, const void *d_buf, uint64_t n, uint32_t *out) {
+  if (!c || !out || (!d_buf && n)) return EWAL_E_INVAL;
+  if (n == 0) { *out = crc; return EWAL_OK; }
+  if (((uintptr_t)d_buf & 15) != 0) return EWAL_E_INVAL;
+  EW_CHECK(hipSetDevice(c->device));
+  DevTables *tb;
+  int rc = get_tables(c, poly, &tb);
+  if (rc) return rc;
+  EW_CHECK(c->small.ensure(sizeof(Small)));
+  rc = run_stream(c, tb, (const uint8_t *)d_buf, n, 0, 0, nullptr);
+  if (rc) return rc;
+  // P(n) = lin(all n bytes) from the stream prefixes (one thread).
+  EW_CHECK(c->sdesc.ensure(sizeof(uint32_t)));
+  hipLaunchKernelGGL(k_prefix_one, dim3(1), dim3(64), 0, c->stream, (const uint8_t *)d_buf, c->pwave.as<uint32_t>(),
+                     c->v.as<uint32_t>(), tb->slice, tb->shift, n, c->sdesc.as<uint32_t>());
+  uint32_t P = 0;
+  EW_CHECK(hipMemcpyAsync(&P, c->sdesc.p, 4, hipMemcpyDeviceToHost, c->stream));
+  EW_CHECK(hipStreamSynchronize(c->stream));
+  const ewal::CrcTables &ht = *c->host_tables[poly];
+  // Update(crc, D) = S_n(crc ^ ~0) ^ lin(D) ^ ~0
+  *out = ht.shift_n(n, crc ^ 0xffffffffu) ^ P ^ 0xffffffffu;
+  return EWAL_OK;
+}
+
+int esnap_verify_packed(ewal_ctx *c, const void *d_buf, uint64_t buf_len, const uint64_t *offs, const uint64_t *lens,
+                        uint32_t n, uint32_t poly, int32_t *status, uint32_t *stored_crc, uint32_t *computed_crc) {
+  if (!c || (!d_buf && buf_len) || (n && (!offs || !lens || !status))) return EWAL_E_INVAL;
+  if (((uintptr_t)d_buf & 15) != 0) return EWAL_E_INVAL;
+  EW_CHECK(hipSetDevice(c->device));
+  for (uint32_t i = 0; i < n; ++i)
+    if (offs[i] + lens[i] > buf_len || offs[i] + lens[i] < offs[i]) return EWAL_E_INVAL;
+  DevTables *tb;
+  int rc = get_tables(c, poly, &tb);
+  if (rc) return rc;
+  EW_CHECK(c->small.ensure(sizeof(Small)));
+  EW_CHECK(hipEventRecord(c->ev0, c->stream));
+  if (buf_len) {
+    rc = run_stream(c, tb, (const uint8_t *)d_buf, buf_len, 0, 0, nullptr);
+    if (rc) return rc;
+  }
+  std::vector<SnapDesc> h(n);
+  for (uint32_t i = 0; i < n; ++i) {
+    std::memset(&h[i], 0, sizeof(SnapDesc));
+    h[i].off = offs[i];
+    h[i].len = lens[i];
+  }
+  if (n) {
+    EW_CHECK(c->sdesc.ensure((size_t)n * sizeof(SnapDesc)));
+    EW_CHECK(hipMemcpyAsync(c->sdesc.p, h.data(), (size_t)n * sizeof(SnapDesc), hipMemcpyHostToDevice, c->stream));
+    EW_CHECK(c->snaps.ensure((size_t)n * sizeof(esnap_snapshot)));
+    hipLaunchKernelGGL(k_snap, dim3(grid_for(n, 256)), dim3(256), 0, c->stream, (const uint8_t *)d_buf,
+                       c->pwave.as<uint32_t>(), c->v.as<uint32_t>(), tb->slice, tb->shift, c->sdesc.as<SnapDesc>(),
+                       c->snaps.as<esnap_snapshot>(), n);
+    EW_CHECK(hipMemcpyAsync(h.data(), c->sdesc.p, (size_t)n * sizeof(SnapDesc), hipMemcpyDeviceToHost, c->stream));
+  }
+  EW_CHECK(hipEventRecord(c->ev1, c->stream));
+  EW_CHECK(hipStreamSynchronize(c->stream));
+  for (uint32_t i = 0; i < n; ++i) {
+    status[i] = h[i].st;
+    if (stored_crc) stored_crc[i] = h[i].stored;
+    if (computed_crc) computed_crc[i] = h[i].computed;
+  }
+  return EWAL_OK;
+}
+
+int esnap_copy_snapshot(ewal_ctx *c, uint32_t i, esnap_snapshot *out) {
+  if (!c || !out) return EWAL_E_INVAL;
+  EW_CHECK(hipMemcpy(out, c->snaps.as<esnap_snapshot>() + i, sizeof(*out), hipMemcpyDeviceToHost));
+  return EWAL_OK;
+}
+
+float ewal_last_device_ms(ewal_ctx *c) {
+  float ms = 0;
+  if (hipEventElapsedTime(&ms, c->ev0, c->ev1) != hipSuccess) return -1.f;
+  return ms;
+}
+
+int ecommit_batch_device(ewal_ctx *c, uint64_t G, const uint64_t *match, const uint8_t *nvoters, const uint64_t *term,
+                         uint64_t *committed, const uint64_t *log_offset, const uint64_t *log_ptr,
+                         const uint64_t *log_terms, uint8_t *changed, uint8_t *status, double *device_ms) {
+  if (!c) return EWAL_E_INVAL;
+  EW_CHECK(hipSetDevice(c->device));
+  EW_CHECK(hipEventRecord(c->ev0, c->stream));
+  if (G)
+    hipLaunchKernelGGL(k_commit, dim3((unsigned)((G + 255) / 256)), dim3(256), 0, c->stream, G, match, nvoters, term,
+                       committed, log_offset, log_ptr, log_terms, changed, status);
+  EW_CHECK(hipGetLastError());
+  EW_CHECK(hipEventRecord(c->ev1, c->stream));
+  EW_CHECK(hipEventSynchronize(c->ev1));
+  if (device_ms) {
+    float ms = 0;
+    EW_CHECK(hipEventElapsedTime(&ms, c->ev0, c->ev1));
+    *device_ms = ms;
+  }
+  return EWAL_OK;
+}
+
+}  // extern "C"

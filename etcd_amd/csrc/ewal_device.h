@@ -1,0 +1,147 @@
+// ewal_device.h -- device-side building blocks shared by the WAL, snapshot and
+// commit kernels (gfx950, wave64).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+#define EW_PIECE 64                      // bytes per lane in the stream pass
+#define EW_WAVE_BYTES 4096               // 64 lanes x 64 B
+#define EW_WAVES 16                      // waves per workgroup (1024 threads)
+#define EW_THREADS (EW_WAVES * 64)
+#define EW_TILE (EW_WAVES * EW_WAVE_BYTES)  // 64 KiB per tile (one look-back step)
+#define EW_TILE_LOG2 16
+#define EW_R 16                          // LDS replicas of each slicing table
+#define EW_NIL 0xFFFFFFFFu
+#define EW_LDS_SHIFT0 6                  // LDS holds S_{2^6} .. S_{2^15}
+#define EW_LDS_SHIFTS 10
+
+// ---- shift operators S_{2^m} -------------------------------------------
+// Byte tables: tb[k*256 + b] = S_{2^m}(b << 8k).
+__device__ __forceinline__ uint32_t tab_apply(const uint32_t *tb, uint32_t x) {
+  return tb[x & 0xff] ^ tb[256 + ((x >> 8) & 0xff)] ^ tb[512 + ((x >> 16) & 0xff)] ^ tb[768 + (x >> 24)];
+}
+// global tables, m = 0..47
+__device__ __forceinline__ uint32_t gshift_pow2(const uint32_t *g, int m, uint32_t x) {
+  return tab_apply(g + (size_t)m * 1024, x);
+}
+__device__ __forceinline__ uint32_t gshift_n(const uint32_t *g, uint64_t n, uint32_t x) {
+  while (n) {
+    int m = __builtin_ctzll(n);
+    n &= n - 1;
+    x = gshift_pow2(g, m, x);
+  }
+  return x;
+}
+
+// Slicing-by-4 step on a register already XORed with the next data word;
+// tables t[4][256] (t[0] = MakeTable(poly)), non-replicated layout.
+__device__ __forceinline__ uint32_t step4_flat(const uint32_t *t, uint32_t c) {
+  return t[768 + (c & 0xff)] ^ t[512 + ((c >> 8) & 0xff)] ^ t[256 + ((c >> 16) & 0xff)] ^ t[c >> 24];
+}
+// raw register continue over bytes [o, e) of buf (plain global loads).
+__device__ __forceinline__ uint32_t raw_bytes(const uint32_t *t, uint32_t c, const uint8_t *buf, uint64_t o, uint64_t e) {
+  while (o < e && (o & 3)) { c = t[(c ^ buf[o]) & 0xff] ^ (c >> 8); ++o; }
+  while (o + 4 <= e) { c = step4_flat(t, c ^ *(const uint32_t *)(buf + o)); o += 4; }
+  while (o < e) { c = t[(c ^ buf[o]) & 0xff] ^ (c >> 8); ++o; }
+  return c;
+}
+
+// ---- wave helpers ---------------------------------------------------------
+__device__ __forceinline__ uint32_t wave_xor(uint32_t x) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) x ^= __shfl_xor(x, d);
+  return x;
+}
+__device__ __forceinline__ unsigned long long wave_sum64(unsigned long long x) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) x += __shfl_xor(x, d);
+  return x;
+}
+
+// Tile descriptor for the decoupled look-back (one per 64 KiB tile).
+// agg  : VALID | count << 32 | lin(tile)        (one 8-byte sc1 store)
+// inc  : VALID | prefix lin through this tile   (stored after inc_cnt, drained)
+// inc_cnt: inclusive candidate count
+struct TileDesc {
+  unsigned long long agg, inc, inc_cnt, pad;
+};
+#define EW_DESC_VALID (1ull << 63)
+
+template <typename T>
+__device__ __forceinline__ T ld_agent(T *p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <typename T>
+__device__ __forceinline__ void st_agent(T *p, T v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// ---- Go varint readers (shifts >= width give 0) --------------------------
+// Reads buf[base+i...] while i < l; returns 0 or EWAL_ERR_UNEXPECTED_EOF (2).
+// width 32 keeps Go's uint32/int32 truncation ((uint32(b)&0x7F) << 28 loses bits).
+__device__ __forceinline__ int rd_varint(const uint8_t *p, int64_t &i, int64_t l, uint64_t &v, int width) {
+  for (uint32_t shift = 0;; shift += 7) {
+    if (i >= l) return 2;
+    uint8_t b = p[i++];
+    if (shift < (uint32_t)width) v |= (uint64_t)(b & 0x7F) << shift;
+    if (width == 32) v &= 0xffffffffull;
+    if (b < 0x80) return 0;
+  }
+}
+
+// ---- gogoprotobuf Unmarshal walker (exact Go semantics on the supported set)
+// kind[f] for field numbers 1..7: 0 unknown, PB_VAR64/PB_VAR32 (|= accumulate),
+// PB_BYTES (append; nil when empty), PB_REP64 (append to a repeated list).
+// Returns 0, 2 (io.ErrUnexpectedEOF), 7 (proto.ErrWrongType), 33 (bounds
+// panic) or 48 (EWAL_UNSUPPORTED_ENCODING: an unknown field needing proto.Skip,
+// or a bytes field whose repeats would concatenate two non-empty segments).
+#define PB_VAR64 1
+#define PB_VAR32 2
+#define PB_BYTES 3
+#define PB_REP64 4
+struct PbOut {
+  uint64_t v[8];
+  int64_t boff[8];
+  int64_t blen[8];
+  uint32_t nrep[8];
+};
+__device__ __forceinline__ void pb_init(PbOut &o) {
+#pragma unroll
+  for (int k = 0; k < 8; ++k) { o.v[k] = 0; o.boff[k] = -1; o.blen[k] = 0; o.nrep[k] = 0; }
+}
+__device__ inline int pb_walk(const uint8_t *p, int64_t l, const uint8_t *kind, PbOut &o,
+                              uint64_t *rep, uint32_t repcap) {
+  int64_t i = 0;
+  while (i < l) {
+    uint64_t wire = 0;
+    if (rd_varint(p, i, l, wire, 64)) return 2;
+    uint32_t fn = (uint32_t)(wire >> 3);   // int32(wire >> 3)
+    int wt = (int)(wire & 7);
+    int k = (fn >= 1 && fn <= 7) ? kind[fn] : 0;
+    if (k == 0) return 48;
+    if (k == PB_BYTES) {
+      if (wt != 2) return 7;
+      uint64_t bl = 0;
+      if (rd_varint(p, i, l, bl, 64)) return 2;
+      int64_t post = (int64_t)((uint64_t)i + bl);
+      if (post > l) return 2;
+      if (post < i) return 33;
+      if (post > i) {
+        if (o.blen[fn] > 0) return 48;
+        o.boff[fn] = i;
+        o.blen[fn] = post - i;
+      }
+      i = post;
+    } else if (k == PB_REP64) {
+      if (wt != 0) return 7;
+      uint64_t v = 0;
+      if (rd_varint(p, i, l, v, 64)) return 2;
+      if (o.nrep[fn] >= repcap) return 48;
+      rep[(fn == 2 ? 0 : repcap) + o.nrep[fn]++] = v;
+    } else {
+      if (wt != 0) return 7;
+      if (rd_varint(p, i, l, o.v[fn], k == PB_VAR32 ? 32 : 64)) return 2;
+    }
+  }
+  return 0;
+}

@@ -1,0 +1,598 @@
+// ewal_host.cpp -- host-side C++ of the engine: wal.OpenAtIndex file
+// selection, the write path (encoder/Create/Cut/Save), Snapshotter.Load
+// ordering, host CRC helpers and the synthetic WAL generator.
+//
+// None of this decodes or verifies WAL records: ReadAll/loadSnap
+// verification runs on the GPU (ewal_api.hip).  The write path computes the
+// chained CRC the way wal/encoder.go:25-37 does (crc.Write(Data) then
+// rec.Crc = Sum32), with the SSE4.2 crc32 instruction like Go's amd64 path.
+#include <dirent.h>
+#include <fcntl.h>
+#include <sys/stat.h>
+#include <unistd.h>
+#include <nmmintrin.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cerrno>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/ewal.h"
+#include "crc_math.h"
+
+namespace {
+
+const uint32_t kCastagnoli = 0x82F63B78u;
+
+std::mutex g_tab_mu;
+std::map<uint32_t, std::unique_ptr<ewal::CrcTables>> g_tabs;
+
+const ewal::CrcTables &tables(uint32_t poly) {
+  std::lock_guard<std::mutex> lk(g_tab_mu);
+  auto it = g_tabs.find(poly);
+  if (it != g_tabs.end()) return *it->second;
+  auto t = std::make_unique<ewal::CrcTables>(poly);
+  const ewal::CrcTables &r = *t;
+  g_tabs[poly] = std::move(t);
+  return r;
+}
+
+__attribute__((target("sse4.2"))) uint32_t crc32c_hw(uint32_t crc, const uint8_t *p, size_t n) {
+  uint64_t c = (uint32_t)~crc;
+  while (n && ((uintptr_t)p & 7)) { c = _mm_crc32_u8((uint32_t)c, *p++); n--; }
+  // three independent streams hide the instruction latency on long buffers
+  while (n >= 3 * 4096) {
+    uint64_t c1 = 0, c2 = 0;
+    const uint8_t *p1 = p + 4096, *p2 = p + 8192;
+    for (int i = 0; i < 4096; i += 8) {
+      uint64_t a, b, d;
+      std::memcpy(&a, p + i, 8);
+      std::memcpy(&b, p1 + i, 8);
+      std::memcpy(&d, p2 + i, 8);
+      c = _mm_crc32_u64(c, a);
+      c1 = _mm_crc32_u64(c1, b);
+      c2 = _mm_crc32_u64(c2, d);
+    }
+    // raw(c, A||B||C) = S_8192(c) ^ S_4096(lin B) ^ lin C  (registers, no inversion)
+    static const ewal::CrcTables &t = tables(kCastagnoli);
+    c = t.shift_pow2(13, (uint32_t)c) ^ t.shift_pow2(12, (uint32_t)c1) ^ (uint32_t)c2;
+    p += 3 * 4096;
+    n -= 3 * 4096;
+  }
+  while (n >= 8) { uint64_t v; std::memcpy(&v, p, 8); c = _mm_crc32_u64(c, v); p += 8; n -= 8; }
+  while (n) { c = _mm_crc32_u8((uint32_t)c, *p++); n--; }
+  return ~(uint32_t)c;
+}
+
+uint32_t crc_update(uint32_t crc, uint32_t poly, const uint8_t *p, size_t n) {
+  if (poly == kCastagnoli && __builtin_cpu_supports("sse4.2")) return crc32c_hw(crc, p, n);
+  return tables(poly).update(crc, p, n);
+}
+
+// ---- protobuf marshal (MarshalTo of the generated code) --------------------
+inline size_t sov(uint64_t x) { size_t n = 0; do { n++; x >>= 7; } while (x); return n; }
+inline uint8_t *put_varint(uint8_t *o, uint64_t v) {
+  while (v >= 0x80) { *o++ = (uint8_t)(v | 0x80); v >>= 7; }
+  *o++ = (uint8_t)v;
+  return o;
+}
+// raftpb.Entry.MarshalTo, raft/raftpb/raft.pb.go:921-943
+size_t entry_size(int32_t type, uint64_t term, uint64_t index, uint64_t n) {
+  return 1 + sov((uint64_t)(int64_t)type) + 1 + sov(term) + 1 + sov(index) + 1 + sov(n) + n;
+}
+uint8_t *entry_marshal(uint8_t *o, int32_t type, uint64_t term, uint64_t index, const uint8_t *d, uint64_t n) {
+  *o++ = 0x08; o = put_varint(o, (uint64_t)(int64_t)type);
+  *o++ = 0x10; o = put_varint(o, term);
+  *o++ = 0x18; o = put_varint(o, index);
+  *o++ = 0x22; o = put_varint(o, n);
+  if (n) std::memcpy(o, d, n);
+  return o + n;
+}
+// raftpb.HardState.MarshalTo, raft.pb.go:1079-1097
+size_t state_marshal(uint8_t *o, uint64_t term, uint64_t vote, uint64_t commit) {
+  uint8_t *s = o;
+  *o++ = 0x08; o = put_varint(o, term);
+  *o++ = 0x10; o = put_varint(o, vote);
+  *o++ = 0x18; o = put_varint(o, commit);
+  return (size_t)(o - s);
+}
+// walpb.Record.MarshalTo, wal/walpb/record.pb.go:175-196, prefixed by the
+// int64 LE length (wal/encoder.go:32-35).
+size_t frame_size(int64_t type, uint32_t crc, uint64_t n, bool nil) {
+  size_t r = 1 + sov((uint64_t)type) + 1 + sov(crc);
+  if (!nil) r += 1 + sov(n) + n;
+  return 8 + r;
+}
+uint8_t *frame_write(uint8_t *o, int64_t type, uint32_t crc, const uint8_t *d, uint64_t n, bool nil) {
+  int64_t L = (int64_t)frame_size(type, crc, n, nil) - 8;
+  std::memcpy(o, &L, 8);
+  o += 8;
+  *o++ = 0x08; o = put_varint(o, (uint64_t)type);
+  *o++ = 0x10; o = put_varint(o, crc);
+  if (!nil) {
+    *o++ = 0x1a; o = put_varint(o, n);
+    if (n) std::memcpy(o, d, n);
+    o += n;
+  }
+  return o;
+}
+
+// ---- wal file names, wal/util.go:20-88 -------------------------------------
+// fmt.Sscanf(str, "%016x-%016x.wal", &seq, &index): hex fields of at most 16
+// digits, literal '-' and ".wal"; trailing text is not examined.
+bool scan_hex16(const char *&s, uint64_t &v) {
+  v = 0;
+  int n = 0;
+  while (n < 16) {
+    char ch = *s;
+    int d;
+    if (ch >= '0' && ch <= '9') d = ch - '0';
+    else if (ch >= 'a' && ch <= 'f') d = ch - 'a' + 10;
+    else if (ch >= 'A' && ch <= 'F') d = ch - 'A' + 10;
+    else break;
+    v = (v << 4) | (uint64_t)d;
+    ++s;
+    ++n;
+  }
+  return n > 0;
+}
+bool parse_wal_name(const std::string &name, uint64_t *seq, uint64_t *index) {
+  const char *s = name.c_str();
+  uint64_t a = 0, b = 0;
+  if (!scan_hex16(s, a)) return false;
+  if (*s != '-') return false;
+  ++s;
+  if (!scan_hex16(s, b)) return false;
+  if (std::strncmp(s, ".wal", 4) != 0) return false;
+  *seq = a;
+  *index = b;
+  return true;
+}
+std::string wal_name(uint64_t seq, uint64_t index) {
+  char b[64];
+  std::snprintf(b, sizeof b, "%016llx-%016llx.wal", (unsigned long long)seq, (unsigned long long)index);
+  return b;
+}
+bool read_dir(const std::string &dir, std::vector<std::string> *names) {
+  DIR *d = opendir(dir.c_str());
+  if (!d) return false;
+  while (dirent *e = readdir(d)) {
+    std::string n = e->d_name;
+    if (n == "." || n == "..") continue;
+    names->push_back(n);
+  }
+  closedir(d);
+  return true;
+}
+bool read_file(const std::string &path, std::vector<uint8_t> *out, size_t pad) {
+  FILE *f = std::fopen(path.c_str(), "rb");
+  if (!f) return false;
+  std::fseek(f, 0, SEEK_END);
+  long sz = std::ftell(f);
+  std::fseek(f, 0, SEEK_SET);
+  size_t base = out->size();
+  out->resize(base + (size_t)sz + pad);
+  size_t got = sz ? std::fread(out->data() + base, 1, (size_t)sz, f) : 0;
+  std::fclose(f);
+  out->resize(base + got);
+  return got == (size_t)sz;
+}
+
+}  // namespace
+
+// ===========================================================================
+struct ewal_wal {
+  std::string dir;
+  uint64_t ri = 0;
+  uint64_t seq = 0;
+  std::vector<uint8_t> bytes;
+};
+
+struct ewal_encoder {
+  std::vector<uint8_t> buf;
+  uint32_t crc = 0;
+};
+
+struct ewal_writer {
+  std::string dir;
+  std::vector<uint8_t> md;
+  bool md_nil = true;
+  uint64_t seq = 0, enti = 0;
+  int fd = -1;
+  ewal_encoder enc;
+};
+
+extern "C" {
+
+const char *ewal_status_string(int st) {
+  switch (st) {
+  case EWAL_OK: return "ok";
+  case EWAL_EOF: return "EOF";
+  case EWAL_ERR_UNEXPECTED_EOF: return "unexpected EOF";
+  case EWAL_ERR_RECORD_CRC: return "walpb: crc mismatch";
+  case EWAL_ERR_WAL_CRC: return "wal: crc mismatch";
+  case EWAL_ERR_METADATA_CONFLICT: return "wal: conflicting metadata found";
+  case EWAL_ERR_INDEX_NOT_FOUND: return "wal: index not found in file";
+  case EWAL_ERR_WRONG_TYPE: return "proto: field/encoding mismatch: wrong type for field";
+  case EWAL_ERR_UNEXPECTED_TYPE: return "unexpected block type";
+  case EWAL_ERR_FILE_NOT_FOUND: return "wal: file not found";
+  case EWAL_ERR_SNAP_CRC: return "snap: crc mismatch";
+  case EWAL_ERR_NO_SNAPSHOT: return "snap: no available snapshot";
+  case EWAL_PANIC_NEG_LENGTH: return "panic: makeslice: len out of range";
+  case EWAL_PANIC_BOUNDS: return "panic: runtime error: slice bounds out of range";
+  case EWAL_PANIC_ENTRY: return "panic: mustUnmarshalEntry";
+  case EWAL_PANIC_STATE: return "panic: mustUnmarshalState";
+  case EWAL_PANIC_INDEX_GAP: return "panic: ents index gap";
+  case EWAL_NONTERMINATING: return "reference does not terminate";
+  case EWAL_UNSUPPORTED_ENCODING: return "unsupported (non-canonical) record encoding";
+  case EWAL_E_HIP: return "HIP error";
+  case EWAL_E_INVAL: return "invalid argument";
+  case EWAL_E_NOMEM: return "out of memory";
+  case EWAL_E_NODEVICE: return "no GPU device";
+  case EWAL_E_TIMEOUT: return "device timeout";
+  case EWAL_E_IO: return "I/O error";
+  default: return "unknown";
+  }
+}
+
+uint32_t ewal_crc32_update_host(uint32_t crc, uint32_t poly, const uint8_t *p, uint64_t n) {
+  return crc_update(crc, poly, p, (size_t)n);
+}
+
+uint32_t ewal_crc32_combine(uint32_t poly, uint32_t crc_a, uint32_t crc_b, uint64_t len_b) {
+  return tables(poly).combine(crc_a, crc_b, len_b);
+}
+
+// ---- wal.OpenAtIndex, wal/wal.go:108-159 ------------------------------------
+int ewal_open_at_index(const char *dirpath, uint64_t index, ewal_wal **out) {
+  *out = nullptr;
+  std::vector<std::string> all, names;
+  if (!read_dir(dirpath, &all)) return EWAL_E_IO;
+  for (auto &n : all) {   // checkWalNames
+    uint64_t s, i;
+    if (parse_wal_name(n, &s, &i)) names.push_back(n);
+  }
+  if (names.empty()) return EWAL_ERR_FILE_NOT_FOUND;
+  std::sort(names.begin(), names.end());
+  // searchIndex: last name whose start index <= index
+  long ni = -1;
+  for (long k = (long)names.size() - 1; k >= 0; --k) {
+    uint64_t s, i;
+    parse_wal_name(names[(size_t)k], &s, &i);
+    if (index >= i) { ni = k; break; }
+  }
+  if (ni < 0) return EWAL_ERR_FILE_NOT_FOUND;
+  // isValidSeq(names[nameIndex:])
+  uint64_t last = 0;
+  for (size_t k = (size_t)ni; k < names.size(); ++k) {
+    uint64_t s, i;
+    parse_wal_name(names[k], &s, &i);
+    if (last != 0 && last != s - 1) return EWAL_ERR_FILE_NOT_FOUND;
+    last = s;
+  }
+  auto *w = new ewal_wal();
+  w->dir = dirpath;
+  w->ri = index;
+  for (size_t k = (size_t)ni; k < names.size(); ++k) {
+    if (!read_file(std::string(dirpath) + "/" + names[k], &w->bytes, 0)) {
+      delete w;
+      return EWAL_E_IO;
+    }
+  }
+  uint64_t s, i;
+  parse_wal_name(names.back(), &s, &i);
+  w->seq = s;
+  *out = w;
+  return EWAL_OK;
+}
+
+int ewal_wal_readall(ewal_wal *w, ewal_ctx *ctx, ewal_result *out) {
+  if (!w) return EWAL_E_INVAL;
+  return ewal_readall_host(ctx, w->bytes.data(), w->bytes.size(), w->ri, out);
+}
+
+const uint8_t *ewal_wal_bytes(ewal_wal *w, uint64_t *len) {
+  if (len) *len = w->bytes.size();
+  return w->bytes.data();
+}
+uint64_t ewal_wal_seq(ewal_wal *w) { return w->seq; }
+void ewal_wal_close(ewal_wal *w) { delete w; }
+
+// ---- encoder.encode, wal/encoder.go:25-37 ------------------------------------
+ewal_encoder *ewal_encoder_new(uint32_t prev_crc, uint64_t reserve) {
+  auto *e = new ewal_encoder();
+  e->crc = prev_crc;
+  if (reserve) e->buf.reserve((size_t)reserve);
+  return e;
+}
+int ewal_encoder_encode(ewal_encoder *e, int64_t type, const uint8_t *data, uint64_t n, int data_nil) {
+  const bool nil = data_nil != 0;
+  e->crc = crc_update(e->crc, kCastagnoli, data, nil ? 0 : (size_t)n);
+  const size_t sz = frame_size(type, e->crc, n, nil);
+  const size_t base = e->buf.size();
+  e->buf.resize(base + sz);
+  frame_write(e->buf.data() + base, type, e->crc, data, n, nil);
+  return EWAL_OK;
+}
+int ewal_encoder_save_entry(ewal_encoder *e, int32_t type, uint64_t term, uint64_t index, const uint8_t *data,
+                            uint64_t n) {
+  std::vector<uint8_t> b(entry_size(type, term, index, n));
+  entry_marshal(b.data(), type, term, index, data, n);
+  return ewal_encoder_encode(e, EWAL_ENTRY, b.data(), b.size(), 0);
+}
+int ewal_encoder_save_state(ewal_encoder *e, uint64_t term, uint64_t vote, uint64_t commit) {
+  if (term == 0 && vote == 0 && commit == 0) return EWAL_OK;   // raft.IsEmptyHardState
+  uint8_t b[40];
+  size_t n = state_marshal(b, term, vote, commit);
+  return ewal_encoder_encode(e, EWAL_STATE, b, n, 0);
+}
+const uint8_t *ewal_encoder_bytes(ewal_encoder *e, uint64_t *len) {
+  if (len) *len = e->buf.size();
+  return e->buf.data();
+}
+uint32_t ewal_encoder_crc(ewal_encoder *e) { return e->crc; }
+void ewal_encoder_free(ewal_encoder *e) { delete e; }
+
+// ---- Create / Cut / Save / Sync, wal/wal.go:72-100, 219-292 ------------------
+static int writer_flush(ewal_writer *w) {
+  const uint8_t *p = w->enc.buf.data();
+  size_t n = w->enc.buf.size();
+  while (n) {
+    ssize_t k = ::write(w->fd, p, n);
+    if (k < 0) {
+      if (errno == EINTR) continue;
+      return EWAL_E_IO;
+    }
+    p += k;
+    n -= (size_t)k;
+  }
+  w->enc.buf.clear();
+  return EWAL_OK;
+}
+static int writer_open(ewal_writer *w, uint64_t seq, uint64_t index) {
+  std::string p = w->dir + "/" + wal_name(seq, index);
+  w->fd = ::open(p.c_str(), O_WRONLY | O_APPEND | O_CREAT, 0600);
+  return w->fd < 0 ? EWAL_E_IO : EWAL_OK;
+}
+int ewal_create(const char *dirpath, const uint8_t *md, uint64_t mlen, int md_nil, ewal_writer **out) {
+  *out = nullptr;
+  std::vector<std::string> names;
+  if (read_dir(dirpath, &names) && !names.empty()) { errno = EEXIST; return EWAL_E_IO; }   // os.ErrExist
+  std::string cmd = dirpath;
+  // os.MkdirAll(dirpath, 0700)
+  for (size_t i = 1; i <= cmd.size(); ++i)
+    if (i == cmd.size() || cmd[i] == '/') ::mkdir(cmd.substr(0, i).c_str(), 0700);
+  auto *w = new ewal_writer();
+  w->dir = dirpath;
+  w->md.assign(md, md + (md_nil ? 0 : mlen));
+  w->md_nil = md_nil != 0;
+  if (writer_open(w, 0, 0) != EWAL_OK) { delete w; return EWAL_E_IO; }
+  w->enc.crc = 0;
+  ewal_encoder_encode(&w->enc, EWAL_CRC, nullptr, 0, 1);        // saveCrc(0)
+  ewal_encoder_encode(&w->enc, EWAL_METADATA, w->md.data(), w->md.size(), w->md_nil);
+  *out = w;
+  return EWAL_OK;
+}
+int ewal_writer_save_entry(ewal_writer *w, int32_t type, uint64_t term, uint64_t index, const uint8_t *data,
+                           uint64_t n) {
+  ewal_encoder_save_entry(&w->enc, type, term, index, data, n);
+  w->enti = index;
+  return EWAL_OK;
+}
+int ewal_writer_save_state(ewal_writer *w, uint64_t term, uint64_t vote, uint64_t commit) {
+  return ewal_encoder_save_state(&w->enc, term, vote, commit);
+}
+int ewal_writer_sync(ewal_writer *w) {
+  int rc = writer_flush(w);
+  if (rc) return rc;
+  return ::fsync(w->fd) == 0 ? EWAL_OK : EWAL_E_IO;
+}
+int ewal_writer_cut(ewal_writer *w) {
+  const uint64_t nseq = w->seq + 1, nidx = w->enti + 1;
+  int rc = ewal_writer_sync(w);
+  if (rc) return rc;
+  ::close(w->fd);
+  w->fd = -1;
+  if (writer_open(w, nseq, nidx) != EWAL_OK) return EWAL_E_IO;
+  w->seq = nseq;
+  const uint32_t prev = w->enc.crc;   // encoder re-created with prevCrc
+  w->enc.crc = prev;
+  ewal_encoder_encode(&w->enc, EWAL_CRC, nullptr, 0, 1);          // saveCrc(prevCrc)
+  return ewal_encoder_encode(&w->enc, EWAL_METADATA, w->md.data(), w->md.size(), w->md_nil);
+}
+void ewal_writer_close(ewal_writer *w) {
+  if (!w) return;
+  if (w->fd >= 0) {
+    ewal_writer_sync(w);
+    ::close(w->fd);
+  }
+  delete w;
+}
+
+// ---- synthetic WAL generator -------------------------------------------------
+// Create(Info{ID:1}) + Save(HardState{Term:1,Vote:1}, ents) where ents[i] =
+// Entry{Type:0, Term:1, Index:i+1, Data: len_i bytes}, len_i log-uniform in
+// [min_data, max_data] and the payload from xorshift64* seeded per entry.
+// Two parallel passes: (1) CRC-32C of each entry's marshalled bytes,
+// (2) layout from the chained CRCs (varint widths), then bytes in place.
+static inline uint64_t mix64(uint64_t z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+static void fill_payload(uint8_t *o, uint64_t n, uint64_t seed) {
+  uint64_t x = mix64(seed) | 1;
+  uint64_t i = 0;
+  for (; i + 8 <= n; i += 8) {
+    x ^= x >> 12; x ^= x << 25; x ^= x >> 27;
+    uint64_t v = x * 0x2545F4914F6CDD1Dull;
+    std::memcpy(o + i, &v, 8);
+  }
+  if (i < n) {
+    x ^= x >> 12; x ^= x << 25; x ^= x >> 27;
+    uint64_t v = x * 0x2545F4914F6CDD1Dull;
+    std::memcpy(o + i, &v, (size_t)(n - i));
+  }
+}
+
+int64_t ewal_synth_wal(uint64_t seed, uint64_t target, uint32_t min_data, uint32_t max_data, int64_t corrupt_record,
+                       uint8_t *out, uint64_t cap, int64_t *n_records) {
+  if (min_data == 0 || max_data < min_data) return EWAL_E_INVAL;
+  // entry sizes
+  std::vector<uint32_t> sz;
+  const double lo = std::log((double)min_data), hi = std::log((double)max_data + 1.0);
+  uint64_t rng = mix64(seed ^ 0x5157A11ull);
+  uint64_t approx = 64;
+  while (approx < target) {
+    rng = mix64(rng);
+    double u = (double)(rng >> 11) * (1.0 / 9007199254740992.0);
+    uint32_t s = (uint32_t)std::exp(lo + u * (hi - lo));
+    s = std::min(std::max(s, min_data), max_data);
+    sz.push_back(s);
+    approx += 8 + 2 + 5 + 1 + sov(s + 32) + entry_size(0, 1, sz.size(), s);
+  }
+  const size_t N = sz.size();
+  const uint8_t md[2] = {0x08, 0x01};   // etcdserverpb.Info{ID: 1}
+  uint8_t st[40];
+  const size_t stn = state_marshal(st, 1, 1, 0);
+  // pass 1: Update(0, entry bytes) per entry, in parallel
+  std::vector<uint32_t> ecrc(N);
+  unsigned nth = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  {
+    std::atomic<size_t> next(0);
+    std::vector<std::thread> th;
+    for (unsigned t = 0; t < nth; ++t)
+      th.emplace_back([&]() {
+        std::vector<uint8_t> tmp;
+        for (;;) {
+          size_t i = next.fetch_add(256);
+          if (i >= N) break;
+          for (size_t j = i; j < std::min(N, i + 256); ++j) {
+            tmp.resize(entry_size(0, 1, j + 1, sz[j]));
+            uint8_t *o = tmp.data();
+            *o++ = 0x08; o = put_varint(o, 0);
+            *o++ = 0x10; o = put_varint(o, 1);
+            *o++ = 0x18; o = put_varint(o, j + 1);
+            *o++ = 0x22; o = put_varint(o, sz[j]);
+            fill_payload(o, sz[j], seed * 1000003ull + j);
+            ecrc[j] = crc_update(0, kCastagnoli, tmp.data(), tmp.size());
+          }
+        }
+      });
+    for (auto &x : th) x.join();
+  }
+  // pass 2 (serial, O(N)): chained CRCs and frame offsets
+  const ewal::CrcTables &T = tables(kCastagnoli);
+  std::vector<uint64_t> foff(N);
+  std::vector<uint32_t> fcrc(N);
+  uint32_t c = 0;
+  uint64_t off = 0;
+  // crc record, metadata, state
+  const uint32_t c_crc = c;
+  off += frame_size(4, c_crc, 0, true);
+  c = crc_update(c, kCastagnoli, md, 2);
+  const uint32_t c_md = c;
+  off += frame_size(1, c_md, 2, false);
+  c = crc_update(c, kCastagnoli, st, stn);
+  const uint32_t c_st = c;
+  off += frame_size(3, c_st, stn, false);
+  const uint64_t head = off;
+  for (size_t j = 0; j < N; ++j) {
+    const uint64_t en = entry_size(0, 1, j + 1, sz[j]);
+    c = T.combine(c, ecrc[j], en);
+    fcrc[j] = c;
+    foff[j] = off;
+    off += frame_size(2, c, en, false);
+  }
+  if (off > cap) return EWAL_E_NOMEM;
+  // write head frames
+  uint8_t *o = out;
+  o = frame_write(o, 4, c_crc, nullptr, 0, true);
+  o = frame_write(o, 1, c_md, md, 2, false);
+  o = frame_write(o, 3, c_st, st, stn, false);
+  (void)head;
+  // pass 3: frames in place, in parallel
+  {
+    std::atomic<size_t> next(0);
+    std::vector<std::thread> th;
+    for (unsigned t = 0; t < nth; ++t)
+      th.emplace_back([&]() {
+        for (;;) {
+          size_t i = next.fetch_add(256);
+          if (i >= N) break;
+          for (size_t j = i; j < std::min(N, i + 256); ++j) {
+            const uint64_t en = entry_size(0, 1, j + 1, sz[j]);
+            uint8_t *f = out + foff[j];
+            int64_t L = (int64_t)frame_size(2, fcrc[j], en, false) - 8;
+            std::memcpy(f, &L, 8);
+            uint8_t *p = f + 8;
+            *p++ = 0x08; p = put_varint(p, 2);
+            *p++ = 0x10; p = put_varint(p, fcrc[j]);
+            *p++ = 0x1a; p = put_varint(p, en);
+            *p++ = 0x08; p = put_varint(p, 0);
+            *p++ = 0x10; p = put_varint(p, 1);
+            *p++ = 0x18; p = put_varint(p, j + 1);
+            *p++ = 0x22; p = put_varint(p, sz[j]);
+            fill_payload(p, sz[j], seed * 1000003ull + j);
+            if ((int64_t)(j + 3) == corrupt_record) p[sz[j] / 2] ^= 0x5a;
+          }
+        }
+      });
+    for (auto &x : th) x.join();
+  }
+  if (n_records) *n_records = (int64_t)(N + 3);
+  return (int64_t)off;
+}
+
+// ---- Snapshotter.Load, snap/snapshotter.go:62-74, 76-111, 115-150 ----------
+int esnap_load_dir(ewal_ctx *ctx, const char *dirpath, uint32_t poly, esnap_snapshot *out, char **out_name) {
+  if (out_name) *out_name = nullptr;
+  std::vector<std::string> all, snaps;
+  if (!read_dir(dirpath, &all)) return EWAL_E_IO;
+  for (auto &n : all)   // checkSuffix
+    if (n.size() >= 5 && n.compare(n.size() - 5, 5, ".snap") == 0) snaps.push_back(n);
+  if (snaps.empty()) return EWAL_ERR_NO_SNAPSHOT;
+  std::sort(snaps.rbegin(), snaps.rend());   // sort.Reverse(sort.StringSlice)
+  int err = EWAL_ERR_NO_SNAPSHOT;
+  for (auto &name : snaps) {
+    const std::string path = std::string(dirpath) + "/" + name;
+    std::vector<uint8_t> b;
+    int st;
+    if (!read_file(path, &b, 0)) {
+      st = EWAL_E_IO;
+    } else {
+      // one-file batch on the GPU
+      void *d = nullptr;
+      int rc = ewal_stage_to_device(ctx, b.data(), b.size(), &d);
+      if (rc) return rc;
+      uint64_t off = 0, len = b.size();
+      int32_t s = 0;
+      rc = esnap_verify_packed(ctx, d, len, &off, &len, 1, poly, &s, nullptr, nullptr);
+      if (rc) return rc;
+      st = s;
+      if (st == EWAL_OK) {
+        rc = esnap_copy_snapshot(ctx, 0, out);
+        if (rc) return rc;
+        if (out_name) *out_name = strdup(name.c_str());
+        return EWAL_OK;
+      }
+    }
+    err = st;
+    std::string broken = path + ".broken";   // renameBroken
+    if (std::rename(path.c_str(), broken.c_str()) != 0)
+      std::fprintf(stderr, "Cannot rename broken snapshot file %s to %s\n", path.c_str(), broken.c_str());
+  }
+  return err;
+}
+
+}  // extern "C"

@@ -1,0 +1,58 @@
+// ewal_internal.h -- structures shared between the kernels and the host driver.
+#pragma once
+#include <cstdint>
+#include "../../include/ewal.h"
+
+struct TileDesc;
+
+struct StreamArgs {
+  const uint8_t *buf;      // WAL bytes (device, 16-B aligned)
+  uint64_t B;              // byte count
+  uint32_t ntiles;         // ceil(B / EW_TILE)
+  int find_cand;           // 1: WAL framing candidates, 0: CRC prefixes only
+  const uint32_t *g_slice; // [4][256]
+  const uint32_t *g_shift; // [48][4][256]
+  uint32_t *v;             // lin of every 64-B piece        [ntiles*1024]
+  uint32_t *pwave;         // stream prefix at every 4 KiB    [ntiles*16]
+  uint64_t *cpos;          // candidate frame offsets (sorted)
+  uint64_t *clen;          // candidate frame lengths (int64 prefix)
+  uint64_t ccap;
+  TileDesc *desc;          // [ntiles], zeroed per launch
+  uint32_t *ticket;        // zeroed per launch
+  uint32_t *errflag;
+};
+
+// Per-frame descriptor (device), 96 B.
+struct RecDesc {
+  uint64_t off;            // frame start
+  uint64_t doff, dlen;     // Record.Data
+  int64_t type;            // Record.Type
+  uint32_t crc;            // Record.Crc (stored)
+  uint32_t chained;        // decoder CRC after this frame
+  int32_t st;              // EWAL_* status of this frame
+  int32_t sub_st;          // Entry/HardState Unmarshal status
+  uint64_t f0, f1, f2;     // Entry: Term, Index; HardState: Term, Vote, Commit
+  uint64_t edoff, edlen;   // Entry.Data
+  int32_t etype;           // Entry.Type
+  uint8_t dnil, enil, pad0, pad1;
+};
+
+struct ChainInfo {
+  uint32_t last_cand;      // candidate index of the chain's last frame
+  uint32_t pad;
+};
+
+struct ReadAllAgg {
+  unsigned long long first_fail;  // min ordinal with st != 0
+  long long last_entry;           // max ordinal of an entry frame
+  long long last_state;           // max ordinal of a state frame
+  unsigned long long first_meta;  // min ordinal of a non-empty metadata frame
+};
+
+// Snapshot verify per-file descriptor.
+struct SnapDesc {
+  uint64_t off, len;       // file within the packed buffer
+  uint64_t doff, dlen;     // snappb.Snapshot.Data
+  uint32_t stored, computed;
+  int32_t st, pad;
+};

@@ -1,0 +1,316 @@
+"""Host-side mirror of etcd's `wal` package over the MI355X engine.
+
+Names, argument meaning and error behaviour follow the reference
+(mzsanford/etcd v0.5.0-alpha):
+  OpenAtIndex(dirpath, index)      wal/wal.go:108-159
+  WAL.ReadAll() -> (metadata, state, ents)   wal/wal.go:164-216
+  Create(dirpath, metadata) / SaveEntry / SaveState / Save / Cut / Sync / Close
+                                   wal/wal.go:72-100, 219-292
+Errors are raised as exceptions carrying the Go sentinel they stand for
+(see ERRORS); Go panics are raised as GoPanic.  All verification runs on
+the GPU through libewal.so.
+"""
+import ctypes as C
+from dataclasses import dataclass, field
+from typing import List, Optional
+
+from . import _lib as L
+from ._lib import lib, check, EwalError, GoPanic  # noqa: F401
+
+# Go sentinel name for each status (for messages and test readability)
+ERRORS = {
+    L.ERR_UNEXPECTED_EOF: "io.ErrUnexpectedEOF",
+    L.ERR_RECORD_CRC: "walpb.ErrCRCMismatch",
+    L.ERR_WAL_CRC: "wal.ErrCRCMismatch",
+    L.ERR_METADATA_CONFLICT: "wal.ErrMetadataConflict",
+    L.ERR_INDEX_NOT_FOUND: "wal.ErrIndexNotFound",
+    L.ERR_WRONG_TYPE: "proto.ErrWrongType",
+    L.ERR_UNEXPECTED_TYPE: "unexpected block type",
+    L.ERR_FILE_NOT_FOUND: "wal.ErrFileNotFound",
+}
+
+metadataType, entryType, stateType, crcType = 1, 2, 3, 4
+
+
+@dataclass
+class HardState:
+    """raftpb.HardState, raft/raftpb/raft.pb.go:143-148"""
+    Term: int = 0
+    Vote: int = 0
+    Commit: int = 0
+
+
+@dataclass
+class Entry:
+    """raftpb.Entry, raft/raftpb/raft.pb.go:100-106 (Data None == Go nil)"""
+    Type: int = 0
+    Term: int = 0
+    Index: int = 0
+    Data: Optional[bytes] = None
+
+
+class Context:
+    """One GPU context (device workspace + stream), ewal_ctx_create."""
+
+    def __init__(self, device=0):
+        self._p = C.c_void_p()
+        check(lib.ewal_ctx_create(device, C.byref(self._p)))
+        self.device = device
+
+    @property
+    def handle(self):
+        return self._p
+
+    def close(self):
+        if self._p:
+            lib.ewal_ctx_destroy(self._p)
+            self._p = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def alloc(self, n):
+        d = C.c_void_p()
+        check(lib.ewal_device_alloc(self._p, n, C.byref(d)))
+        return DeviceBuffer(self, d, n)
+
+
+class DeviceBuffer:
+    """Device memory owned through the library (ewal_device_alloc)."""
+
+    def __init__(self, ctx, ptr, n):
+        self.ctx, self.ptr, self.n = ctx, ptr, n
+
+    def upload(self, data, offset=0):
+        b = bytes(data) if not isinstance(data, (bytes, bytearray)) else data
+        src = (C.c_char * len(b)).from_buffer_copy(b) if isinstance(b, bytes) else (C.c_char * len(b)).from_buffer(b)
+        check(lib.ewal_upload(self.ctx.handle, C.c_void_p(self.ptr.value + offset), src, len(b)))
+
+    def upload_ptr(self, host_ptr, n, offset=0):
+        check(lib.ewal_upload(self.ctx.handle, C.c_void_p(self.ptr.value + offset), C.c_void_p(host_ptr), n))
+
+    def download(self, n=None, offset=0):
+        n = self.n if n is None else n
+        out = (C.c_char * n)()
+        check(lib.ewal_download(self.ctx.handle, out, C.c_void_p(self.ptr.value + offset), n))
+        return out.raw
+
+    def free(self):
+        if self.ptr:
+            lib.ewal_device_free(self.ctx.handle, self.ptr)
+            self.ptr = C.c_void_p()
+
+
+_default_ctx = None
+
+
+def default_context():
+    global _default_ctx
+    if _default_ctx is None:
+        _default_ctx = Context(0)
+    return _default_ctx
+
+
+@dataclass
+class ReadAllResult:
+    status: int
+    detail: int
+    fail_record: int
+    fail_offset: int
+    n_records: int
+    last_crc: int
+    enti: int
+    metadata: Optional[bytes]
+    state: HardState
+    ents: List[Entry] = field(default_factory=list)
+    n_candidates: int = 0
+    n_runs: int = 0
+    device_ms: float = 0.0
+    stream_ms: float = 0.0
+
+    def as_dict(self):
+        return dict(status=self.status, detail=self.detail, fail_record=self.fail_record,
+                    fail_offset=self.fail_offset, n_records=self.n_records, last_crc=self.last_crc, enti=self.enti,
+                    metadata=self.metadata, state=dict(term=self.state.Term, vote=self.state.Vote,
+                                                       commit=self.state.Commit),
+                    ents=[dict(type=e.Type, term=e.Term, index=e.Index, data=e.Data) for e in self.ents])
+
+
+def _collect(ctx, r, buf_view, with_ents=True):
+    ok = r.status == L.OK
+    md = None
+    if ok and r.metadata_off >= 0:
+        md = bytes(buf_view[r.metadata_off:r.metadata_off + r.metadata_len])
+    st = HardState(r.state_term, r.state_vote, r.state_commit) if (ok and r.has_state) else HardState()
+    ents = []
+    if ok and with_ents and r.n_ents:
+        arr = (L.EntryDesc * r.n_ents)()
+        n = lib.ewal_copy_entries(ctx.handle, arr, r.n_ents)
+        check(0 if n >= 0 else int(n))
+        for e in arr[:n]:
+            data = None if e.data_nil else bytes(buf_view[e.data_off:e.data_off + e.data_len])
+            ents.append(Entry(e.type, e.term, e.index, data))
+    return ReadAllResult(r.status, r.detail, r.fail_record, r.fail_offset, r.n_records, r.last_crc if ok else 0,
+                         r.enti, md, st, ents, r.n_candidates, r.n_runs, r.device_ms, r.stream_ms)
+
+
+def readall_bytes(buf: bytes, ri: int = 0, ctx: Context = None, with_ents=True) -> ReadAllResult:
+    """ReadAll over the concatenated WAL bytes (host memory, staged to HBM)."""
+    ctx = ctx or default_context()
+    r = L.Result()
+    b = bytes(buf)
+    rc = lib.ewal_readall_host(ctx.handle, b, len(b), ri, C.byref(r))
+    if rc < 0:
+        check(rc)
+    return _collect(ctx, r, memoryview(b), with_ents)
+
+
+def readall_device(dbuf: DeviceBuffer, n: int, ri: int = 0, host_view=None, with_ents=False) -> ReadAllResult:
+    """ReadAll over WAL bytes already resident in HBM."""
+    r = L.Result()
+    rc = lib.ewal_readall_device(dbuf.ctx.handle, dbuf.ptr, n, ri, C.byref(r))
+    if rc < 0:
+        check(rc)
+    return _collect(dbuf.ctx, r, host_view if host_view is not None else b"", with_ents and host_view is not None)
+
+
+def records(ctx: Context, n: int):
+    """Per-frame descriptors of the last ReadAll on ctx."""
+    arr = (L.RecordDesc * max(n, 1))()
+    k = lib.ewal_copy_records(ctx.handle, arr, n)
+    check(0 if k >= 0 else int(k))
+    return [dict(offset=x.offset, data_off=x.data_off, data_len=x.data_len, type=x.type, crc=x.crc,
+                 chained_crc=x.chained_crc) for x in arr[:k]]
+
+
+class WAL:
+    """wal.WAL opened for reading (OpenAtIndex) -- ReadAll runs on the GPU."""
+
+    def __init__(self, handle, ctx):
+        self._h, self._ctx = handle, ctx
+
+    def ReadAll(self):
+        if self._ctx is None:
+            self._ctx = default_context()
+        r = L.Result()
+        rc = lib.ewal_wal_readall(self._h, self._ctx.handle, C.byref(r))
+        if rc < 0:
+            check(rc)
+        n = C.c_uint64(0)
+        p = lib.ewal_wal_bytes(self._h, C.byref(n))
+        view = C.string_at(p, n.value) if n.value else b""
+        res = _collect(self._ctx, r, memoryview(view))
+        if res.status != L.OK:
+            check(res.status, res.detail, res.fail_record, res.fail_offset)
+        return res.metadata, res.state, res.ents
+
+    @property
+    def seq(self):
+        return lib.ewal_wal_seq(self._h)
+
+    def Close(self):
+        if self._h:
+            lib.ewal_wal_close(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.Close()
+        except Exception:
+            pass
+
+
+def OpenAtIndex(dirpath: str, index: int, ctx: Context = None) -> WAL:
+    h = C.c_void_p()
+    st = lib.ewal_open_at_index(dirpath.encode(), index, C.byref(h))
+    check(st)
+    return WAL(h, ctx)
+
+
+class Writer:
+    """wal.WAL in append mode (Create / Cut / Save*)."""
+
+    def __init__(self, h):
+        self._h = h
+
+    def SaveEntry(self, e: Entry):
+        check(lib.ewal_writer_save_entry(self._h, e.Type, e.Term, e.Index, e.Data or b"", len(e.Data or b"")))
+
+    def SaveState(self, s: HardState):
+        check(lib.ewal_writer_save_state(self._h, s.Term, s.Vote, s.Commit))
+
+    def Save(self, st: HardState, ents: List[Entry]):
+        self.SaveState(st)
+        for e in ents:
+            self.SaveEntry(e)
+        self.Sync()
+
+    def Cut(self):
+        check(lib.ewal_writer_cut(self._h))
+
+    def Sync(self):
+        check(lib.ewal_writer_sync(self._h))
+
+    def Close(self):
+        if self._h:
+            lib.ewal_writer_close(self._h)
+            self._h = None
+
+
+def Create(dirpath: str, metadata: Optional[bytes]) -> Writer:
+    h = C.c_void_p()
+    md = metadata or b""
+    st = lib.ewal_create(dirpath.encode(), md, len(md), int(metadata is None), C.byref(h))
+    if st == L.E_IO:
+        raise FileExistsError(dirpath)
+    check(st)
+    return Writer(h)
+
+
+class Encoder:
+    """In-memory encoder.encode (wal/encoder.go:25-37)."""
+
+    def __init__(self, prev_crc=0, reserve=0):
+        self._h = lib.ewal_encoder_new(prev_crc, reserve)
+
+    def encode(self, type_, data):
+        d = data if data is not None else b""
+        check(lib.ewal_encoder_encode(self._h, type_, d, len(d), int(data is None)))
+
+    def save_entry(self, type_=0, term=0, index=0, data=None):
+        d = data or b""
+        check(lib.ewal_encoder_save_entry(self._h, type_, term, index, d, len(d)))
+
+    def save_state(self, term=0, vote=0, commit=0):
+        check(lib.ewal_encoder_save_state(self._h, term, vote, commit))
+
+    def getvalue(self):
+        n = C.c_uint64(0)
+        p = lib.ewal_encoder_bytes(self._h, C.byref(n))
+        return C.string_at(p, n.value) if n.value else b""
+
+    @property
+    def crc(self):
+        return lib.ewal_encoder_crc(self._h)
+
+    def __del__(self):
+        try:
+            lib.ewal_encoder_free(self._h)
+        except Exception:
+            pass
+
+
+def synth_wal(target_bytes, min_data=64, max_data=65536, seed=2, corrupt_record=-1):
+    """Synthetic WAL (bench/test input); returns (bytearray, n_records)."""
+    cap = target_bytes + max_data * 2 + (1 << 20)
+    out = bytearray(cap)
+    nrec = C.c_int64(0)
+    n = lib.ewal_synth_wal(seed, target_bytes, min_data, max_data, corrupt_record,
+                           (C.c_char * cap).from_buffer(out), cap, C.byref(nrec))
+    if n < 0:
+        check(int(n))
+    del out[n:]
+    return out, nrec.value

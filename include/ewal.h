@@ -1,0 +1,224 @@
+/*
+ * ewal.h -- C ABI of the MI355X-native etcd WAL replay-and-verify engine.
+ *
+ * Drop-in boundary for the reference's (mzsanford/etcd v0.5.0-alpha) hot
+ * path.  Each entry point names the Go interface it replaces (file:line,
+ * relative to the reference root).  A cgo shim binds these
+ * with plain pointers and sizes; no HIP or torch types cross the boundary
+ * except opaque handles and device pointers given as `const void *`.
+ *
+ * Ownership: the caller owns every buffer passed in; the library owns its
+ * device workspace and stream inside an ewal_ctx.  Threading: one ctx per
+ * host thread; calls are blocking.  Errors: a negative return is an
+ * infrastructure failure (HIP); a non-negative return is an EWAL_* status
+ * that maps 1:1 onto the reference's sentinel errors and panic classes.
+ * There is no CPU fallback: without a usable GPU every compute entry point
+ * returns EWAL_E_NODEVICE.
+ */
+#ifndef EWAL_H
+#define EWAL_H
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes (same numbering as oracle/ewal_oracle.h) ------------ */
+enum {
+  EWAL_OK = 0,
+  EWAL_EOF = 1,                    /* io.EOF: clean end (internal only) */
+  EWAL_ERR_UNEXPECTED_EOF = 2,     /* io.ErrUnexpectedEOF */
+  EWAL_ERR_RECORD_CRC = 3,         /* walpb.ErrCRCMismatch   wal/walpb/record.go:22 */
+  EWAL_ERR_WAL_CRC = 4,            /* wal.ErrCRCMismatch     wal/wal.go:48 */
+  EWAL_ERR_METADATA_CONFLICT = 5,  /* wal.ErrMetadataConflict wal/wal.go:45 */
+  EWAL_ERR_INDEX_NOT_FOUND = 6,    /* wal.ErrIndexNotFound   wal/wal.go:47 */
+  EWAL_ERR_WRONG_TYPE = 7,         /* proto.ErrWrongType */
+  EWAL_ERR_UNEXPECTED_TYPE = 8,    /* "unexpected block type %d" wal/wal.go:194; detail = type */
+  EWAL_ERR_FILE_NOT_FOUND = 9,     /* wal.ErrFileNotFound    wal/wal.go:46 */
+  EWAL_ERR_SNAP_CRC = 10,          /* snap.ErrCRCMismatch    snap/snapshotter.go:25 */
+  EWAL_ERR_NO_SNAPSHOT = 11,       /* snap.ErrNoSnapshot     snap/snapshotter.go:24 */
+  EWAL_PANIC_NEG_LENGTH = 32,      /* make([]byte, l<0)      wal/decoder.go:34 */
+  EWAL_PANIC_BOUNDS = 33,          /* runtime bounds panic in Unmarshal/Skip */
+  EWAL_PANIC_ENTRY = 34,           /* mustUnmarshalEntry     wal/decoder.go:61-69 */
+  EWAL_PANIC_STATE = 35,           /* mustUnmarshalState     wal/decoder.go:71-77 */
+  EWAL_PANIC_INDEX_GAP = 36,       /* ents[:e.Index-ri] past len wal/wal.go:173 */
+  EWAL_NONTERMINATING = 37,        /* the reference never returns */
+  EWAL_UNSUPPORTED_ENCODING = 48,  /* a record the GPU decoder does not handle yet
+                                      (non-canonical protobuf); reported, never guessed */
+  /* infrastructure (negative) */
+  EWAL_E_HIP = -1,
+  EWAL_E_INVAL = -2,
+  EWAL_E_NOMEM = -3,
+  EWAL_E_NODEVICE = -4,
+  EWAL_E_TIMEOUT = -5,
+  EWAL_E_IO = -6
+};
+
+/* Record types, wal/wal.go:34-39 */
+enum { EWAL_METADATA = 1, EWAL_ENTRY = 2, EWAL_STATE = 3, EWAL_CRC = 4 };
+
+typedef struct ewal_ctx ewal_ctx;
+
+/* Result of (*WAL).ReadAll, wal/wal.go:164-216.  On error the reference
+ * returns (nil, HardState{}, nil, err): only status/detail/fail_* and
+ * n_records are meaningful then. */
+typedef struct ewal_result {
+  int32_t status;          /* EWAL_OK or an EWAL_ERR_/EWAL_PANIC_ class */
+  int32_t flags;
+  int64_t detail;          /* unexpected block type value; gap index */
+  int64_t fail_record;     /* ordinal of the frame that failed, -1 if none */
+  int64_t fail_offset;     /* byte offset of that frame in the stream, -1 */
+  int64_t n_records;       /* frames decoded before the end / failure */
+  uint32_t last_crc;       /* decoder.lastCRC() -> seeds the encoder, wal/wal.go:213 */
+  uint32_t reserved0;
+  uint64_t enti;           /* w.enti: Index of the last entry record */
+  int64_t metadata_off;    /* metadata []byte as (offset,len) into the stream; -1 == nil */
+  int64_t metadata_len;
+  int32_t has_state;       /* 0 -> HardState{} */
+  int32_t reserved1;
+  uint64_t state_term, state_vote, state_commit;
+  int64_t n_ents;          /* len(ents); fetch with ewal_copy_entries */
+  int64_t n_candidates;    /* diagnostics: frame-start candidates found */
+  int64_t n_runs;          /* diagnostics: chain runs in the framing pass */
+  double device_ms;        /* device time of the pipeline (HIP events) */
+  double stream_ms;        /* device time of the k_stream HBM pass alone */
+} ewal_result;
+
+/* raftpb.Entry, raft/raftpb/raft.pb.go:100-106.  Data is a zero-copy
+ * (offset,len) view of the stream; data_nil mirrors Go's nil slice. */
+typedef struct ewal_entry {
+  uint64_t term;
+  uint64_t index;
+  uint64_t data_off;
+  uint64_t data_len;
+  int32_t type;
+  int32_t data_nil;
+} ewal_entry;
+
+/* One decoded frame (walpb.Record + chain state), wal/walpb/record.pb.go:30-35 */
+typedef struct ewal_record {
+  uint64_t offset;         /* frame start (int64 length prefix) */
+  uint64_t data_off;
+  uint64_t data_len;
+  int64_t type;
+  uint32_t crc;            /* stored Record.Crc */
+  uint32_t chained_crc;    /* decoder crc after this frame (== crc when it verified) */
+} ewal_record;
+
+/* ---- context ------------------------------------------------------------ */
+int ewal_ctx_create(int device, ewal_ctx **out);
+void ewal_ctx_destroy(ewal_ctx *ctx);
+/* Run on a caller-owned hipStream_t (NULL = the ctx's own stream). */
+int ewal_ctx_set_stream(ewal_ctx *ctx, void *hip_stream);
+const char *ewal_status_string(int status);
+/* Device time (ms) of the last pipeline call on this ctx (HIP events). */
+float ewal_last_device_ms(ewal_ctx *ctx);
+int ewal_device_count(void);
+
+/* ---- WAL replay/verify -------------------------------------------------- */
+/* (*WAL).ReadAll over the concatenated bytes of OpenAtIndex's files
+ * names[nameIndex:] (wal/wal.go:126-134, MultiReadCloser semantics), with
+ * w.ri = ri.  d_buf is DEVICE memory, 16-byte aligned, len bytes. */
+int ewal_readall_device(ewal_ctx *ctx, const void *d_buf, uint64_t len, uint64_t ri, ewal_result *out);
+/* Copy host bytes into ctx-owned device memory (16-B aligned; valid until
+ * the next staging call on this ctx). */
+int ewal_stage_to_device(ewal_ctx *ctx, const void *h_buf, uint64_t len, void **d_out);
+/* Device memory owned by the caller through the library (for callers that
+ * have no HIP runtime of their own, e.g. cgo): alloc/free/copy. */
+int ewal_device_alloc(ewal_ctx *ctx, uint64_t len, void **d_out);
+int ewal_device_free(ewal_ctx *ctx, void *d_buf);
+int ewal_upload(ewal_ctx *ctx, void *d_dst, const void *h_src, uint64_t len);
+int ewal_download(ewal_ctx *ctx, void *h_dst, const void *d_src, uint64_t len);
+/* Same, from host memory: staged to the device first (PCIe-inclusive). */
+int ewal_readall_host(ewal_ctx *ctx, const void *h_buf, uint64_t len, uint64_t ri, ewal_result *out);
+/* After a successful readall: copy the ents / per-frame descriptors out.
+ * Return the number copied (<= cap) or a negative error. */
+int64_t ewal_copy_entries(ewal_ctx *ctx, ewal_entry *out, int64_t cap);
+int64_t ewal_copy_records(ewal_ctx *ctx, ewal_record *out, int64_t cap);
+
+/* ---- directory-level API: wal.OpenAtIndex + ReadAll + writer ----------- */
+typedef struct ewal_wal ewal_wal;
+/* wal.OpenAtIndex(dirpath, index), wal/wal.go:108-159 (file selection:
+ * wal/util.go:20-88).  Reads names[nameIndex:] into one buffer. */
+int ewal_open_at_index(const char *dirpath, uint64_t index, ewal_wal **out);
+int ewal_wal_readall(ewal_wal *w, ewal_ctx *ctx, ewal_result *out);
+const uint8_t *ewal_wal_bytes(ewal_wal *w, uint64_t *len);
+uint64_t ewal_wal_seq(ewal_wal *w);
+void ewal_wal_close(ewal_wal *w);
+
+/* Write path (the on-disk format the hot path reads), wal/wal.go:72-100,
+ * 219-292, wal/encoder.go:25-37.  Host C++; CRC via SSE4.2. */
+typedef struct ewal_writer ewal_writer;
+int ewal_create(const char *dirpath, const uint8_t *metadata, uint64_t mlen, int metadata_nil, ewal_writer **out);
+int ewal_writer_save_entry(ewal_writer *w, int32_t type, uint64_t term, uint64_t index, const uint8_t *data, uint64_t n);
+int ewal_writer_save_state(ewal_writer *w, uint64_t term, uint64_t vote, uint64_t commit);
+int ewal_writer_cut(ewal_writer *w);
+int ewal_writer_sync(ewal_writer *w);
+void ewal_writer_close(ewal_writer *w);
+
+/* In-memory encoder (encoder.encode over a growing buffer). */
+typedef struct ewal_encoder ewal_encoder;
+ewal_encoder *ewal_encoder_new(uint32_t prev_crc, uint64_t reserve);
+int ewal_encoder_encode(ewal_encoder *e, int64_t type, const uint8_t *data, uint64_t n, int data_nil);
+int ewal_encoder_save_entry(ewal_encoder *e, int32_t type, uint64_t term, uint64_t index, const uint8_t *data, uint64_t n);
+int ewal_encoder_save_state(ewal_encoder *e, uint64_t term, uint64_t vote, uint64_t commit);
+const uint8_t *ewal_encoder_bytes(ewal_encoder *e, uint64_t *len);
+uint32_t ewal_encoder_crc(ewal_encoder *e);
+void ewal_encoder_free(ewal_encoder *e);
+
+/* Synthetic WAL generator used by bench.py (BASELINE.json configs):
+ * Create(metadata) + Save(HardState{1,1,0}, ents) with entry Data sizes
+ * log-uniform in [min_data, max_data], payload bytes from xorshift64*(seed),
+ * until at least target_bytes.  Writes into out (cap bytes).  Optionally
+ * flips one payload byte of record ordinal corrupt_record (-1 = none).
+ * Returns bytes written; *n_records receives the frame count. */
+int64_t ewal_synth_wal(uint64_t seed, uint64_t target_bytes, uint32_t min_data, uint32_t max_data,
+                       int64_t corrupt_record, uint8_t *out, uint64_t cap, int64_t *n_records);
+
+/* ---- CRC primitives (pkg/crc, pkg/crc/crc.go:23-41) ---------------------- */
+/* crc32.Update(crc, MakeTable(poly), p) on a DEVICE buffer. */
+int ewal_crc32_update_device(ewal_ctx *ctx, uint32_t crc, uint32_t poly, const void *d_buf, uint64_t n,
+                             uint32_t *out);
+/* crc32.Update on host memory (SSE4.2 for Castagnoli) -- for small writes. */
+uint32_t ewal_crc32_update_host(uint32_t crc, uint32_t poly, const uint8_t *p, uint64_t n);
+/* Update(c1, A || B) from c1=Update(0,A)... : returns Update(crc_a, B) given
+ * crc_b = Update(0, B) and len_b, without touching the bytes. */
+uint32_t ewal_crc32_combine(uint32_t poly, uint32_t crc_a, uint32_t crc_b, uint64_t len_b);
+
+/* ---- snapshots: snap.loadSnap / Snapshotter.Load, snap/snapshotter.go:62-111 */
+/* Batch-verify snapshot FILES (snappb.Snapshot envelopes) resident in one
+ * device buffer at offs[i], lens[i].  status[i] = EWAL_OK / EWAL_ERR_SNAP_CRC /
+ * unmarshal class; crc outputs are the stored and recomputed CRCs. */
+int esnap_verify_packed(ewal_ctx *ctx, const void *d_buf, uint64_t buf_len, const uint64_t *offs,
+                        const uint64_t *lens, uint32_t n, uint32_t poly, int32_t *status,
+                        uint32_t *stored_crc, uint32_t *computed_crc);
+/* Snapshotter.Load(): newest-first over dir's *.snap, first success wins,
+ * tried failures renamed *.broken.  On success *out_name (malloc'd, caller
+ * frees with free()) names the snapshot file loaded; snapshot fields out. */
+typedef struct esnap_snapshot {
+  uint64_t index, term;
+  uint64_t data_off, data_len;   /* raftpb.Snapshot.Data within the file */
+  int64_t n_nodes, n_removed;
+  uint64_t nodes[64], removed[64];
+} esnap_snapshot;
+/* After esnap_verify_packed: the decoded raftpb.Snapshot of file i (only
+ * meaningful when status[i] == EWAL_OK). */
+int esnap_copy_snapshot(ewal_ctx *ctx, uint32_t i, esnap_snapshot *out);
+int esnap_load_dir(ewal_ctx *ctx, const char *dirpath, uint32_t poly, esnap_snapshot *out, char **out_name);
+
+/* ---- raft quorum commit: raft.maybeCommit, raft/raft.go:248-258 ---------- */
+/* Batched over G independent raft groups (SoA).  match[v*G + g] for voter
+ * v < nvoters[g] (<= 16); log terms for group g are log_terms[log_ptr[g] ..
+ * log_ptr[g+1]) at raft indices log_offset[g] + k.  committed[] is updated in
+ * place; changed[g] = maybeCommit's return; status[g] = 0 or EWAL_PANIC_BOUNDS.
+ * All pointers are DEVICE pointers. */
+int ecommit_batch_device(ewal_ctx *ctx, uint64_t G, const uint64_t *match, const uint8_t *nvoters,
+                         const uint64_t *term, uint64_t *committed, const uint64_t *log_offset,
+                         const uint64_t *log_ptr, const uint64_t *log_terms, uint8_t *changed,
+                         uint8_t *status, double *device_ms);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,272 @@
+"""ctypes bindings for the CPU oracle (oracle/libewal_oracle.so).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and
+bench.py's cpu_baseline leg, never by the product (etcd_amd/).  The C code
+restates the reference's Go functions; see ewal_oracle.h for citations.
+"""
+import ctypes as C
+import os
+import subprocess
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = os.path.join(_HERE, "libewal_oracle.so")
+
+OK, EOF, ERR_UNEXPECTED_EOF, ERR_RECORD_CRC, ERR_WAL_CRC = 0, 1, 2, 3, 4
+ERR_METADATA_CONFLICT, ERR_INDEX_NOT_FOUND, ERR_WRONG_TYPE, ERR_UNEXPECTED_TYPE = 5, 6, 7, 8
+ERR_FILE_NOT_FOUND, ERR_SNAP_CRC, ERR_NO_SNAPSHOT = 9, 10, 11
+PANIC_NEG_LENGTH, PANIC_BOUNDS, PANIC_ENTRY, PANIC_STATE, PANIC_INDEX_GAP, NONTERMINATING = 32, 33, 34, 35, 36, 37
+
+CASTAGNOLI, IEEE, KOOPMAN = 0x82F63B78, 0xEDB88320, 0xEB31D82E
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", _HERE])
+
+
+def _load():
+    if not os.path.exists(_LIB):
+        build()
+    return C.CDLL(_LIB)
+
+
+lib = _load()
+u8p = C.POINTER(C.c_uint8)
+
+
+class Record(C.Structure):
+    _fields_ = [("type", C.c_int64), ("crc", C.c_uint32), ("data", u8p), ("data_len", C.c_int64),
+                ("unrec_len", C.c_int64)]
+
+
+class Entry(C.Structure):
+    _fields_ = [("type", C.c_int32), ("term", C.c_uint64), ("index", C.c_uint64), ("data", u8p),
+                ("data_len", C.c_int64), ("unrec_len", C.c_int64)]
+
+
+class HardState(C.Structure):
+    _fields_ = [("term", C.c_uint64), ("vote", C.c_uint64), ("commit", C.c_uint64), ("unrec_len", C.c_int64)]
+
+
+class Snapshot(C.Structure):
+    _fields_ = [("data", u8p), ("data_len", C.c_int64), ("nodes", C.POINTER(C.c_uint64)), ("n_nodes", C.c_int64),
+                ("index", C.c_uint64), ("term", C.c_uint64), ("removed", C.POINTER(C.c_uint64)),
+                ("n_removed", C.c_int64), ("unrec_len", C.c_int64)]
+
+
+class ReadAllResult(C.Structure):
+    _fields_ = [("status", C.c_int), ("detail", C.c_int64), ("fail_record", C.c_int64), ("fail_offset", C.c_int64),
+                ("n_records", C.c_int64), ("last_crc", C.c_uint32), ("enti", C.c_uint64), ("metadata", u8p),
+                ("metadata_len", C.c_int64), ("state", HardState), ("has_state", C.c_int),
+                ("ents", C.POINTER(Entry)), ("n_ents", C.c_int64)]
+
+
+class Encoder(C.Structure):
+    _fields_ = [("buf", u8p), ("len", C.c_int64), ("cap", C.c_int64), ("crc", C.c_uint32)]
+
+
+class Decoder(C.Structure):
+    _fields_ = [("buf", u8p), ("len", C.c_int64), ("pos", C.c_int64), ("crc", C.c_uint32)]
+
+
+class LoadSnapResult(C.Structure):
+    _fields_ = [("status", C.c_int), ("stored_crc", C.c_uint32), ("computed_crc", C.c_uint32), ("snap", Snapshot)]
+
+
+lib.or_crc32_update.restype = C.c_uint32
+lib.or_crc32_update.argtypes = [C.c_uint32, C.c_uint32, C.c_char_p, C.c_size_t]
+lib.or_crc32_update_table.restype = C.c_uint32
+lib.or_crc32_update_table.argtypes = [C.c_uint32, C.c_uint32, C.c_char_p, C.c_size_t]
+lib.or_readall.argtypes = [C.c_char_p, C.c_int64, C.c_uint64, C.POINTER(ReadAllResult)]
+lib.or_readall_free.argtypes = [C.POINTER(ReadAllResult)]
+lib.or_encoder_init.argtypes = [C.POINTER(Encoder), C.c_uint32]
+lib.or_encode.argtypes = [C.POINTER(Encoder), C.c_int64, C.c_char_p, C.c_int64, C.c_int]
+lib.or_encoder_free.argtypes = [C.POINTER(Encoder)]
+lib.or_decoder_init.argtypes = [C.POINTER(Decoder), C.c_char_p, C.c_int64]
+lib.or_decode.argtypes = [C.POINTER(Decoder), C.POINTER(Record)]
+lib.or_record_free.argtypes = [C.POINTER(Record)]
+for _n, _t in (("record", Record), ("entry", Entry), ("hardstate", HardState), ("snapshot", Snapshot)):
+    getattr(lib, "or_%s_unmarshal" % _n).argtypes = [C.c_char_p, C.c_int64, C.POINTER(_t)]
+lib.or_proto_skip.argtypes = [C.c_char_p, C.c_int64, C.POINTER(C.c_int64)]
+lib.or_record_marshal.restype = C.c_int64
+lib.or_record_marshal.argtypes = [C.c_int64, C.c_uint32, C.c_char_p, C.c_int64, C.c_int, C.c_char_p]
+lib.or_entry_marshal.restype = C.c_int64
+lib.or_entry_marshal.argtypes = [C.c_int32, C.c_uint64, C.c_uint64, C.c_char_p, C.c_int64, C.c_char_p]
+lib.or_hardstate_marshal.restype = C.c_int64
+lib.or_hardstate_marshal.argtypes = [C.c_uint64, C.c_uint64, C.c_uint64, C.c_char_p]
+lib.or_snapshot_marshal.restype = C.c_int64
+lib.or_snapshot_marshal.argtypes = [C.c_char_p, C.c_int64, C.POINTER(C.c_uint64), C.c_int64, C.c_uint64, C.c_uint64,
+                                    C.POINTER(C.c_uint64), C.c_int64, C.c_char_p]
+lib.or_snappb_marshal.restype = C.c_int64
+lib.or_snappb_marshal.argtypes = [C.c_uint32, C.c_char_p, C.c_int64, C.c_int, C.c_char_p]
+lib.or_loadsnap.argtypes = [C.c_char_p, C.c_int64, C.c_uint32, C.POINTER(LoadSnapResult)]
+lib.or_loadsnap_free.argtypes = [C.POINTER(LoadSnapResult)]
+lib.or_maybe_commit.argtypes = [C.POINTER(C.c_uint64), C.c_int, C.c_uint64, C.POINTER(C.c_uint64),
+                                C.POINTER(C.c_uint64), C.c_uint64, C.c_uint64]
+lib.or_chain_crcs.restype = C.c_int64
+lib.or_chain_crcs.argtypes = [C.c_char_p, C.c_int64, C.POINTER(C.c_uint32), C.c_int64, C.POINTER(C.c_int64)]
+
+
+def _bytes(p, n):
+    """Go []byte view: None for nil."""
+    if not p:
+        return None
+    return C.string_at(p, n)
+
+
+def crc32_update(crc, data, poly=CASTAGNOLI):
+    return lib.or_crc32_update(crc, poly, bytes(data), len(data))
+
+
+def crc32_update_table(crc, data, poly=CASTAGNOLI):
+    return lib.or_crc32_update_table(crc, poly, bytes(data), len(data))
+
+
+def _marshal(fn, *args):
+    n = fn(*args, None)
+    out = C.create_string_buffer(max(n, 1))
+    fn(*args, out)
+    return out.raw[:n]
+
+
+def record_marshal(type_, crc, data):
+    return _marshal(lib.or_record_marshal, type_, crc, data or b"", len(data or b""), int(data is None))
+
+
+def entry_marshal(type_=0, term=0, index=0, data=None):
+    d = data or b""
+    return _marshal(lib.or_entry_marshal, type_, term, index, d, len(d))
+
+
+def hardstate_marshal(term=0, vote=0, commit=0):
+    return _marshal(lib.or_hardstate_marshal, term, vote, commit)
+
+
+def snapshot_marshal(data=b"", nodes=(), index=0, term=0, removed=()):
+    na = (C.c_uint64 * max(len(nodes), 1))(*nodes)
+    ra = (C.c_uint64 * max(len(removed), 1))(*removed)
+    return _marshal(lib.or_snapshot_marshal, data, len(data), na, len(nodes), index, term, ra, len(removed))
+
+
+def snappb_marshal(crc, data):
+    return _marshal(lib.or_snappb_marshal, crc, data or b"", len(data or b""), int(data is None))
+
+
+def record_unmarshal(b):
+    r = Record()
+    st = lib.or_record_unmarshal(b, len(b), C.byref(r))
+    out = dict(type=r.type, crc=r.crc, data=_bytes(r.data, r.data_len), unrec_len=r.unrec_len)
+    lib.or_record_free(C.byref(r))
+    return st, out
+
+
+def entry_unmarshal(b):
+    e = Entry()
+    st = lib.or_entry_unmarshal(b, len(b), C.byref(e))
+    return st, dict(type=e.type, term=e.term, index=e.index, data=_bytes(e.data, e.data_len), unrec_len=e.unrec_len)
+
+
+def hardstate_unmarshal(b):
+    h = HardState()
+    st = lib.or_hardstate_unmarshal(b, len(b), C.byref(h))
+    return st, dict(term=h.term, vote=h.vote, commit=h.commit)
+
+
+def proto_skip(b):
+    n = C.c_int64(0)
+    st = lib.or_proto_skip(b, len(b), C.byref(n))
+    return st, n.value
+
+
+def decode(buf):
+    """Drive decoder.decode over buf; list of (status, record dict, crc)."""
+    d = Decoder()
+    lib.or_decoder_init(C.byref(d), buf, len(buf))
+    r = Record()
+    out = []
+    while True:
+        st = lib.or_decode(C.byref(d), C.byref(r))
+        out.append((st, dict(type=r.type, crc=r.crc, data=_bytes(r.data, r.data_len)), d.crc))
+        if st != OK:
+            break
+    lib.or_record_free(C.byref(r))
+    return out
+
+
+def readall(buf, ri=0):
+    """(*WAL).ReadAll over the concatenated files; returns a dict."""
+    r = ReadAllResult()
+    lib.or_readall(buf, len(buf), ri, C.byref(r))
+    out = dict(status=r.status, detail=r.detail, fail_record=r.fail_record, fail_offset=r.fail_offset,
+               n_records=r.n_records, last_crc=r.last_crc, enti=r.enti,
+               metadata=_bytes(r.metadata, r.metadata_len),
+               state=dict(term=r.state.term, vote=r.state.vote, commit=r.state.commit) if r.has_state else
+               dict(term=0, vote=0, commit=0),
+               ents=[dict(type=r.ents[i].type, term=r.ents[i].term, index=r.ents[i].index,
+                          data=_bytes(r.ents[i].data, r.ents[i].data_len)) for i in range(r.n_ents)])
+    lib.or_readall_free(C.byref(r))
+    return out
+
+
+def chain_crcs(buf, cap=None):
+    cap = cap if cap is not None else max(1, len(buf) // 8)
+    arr = (C.c_uint32 * cap)()
+    offs = (C.c_int64 * cap)()
+    n = lib.or_chain_crcs(buf, len(buf), arr, cap, offs)
+    n = min(n, cap)
+    return list(arr[:n]), list(offs[:n])
+
+
+class WalEncoder:
+    """encoder + the WAL record helpers (wal/encoder.go, wal/wal.go:256-292)."""
+
+    def __init__(self, prev_crc=0):
+        self._e = Encoder()
+        lib.or_encoder_init(C.byref(self._e), prev_crc)
+
+    def encode(self, type_, data):
+        d = data if data is not None else b""
+        lib.or_encode(C.byref(self._e), type_, d, len(d), int(data is None))
+
+    def save_crc(self, prev_crc):           # wal/wal.go:290-292
+        self.encode(4, None)
+
+    def save_entry(self, type_=0, term=0, index=0, data=None):   # wal/wal.go:256-267
+        self.encode(2, entry_marshal(type_, term, index, data))
+
+    def save_state(self, term=0, vote=0, commit=0):              # wal/wal.go:269-279
+        if term == 0 and vote == 0 and commit == 0:
+            return
+        self.encode(3, hardstate_marshal(term, vote, commit))
+
+    @property
+    def crc(self):
+        return self._e.crc
+
+    def getvalue(self):
+        return C.string_at(self._e.buf, self._e.len) if self._e.len else b""
+
+    def __del__(self):
+        try:
+            lib.or_encoder_free(C.byref(self._e))
+        except Exception:
+            pass
+
+
+def loadsnap(b, poly=CASTAGNOLI):
+    r = LoadSnapResult()
+    st = lib.or_loadsnap(b, len(b), poly, C.byref(r))
+    s = r.snap
+    out = dict(status=st, stored_crc=r.stored_crc, computed_crc=r.computed_crc)
+    if st == OK:
+        out["snap"] = dict(data=_bytes(s.data, s.data_len), nodes=[s.nodes[i] for i in range(s.n_nodes)],
+                           index=s.index, term=s.term, removed=[s.removed[i] for i in range(s.n_removed)])
+    lib.or_loadsnap_free(C.byref(r))
+    return out
+
+
+def maybe_commit(matches, term, committed, log_terms, offset=0):
+    m = (C.c_uint64 * max(len(matches), 1))(*matches)
+    lt = (C.c_uint64 * max(len(log_terms), 1))(*log_terms)
+    c = C.c_uint64(committed)
+    rc = lib.or_maybe_commit(m, len(matches), term, C.byref(c), lt, len(log_terms), offset)
+    return rc, c.value

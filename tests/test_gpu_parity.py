@@ -1,0 +1,358 @@
+"""GPU parity: the HIP pipeline (through libewal.so's C ABI) against the CPU
+oracle on the same seeded inputs.  Bit-exact: status, failing frame, every
+chained CRC, metadata, HardState, ents, enti, lastCRC."""
+import ctypes as C
+import random
+import struct
+
+import pytest
+
+from oracle import oracle as O
+from etcd_amd import _lib as L
+from etcd_amd import wal as W
+
+pytestmark = pytest.mark.gpu
+
+
+def gpu_readall(ctx, buf, ri):
+    return W.readall_bytes(bytes(buf), ri, ctx).as_dict()
+
+
+UNSUPPORTED_SEEN = []
+
+
+def assert_parity(ctx, buf, ri=0, check_chain=True, allow_unsupported=False):
+    buf = bytes(buf)
+    o = O.readall(buf, ri)
+    g = gpu_readall(ctx, buf, ri)
+    if allow_unsupported and g["status"] == L.UNSUPPORTED_ENCODING:
+        # the GPU stops at a non-canonical frame it does not decode yet; every
+        # frame before it was verified identically, so the oracle cannot
+        # have failed earlier
+        assert o["status"] == O.OK or o["fail_record"] >= g["fail_record"] or o["fail_record"] < 0
+        UNSUPPORTED_SEEN.append((g["fail_record"], o["status"]))
+        return o, g
+    assert g["status"] == o["status"], (g["status"], o["status"], g["fail_record"], o["fail_record"])
+    if o["status"] == O.OK:
+        for k in ("n_records", "last_crc", "enti", "metadata", "state"):
+            assert g[k] == o[k], k
+        assert g["ents"] == o["ents"]
+    elif o["status"] != O.ERR_INDEX_NOT_FOUND:
+        assert g["fail_record"] == o["fail_record"]
+        assert g["fail_offset"] == o["fail_offset"]
+        if o["status"] == O.ERR_UNEXPECTED_TYPE:
+            assert g["detail"] == o["detail"]
+    else:
+        assert g["enti"] == o["enti"]
+    if check_chain and o["status"] == O.OK:
+        crcs, offs = O.chain_crcs(buf)
+        recs = W.records(ctx, g["n_records"])
+        assert [r["chained_crc"] for r in recs] == crcs
+        assert [r["offset"] for r in recs] == offs
+    return o, g
+
+
+def build_wal(rng, n_entries=50, max_data=3000, cuts=0, states=True, md=b"metadata", start_index=0):
+    """Random WAL bytes via the oracle's encoder (wal/wal.go write path)."""
+    e = O.WalEncoder(0)
+    e.save_crc(0)
+    e.encode(1, md)
+    idx = start_index
+    cut_at = set(rng.sample(range(1, max(2, n_entries)), min(cuts, max(0, n_entries - 1)))) if cuts else set()
+    for i in range(n_entries):
+        if i in cut_at:
+            prev = e.crc
+            chunk = e.getvalue()
+            e2 = O.WalEncoder(prev)
+            e2.save_crc(prev)
+            e2.encode(1, md)
+            e = _Concat(chunk, e2)
+        r = rng.random()
+        if states and r < 0.1:
+            e.save_state(rng.randrange(1, 100), rng.randrange(100), rng.randrange(1000))
+        n = rng.choice([0, 1, 2, 5, 17, 64, 100, 255, 256, 1000, rng.randrange(0, max_data + 1)])
+        d = bytes(rng.getrandbits(8) for _ in range(n)) if n else (None if rng.random() < 0.5 else b"")
+        e.save_entry(rng.choice([0, 1]), rng.randrange(1, 1 << rng.choice([3, 20, 40, 63])), idx, d)
+        idx += 1
+    return e.getvalue()
+
+
+class _Concat:
+    """Encoder continuing after a Cut: earlier files' bytes + a new encoder."""
+
+    def __init__(self, head, enc):
+        self.head, self.enc = head, enc
+
+    def __getattr__(self, k):
+        return getattr(self.enc, k)
+
+    def getvalue(self):
+        return self.head + self.enc.getvalue()
+
+
+# ---------------------------------------------------------------------------
+INFO = bytes.fromhex("0e0000000000000008011099b5e4d0031a0408effd02")
+
+
+def test_info_record_and_read_record_cases(ctx):
+    assert_parity(ctx, INFO)
+    for cut in (0, 8, 10, 14, 18):
+        assert_parity(ctx, INFO[:cut])
+    assert_parity(ctx, INFO[:-1] + b"a")
+
+
+def test_recover_and_cut(ctx):
+    rng = random.Random(1)
+    assert_parity(ctx, build_wal(rng, 3, 10, states=True), 0)
+    w = build_wal(rng, 40, 500, cuts=6)
+    for ri in (0, 1, 5, 39, 40, 41):
+        assert_parity(ctx, w, ri)
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_random_wals(ctx, seed):
+    rng = random.Random(100 + seed)
+    w = build_wal(rng, rng.randrange(1, 300), rng.choice([100, 3000, 70000]), cuts=rng.randrange(0, 4))
+    assert_parity(ctx, w, 0)
+
+
+@pytest.mark.parametrize("seed", range(40))
+def test_corruptions(ctx, seed):
+    rng = random.Random(1000 + seed)
+    w = bytearray(build_wal(rng, rng.randrange(5, 120), 2000, cuts=rng.randrange(0, 3)))
+    kind = seed % 5
+    if kind == 0:      # flip a byte anywhere
+        p = rng.randrange(len(w))
+        w[p] ^= 1 << rng.randrange(8)
+    elif kind == 1:    # truncate
+        del w[rng.randrange(len(w)):]
+    elif kind == 2:    # trailing garbage
+        w += bytes(rng.getrandbits(8) for _ in range(rng.randrange(1, 20)))
+    elif kind == 3:    # corrupt a length prefix high byte (negative / huge)
+        offs = O.chain_crcs(bytes(w))[1]
+        p = rng.choice(offs)
+        w[p + 7] = rng.choice([0x80, 0x7f, 0x01])
+    else:              # trailing bare length prefix: io.EOF from io.ReadFull
+        w += struct.pack("<q", rng.randrange(1, 1000))
+    assert_parity(ctx, w, 0, allow_unsupported=True)
+
+
+def test_unsupported_rate_is_low():
+    # corruption-driven non-canonical frames must stay rare
+    assert len(UNSUPPORTED_SEEN) <= 8, UNSUPPORTED_SEEN
+
+
+def test_edge_statuses(ctx):
+    rng = random.Random(5)
+    # unexpected block type after a valid CRC (wal/wal.go:193-195)
+    e = O.WalEncoder(0)
+    e.save_crc(0)
+    e.encode(1, b"m")
+    e.encode(9, b"payload")
+    assert_parity(ctx, e.getvalue())
+    # metadata conflict (wal/wal.go:178-183)
+    e = O.WalEncoder(0)
+    e.save_crc(0)
+    e.encode(1, b"m1")
+    e.save_entry(0, 1, 0, b"x")
+    e.encode(1, b"m2")
+    assert_parity(ctx, e.getvalue())
+    # empty metadata first, then non-empty: no conflict
+    e = O.WalEncoder(0)
+    e.save_crc(0)
+    e.encode(1, None)
+    e.encode(1, b"m2")
+    e.encode(1, b"m2")
+    assert_parity(ctx, e.getvalue())
+    # crc-record seam mismatch (wal.ErrCRCMismatch, wal/wal.go:184-192)
+    a = O.WalEncoder(0)
+    a.save_crc(0)
+    a.encode(1, b"m")
+    a.save_entry(0, 1, 0, b"abc")
+    b = O.WalEncoder(a.crc ^ 1)
+    b.save_crc(0)
+    b.encode(1, b"m")
+    assert_parity(ctx, a.getvalue() + b.getvalue())
+    # index gap -> slice panic class; ri beyond enti -> ErrIndexNotFound
+    e = O.WalEncoder(0)
+    e.save_crc(0)
+    e.encode(1, b"m")
+    e.save_entry(0, 1, 0, b"a")
+    e.save_entry(0, 1, 2, b"b")
+    assert_parity(ctx, e.getvalue(), 0)
+    w = build_wal(rng, 10, 100)
+    assert_parity(ctx, w, 11)
+    # index rewind truncates ents (leader change overwrite)
+    e = O.WalEncoder(0)
+    e.save_crc(0)
+    e.encode(1, b"m")
+    for i in (0, 1, 2, 3, 4, 2, 3, 1, 2, 3):
+        e.save_entry(0, i, i, bytes([i]) * i)
+    assert_parity(ctx, e.getvalue(), 0)
+    assert_parity(ctx, e.getvalue(), 2)
+    assert_parity(ctx, b"")
+
+
+def test_non_canonical_is_reported_not_guessed(ctx):
+    # a Record with an unknown field: the oracle decodes it; the GPU path
+    # reports EWAL_UNSUPPORTED_ENCODING at that frame instead of guessing
+    body = bytes([0x08, 0x01, 0x10, 0x00, 0x2a, 0x01, 0x00])   # field 5 (unknown)
+    w = struct.pack("<q", len(body)) + body
+    g = gpu_readall(ctx, w, 0)
+    assert g["status"] == L.UNSUPPORTED_ENCODING and g["fail_record"] == 0
+
+
+def test_synth_medium_with_corruption(ctx):
+    buf, n = W.synth_wal(48 << 20, 64, 65536, seed=2)
+    assert_parity(ctx, buf, 1, check_chain=True)
+    bad, _ = W.synth_wal(48 << 20, 64, 65536, seed=2, corrupt_record=int(0.73 * n))
+    o, g = assert_parity(ctx, bad, 1)
+    assert g["status"] == L.ERR_RECORD_CRC and g["fail_record"] == int(0.73 * n)
+
+
+def test_synth_small_records(ctx):
+    buf, n = W.synth_wal(8 << 20, 1, 300, seed=9)
+    assert_parity(ctx, buf, 1)
+
+
+def test_full_size_properties(ctx):
+    """configs[1] scale (8 GiB, mixed 64 B-64 KiB): size-independent checks --
+    a clean WAL verifies end to end, and one flipped payload byte at frame
+    k = 0.73 N is reported as walpb.ErrCRCMismatch at exactly frame k."""
+    size = 8 << 30
+    buf, n = W.synth_wal(size, 64, 65536, seed=2)
+    nb = len(buf)
+    d = ctx.alloc(nb + 64)
+    try:
+        d.upload_ptr(C.addressof((C.c_char * nb).from_buffer(buf)), nb)
+        del buf
+        r = W.readall_device(d, nb, 1)
+        assert r.status == L.OK and r.n_records == n and r.enti == n - 3
+        k = int(0.73 * n)
+        rec = W.records(ctx, n)[k]
+        p = rec["data_off"] + rec["data_len"] // 2
+        b = bytearray(d.download(1, p))
+        b[0] ^= 0x5A
+        d.upload(bytes(b), p)
+        r2 = W.readall_device(d, nb, 1)
+        assert r2.status == L.ERR_RECORD_CRC and r2.fail_record == k and r2.fail_offset == rec["offset"]
+    finally:
+        d.free()
+
+
+def test_crc_device(ctx):
+    rng = random.Random(3)
+    for n in (1, 7, 64, 4095, 4096, 65536, 65537, 1 << 20, (3 << 20) + 11):
+        data = bytes(rng.getrandbits(8) for _ in range(n)) if n < 70000 else rng.randbytes(n)
+        d = ctx.alloc(n + 64)
+        d.upload(data)
+        for poly in (L.CASTAGNOLI, L.KOOPMAN):
+            out = C.c_uint32()
+            seed = rng.getrandbits(32)
+            assert L.lib.ewal_crc32_update_device(ctx.handle, seed, poly, d.ptr, n, C.byref(out)) == 0
+            assert out.value == O.crc32_update(seed, data, poly)
+        d.free()
+
+
+def _snap_file(rng, n, nodes, index, term, corrupt=False):
+    body = O.snapshot_marshal(rng.randbytes(n), nodes, index, term)
+    crc = O.crc32_update(0, body)
+    f = bytearray(O.snappb_marshal(crc, body))
+    if corrupt:
+        f[len(f) // 2] ^= 0x10
+    return bytes(f)
+
+
+def test_snapshot_batch(ctx):
+    rng = random.Random(8)
+    files = [_snap_file(rng, rng.choice([0, 1, 100, 5000, 200000]), [1, 2, 3][:rng.randrange(4)], i + 1, 2,
+                        corrupt=(i % 4 == 3)) for i in range(24)]
+    files.append(b"bad data")
+    files.append(b"")
+    offs, packed = [], bytearray()
+    for f in files:
+        offs.append(len(packed))
+        packed += f
+        packed += b"\0" * rng.randrange(0, 40)
+    d = ctx.alloc(len(packed) + 64)
+    d.upload(bytes(packed))
+    n = len(files)
+    for poly in (L.CASTAGNOLI, L.KOOPMAN):
+        st = (C.c_int32 * n)()
+        sc = (C.c_uint32 * n)()
+        cc = (C.c_uint32 * n)()
+        rc = L.lib.esnap_verify_packed(ctx.handle, d.ptr, len(packed), (C.c_uint64 * n)(*offs),
+                                       (C.c_uint64 * n)(*[len(f) for f in files]), n, poly, st, sc, cc)
+        assert rc == 0
+        for i, f in enumerate(files):
+            o = O.loadsnap(f, poly)
+            assert st[i] == o["status"], (i, st[i], o["status"])
+            if o["status"] in (O.OK, O.ERR_SNAP_CRC):
+                assert cc[i] == o["computed_crc"] and sc[i] == o["stored_crc"]
+            if o["status"] == O.OK:
+                s = L.SnapshotDesc()
+                assert L.lib.esnap_copy_snapshot(ctx.handle, i, C.byref(s)) == 0
+                assert (s.index, s.term, list(s.nodes[:s.n_nodes])) == (o["snap"]["index"], o["snap"]["term"],
+                                                                        o["snap"]["nodes"])
+                assert packed[s.data_off:s.data_off + s.data_len] == o["snap"]["data"]
+    d.free()
+
+
+def test_snapshotter_load_dir(ctx, tmp_path):
+    """TestSaveAndLoad / TestFailback / TestLoadNewestSnap / TestNoSnapshot."""
+    rng = random.Random(4)
+    dd = tmp_path / "snap"
+    dd.mkdir()
+    s = L.SnapshotDesc()
+    name = C.c_char_p()
+    assert L.lib.esnap_load_dir(ctx.handle, str(dd).encode(), L.CASTAGNOLI, C.byref(s), C.byref(name)) == \
+        L.ERR_NO_SNAPSHOT
+    good = _snap_file(rng, 13, [1, 2, 3], 1, 1)
+    (dd / ("%016x-%016x.snap" % (1, 1))).write_bytes(good)
+    newer = _snap_file(rng, 13, [1, 2, 3], 5, 1)
+    (dd / ("%016x-%016x.snap" % (1, 5))).write_bytes(newer)
+    large = "%016x-%016x-%016x.snap" % (0xFFFF, 0xFFFF, 0xFFFF)
+    (dd / large).write_bytes(b"bad data")
+    rc = L.lib.esnap_load_dir(ctx.handle, str(dd).encode(), L.CASTAGNOLI, C.byref(s), C.byref(name))
+    assert rc == 0 and s.index == 5 and name.value.decode() == "%016x-%016x.snap" % (1, 5)
+    assert (dd / (large + ".broken")).exists()
+
+
+def test_commit_batch(ctx):
+    rng = random.Random(6)
+    G = 5000
+    nv = [rng.choice([1, 3, 4, 5, 7, 16]) for _ in range(G)]
+    match = [[0] * G for _ in range(16)]
+    terms, committed, offs, ptr, logs = [], [], [], [0], []
+    for g in range(G):
+        for v in range(nv[g]):
+            match[v][g] = rng.randrange(0, 40)
+        off = rng.choice([0, 0, 5, 10])
+        nlog = rng.randrange(1, 40)
+        logs += [rng.randrange(1, 4) for _ in range(nlog)]
+        ptr.append(len(logs))
+        offs.append(off)
+        terms.append(rng.randrange(1, 4))
+        committed.append(rng.randrange(0, 20))
+    flat = [x for row in match for x in row]
+
+    def dev(arr, ctype):
+        a = (ctype * len(arr))(*arr)
+        b = ctx.alloc(C.sizeof(a))
+        b.upload(bytes(a))
+        return b
+
+    dm, dn, dt, dc = dev(flat, C.c_uint64), dev(nv, C.c_uint8), dev(terms, C.c_uint64), dev(committed, C.c_uint64)
+    do, dp, dl = dev(offs, C.c_uint64), dev(ptr, C.c_uint64), dev(logs, C.c_uint64)
+    dch, dst = ctx.alloc(G), ctx.alloc(G)
+    ms = C.c_double()
+    assert L.lib.ecommit_batch_device(ctx.handle, G, dm.ptr, dn.ptr, dt.ptr, dc.ptr, do.ptr, dp.ptr, dl.ptr,
+                                      dch.ptr, dst.ptr, C.byref(ms)) == 0
+    newc = struct.unpack("<%dQ" % G, dc.download(8 * G))
+    chg = dch.download(G)
+    for g in range(G):
+        rc, c = O.maybe_commit([match[v][g] for v in range(nv[g])], terms[g], committed[g],
+                               logs[ptr[g]:ptr[g + 1]], offs[g])
+        assert newc[g] == c and chg[g] == (1 if rc == 1 else 0), g
+    for b in (dm, dn, dt, dc, do, dp, dl, dch, dst):
+        b.free()
