@@ -22,7 +22,7 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-# load libewal.so (and its HIP runtime) before torch
+import torch  # noqa: E402  (first: its HIP runtime is the one libewal.so binds to)
 from etcd_amd import wal as W, _lib as L  # noqa: E402
 
 HBM_PEAK_GBPS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
@@ -58,7 +58,6 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
 
-    import torch
     dist = None
     if world > 1:
         import torch.distributed as dist

@@ -16,6 +16,17 @@ HEADER = os.path.join(os.path.dirname(_HERE), "include", "ewal.h")
 if not os.path.exists(LIB_PATH):
     raise ImportError("etcd_amd: %s is missing -- run etcd_amd/build.sh (hipcc --offload-arch=gfx950)" % LIB_PATH)
 
+# One HIP runtime per process: torch ships its own libamdhip64 (SONAME
+# libamdhip64.so.7).  Loaded first, our DT_NEEDED libamdhip64.so.7 resolves
+# to it; loaded after us, torch would map a second runtime and one of the two
+# sees no device (measured on the MI355X box).  So torch, when importable,
+# is imported before libewal.so is mapped.
+if os.environ.get("EWAL_NO_TORCH") != "1":
+    try:
+        import torch  # noqa: F401
+    except Exception:
+        pass
+
 lib = C.CDLL(LIB_PATH)
 
 # ---- status codes (include/ewal.h) --------------------------------------

@@ -64,6 +64,7 @@ __global__ void k_snap(const uint8_t *__restrict__ buf, const uint32_t *__restri
       pb_init(s);
       uint64_t rep[128];
       int s2 = d.dlen ? pb_walk(buf + d.doff, (int64_t)d.dlen, c_kind_snapshot, s, rep, 64) : 0;
+      if (s2 == 0 && s.unrec) s2 = EWAL_UNSUPPORTED_ENCODING;  // Snapshot.XXX_unrecognized is returned
       st = s2;
       esnap_snapshot out;
       out.index = s.v[3];

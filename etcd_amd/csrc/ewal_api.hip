@@ -122,9 +122,11 @@ static int select_flagged(ewal_ctx *c, const uint8_t *flags, uint32_t n, uint32_
 // find_cand).  Returns the candidate count via *K (synchronises).
 static int run_stream(ewal_ctx *c, DevTables *tb, const uint8_t *d_buf, uint64_t B, int find_cand, uint64_t ccap,
                       uint64_t *K) {
-  const uint64_t ntiles64 = (B + EW_TILE - 1) / EW_TILE;
+  // B / TILE + 1 tiles: P(x) is read at x == B, which needs the wave prefix
+  // of the wave containing B even when B is tile-aligned.
+  const uint64_t ntiles64 = B / EW_TILE + 1;
   if (ntiles64 >= 0xffffffffull) return EWAL_E_INVAL;
-  const uint32_t ntiles = (uint32_t)std::max<uint64_t>(ntiles64, 1);
+  const uint32_t ntiles = (uint32_t)ntiles64;
   EW_CHECK(c->v.ensure((size_t)ntiles * EW_THREADS * 4));
   EW_CHECK(c->pwave.ensure((size_t)ntiles * EW_WAVES * 4));
   EW_CHECK(c->desc.ensure((size_t)ntiles * sizeof(TileDesc)));

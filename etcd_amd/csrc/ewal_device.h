@@ -89,12 +89,102 @@ __device__ __forceinline__ int rd_varint(const uint8_t *p, int64_t &i, int64_t l
   }
 }
 
+// ---- proto.Skip (third_party/code.google.com/p/gogoprotobuf/proto/skip_gogo.go:33-116)
+// Iterative restatement of the group recursion with a bounded frame stack.
+// Exact non-termination tests: a frame looping more times than it has byte
+// positions must revisit one (deterministic => forever), and a child group
+// pushed at local start 0 re-enters its parent (infinite recursion) -> 37.
+#define PB_SKIP_DEPTH 16
+__device__ __forceinline__ int skip_wire(const uint8_t *p, int64_t &i, int64_t l, uint64_t &w) {
+  w = 0;
+  for (uint32_t shift = 0;; shift += 7) {
+    if (i >= l) return 2;       // io.ErrUnexpectedEOF
+    if (i < 0) return 33;       // data[index] with index < 0: runtime panic
+    uint8_t b = p[i++];
+    if (shift < 64) w |= (uint64_t)(b & 0x7F) << shift;
+    if (b < 0x80) return 0;
+  }
+}
+__device__ __forceinline__ int skip_simple(const uint8_t *p, int64_t l, int wt, int64_t i, int64_t &n) {
+  switch (wt) {
+  case 0:
+    for (;;) {
+      if (i >= l) return 2;
+      ++i;
+      if (p[i - 1] < 0x80) break;
+    }
+    n = i;
+    return 0;
+  case 1: n = (int64_t)((uint64_t)i + 8); return 0;
+  case 2: {
+    uint64_t len = 0;
+    for (uint32_t shift = 0;; shift += 7) {
+      if (i >= l) return 2;
+      uint8_t b = p[i++];
+      if (shift < 64) len |= (uint64_t)(b & 0x7F) << shift;
+      if (b < 0x80) break;
+    }
+    n = (int64_t)((uint64_t)i + len);
+    return 0;
+  }
+  case 4: n = i; return 0;
+  case 5: n = (int64_t)((uint64_t)i + 4); return 0;
+  default: return 7;            // proto.ErrWrongType
+  }
+}
+__device__ inline int pb_skip(const uint8_t *p, int64_t l, int64_t &out) {
+  if (l <= 0) return 33;        // panic("unreachable")
+  int64_t i = 0;
+  uint64_t w;
+  int st = skip_wire(p, i, l, w);
+  if (st) return st;
+  int wt = (int)(w & 7);
+  if (wt != 3) return skip_simple(p, l, wt, i, out);
+  int64_t sb[PB_SKIP_DEPTH], ss[PB_SKIP_DEPTH], si[PB_SKIP_DEPTH];
+  int depth = 0;
+  int64_t base = 0, idx = i, iters = 0;
+  for (;;) {
+    const uint8_t *d = p + base;
+    const int64_t ll = l - base;
+    if (++iters > ll + 1) return 37;
+    const int64_t start = idx;
+    int64_t j = idx;
+    st = skip_wire(d, j, ll, w);
+    if (st) return st;
+    const int wt2 = (int)(w & 7);
+    if (wt2 == 4) {
+      if (depth == 0) { out = j; return 0; }
+      --depth;
+      base = sb[depth];
+      idx = (int64_t)((uint64_t)ss[depth] + (uint64_t)j);
+      iters = si[depth];
+      continue;
+    }
+    if (wt2 == 3) {
+      if (start == 0) return 37;
+      if (depth == PB_SKIP_DEPTH) return 48;
+      sb[depth] = base; ss[depth] = start; si[depth] = iters;
+      ++depth;
+      base += start;
+      idx = j - start;
+      iters = 0;
+      continue;
+    }
+    int64_t nn;
+    st = skip_simple(d + start, ll - start, wt2, j - start, nn);
+    if (st) return st;
+    idx = (int64_t)((uint64_t)start + (uint64_t)nn);
+  }
+}
+
 // ---- gogoprotobuf Unmarshal walker (exact Go semantics on the supported set)
-// kind[f] for field numbers 1..7: 0 unknown, PB_VAR64/PB_VAR32 (|= accumulate),
-// PB_BYTES (append; nil when empty), PB_REP64 (append to a repeated list).
+// kind[f] for field numbers 1..7: 0 unknown (proto.Skip into XXX_unrecognized,
+// sets o.unrec), PB_VAR64/PB_VAR32 (|= accumulate), PB_BYTES (append; nil
+// when empty), PB_REP64 (append to a repeated list).
 // Returns 0, 2 (io.ErrUnexpectedEOF), 7 (proto.ErrWrongType), 33 (bounds
-// panic) or 48 (EWAL_UNSUPPORTED_ENCODING: an unknown field needing proto.Skip,
-// or a bytes field whose repeats would concatenate two non-empty segments).
+// panic), 37 (never terminates) or 48 (EWAL_UNSUPPORTED_ENCODING: a bytes
+// field whose repeats concatenate two non-empty segments, or a deeper group
+// nesting than the device stack).
 #define PB_VAR64 1
 #define PB_VAR32 2
 #define PB_BYTES 3
@@ -104,10 +194,12 @@ struct PbOut {
   int64_t boff[8];
   int64_t blen[8];
   uint32_t nrep[8];
+  int unrec;
 };
 __device__ __forceinline__ void pb_init(PbOut &o) {
 #pragma unroll
   for (int k = 0; k < 8; ++k) { o.v[k] = 0; o.boff[k] = -1; o.blen[k] = 0; o.nrep[k] = 0; }
+  o.unrec = 0;
 }
 __device__ inline int pb_walk(const uint8_t *p, int64_t l, const uint8_t *kind, PbOut &o,
                               uint64_t *rep, uint32_t repcap) {
@@ -118,7 +210,23 @@ __device__ inline int pb_walk(const uint8_t *p, int64_t l, const uint8_t *kind, 
     uint32_t fn = (uint32_t)(wire >> 3);   // int32(wire >> 3)
     int wt = (int)(wire & 7);
     int k = (fn >= 1 && fn <= 7) ? kind[fn] : 0;
-    if (k == 0) return 48;
+    if (k == 0) {
+      // default: index -= sizeOfWire; Skip(data[index:]); bounds; append
+      int64_t sow = 0;
+      uint64_t w = wire;
+      do { ++sow; w >>= 7; } while (w);
+      i -= sow;
+      int64_t skippy;
+      int st = pb_skip(p + i, l - i, skippy);
+      if (st) return st;
+      int64_t hi = (int64_t)((uint64_t)i + (uint64_t)skippy);
+      if (hi > l) return 2;
+      if (hi < i) return 33;
+      if (skippy == 0) return 37;
+      o.unrec = 1;
+      i = hi;
+      continue;
+    }
     if (k == PB_BYTES) {
       if (wt != 2) return 7;
       uint64_t bl = 0;

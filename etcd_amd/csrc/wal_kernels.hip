@@ -385,6 +385,7 @@ __global__ void k_decode(const uint8_t *__restrict__ buf, const uint64_t *__rest
       PbOut e;
       pb_init(e);
       int s2 = d.dnil ? 0 : pb_walk(dp, (int64_t)d.dlen, c_kind_entry, e, nullptr, 0);
+      if (s2 == 0 && e.unrec) s2 = 48;   // Entry.XXX_unrecognized is returned by ReadAll
       d.sub_st = s2;
       d.etype = (int32_t)(uint32_t)e.v[1];
       d.f0 = e.v[2];            // Term
@@ -394,6 +395,7 @@ __global__ void k_decode(const uint8_t *__restrict__ buf, const uint64_t *__rest
       PbOut h;
       pb_init(h);
       int s2 = d.dnil ? 0 : pb_walk(dp, (int64_t)d.dlen, c_kind_state, h, nullptr, 0);
+      if (s2 == 0 && h.unrec) s2 = 48;   // HardState.XXX_unrecognized is returned
       d.sub_st = s2;
       d.f0 = h.v[1]; d.f1 = h.v[2]; d.f2 = h.v[3];
     }
@@ -451,11 +453,11 @@ __global__ void k_verify(const uint8_t *__restrict__ buf, const uint32_t *__rest
         st = EWAL_ERR_RECORD_CRC;
       } else if (d.type == 2) {
         if (d.sub_st == 48) st = EWAL_UNSUPPORTED_ENCODING;
-        else if (d.sub_st == 33) st = EWAL_PANIC_BOUNDS;
+        else if (d.sub_st == 33 || d.sub_st == 37) st = d.sub_st;
         else if (d.sub_st) st = EWAL_PANIC_ENTRY;
       } else if (d.type == 3) {
         if (d.sub_st == 48) st = EWAL_UNSUPPORTED_ENCODING;
-        else if (d.sub_st == 33) st = EWAL_PANIC_BOUNDS;
+        else if (d.sub_st == 33 || d.sub_st == 37) st = d.sub_st;
         else if (d.sub_st) st = EWAL_PANIC_STATE;
       } else if (d.type != 1) {
         st = EWAL_ERR_UNEXPECTED_TYPE;

@@ -193,13 +193,23 @@ def test_edge_statuses(ctx):
     assert_parity(ctx, b"")
 
 
-def test_non_canonical_is_reported_not_guessed(ctx):
-    # a Record with an unknown field: the oracle decodes it; the GPU path
-    # reports EWAL_UNSUPPORTED_ENCODING at that frame instead of guessing
+def test_unknown_fields_and_unsupported(ctx):
+    # a walpb.Record with an unknown field is decoded exactly (proto.Skip on the GPU)
     body = bytes([0x08, 0x01, 0x10, 0x00, 0x2a, 0x01, 0x00])   # field 5 (unknown)
     w = struct.pack("<q", len(body)) + body
-    g = gpu_readall(ctx, w, 0)
-    assert g["status"] == L.UNSUPPORTED_ENCODING and g["fail_record"] == 0
+    assert_parity(ctx, w, 0)
+    # ... and Skip's own errors are exact too (length runs past the record)
+    body = bytes([0x08, 0x01, 0x10, 0x00, 0x2a, 0x7f, 0x00])
+    assert_parity(ctx, struct.pack("<q", len(body)) + body, 0)
+    # an Entry with an unknown field would have to return XXX_unrecognized:
+    # reported as EWAL_UNSUPPORTED_ENCODING at that frame, never guessed
+    e = O.WalEncoder(0)
+    e.save_crc(0)
+    e.encode(1, b"m")
+    e.encode(2, O.entry_marshal(0, 1, 0, b"x") + bytes([0x38, 0x05]))   # field 7 varint
+    g = gpu_readall(ctx, e.getvalue(), 0)
+    assert O.readall(e.getvalue(), 0)["status"] == O.OK
+    assert g["status"] == L.UNSUPPORTED_ENCODING and g["fail_record"] == 2
 
 
 def test_synth_medium_with_corruption(ctx):
@@ -208,6 +218,35 @@ def test_synth_medium_with_corruption(ctx):
     bad, _ = W.synth_wal(48 << 20, 64, 65536, seed=2, corrupt_record=int(0.73 * n))
     o, g = assert_parity(ctx, bad, 1)
     assert g["status"] == L.ERR_RECORD_CRC and g["fail_record"] == int(0.73 * n)
+
+
+def test_tile_aligned_lengths(ctx):
+    """WALs whose byte length is an exact multiple of the 64 KiB tile (the
+    stream prefix is read at x == len)."""
+    for total in (65536, 3 * 65536, 1 << 20):
+        e = O.WalEncoder(0)
+        e.save_crc(0)
+        e.encode(1, b"m")
+        i = 0
+        while True:
+            cur = len(e.getvalue())
+            left = total - cur
+            if left < 200:
+                break
+            n = min(3000, left - 100)
+            e.save_entry(0, 1, i, bytes([i & 0xff]) * n)
+            i += 1
+        # pad the final entry so the stream ends exactly at `total`
+        cur = len(e.getvalue())
+        for pad in range(0, 200):
+            trial = O.WalEncoder(e.crc)
+            trial.save_entry(0, 1, i, b"z" * pad)
+            if cur + len(trial.getvalue()) == total:
+                e.save_entry(0, 1, i, b"z" * pad)
+                break
+        w = e.getvalue()
+        assert len(w) == total
+        assert_parity(ctx, w, 0)
 
 
 def test_synth_small_records(ctx):
@@ -294,7 +333,8 @@ def test_snapshot_batch(ctx):
                 assert L.lib.esnap_copy_snapshot(ctx.handle, i, C.byref(s)) == 0
                 assert (s.index, s.term, list(s.nodes[:s.n_nodes])) == (o["snap"]["index"], o["snap"]["term"],
                                                                         o["snap"]["nodes"])
-                assert packed[s.data_off:s.data_off + s.data_len] == o["snap"]["data"]
+                got = bytes(packed[s.data_off:s.data_off + s.data_len]) if s.data_len else None
+                assert got == o["snap"]["data"]
     d.free()
 
 
