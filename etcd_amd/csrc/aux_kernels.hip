@@ -12,22 +12,7 @@
 #include "ewal_device.h"
 #include "ewal_internal.h"
 
-__constant__ uint8_t c_kind_snappb[8] = {0, PB_VAR32, PB_BYTES, 0, 0, 0, 0, 0};
-__constant__ uint8_t c_kind_snapshot[8] = {0, PB_BYTES, PB_REP64, PB_VAR64, PB_VAR64, PB_REP64, 0, 0};
-
-__device__ __forceinline__ uint32_t prefix_at_g(uint64_t x, const uint32_t *__restrict__ pwave,
-                                                const uint32_t *__restrict__ v, const uint8_t *__restrict__ buf,
-                                                const uint32_t *t4, const uint32_t *s64) {
-  const uint64_t w = x >> 12;
-  uint32_t acc = pwave[w];
-  const uint64_t x0 = x & ~(uint64_t)(EW_PIECE - 1);
-  const uint32_t k = (uint32_t)((x0 >> 6) & 63);
-  const uint32_t *vp = v + (w << 6);
-  for (uint32_t j = 0; j < k; ++j) acc = tab_apply(s64, acc) ^ vp[j];
-  return raw_bytes(t4, acc, buf, x0, x);
-}
-
-__global__ void k_snap(const uint8_t *__restrict__ buf, const uint32_t *__restrict__ pwave,
+__global__ __launch_bounds__(256) void k_snap(const uint8_t *__restrict__ buf, const uint32_t *__restrict__ pwave,
                        const uint32_t *__restrict__ v, const uint32_t *__restrict__ g_slice,
                        const uint32_t *__restrict__ g_shift, SnapDesc *__restrict__ sd,
                        esnap_snapshot *__restrict__ snaps, uint32_t n) {
@@ -41,43 +26,42 @@ __global__ void k_snap(const uint8_t *__restrict__ buf, const uint32_t *__restri
   uint32_t f = blockIdx.x * blockDim.x + threadIdx.x;
   if (f >= n) return;
   SnapDesc d = sd[f];
-  PbOut o;
-  pb_init(o);
-  int st = pb_walk(buf + d.off, (int64_t)d.len, c_kind_snappb, o, nullptr, 0);
-  d.stored = (uint32_t)o.v[1];
-  d.doff = d.off + (o.blen[2] > 0 ? (uint64_t)o.boff[2] : 0);
-  d.dlen = o.blen[2] > 0 ? (uint64_t)o.blen[2] : 0;
+  PbField a1, a2, a3, a4, a5;
+  pbf_init(a1); pbf_init(a2); pbf_init(a3); pbf_init(a4); pbf_init(a5);
+  int unrec;
+  int st = pb_walk<PB_VAR32, PB_BYTES, PB_NONE, PB_NONE, PB_NONE>(buf + d.off, (int64_t)d.len, a1, a2, a3, a4, a5,
+                                                                  unrec, nullptr, nullptr, 0);
+  d.stored = (uint32_t)a1.v;
+  d.doff = d.off + (a2.blen > 0 ? (uint64_t)a2.boff : 0);
+  d.dlen = a2.blen > 0 ? (uint64_t)a2.blen : 0;
   d.computed = 0;
   if (st == 0) {
     // crc32.Update(0, crcTable, Data) = S_n(~0 ^ P(s)) ^ P(e) ^ ~0
     if (d.dlen == 0) {
       d.computed = 0;
     } else {
-      const uint32_t Ps = prefix_at_g(d.doff, pwave, v, buf, s_t4, s_s64);
-      const uint32_t Pe = prefix_at_g(d.doff + d.dlen, pwave, v, buf, s_t4, s_s64);
+      const uint32_t Ps = prefix_at(d.doff, pwave, v, buf, s_t4, s_s64);
+      const uint32_t Pe = prefix_at(d.doff + d.dlen, pwave, v, buf, s_t4, s_s64);
       d.computed = gshift_n(g_shift, d.dlen, 0xffffffffu ^ Ps) ^ Pe ^ 0xffffffffu;
     }
     if (d.computed != d.stored) {
       st = EWAL_ERR_SNAP_CRC;
     } else {
-      PbOut s;
-      pb_init(s);
-      uint64_t rep[128];
-      int s2 = d.dlen ? pb_walk(buf + d.doff, (int64_t)d.dlen, c_kind_snapshot, s, rep, 64) : 0;
-      if (s2 == 0 && s.unrec) s2 = EWAL_UNSUPPORTED_ENCODING;  // Snapshot.XXX_unrecognized is returned
-      st = s2;
-      esnap_snapshot out;
-      out.index = s.v[3];
-      out.term = s.v[4];
-      out.data_off = s.blen[1] > 0 ? d.doff + (uint64_t)s.boff[1] : d.doff;
-      out.data_len = s.blen[1] > 0 ? (uint64_t)s.blen[1] : 0;
-      out.n_nodes = s.nrep[2];
-      out.n_removed = s.nrep[5];
-      for (int k = 0; k < 64; ++k) {
-        out.nodes[k] = k < (int)s.nrep[2] ? rep[k] : 0;
-        out.removed[k] = k < (int)s.nrep[5] ? rep[64 + k] : 0;
-      }
-      if (snaps) snaps[f] = out;
+      PbField s1, s2, s3, s4, s5;
+      pbf_init(s1); pbf_init(s2); pbf_init(s3); pbf_init(s4); pbf_init(s5);
+      esnap_snapshot *o = snaps + f;
+      int ur = 0;
+      int st2 = d.dlen ? pb_walk<PB_BYTES, PB_REP64, PB_VAR64, PB_VAR64, PB_REP64>(
+                             buf + d.doff, (int64_t)d.dlen, s1, s2, s3, s4, s5, ur, o->nodes, o->removed, 64)
+                       : 0;
+      if (st2 == 0 && ur) st2 = EWAL_UNSUPPORTED_ENCODING;  // Snapshot.XXX_unrecognized is returned
+      st = st2;
+      o->index = s3.v;
+      o->term = s4.v;
+      o->data_off = s1.blen > 0 ? d.doff + (uint64_t)s1.boff : d.doff;
+      o->data_len = s1.blen > 0 ? (uint64_t)s1.blen : 0;
+      o->n_nodes = (int64_t)s2.v;
+      o->n_removed = (int64_t)s5.v;
     }
   }
   d.st = st;

@@ -62,6 +62,9 @@ struct DevBuf {
 struct Small {  // per-call device scratch (zeroed / initialised each call)
   uint32_t ticket;
   uint32_t errflag;
+  uint32_t novf;
+  uint32_t pad0;
+  unsigned long long total;
   ChainInfo ci;
   ReadAllAgg agg;
   uint32_t nsel;      // hipcub select counts
@@ -75,12 +78,14 @@ struct Small {  // per-call device scratch (zeroed / initialised each call)
 struct ewal_ctx {
   int device = 0;
   int num_cu = 256;
+  int stream_r = 16;
+  int ablate = 0;      // EWAL_STREAM_ABLATE (timing experiments only; results are wrong)   // LDS replicas of the slicing tables (EWAL_STREAM_R=16|32)
   hipStream_t stream = nullptr;
   bool own_stream = false;
   hipEvent_t ev0 = nullptr, ev1 = nullptr, evs0 = nullptr, evs1 = nullptr;
   std::map<uint32_t, DevTables> tables;
   std::map<uint32_t, std::unique_ptr<ewal::CrcTables>> host_tables;
-  DevBuf v, pwave, desc, cpos, clen, nxt, exc, E, rs, jl, vis, entry, on, rec_cand, rd, opf, ops, kk, kkrev, suf,
+  DevBuf pf, v, pwave, desc, wagg, wcnt, slots, cbase, ovf, cpos, clen, nxt, exc, E, rs, jl, vis, entry, on, rec_cand, rd, opf, ops, kk, kkrev, suf,
       ents, recs, tmp, small, sdesc, snaps, hbuf_dev;
   Small *h_small = nullptr;  // pinned mirror
   // results of the last readall
@@ -118,48 +123,81 @@ static int select_flagged(ewal_ctx *c, const uint8_t *flags, uint32_t n, uint32_
   return 0;
 }
 
-// Run k_stream over d_buf[0..B): fills c->v, c->pwave (and candidates when
-// find_cand).  Returns the candidate count via *K (synchronises).
+// Run the HBM pass (k_stream) and the unit scan (k_uscan) over d_buf[0..B):
+// fills c->v, c->pwave; with find_cand also the dense, sorted candidate list
+// (k_compact + k_rescan) and returns its size via *K (synchronises).
+static int compact_cands(ewal_ctx *c, const uint8_t *d_buf, uint64_t B, uint32_t nunits, uint64_t ccap) {
+  Small *ds = c->small.as<Small>();
+  EW_CHECK(hipMemsetAsync(&ds->novf, 0, 4, c->stream));
+  hipLaunchKernelGGL(k_compact, dim3(grid_for(nunits, 256)), dim3(256), 0, c->stream, d_buf, nunits,
+                     c->wcnt.as<uint32_t>(), c->cbase.as<unsigned long long>(), c->slots.as<uint16_t>(),
+                     c->cpos.as<uint64_t>(), c->clen.as<uint64_t>(), ccap, c->ovf.as<uint32_t>(), &ds->novf);
+  hipLaunchKernelGGL(k_rescan, dim3(64), dim3(256), 0, c->stream, d_buf, B, c->ovf.as<uint32_t>(), &ds->novf,
+                     c->cbase.as<unsigned long long>(), c->cpos.as<uint64_t>(), c->clen.as<uint64_t>(), ccap);
+  EW_CHECK(hipGetLastError());
+  return 0;
+}
+
 static int run_stream(ewal_ctx *c, DevTables *tb, const uint8_t *d_buf, uint64_t B, int find_cand, uint64_t ccap,
                       uint64_t *K) {
-  // B / TILE + 1 tiles: P(x) is read at x == B, which needs the wave prefix
-  // of the wave containing B even when B is tile-aligned.
-  const uint64_t ntiles64 = B / EW_TILE + 1;
-  if (ntiles64 >= 0xffffffffull) return EWAL_E_INVAL;
-  const uint32_t ntiles = (uint32_t)ntiles64;
-  EW_CHECK(c->v.ensure((size_t)ntiles * EW_THREADS * 4));
-  EW_CHECK(c->pwave.ensure((size_t)ntiles * EW_WAVES * 4));
-  EW_CHECK(c->desc.ensure((size_t)ntiles * sizeof(TileDesc)));
-  EW_CHECK(hipMemsetAsync(c->desc.p, 0, (size_t)ntiles * sizeof(TileDesc), c->stream));
+  const uint64_t nunits64 = B / EW_WAVE_BYTES + 1;
+  if (nunits64 >= 0xffff0000ull) return EWAL_E_INVAL;
+  const uint32_t nunits = (uint32_t)nunits64;
+  const uint32_t nstiles = (nunits + 1023) / 1024;
+  EW_CHECK(c->v.ensure((size_t)nunits * 64 * 4));
+  EW_CHECK(c->pwave.ensure((size_t)nunits * 4));
+  EW_CHECK(c->wagg.ensure((size_t)nunits * 4));
+  EW_CHECK(c->wcnt.ensure((size_t)nunits * 4));
+  EW_CHECK(c->cbase.ensure((size_t)nunits * 8));
+  if (find_cand) {
+    EW_CHECK(c->slots.ensure((size_t)nunits * EW_SLOTS * 2));
+    EW_CHECK(c->ovf.ensure((size_t)nunits * 4));
+  }
+  EW_CHECK(c->desc.ensure((size_t)nstiles * sizeof(TileDesc)));
+  EW_CHECK(hipMemsetAsync(c->desc.p, 0, (size_t)nstiles * sizeof(TileDesc), c->stream));
   EW_CHECK(hipMemsetAsync(c->small.p, 0, sizeof(Small), c->stream));
+  Small *ds = c->small.as<Small>();
   StreamArgs a;
   a.buf = d_buf;
   a.B = B;
-  a.ntiles = ntiles;
+  a.nunits = nunits;
   a.find_cand = find_cand;
+  a.ablate = c->ablate;
   a.g_slice = tb->slice;
   a.g_shift = tb->shift;
   a.v = c->v.as<uint32_t>();
-  a.pwave = c->pwave.as<uint32_t>();
-  a.cpos = c->cpos.as<uint64_t>();
-  a.clen = c->clen.as<uint64_t>();
-  a.ccap = ccap;
-  a.desc = c->desc.as<TileDesc>();
-  a.ticket = &c->small.as<Small>()->ticket;
-  a.errflag = &c->small.as<Small>()->errflag;
-  const unsigned grid = (unsigned)std::min<uint64_t>(ntiles, (uint64_t)c->num_cu);
+  a.wagg = c->wagg.as<uint32_t>();
+  a.wcnt = c->wcnt.as<uint32_t>();
+  a.slots = find_cand ? c->slots.as<uint16_t>() : nullptr;
+  const unsigned grid = (unsigned)std::min<uint64_t>((nunits + EW_WAVES - 1) / EW_WAVES, (uint64_t)c->num_cu);
   EW_CHECK(hipEventRecord(c->evs0, c->stream));
-  hipLaunchKernelGGL(k_stream, dim3(grid), dim3(EW_THREADS), 0, c->stream, a);
+  if (c->stream_r == 32)
+    hipLaunchKernelGGL(k_stream<32>, dim3(grid), dim3(EW_THREADS), 0, c->stream, a);
+  else
+    hipLaunchKernelGGL(k_stream<16>, dim3(grid), dim3(EW_THREADS), 0, c->stream, a);
   EW_CHECK(hipGetLastError());
   EW_CHECK(hipEventRecord(c->evs1, c->stream));
-  if (K) {
-    unsigned long long tot = 0;
-    EW_CHECK(hipMemcpyAsync(&tot, &a.desc[ntiles - 1].inc_cnt, 8, hipMemcpyDeviceToHost, c->stream));
-    EW_CHECK(hipMemcpyAsync(c->h_small, c->small.p, sizeof(Small), hipMemcpyDeviceToHost, c->stream));
-    EW_CHECK(hipStreamSynchronize(c->stream));
-    if (c->h_small->errflag) return EWAL_E_TIMEOUT;
-    *K = tot;
-  }
+  ScanArgs s;
+  s.nunits = nunits;
+  s.ntiles = nstiles;
+  s.wagg = a.wagg;
+  s.wcnt = a.wcnt;
+  s.g_shift = tb->shift;
+  s.pwave = c->pwave.as<uint32_t>();
+  s.cbase = c->cbase.as<unsigned long long>();
+  s.desc = c->desc.as<TileDesc>();
+  s.ticket = &ds->ticket;
+  s.errflag = &ds->errflag;
+  s.total = &ds->total;
+  hipLaunchKernelGGL(k_uscan, dim3(nstiles), dim3(1024), 0, c->stream, s);
+  EW_CHECK(hipGetLastError());
+  if (!find_cand) return 0;
+  int rc = compact_cands(c, d_buf, B, nunits, ccap);
+  if (rc) return rc;
+  EW_CHECK(hipMemcpyAsync(c->h_small, c->small.p, sizeof(Small), hipMemcpyDeviceToHost, c->stream));
+  EW_CHECK(hipStreamSynchronize(c->stream));
+  if (c->h_small->errflag) return EWAL_E_TIMEOUT;
+  *K = c->h_small->total;
   return 0;
 }
 
@@ -198,14 +236,17 @@ static int readall_impl(ewal_ctx *c, const uint8_t *d_buf, uint64_t B, uint64_t 
   uint64_t K = 0;
   if (B > 0) {
     uint64_t ccap = std::min<uint64_t>(B / 128 + 65536, 0xfffffff0ull);
-    for (;;) {
-      EW_CHECK(c->cpos.ensure(ccap * 8));
-      EW_CHECK(c->clen.ensure(ccap * 8));
-      rc = run_stream(c, tb, d_buf, B, 1, ccap, &K);
-      if (rc) return rc;
-      if (K <= ccap) break;
+    EW_CHECK(c->cpos.ensure(ccap * 8));
+    EW_CHECK(c->clen.ensure(ccap * 8));
+    rc = run_stream(c, tb, d_buf, B, 1, ccap, &K);
+    if (rc) return rc;
+    if (K > ccap) {   // grow and redo only the compaction (the slots stay valid)
       if (K >= 0xfffffff0ull) return EWAL_E_NOMEM;
       ccap = K + 1024;
+      EW_CHECK(c->cpos.ensure(ccap * 8));
+      EW_CHECK(c->clen.ensure(ccap * 8));
+      rc = compact_cands(c, d_buf, B, (uint32_t)(B / EW_WAVE_BYTES + 1), ccap);
+      if (rc) return rc;
     }
   }
   out->n_candidates = (int64_t)K;
@@ -278,10 +319,12 @@ static int readall_impl(ewal_ctx *c, const uint8_t *d_buf, uint64_t B, uint64_t 
     EW_CHECK(c->rd.ensure((size_t)n * sizeof(RecDesc)));
     EW_CHECK(hipMemcpyAsync(&ds->agg, &hagg, sizeof(hagg), hipMemcpyHostToDevice, c->stream));
     RecDesc *rd = c->rd.as<RecDesc>();
+    EW_CHECK(c->pf.ensure((size_t)n * 8));
     hipLaunchKernelGGL(k_decode, dim3(grid_for(n, 256)), dim3(256), 0, c->stream, d_buf, c->cpos.as<uint64_t>(),
-                       c->clen.as<uint64_t>(), c->rec_cand.as<uint32_t>(), n32, rd);
-    hipLaunchKernelGGL(k_verify, dim3(grid_for(n, 256)), dim3(256), 0, c->stream, d_buf, c->pwave.as<uint32_t>(),
-                       c->v.as<uint32_t>(), tb->slice, tb->shift, rd, n32, &ds->agg);
+                       c->clen.as<uint64_t>(), c->rec_cand.as<uint32_t>(), n32, c->pwave.as<uint32_t>(),
+                       c->v.as<uint32_t>(), tb->slice, tb->shift, rd, c->pf.as<uint32_t>());
+    hipLaunchKernelGGL(k_verify, dim3(grid_for(n, 1024)), dim3(1024), 0, c->stream, d_buf, c->pwave.as<uint32_t>(),
+                       c->v.as<uint32_t>(), tb->slice, tb->shift, rd, n32, c->pf.as<uint32_t>(), &ds->agg);
     hipLaunchKernelGGL(k_meta, dim3(grid_for(n, 256)), dim3(256), 0, c->stream, d_buf, rd, n32, &ds->agg);
     EW_CHECK(c->opf.ensure(n));
     EW_CHECK(c->ops.ensure((size_t)n * 4));
@@ -409,6 +452,8 @@ int ewal_ctx_create(int device, ewal_ctx **out) {
     c->num_cu = prop.multiProcessorCount;
   EW_CHECK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
   c->own_stream = true;
+  if (const char *e = std::getenv("EWAL_STREAM_R")) c->stream_r = std::atoi(e) == 32 ? 32 : 16;
+  if (const char *e = std::getenv("EWAL_STREAM_ABLATE")) c->ablate = std::atoi(e);
   EW_CHECK(hipEventCreate(&c->ev0));
   EW_CHECK(hipEventCreate(&c->ev1));
   EW_CHECK(hipEventCreate(&c->evs0));
@@ -423,7 +468,7 @@ void ewal_ctx_destroy(ewal_ctx *c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
   (void)hipStreamSynchronize(c->stream);
-  DevBuf *bufs[] = {&c->v, &c->pwave, &c->desc, &c->cpos, &c->clen, &c->nxt, &c->exc, &c->E, &c->rs, &c->jl,
+  DevBuf *bufs[] = {&c->pf, &c->v, &c->pwave, &c->desc, &c->wagg, &c->wcnt, &c->slots, &c->cbase, &c->ovf, &c->cpos, &c->clen, &c->nxt, &c->exc, &c->E, &c->rs, &c->jl,
                     &c->vis, &c->entry, &c->on, &c->rec_cand, &c->rd, &c->opf, &c->ops, &c->kk, &c->kkrev,
                     &c->suf, &c->ents, &c->recs, &c->tmp, &c->small, &c->sdesc, &c->snaps, &c->hbuf_dev};
   for (DevBuf *b : bufs) b->release();

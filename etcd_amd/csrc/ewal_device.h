@@ -12,6 +12,7 @@
 #define EW_TILE_LOG2 16
 #define EW_R 16                          // LDS replicas of each slicing table
 #define EW_NIL 0xFFFFFFFFu
+#define EW_SLOTS 32                      // candidate slots per 4 KiB unit
 #define EW_LDS_SHIFT0 6                  // LDS holds S_{2^6} .. S_{2^15}
 #define EW_LDS_SHIFTS 10
 
@@ -132,7 +133,7 @@ __device__ __forceinline__ int skip_simple(const uint8_t *p, int64_t l, int wt, 
   default: return 7;            // proto.ErrWrongType
   }
 }
-__device__ inline int pb_skip(const uint8_t *p, int64_t l, int64_t &out) {
+__device__ __noinline__ int pb_skip(const uint8_t *p, int64_t l, int64_t &out) {
   if (l <= 0) return 33;        // panic("unreachable")
   int64_t i = 0;
   uint64_t w;
@@ -178,78 +179,92 @@ __device__ inline int pb_skip(const uint8_t *p, int64_t l, int64_t &out) {
 }
 
 // ---- gogoprotobuf Unmarshal walker (exact Go semantics on the supported set)
-// kind[f] for field numbers 1..7: 0 unknown (proto.Skip into XXX_unrecognized,
-// sets o.unrec), PB_VAR64/PB_VAR32 (|= accumulate), PB_BYTES (append; nil
-// when empty), PB_REP64 (append to a repeated list).
+// Field kinds are compile-time template arguments (no runtime-indexed state,
+// so nothing spills to scratch): PB_NONE (unknown -> proto.Skip into
+// XXX_unrecognized, sets unrec), PB_VAR64/PB_VAR32 (|= accumulate), PB_BYTES
+// (append; nil when empty), PB_REP64 (append to a repeated list in rep[]).
 // Returns 0, 2 (io.ErrUnexpectedEOF), 7 (proto.ErrWrongType), 33 (bounds
 // panic), 37 (never terminates) or 48 (EWAL_UNSUPPORTED_ENCODING: a bytes
-// field whose repeats concatenate two non-empty segments, or a deeper group
-// nesting than the device stack).
+// field whose repeats concatenate two non-empty segments, a repeated list
+// longer than rep's capacity, or group nesting deeper than the device stack).
+#define PB_NONE 0
 #define PB_VAR64 1
 #define PB_VAR32 2
 #define PB_BYTES 3
 #define PB_REP64 4
-struct PbOut {
-  uint64_t v[8];
-  int64_t boff[8];
-  int64_t blen[8];
-  uint32_t nrep[8];
-  int unrec;
+struct PbField {
+  uint64_t v;      // varint value (OR-accumulated) / repeated count
+  int64_t boff;    // bytes field offset (-1: nil)
+  int64_t blen;
 };
-__device__ __forceinline__ void pb_init(PbOut &o) {
-#pragma unroll
-  for (int k = 0; k < 8; ++k) { o.v[k] = 0; o.boff[k] = -1; o.blen[k] = 0; o.nrep[k] = 0; }
-  o.unrec = 0;
+__device__ __forceinline__ void pbf_init(PbField &f) { f.v = 0; f.boff = -1; f.blen = 0; }
+
+template <int K>
+__device__ __forceinline__ int pb_field(const uint8_t *p, int64_t &i, int64_t l, int wt, PbField &f, uint64_t *rep,
+                                        uint32_t repcap) {
+  if (K == PB_BYTES) {
+    if (wt != 2) return 7;
+    uint64_t bl = 0;
+    if (rd_varint(p, i, l, bl, 64)) return 2;
+    int64_t post = (int64_t)((uint64_t)i + bl);
+    if (post > l) return 2;
+    if (post < i) return 33;
+    if (post > i) {
+      if (f.blen > 0) return 48;
+      f.boff = i;
+      f.blen = post - i;
+    }
+    i = post;
+    return 0;
+  } else if (K == PB_REP64) {
+    if (wt != 0) return 7;
+    uint64_t v = 0;
+    if (rd_varint(p, i, l, v, 64)) return 2;
+    if (f.v >= repcap) return 48;
+    if (rep) rep[f.v] = v;
+    f.v++;
+    return 0;
+  } else {
+    if (wt != 0) return 7;
+    return rd_varint(p, i, l, f.v, K == PB_VAR32 ? 32 : 64) ? 2 : 0;
+  }
 }
-__device__ inline int pb_walk(const uint8_t *p, int64_t l, const uint8_t *kind, PbOut &o,
-                              uint64_t *rep, uint32_t repcap) {
+
+template <int K1, int K2, int K3, int K4, int K5>
+__device__ inline int pb_walk(const uint8_t *p, int64_t l, PbField &f1, PbField &f2, PbField &f3, PbField &f4,
+                              PbField &f5, int &unrec, uint64_t *rep2, uint64_t *rep5, uint32_t repcap) {
   int64_t i = 0;
+  unrec = 0;
   while (i < l) {
     uint64_t wire = 0;
     if (rd_varint(p, i, l, wire, 64)) return 2;
-    uint32_t fn = (uint32_t)(wire >> 3);   // int32(wire >> 3)
-    int wt = (int)(wire & 7);
-    int k = (fn >= 1 && fn <= 7) ? kind[fn] : 0;
-    if (k == 0) {
-      // default: index -= sizeOfWire; Skip(data[index:]); bounds; append
-      int64_t sow = 0;
-      uint64_t w = wire;
-      do { ++sow; w >>= 7; } while (w);
-      i -= sow;
-      int64_t skippy;
-      int st = pb_skip(p + i, l - i, skippy);
-      if (st) return st;
-      int64_t hi = (int64_t)((uint64_t)i + (uint64_t)skippy);
-      if (hi > l) return 2;
-      if (hi < i) return 33;
-      if (skippy == 0) return 37;
-      o.unrec = 1;
-      i = hi;
-      continue;
+    const uint32_t fn = (uint32_t)(wire >> 3);   // int32(wire >> 3)
+    const int wt = (int)(wire & 7);
+    int st = -1;
+    switch (fn) {
+    case 1: if (K1 != PB_NONE) st = pb_field<K1>(p, i, l, wt, f1, nullptr, 0); break;
+    case 2: if (K2 != PB_NONE) st = pb_field<K2>(p, i, l, wt, f2, rep2, repcap); break;
+    case 3: if (K3 != PB_NONE) st = pb_field<K3>(p, i, l, wt, f3, nullptr, 0); break;
+    case 4: if (K4 != PB_NONE) st = pb_field<K4>(p, i, l, wt, f4, nullptr, 0); break;
+    case 5: if (K5 != PB_NONE) st = pb_field<K5>(p, i, l, wt, f5, rep5, repcap); break;
+    default: break;
     }
-    if (k == PB_BYTES) {
-      if (wt != 2) return 7;
-      uint64_t bl = 0;
-      if (rd_varint(p, i, l, bl, 64)) return 2;
-      int64_t post = (int64_t)((uint64_t)i + bl);
-      if (post > l) return 2;
-      if (post < i) return 33;
-      if (post > i) {
-        if (o.blen[fn] > 0) return 48;
-        o.boff[fn] = i;
-        o.blen[fn] = post - i;
-      }
-      i = post;
-    } else if (k == PB_REP64) {
-      if (wt != 0) return 7;
-      uint64_t v = 0;
-      if (rd_varint(p, i, l, v, 64)) return 2;
-      if (o.nrep[fn] >= repcap) return 48;
-      rep[(fn == 2 ? 0 : repcap) + o.nrep[fn]++] = v;
-    } else {
-      if (wt != 0) return 7;
-      if (rd_varint(p, i, l, o.v[fn], k == PB_VAR32 ? 32 : 64)) return 2;
-    }
+    if (st > 0) return st;
+    if (st == 0) continue;
+    // default: index -= sizeOfWire; Skip(data[index:]); bounds; append
+    int64_t sow = 0;
+    uint64_t w = wire;
+    do { ++sow; w >>= 7; } while (w);
+    i -= sow;
+    int64_t skippy;
+    st = pb_skip(p + i, l - i, skippy);
+    if (st) return st;
+    int64_t hi = (int64_t)((uint64_t)i + (uint64_t)skippy);
+    if (hi > l) return 2;
+    if (hi < i) return 33;
+    if (skippy == 0) return 37;
+    unrec = 1;
+    i = hi;
   }
   return 0;
 }

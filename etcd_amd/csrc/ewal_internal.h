@@ -8,18 +8,26 @@ struct TileDesc;
 struct StreamArgs {
   const uint8_t *buf;      // WAL bytes (device, 16-B aligned)
   uint64_t B;              // byte count
-  uint32_t ntiles;         // ceil(B / EW_TILE)
+  uint32_t nunits;         // B / 4096 + 1 (P is read at x == B)
   int find_cand;           // 1: WAL framing candidates, 0: CRC prefixes only
+  int ablate;              // timing-only ablations (EWAL_STREAM_ABLATE): 1 no CRC, 2 no candidates
   const uint32_t *g_slice; // [4][256]
   const uint32_t *g_shift; // [48][4][256]
-  uint32_t *v;             // lin of every 64-B piece        [ntiles*1024]
-  uint32_t *pwave;         // stream prefix at every 4 KiB    [ntiles*16]
-  uint64_t *cpos;          // candidate frame offsets (sorted)
-  uint64_t *clen;          // candidate frame lengths (int64 prefix)
-  uint64_t ccap;
-  TileDesc *desc;          // [ntiles], zeroed per launch
-  uint32_t *ticket;        // zeroed per launch
-  uint32_t *errflag;
+  uint32_t *v;             // lin of every 64-B piece        [nunits*64]
+  uint32_t *wagg;          // lin of every 4 KiB unit        [nunits]
+  uint32_t *wcnt;          // candidates in the unit         [nunits]
+  uint16_t *slots;         // first EW_SLOTS candidate offsets per unit
+};
+
+struct ScanArgs {
+  uint32_t nunits, ntiles;        // ntiles = ceil(nunits / 1024)
+  const uint32_t *wagg, *wcnt;
+  const uint32_t *g_shift;
+  uint32_t *pwave;                // stream prefix at every unit start
+  unsigned long long *cbase;      // candidates before every unit
+  TileDesc *desc;                 // [ntiles], zeroed per launch
+  uint32_t *ticket, *errflag;
+  unsigned long long *total;      // all candidates
 };
 
 // Per-frame descriptor (device), 96 B.

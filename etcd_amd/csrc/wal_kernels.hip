@@ -29,10 +29,11 @@
 // ===========================================================================
 // k_stream
 // ===========================================================================
+template <int R>
 __device__ __forceinline__ uint32_t lds_step4(const uint32_t *s, int cl, uint32_t c) {
-  // s[(t*256 + b) * EW_R + cl]
-  return s[((3 * 256 + (c & 0xff)) * EW_R) + cl] ^ s[((2 * 256 + ((c >> 8) & 0xff)) * EW_R) + cl] ^
-         s[((1 * 256 + ((c >> 16) & 0xff)) * EW_R) + cl] ^ s[((0 * 256 + (c >> 24)) * EW_R) + cl];
+  // s[(t*256 + b) * R + cl]
+  return s[((3 * 256 + (c & 0xff)) * R) + cl] ^ s[((2 * 256 + ((c >> 8) & 0xff)) * R) + cl] ^
+         s[((1 * 256 + ((c >> 16) & 0xff)) * R) + cl] ^ s[((0 * 256 + (c >> 24)) * R) + cl];
 }
 __device__ __forceinline__ uint32_t lds_shift(const uint32_t *s, int m, uint32_t x) {
   return tab_apply(s + (m - EW_LDS_SHIFT0) * 1024, x);
@@ -79,6 +80,7 @@ __device__ __forceinline__ uint32_t count_cands(const uint32_t (&D)[19], uint64_
   return cnt;
 }
 
+// dense write of a lane's candidates (k_rescan: overflow units)
 __device__ __forceinline__ void write_cands(const uint32_t (&D)[19], uint64_t off, uint64_t B, uint64_t base,
                                             uint64_t *cpos, uint64_t *clen, uint64_t ccap) {
   uint64_t w = base;
@@ -90,10 +92,56 @@ __device__ __forceinline__ void write_cands(const uint32_t (&D)[19], uint64_t of
 #undef CAND_ACTION
 }
 
-// Decoupled look-back (Merrill & Garland) over 64 predecessors per step.
-// Returns (X, N): the stream prefix lin(stream[0 .. t*TILE)) and the number
-// of candidates before tile t; publishes tile t's inclusive values.
-__device__ __forceinline__ void lookback(TileDesc *desc, uint32_t t, uint32_t agg, uint32_t cnt,
+// slot write of a lane's candidates as 12-bit offsets inside the 4 KiB unit
+__device__ __forceinline__ void slot_cands(const uint32_t (&D)[19], uint64_t off, uint64_t B, uint32_t base,
+                                           uint16_t *slots, uint32_t unit_off) {
+  uint32_t w = base;
+#define CAND_ACTION                                                           \
+  if (w < EW_SLOTS) slots[w] = (uint16_t)(unit_off + (uint32_t)(p_ - off));   \
+  ++w
+  CAND_TEST(0) CAND_TEST(1) CAND_TEST(2) CAND_TEST(3) CAND_TEST(4) CAND_TEST(5) CAND_TEST(6) CAND_TEST(7)
+  CAND_TEST(8) CAND_TEST(9) CAND_TEST(10) CAND_TEST(11) CAND_TEST(12) CAND_TEST(13) CAND_TEST(14) CAND_TEST(15)
+#undef CAND_ACTION
+}
+
+typedef uint32_t ew_v4u __attribute__((ext_vector_type(4)));
+// The WAL stream is read exactly once: nontemporal loads (measured 7.0 vs
+// 6.1-6.3 TB/s for the plain forms of the same read pattern, tools/membw.hip).
+__device__ __forceinline__ void load_piece(const uint8_t *buf, uint64_t B, uint64_t off, uint32_t (&D)[19]) {
+  if (off + EW_PIECE <= B) {
+    const ew_v4u *p = (const ew_v4u *)(buf + off);
+    ew_v4u q0 = __builtin_nontemporal_load(p), q1 = __builtin_nontemporal_load(p + 1),
+           q2 = __builtin_nontemporal_load(p + 2), q3 = __builtin_nontemporal_load(p + 3);
+    D[0] = q0.x; D[1] = q0.y; D[2] = q0.z; D[3] = q0.w;
+    D[4] = q1.x; D[5] = q1.y; D[6] = q1.z; D[7] = q1.w;
+    D[8] = q2.x; D[9] = q2.y; D[10] = q2.z; D[11] = q2.w;
+    D[12] = q3.x; D[13] = q3.y; D[14] = q3.z; D[15] = q3.w;
+  } else {
+#pragma unroll
+    for (int k = 0; k < 16; ++k) D[k] = (off < B) ? load_word_guarded(buf, B, off + 4 * k) : 0u;
+  }
+}
+
+// the 12 bytes after a lane's piece: the next lane's first dwords, or for
+// lane 63 a direct load of the following unit
+__device__ __forceinline__ void load_next3(const uint8_t *buf, uint64_t B, uint64_t off, uint32_t (&D)[19]) {
+  const int lane = threadIdx.x & 63;
+  D[16] = __shfl_down(D[0], 1);
+  D[17] = __shfl_down(D[1], 1);
+  D[18] = __shfl_down(D[2], 1);
+  if (lane == 63) {
+    const uint64_t o = off + EW_PIECE;
+    D[16] = load_word_guarded(buf, B, o);
+    D[17] = load_word_guarded(buf, B, o + 4);
+    D[18] = load_word_guarded(buf, B, o + 8);
+  }
+}
+
+// Decoupled look-back (Merrill & Garland) over 64 predecessors per step, for
+// tiles of 2^tile_log2 bytes.  Returns (X, N): the stream prefix
+// lin(stream[0 .. t*TILE)) and the candidate count before tile t, and
+// publishes tile t's inclusive values.  Called by one whole wave.
+__device__ __forceinline__ void lookback(TileDesc *desc, uint32_t t, uint32_t agg, uint32_t cnt, int tile_log2,
                                          const uint32_t *g_shift, uint32_t &X, unsigned long long &N,
                                          uint32_t *errflag) {
   const int lane = threadIdx.x & 63;
@@ -127,11 +175,11 @@ __device__ __forceinline__ void lookback(TileDesc *desc, uint32_t t, uint32_t ag
         uint32_t term = 0;
         unsigned long long tn = 0;
         if (lane < f2) {
-          term = gshift_n(g_shift, (acc_tiles + lane) << EW_TILE_LOG2, (uint32_t)ag);
+          term = gshift_n(g_shift, (acc_tiles + lane) << tile_log2, (uint32_t)ag);
           tn = (ag >> 32) & 0x7fffffffull;
         } else if (lane == f2 && idx >= 0) {
           tn = ld_agent(&desc[idx].inc_cnt);
-          term = gshift_n(g_shift, (acc_tiles + lane) << EW_TILE_LOG2, (uint32_t)inc);
+          term = gshift_n(g_shift, (acc_tiles + lane) << tile_log2, (uint32_t)inc);
         }
         accx ^= wave_xor(term);
         accn += wave_sum64(tn);
@@ -145,7 +193,7 @@ __device__ __forceinline__ void lookback(TileDesc *desc, uint32_t t, uint32_t ag
         __builtin_amdgcn_s_sleep(1);
         continue;
       }
-      uint32_t term = gshift_n(g_shift, (acc_tiles + lane) << EW_TILE_LOG2, (uint32_t)ag);
+      uint32_t term = gshift_n(g_shift, (acc_tiles + lane) << tile_log2, (uint32_t)ag);
       accx ^= wave_xor(term);
       accn += wave_sum64((ag >> 32) & 0x7fffffffull);
       acc_tiles += 64;
@@ -155,117 +203,194 @@ __device__ __forceinline__ void lookback(TileDesc *desc, uint32_t t, uint32_t ag
   X = accx;
   N = accn;
   if (lane == 0) {
-    uint32_t I = gshift_pow2(g_shift, EW_TILE_LOG2, accx) ^ agg;
+    uint32_t I = gshift_pow2(g_shift, tile_log2, accx) ^ agg;
     st_agent(&desc[t].inc_cnt, accn + cnt);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     st_agent(&desc[t].inc, EW_DESC_VALID | (unsigned long long)I);
   }
 }
 
+// One HBM pass, no inter-workgroup communication.  Every wave owns 4 KiB
+// units (grid-stride), 64 B per lane: lin(piece) -> v[], frame-start
+// candidates -> up to EW_SLOTS 12-bit offsets per unit, and the unit's
+// aggregate (lin over 4 KiB, candidate count) -> wagg[], wcnt[].  The next
+// unit's bytes are loaded while the current one is processed.
+template <int R>
 __global__ __launch_bounds__(EW_THREADS, 1) void k_stream(StreamArgs a) {
-  __shared__ uint32_t s_slice[4 * 256 * EW_R];        // 64 KiB, replicated slicing tables
-  __shared__ uint32_t s_shift[EW_LDS_SHIFTS * 1024];  // 40 KiB, S_{2^6}..S_{2^15}
-  __shared__ uint32_t s_wagg[EW_WAVES];
-  __shared__ uint32_t s_wcnt[EW_WAVES];
-  __shared__ unsigned long long s_wbase[EW_WAVES];
-  __shared__ uint32_t s_tile;
-
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  for (int i = tid; i < 4 * 256 * EW_R; i += EW_THREADS) s_slice[i] = a.g_slice[i / EW_R];
-  for (int i = tid; i < EW_LDS_SHIFTS * 1024; i += EW_THREADS) s_shift[i] = a.g_shift[EW_LDS_SHIFT0 * 1024 + i];
-  const int cl = lane & (EW_R - 1);
+  __shared__ uint32_t s_slice[4 * 256 * R];     // replicated slicing tables (R copies, lane % R)
+  __shared__ uint32_t s_shift[6 * 1024];        // 24 KiB, S_{2^6}..S_{2^11}
+  const int tid = threadIdx.x, lane = tid & 63;
+  for (int i = tid; i < 4 * 256 * R; i += EW_THREADS) s_slice[i] = a.g_slice[i / R];
+  for (int i = tid; i < 6 * 1024; i += EW_THREADS) s_shift[i] = a.g_shift[EW_LDS_SHIFT0 * 1024 + i];
+  __syncthreads();
+  const int cl = lane & (R - 1);
   const uint64_t B = a.B;
+  const uint32_t W = gridDim.x * EW_WAVES;
+  uint32_t u = blockIdx.x * EW_WAVES + (tid >> 6);
+  uint32_t D[19], Nx[19];
+  if (u < a.nunits) load_piece(a.buf, B, (uint64_t)u * EW_WAVE_BYTES + lane * EW_PIECE, D);
+  for (; u < a.nunits; u += W) {
+    const uint64_t off = (uint64_t)u * EW_WAVE_BYTES + (uint64_t)lane * EW_PIECE;
+    const uint32_t un = u + W;
+    if (un < a.nunits) load_piece(a.buf, B, (uint64_t)un * EW_WAVE_BYTES + lane * EW_PIECE, Nx);
 
-  for (;;) {
-    __syncthreads();
-    if (tid == 0) s_tile = atomicAdd(a.ticket, 1u);
-    __syncthreads();
-    const uint32_t t = s_tile;
-    if (t >= a.ntiles) break;
-
-    const uint64_t off = (uint64_t)t * EW_TILE + (uint64_t)wv * EW_WAVE_BYTES + (uint64_t)lane * EW_PIECE;
-    uint32_t D[19];
-    if (off + EW_PIECE <= B) {
-      const uint4 *p = (const uint4 *)(a.buf + off);
-      uint4 q0 = p[0], q1 = p[1], q2 = p[2], q3 = p[3];
-      D[0] = q0.x; D[1] = q0.y; D[2] = q0.z; D[3] = q0.w;
-      D[4] = q1.x; D[5] = q1.y; D[6] = q1.z; D[7] = q1.w;
-      D[8] = q2.x; D[9] = q2.y; D[10] = q2.z; D[11] = q2.w;
-      D[12] = q3.x; D[13] = q3.y; D[14] = q3.z; D[15] = q3.w;
-    } else {
-#pragma unroll
-      for (int k = 0; k < 16; ++k) D[k] = (off < B) ? load_word_guarded(a.buf, B, off + 4 * k) : 0u;
-    }
-
-    // lin(piece) with conflict-light replicated slicing tables
     uint32_t c = 0;
+    if (!(a.ablate & 1)) {
 #pragma unroll
-    for (int k = 0; k < 16; ++k) c = lds_step4(s_slice, cl, c ^ D[k]);
-    a.v[(uint64_t)t * EW_THREADS + tid] = c;
+      for (int k = 0; k < 16; ++k) c = lds_step4<R>(s_slice, cl, c ^ D[k]);
+    } else {   // timing-only build path: keep the loads live, skip the CRC
+#pragma unroll
+      for (int k = 0; k < 16; ++k) c ^= D[k];
+    }
+    __builtin_nontemporal_store(c, a.v + (uint64_t)u * 64 + lane);
 
     uint32_t cnt = 0;
-    if (a.find_cand) {
-      D[16] = __shfl_down(D[0], 1);
-      D[17] = __shfl_down(D[1], 1);
-      D[18] = __shfl_down(D[2], 1);
-      if (lane == 63) {
-        const uint64_t o = off + EW_PIECE;
-        D[16] = load_word_guarded(a.buf, B, o);
-        D[17] = load_word_guarded(a.buf, B, o + 4);
-        D[18] = load_word_guarded(a.buf, B, o + 8);
-      }
+    if (a.find_cand && !(a.ablate & 2)) {
+      load_next3(a.buf, B, off, D);
       if (off < B) cnt = count_cands(D, off, B);
     }
-
-    // wave reduction of the affine CRC: lane 0 ends with lin(wave's 4 KiB)
+    // wave reduction of the affine CRC: lane 0 ends with lin(4 KiB)
     uint32_t r = c;
 #pragma unroll
     for (int d = 0; d < 6; ++d) {
       uint32_t o = __shfl_down(r, 1 << d);
       if ((lane & ((2 << d) - 1)) == 0) r = lds_shift(s_shift, EW_LDS_SHIFT0 + d, r) ^ o;
     }
-    // wave inclusive scan of candidate counts
+    uint32_t ci = cnt;
+    if (a.find_cand && __ballot(cnt != 0)) {   // wave-uniform: most 4 KiB units hold no frame start
+#pragma unroll
+      for (int d = 0; d < 6; ++d) {
+        uint32_t o = __shfl_up(ci, 1 << d);
+        if (lane >= (1 << d)) ci += o;
+      }
+      if (cnt) slot_cands(D, off, B, ci - cnt, a.slots + (size_t)u * EW_SLOTS, (uint32_t)(lane * EW_PIECE));
+    }
+    if (lane == 0) a.wagg[u] = r;
+    if (lane == 63) a.wcnt[u] = ci;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) D[k] = Nx[k];
+  }
+}
+
+// Scan of the unit aggregates: 1024 units (4 MiB of stream) per workgroup,
+// wave shuffles + one look-back per workgroup.  Writes pwave[u] = P at the
+// unit's start and cbase[u] = candidates before the unit.
+__global__ __launch_bounds__(1024, 1) void k_uscan(ScanArgs a) {
+  __shared__ uint32_t s_shift[10 * 1024];   // S_{2^12} .. S_{2^21}
+  __shared__ uint32_t s_wq[16], s_wc[16], s_base[16];
+  __shared__ unsigned long long s_cb[16];
+  __shared__ uint32_t s_tile;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  for (int i = tid; i < 10 * 1024; i += 1024) s_shift[i] = a.g_shift[12 * 1024 + i];
+  if (tid == 0) s_tile = atomicAdd(a.ticket, 1u);
+  __syncthreads();
+  const uint32_t t = s_tile;
+  const uint32_t u = t * 1024 + tid;
+  const uint32_t x = u < a.nunits ? a.wagg[u] : 0u;
+  const uint32_t cx = u < a.nunits ? a.wcnt[u] : 0u;
+  // inclusive wave scan (units of 4 KiB -> shift 2^(12+d))
+  uint32_t q = x, qc = cx;
+#pragma unroll
+  for (int d = 0; d < 6; ++d) {
+    uint32_t o = __shfl_up(q, 1 << d);
+    uint32_t oc = __shfl_up(qc, 1 << d);
+    if (lane >= (1 << d)) {
+      q = tab_apply(s_shift + d * 1024, o) ^ q;
+      qc += oc;
+    }
+  }
+  uint32_t ex = __shfl_up(q, 1), exc = __shfl_up(qc, 1);
+  if (lane == 0) { ex = 0; exc = 0; }
+  if (lane == 63) { s_wq[wv] = q; s_wc[wv] = qc; }
+  __syncthreads();
+  if (wv == 0) {
+    uint32_t w = lane < 16 ? s_wq[lane] : 0u, wc = lane < 16 ? s_wc[lane] : 0u;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      uint32_t o = __shfl_up(w, 1 << d), oc = __shfl_up(wc, 1 << d);
+      if (lane >= (1 << d) && lane < 16) {
+        w = tab_apply(s_shift + (6 + d) * 1024, o) ^ w;   // waves of 256 KiB -> 2^(18+d)
+        wc += oc;
+      }
+    }
+    const uint32_t tagg = __shfl(w, 15), tcnt = __shfl(wc, 15);
+    uint32_t we = __shfl_up(w, 1), wce = __shfl_up(wc, 1);
+    if (lane == 0) { we = 0; wce = 0; }
+    uint32_t X;
+    unsigned long long N;
+    lookback(a.desc, t, tagg, tcnt, 22, a.g_shift, X, N, a.errflag);
+    if (lane < 16) {
+      uint32_t xs = X;                         // S_{lane * 2^18}(X)
+#pragma unroll
+      for (int b = 0; b < 4; ++b)
+        if ((lane >> b) & 1) xs = tab_apply(s_shift + (6 + b) * 1024, xs);
+      s_base[lane] = xs ^ we;
+      s_cb[lane] = N + wce;
+    }
+    if (lane == 0 && t == a.ntiles - 1) *a.total = N + tcnt;
+  }
+  __syncthreads();
+  if (u < a.nunits) {
+    uint32_t b = s_base[wv];                   // S_{lane * 4096}(base)
+#pragma unroll
+    for (int k = 0; k < 6; ++k)
+      if ((lane >> k) & 1) b = tab_apply(s_shift + k * 1024, b);
+    a.pwave[u] = b ^ ex;
+    a.cbase[u] = s_cb[wv] + exc;
+  }
+}
+
+__device__ __forceinline__ uint64_t ld_le64(const uint8_t *p) {
+  uint64_t v = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) v |= (uint64_t)p[i] << (8 * i);
+  return v;
+}
+
+// slots -> the dense, position-sorted candidate list
+__global__ void k_compact(const uint8_t *__restrict__ buf, uint32_t nunits, const uint32_t *__restrict__ wcnt,
+                          const unsigned long long *__restrict__ cbase, const uint16_t *__restrict__ slots,
+                          uint64_t *__restrict__ cpos, uint64_t *__restrict__ clen, uint64_t ccap,
+                          uint32_t *__restrict__ ovf, uint32_t *novf) {
+  const uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
+  if (u >= nunits) return;
+  const uint32_t cnt = wcnt[u];
+  if (cnt == 0) return;
+  if (cnt > EW_SLOTS) {
+    ovf[atomicAdd(novf, 1u)] = u;
+    return;
+  }
+  const unsigned long long base = cbase[u];
+  for (uint32_t j = 0; j < cnt; ++j) {
+    const uint64_t p = (uint64_t)u * EW_WAVE_BYTES + slots[(size_t)u * EW_SLOTS + j];
+    if (base + j < ccap) {
+      cpos[base + j] = p;
+      clen[base + j] = ld_le64(buf + p);
+    }
+  }
+}
+
+// units with more than EW_SLOTS candidates: one wave re-derives them
+__global__ void k_rescan(const uint8_t *__restrict__ buf, uint64_t B, const uint32_t *__restrict__ ovf,
+                         const uint32_t *novf, const unsigned long long *__restrict__ cbase,
+                         uint64_t *__restrict__ cpos, uint64_t *__restrict__ clen, uint64_t ccap) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t n = *novf;
+  const uint32_t W = gridDim.x * (blockDim.x >> 6);
+  for (uint32_t i = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); i < n; i += W) {
+    const uint32_t u = ovf[i];
+    const uint64_t off = (uint64_t)u * EW_WAVE_BYTES + (uint64_t)lane * EW_PIECE;
+    uint32_t D[19];
+    load_piece(buf, B, off, D);
+    load_next3(buf, B, off, D);
+    const uint32_t cnt = off < B ? count_cands(D, off, B) : 0u;
     uint32_t ci = cnt;
 #pragma unroll
     for (int d = 0; d < 6; ++d) {
       uint32_t o = __shfl_up(ci, 1 << d);
       if (lane >= (1 << d)) ci += o;
     }
-    if (lane == 0) s_wagg[wv] = r;
-    if (lane == 63) s_wcnt[wv] = ci;
-    __syncthreads();
-
-    if (wv == 0) {
-      uint32_t q = lane < EW_WAVES ? s_wagg[lane] : 0u;
-      uint32_t qc = lane < EW_WAVES ? s_wcnt[lane] : 0u;
-#pragma unroll
-      for (int d = 0; d < 4; ++d) {
-        uint32_t o = __shfl_up(q, 1 << d);
-        uint32_t oc = __shfl_up(qc, 1 << d);
-        if (lane >= (1 << d) && lane < EW_WAVES) {
-          q = lds_shift(s_shift, 12 + d, o) ^ q;
-          qc += oc;
-        }
-      }
-      const uint32_t tagg = __shfl(q, EW_WAVES - 1);
-      const uint32_t tcnt = __shfl(qc, EW_WAVES - 1);
-      uint32_t ex = __shfl_up(q, 1);
-      uint32_t exc = __shfl_up(qc, 1);
-      if (lane == 0) { ex = 0; exc = 0; }
-      uint32_t X;
-      unsigned long long N;
-      lookback(a.desc, t, tagg, tcnt, a.g_shift, X, N, a.errflag);
-      if (lane < EW_WAVES) {
-        uint32_t xs = X;
-#pragma unroll
-        for (int b = 0; b < 4; ++b)
-          if ((lane >> b) & 1) xs = lds_shift(s_shift, 12 + b, xs);
-        a.pwave[(uint64_t)t * EW_WAVES + lane] = xs ^ ex;
-        s_wbase[lane] = N + exc;
-      }
-    }
-    __syncthreads();
-    if (cnt) write_cands(D, off, B, s_wbase[wv] + (ci - cnt), a.cpos, a.clen, a.ccap);
+    if (cnt) write_cands(D, off, B, cbase[u] + (ci - cnt), cpos, clen, ccap);
   }
 }
 
@@ -353,15 +478,80 @@ __global__ void k_member(const uint32_t *__restrict__ E, uint32_t R, const uint8
 }
 
 // ===========================================================================
-// per-frame decode (walpb.Record, raftpb.Entry, raftpb.HardState)
+// per-frame decode (walpb.Record, raftpb.Entry, raftpb.HardState) + verify
 // ===========================================================================
-__constant__ uint8_t c_kind_record[8] = {0, PB_VAR64, PB_VAR32, PB_BYTES, 0, 0, 0, 0};
-__constant__ uint8_t c_kind_entry[8] = {0, PB_VAR32, PB_VAR64, PB_VAR64, PB_BYTES, 0, 0, 0};
-__constant__ uint8_t c_kind_state[8] = {0, PB_VAR64, PB_VAR64, PB_VAR64, 0, 0, 0, 0};
 
-__global__ void k_decode(const uint8_t *__restrict__ buf, const uint64_t *__restrict__ pos,
+// Stream prefix P(x) = lin(stream[0..x)) from the per-unit prefix and the
+// per-piece lins of k_stream.  Every load is issued up front (the unit's 64
+// piece lins, 256 B, and the 64-B piece holding x) so the dependent chain
+// that follows runs out of registers: Horner over the whole pieces before x,
+// then slicing-by-4 / byte steps over the bytes of x's piece before x.
+__device__ __forceinline__ uint32_t prefix_at(uint64_t x, const uint32_t *__restrict__ pwave,
+                                              const uint32_t *__restrict__ v, const uint8_t *__restrict__ buf,
+                                              const uint32_t *t4, const uint32_t *s64) {
+  const uint64_t w = x >> 12;
+  const uint64_t x0 = x & ~(uint64_t)(EW_PIECE - 1);
+  const uint32_t k = (uint32_t)((x0 >> 6) & 63);
+  const uint32_t tail = (uint32_t)(x - x0);
+  const uint4 *vq = (const uint4 *)(v + (w << 6));
+  uint4 vv[16];
+#pragma unroll
+  for (int q = 0; q < 16; ++q) vv[q] = (4u * q < k) ? vq[q] : make_uint4(0, 0, 0, 0);
+  uint4 dd[4];
+  const uint4 *dq = (const uint4 *)(buf + x0);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) dd[q] = (16u * q < tail) ? dq[q] : make_uint4(0, 0, 0, 0);
+  uint32_t acc = pwave[w];
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    if (4u * q + 0 < k) acc = tab_apply(s64, acc) ^ vv[q].x;
+    if (4u * q + 1 < k) acc = tab_apply(s64, acc) ^ vv[q].y;
+    if (4u * q + 2 < k) acc = tab_apply(s64, acc) ^ vv[q].z;
+    if (4u * q + 3 < k) acc = tab_apply(s64, acc) ^ vv[q].w;
+  }
+  const uint32_t nd = tail >> 2;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    if (4u * q + 0 < nd) acc = step4_flat(t4, acc ^ dd[q].x);
+    if (4u * q + 1 < nd) acc = step4_flat(t4, acc ^ dd[q].y);
+    if (4u * q + 2 < nd) acc = step4_flat(t4, acc ^ dd[q].z);
+    if (4u * q + 3 < nd) acc = step4_flat(t4, acc ^ dd[q].w);
+  }
+  // remaining 0..3 bytes live in dword nd
+  const uint32_t rem = tail & 3;
+  if (rem) {
+    uint32_t wd = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      if ((nd >> 2) == (uint32_t)q) {
+        const uint32_t s = nd & 3;
+        wd = s == 0 ? dd[q].x : s == 1 ? dd[q].y : s == 2 ? dd[q].z : dd[q].w;
+      }
+    }
+    for (uint32_t b = 0; b < rem; ++b) {
+      acc = t4[(acc ^ wd) & 0xff] ^ (acc >> 8);
+      wd >>= 8;
+    }
+  }
+  return acc;
+}
+
+// k_decode: parse frame r, and P at its frame start and data start:
+//   Pd[r] = P(doff) = raw(P(off), frame header bytes)
+// plus, for the last frame, P at its data end (the frame after it is not on
+// the chain).
+__global__ __launch_bounds__(256) void k_decode(const uint8_t *__restrict__ buf, const uint64_t *__restrict__ pos,
                          const uint64_t *__restrict__ len, const uint32_t *__restrict__ rec_cand, uint32_t n,
-                         RecDesc *__restrict__ rd) {
+                         const uint32_t *__restrict__ pwave, const uint32_t *__restrict__ v,
+                         const uint32_t *__restrict__ g_slice, const uint32_t *__restrict__ g_shift,
+                         RecDesc *__restrict__ rd, uint32_t *__restrict__ pf) {
+  __shared__ uint32_t s_t4[1024];
+  __shared__ uint32_t s_s64[1024];
+  for (int i = threadIdx.x; i < 1024; i += blockDim.x) {
+    s_t4[i] = g_slice[i];
+    s_s64[i] = g_shift[6 * 1024 + i];
+  }
+  __syncthreads();
   uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= n) return;
   const uint32_t i = rec_cand[r];
@@ -372,61 +562,60 @@ __global__ void k_decode(const uint8_t *__restrict__ buf, const uint64_t *__rest
   d.type = 0; d.crc = 0; d.chained = 0; d.st = 0; d.sub_st = 0;
   d.doff = p + 8; d.dlen = 0; d.dnil = 1;
   d.f0 = d.f1 = d.f2 = 0; d.edoff = 0; d.edlen = 0; d.enil = 1; d.etype = 0;
-  PbOut o;
-  pb_init(o);
-  int st = pb_walk(buf + p + 8, L, c_kind_record, o, nullptr, 0);
-  d.type = (int64_t)o.v[1];
-  d.crc = (uint32_t)o.v[2];
-  if (o.blen[3] > 0) { d.doff = p + 8 + o.boff[3]; d.dlen = o.blen[3]; d.dnil = 0; }
+  PbField a1, a2, a3, a4, a5;
+  pbf_init(a1); pbf_init(a2); pbf_init(a3); pbf_init(a4); pbf_init(a5);
+  int unrec;
+  int st = pb_walk<PB_VAR64, PB_VAR32, PB_BYTES, PB_NONE, PB_NONE>(buf + p + 8, L, a1, a2, a3, a4, a5, unrec,
+                                                                     nullptr, nullptr, 0);
+  d.type = (int64_t)a1.v;
+  d.crc = (uint32_t)a2.v;
+  if (a3.blen > 0) { d.doff = p + 8 + a3.boff; d.dlen = a3.blen; d.dnil = 0; }
   d.st = st;
   if (st == 0) {
     const uint8_t *dp = buf + d.doff;
     if (d.type == 2) {           // entryType: mustUnmarshalEntry
-      PbOut e;
-      pb_init(e);
-      int s2 = d.dnil ? 0 : pb_walk(dp, (int64_t)d.dlen, c_kind_entry, e, nullptr, 0);
-      if (s2 == 0 && e.unrec) s2 = 48;   // Entry.XXX_unrecognized is returned by ReadAll
+      PbField e1, e2, e3, e4, e5;
+      pbf_init(e1); pbf_init(e2); pbf_init(e3); pbf_init(e4); pbf_init(e5);
+      int s2 = 0, ur = 0;
+      if (!d.dnil)
+        s2 = pb_walk<PB_VAR32, PB_VAR64, PB_VAR64, PB_BYTES, PB_NONE>(dp, (int64_t)d.dlen, e1, e2, e3, e4, e5, ur,
+                                                                       nullptr, nullptr, 0);
+      if (s2 == 0 && ur) s2 = 48;   // Entry.XXX_unrecognized is returned by ReadAll
       d.sub_st = s2;
-      d.etype = (int32_t)(uint32_t)e.v[1];
-      d.f0 = e.v[2];            // Term
-      d.f1 = e.v[3];            // Index
-      if (e.blen[4] > 0) { d.edoff = d.doff + e.boff[4]; d.edlen = e.blen[4]; d.enil = 0; }
+      d.etype = (int32_t)(uint32_t)e1.v;
+      d.f0 = e2.v;                  // Term
+      d.f1 = e3.v;                  // Index
+      if (e4.blen > 0) { d.edoff = d.doff + e4.boff; d.edlen = e4.blen; d.enil = 0; }
     } else if (d.type == 3) {    // stateType: mustUnmarshalState
-      PbOut h;
-      pb_init(h);
-      int s2 = d.dnil ? 0 : pb_walk(dp, (int64_t)d.dlen, c_kind_state, h, nullptr, 0);
-      if (s2 == 0 && h.unrec) s2 = 48;   // HardState.XXX_unrecognized is returned
+      PbField h1, h2, h3, h4, h5;
+      pbf_init(h1); pbf_init(h2); pbf_init(h3); pbf_init(h4); pbf_init(h5);
+      int s2 = 0, ur = 0;
+      if (!d.dnil)
+        s2 = pb_walk<PB_VAR64, PB_VAR64, PB_VAR64, PB_NONE, PB_NONE>(dp, (int64_t)d.dlen, h1, h2, h3, h4, h5, ur,
+                                                                      nullptr, nullptr, 0);
+      if (s2 == 0 && ur) s2 = 48;   // HardState.XXX_unrecognized is returned
       d.sub_st = s2;
-      d.f0 = h.v[1]; d.f1 = h.v[2]; d.f2 = h.v[3];
+      d.f0 = h1.v; d.f1 = h2.v; d.f2 = h3.v;
     }
+  }
+  // P at every frame start (the previous frame's data end, in the canonical
+  // layout), and P at this frame's data start from it (header bytes only).
+  const uint32_t Pfo = prefix_at(p, pwave, v, buf, s_t4, s_s64);
+  pf[n + r] = Pfo;
+  if (st == 0 && d.type != 4 && d.dlen > 0) {
+    pf[r] = raw_bytes(s_t4, Pfo, buf, p, d.doff);
+    if (r == n - 1 || d.doff + d.dlen != p + 8 + (uint64_t)L)
+      d.chained = prefix_at(d.doff + d.dlen, pwave, v, buf, s_t4, s_s64);   // P(data end), used by k_verify
   }
   rd[r] = d;
 }
 
-// Stream prefix P(x) = lin(stream[0..x)) from the per-wave prefixes and the
-// per-piece lin values of k_stream.
-__device__ __forceinline__ uint32_t prefix_at(uint64_t x, const uint32_t *__restrict__ pwave,
-                                              const uint32_t *__restrict__ v, const uint8_t *__restrict__ buf,
-                                              const uint32_t *t4, const uint32_t *s64) {
-  const uint64_t w = x >> 12;
-  uint32_t acc = pwave[w];
-  const uint64_t x0 = x & ~(uint64_t)(EW_PIECE - 1);
-  const uint32_t k = (uint32_t)((x0 >> 6) & 63);
-  const uint32_t *vp = v + (w << 6);
-  for (uint32_t j = 0; j < k; ++j) acc = tab_apply(s64, acc) ^ vp[j];
-  return raw_bytes(t4, acc, buf, x0, x);
-}
-
-__global__ void k_verify(const uint8_t *__restrict__ buf, const uint32_t *__restrict__ pwave,
+__global__ __launch_bounds__(1024) void k_verify(const uint8_t *__restrict__ buf, const uint32_t *__restrict__ pwave,
                          const uint32_t *__restrict__ v, const uint32_t *__restrict__ g_slice,
                          const uint32_t *__restrict__ g_shift, RecDesc *__restrict__ rd, uint32_t n,
-                         ReadAllAgg *agg) {
-  __shared__ uint32_t s_t4[1024];
-  __shared__ uint32_t s_s64[1024];
-  for (int i = threadIdx.x; i < 1024; i += blockDim.x) {
-    s_t4[i] = g_slice[i];
-    s_s64[i] = g_shift[6 * 1024 + i];
-  }
+                         const uint32_t *__restrict__ pf, ReadAllAgg *agg) {
+  __shared__ uint32_t s_sh[17 * 1024];   // S_{2^0} .. S_{2^16}
+  for (int i = threadIdx.x; i < 17 * 1024; i += blockDim.x) s_sh[i] = g_shift[i];
   __syncthreads();
   uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= n) return;
@@ -439,14 +628,20 @@ __global__ void k_verify(const uint8_t *__restrict__ buf, const uint32_t *__rest
       if (seed != 0 && d.crc != seed) st = EWAL_ERR_WAL_CRC;
       chained = d.crc;
     } else {                                // decoder.decode: crc.Write(Data); Validate
-      const uint64_t s = d.doff, e = d.doff + d.dlen;
       uint32_t computed;
       if (d.dlen == 0) {
         computed = seed;
       } else {
-        const uint32_t Ps = prefix_at(s, pwave, v, buf, s_t4, s_s64);
-        const uint32_t Pe = prefix_at(e, pwave, v, buf, s_t4, s_s64);
-        computed = gshift_n(g_shift, d.dlen, seed ^ 0xffffffffu ^ Ps) ^ Pe ^ 0xffffffffu;
+        const uint64_t e = d.doff + d.dlen;
+        // P(data end) = P(next frame start) in the canonical layout (pf[n+r+1]),
+        // else k_decode left it in d.chained.  U(seed, D) = S_n(seed ^ ~0 ^ P(s)) ^ P(e) ^ ~0
+        const uint32_t Pe = (r + 1 < n && rd[r + 1].off == e) ? pf[n + r + 1] : d.chained;
+        uint32_t x = seed ^ 0xffffffffu ^ pf[r];
+        uint64_t m = d.dlen;
+        for (int lvl = 0; m; ++lvl, m >>= 1) {
+          if (m & 1) x = lvl <= 16 ? tab_apply(s_sh + lvl * 1024, x) : gshift_pow2(g_shift, lvl, x);
+        }
+        computed = x ^ Pe ^ 0xffffffffu;
       }
       chained = computed;
       if (computed != d.crc) {
