@@ -78,14 +78,13 @@ struct Small {  // per-call device scratch (zeroed / initialised each call)
 struct ewal_ctx {
   int device = 0;
   int num_cu = 256;
-  int stream_r = 16;
-  int ablate = 0;      // EWAL_STREAM_ABLATE (timing experiments only; results are wrong)   // LDS replicas of the slicing tables (EWAL_STREAM_R=16|32)
+  int ablate = 0;      // EWAL_STREAM_ABLATE (timing experiments only; results are wrong)
   hipStream_t stream = nullptr;
   bool own_stream = false;
   hipEvent_t ev0 = nullptr, ev1 = nullptr, evs0 = nullptr, evs1 = nullptr;
   std::map<uint32_t, DevTables> tables;
   std::map<uint32_t, std::unique_ptr<ewal::CrcTables>> host_tables;
-  DevBuf pf, v, pwave, desc, wagg, wcnt, slots, cbase, ovf, cpos, clen, nxt, exc, E, rs, jl, vis, entry, on, rec_cand, rd, opf, ops, kk, kkrev, suf,
+  DevBuf pf, v, pwave, desc, wcnt, slots, cbase, ovf, cpos, clen, nxt, exc, E, rs, jl, vis, entry, on, rec_cand, rd, opf, ops, kk, kkrev, suf,
       ents, recs, tmp, small, sdesc, snaps, hbuf_dev;
   Small *h_small = nullptr;  // pinned mirror
   // results of the last readall
@@ -146,7 +145,6 @@ static int run_stream(ewal_ctx *c, DevTables *tb, const uint8_t *d_buf, uint64_t
   const uint32_t nstiles = (nunits + 1023) / 1024;
   EW_CHECK(c->v.ensure((size_t)nunits * 64 * 4));
   EW_CHECK(c->pwave.ensure((size_t)nunits * 4));
-  EW_CHECK(c->wagg.ensure((size_t)nunits * 4));
   EW_CHECK(c->wcnt.ensure((size_t)nunits * 4));
   EW_CHECK(c->cbase.ensure((size_t)nunits * 8));
   if (find_cand) {
@@ -166,21 +164,17 @@ static int run_stream(ewal_ctx *c, DevTables *tb, const uint8_t *d_buf, uint64_t
   a.g_slice = tb->slice;
   a.g_shift = tb->shift;
   a.v = c->v.as<uint32_t>();
-  a.wagg = c->wagg.as<uint32_t>();
   a.wcnt = c->wcnt.as<uint32_t>();
   a.slots = find_cand ? c->slots.as<uint16_t>() : nullptr;
   const unsigned grid = (unsigned)std::min<uint64_t>((nunits + EW_WAVES - 1) / EW_WAVES, (uint64_t)c->num_cu);
   EW_CHECK(hipEventRecord(c->evs0, c->stream));
-  if (c->stream_r == 32)
-    hipLaunchKernelGGL(k_stream<32>, dim3(grid), dim3(EW_THREADS), 0, c->stream, a);
-  else
-    hipLaunchKernelGGL(k_stream<16>, dim3(grid), dim3(EW_THREADS), 0, c->stream, a);
+  hipLaunchKernelGGL(k_stream, dim3(grid), dim3(EW_THREADS), 0, c->stream, a);
   EW_CHECK(hipGetLastError());
   EW_CHECK(hipEventRecord(c->evs1, c->stream));
   ScanArgs s;
   s.nunits = nunits;
   s.ntiles = nstiles;
-  s.wagg = a.wagg;
+  s.v = a.v;
   s.wcnt = a.wcnt;
   s.g_shift = tb->shift;
   s.pwave = c->pwave.as<uint32_t>();
@@ -452,7 +446,6 @@ int ewal_ctx_create(int device, ewal_ctx **out) {
     c->num_cu = prop.multiProcessorCount;
   EW_CHECK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
   c->own_stream = true;
-  if (const char *e = std::getenv("EWAL_STREAM_R")) c->stream_r = std::atoi(e) == 32 ? 32 : 16;
   if (const char *e = std::getenv("EWAL_STREAM_ABLATE")) c->ablate = std::atoi(e);
   EW_CHECK(hipEventCreate(&c->ev0));
   EW_CHECK(hipEventCreate(&c->ev1));
@@ -468,7 +461,7 @@ void ewal_ctx_destroy(ewal_ctx *c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
   (void)hipStreamSynchronize(c->stream);
-  DevBuf *bufs[] = {&c->pf, &c->v, &c->pwave, &c->desc, &c->wagg, &c->wcnt, &c->slots, &c->cbase, &c->ovf, &c->cpos, &c->clen, &c->nxt, &c->exc, &c->E, &c->rs, &c->jl,
+  DevBuf *bufs[] = {&c->pf, &c->v, &c->pwave, &c->desc, &c->wcnt, &c->slots, &c->cbase, &c->ovf, &c->cpos, &c->clen, &c->nxt, &c->exc, &c->E, &c->rs, &c->jl,
                     &c->vis, &c->entry, &c->on, &c->rec_cand, &c->rd, &c->opf, &c->ops, &c->kk, &c->kkrev,
                     &c->suf, &c->ents, &c->recs, &c->tmp, &c->small, &c->sdesc, &c->snaps, &c->hbuf_dev};
   for (DevBuf *b : bufs) b->release();

@@ -10,18 +10,18 @@ struct StreamArgs {
   uint64_t B;              // byte count
   uint32_t nunits;         // B / 4096 + 1 (P is read at x == B)
   int find_cand;           // 1: WAL framing candidates, 0: CRC prefixes only
-  int ablate;              // timing-only ablations (EWAL_STREAM_ABLATE): 1 no CRC, 2 no candidates
+  int ablate;              // timing-only ablations (EWAL_STREAM_ABLATE): 1 no CRC, 2 no candidates,
+                           // 4 no v store, 16 no lane-63 tail load
   const uint32_t *g_slice; // [4][256]
   const uint32_t *g_shift; // [48][4][256]
   uint32_t *v;             // lin of every 64-B piece        [nunits*64]
-  uint32_t *wagg;          // lin of every 4 KiB unit        [nunits]
   uint32_t *wcnt;          // candidates in the unit         [nunits]
   uint16_t *slots;         // first EW_SLOTS candidate offsets per unit
 };
 
 struct ScanArgs {
   uint32_t nunits, ntiles;        // ntiles = ceil(nunits / 1024)
-  const uint32_t *wagg, *wcnt;
+  const uint32_t *v, *wcnt;       // piece lins, candidate counts (k_stream)
   const uint32_t *g_shift;
   uint32_t *pwave;                // stream prefix at every unit start
   unsigned long long *cbase;      // candidates before every unit

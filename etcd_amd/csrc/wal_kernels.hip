@@ -29,14 +29,41 @@
 // ===========================================================================
 // k_stream
 // ===========================================================================
-template <int R>
-__device__ __forceinline__ uint32_t lds_step4(const uint32_t *s, int cl, uint32_t c) {
-  // s[(t*256 + b) * R + cl]
-  return s[((3 * 256 + (c & 0xff)) * R) + cl] ^ s[((2 * 256 + ((c >> 8) & 0xff)) * R) + cl] ^
-         s[((1 * 256 + ((c >> 16) & 0xff)) * R) + cl] ^ s[((0 * 256 + (c >> 24)) * R) + cl];
+// Slicing-by-4 tables, 32 LDS replicas, laid out so that ONE v_perm_b32 turns
+// a CRC register byte into a conflict-free LDS byte address:
+//   dword (t >> 1) * 16384 + b * 64 + (t & 1) * 32 + (lane & 31)
+// i.e. byte address [lane byte | b << 8 | region << 16] with lane byte =
+// (t & 1) * 128 + 4 * (lane & 31) and region = t >> 1.  The bank of every
+// lookup is lane & 31, so a ds_read_b32 costs the minimum 2 LDS cycles.
+#define EW_SLICE_DWORDS 32768   // 128 KiB
+// byte k of c into address byte 1, lane byte / region from L
+#define EW_PERM_SEL(k) (0x0c020000u | ((4u + (k)) << 8))
+__device__ __forceinline__ uint32_t lds_lookup(const uint8_t *s, uint32_t addr) {
+  return *(const uint32_t *)(s + addr);
 }
-__device__ __forceinline__ uint32_t lds_shift(const uint32_t *s, int m, uint32_t x) {
-  return tab_apply(s + (m - EW_LDS_SHIFT0) * 1024, x);
+__device__ __forceinline__ uint32_t slice_src(int idx) {   // g_slice index (t * 256 + b) of LDS dword idx
+  const int region = idx >> 14, b = (idx >> 6) & 255, t = region * 2 + ((idx >> 5) & 1);
+  return (uint32_t)(t * 256 + b);
+}
+// The same layout holding the byte tables of a shift S_{2^m} (table t <- byte
+// 3 - t), so that the lookup step below applies S_{2^m}: g_shift index.
+__device__ __forceinline__ uint32_t shift_src(int m, int idx) {
+  const uint32_t tb = slice_src(idx);
+  return (uint32_t)m * 1024 + (3 - (tb >> 8)) * 256 + (tb & 255);
+}
+// One table step on x with the data word d folded in:
+//   T3[x.b0] ^ T2[x.b1] ^ T1[x.b2] ^ T0[x.b3] ^ d
+// (slicing tables: the CRC step; shift tables: S_{2^m}(x) ^ d).
+__device__ __forceinline__ uint32_t perm_step(const uint8_t *s, const uint32_t (&Lt)[4], uint32_t x, uint32_t d) {
+  const uint32_t l0 = lds_lookup(s, __builtin_amdgcn_perm(x, Lt[3], EW_PERM_SEL(0)));
+  const uint32_t l1 = lds_lookup(s, __builtin_amdgcn_perm(x, Lt[2], EW_PERM_SEL(1)));
+  const uint32_t l2 = lds_lookup(s, __builtin_amdgcn_perm(x, Lt[1], EW_PERM_SEL(2)));
+  const uint32_t l3 = lds_lookup(s, __builtin_amdgcn_perm(x, Lt[0], EW_PERM_SEL(3)));
+  return __builtin_amdgcn_bitop3_b32(__builtin_amdgcn_bitop3_b32(l0, l1, l2, 0x96), l3, d, 0x96);
+}
+__device__ __forceinline__ void lane_regs(int lane, uint32_t (&Lt)[4]) {
+#pragma unroll
+  for (int t = 0; t < 4; ++t) Lt[t] = ((uint32_t)(t >> 1) << 16) | ((uint32_t)(t & 1) << 7) | (uint32_t)((lane & 31) << 2);
 }
 
 __device__ __forceinline__ uint32_t load_word_guarded(const uint8_t *buf, uint64_t B, uint64_t o) {
@@ -70,6 +97,24 @@ __device__ __forceinline__ uint32_t load_word_guarded(const uint8_t *buf, uint64
       if (ok_) { CAND_ACTION; }                                                      \
     }                                                                                \
   }
+
+// Branch-free filter over all 16 dword positions: nonzero iff some byte
+// position may hold 08 ?? 10 at p+8 / p+10 (the exact test above then runs
+// only for such lanes).  E = D ^ 08080808, so x ^ 08.. = E[J+2] and
+// y ^ 10.. = alignbyte(E[J+3], E[J+2], 2) ^ 18..; one bitop3 each for z and
+// for the accumulated zero-byte test.
+__device__ __forceinline__ uint32_t cand_filter(const uint32_t (&D)[19]) {
+  uint32_t acc = 0, e0 = D[2] ^ 0x08080808u;
+#pragma unroll
+  for (int J = 0; J < 16; ++J) {
+    const uint32_t e1 = D[J + 3] ^ 0x08080808u;
+    const uint32_t y = __builtin_amdgcn_alignbyte(e1, e0, 2) ^ 0x18181818u;
+    const uint32_t z = e0 | y;
+    acc |= (z - 0x01010101u) & ~z;
+    e0 = e1;
+  }
+  return acc & 0x80808080u;
+}
 
 __device__ __forceinline__ uint32_t count_cands(const uint32_t (&D)[19], uint64_t off, uint64_t B) {
   uint32_t cnt = 0;
@@ -107,15 +152,19 @@ __device__ __forceinline__ void slot_cands(const uint32_t (&D)[19], uint64_t off
 typedef uint32_t ew_v4u __attribute__((ext_vector_type(4)));
 // The WAL stream is read exactly once: nontemporal loads (measured 7.0 vs
 // 6.1-6.3 TB/s for the plain forms of the same read pattern, tools/membw.hip).
+__device__ __forceinline__ void load_piece_fast(const uint8_t *buf, uint64_t off, uint32_t (&D)[19]) {
+  const ew_v4u *p = (const ew_v4u *)(buf + off);
+  ew_v4u q0 = __builtin_nontemporal_load(p), q1 = __builtin_nontemporal_load(p + 1),
+         q2 = __builtin_nontemporal_load(p + 2), q3 = __builtin_nontemporal_load(p + 3);
+  D[0] = q0.x; D[1] = q0.y; D[2] = q0.z; D[3] = q0.w;
+  D[4] = q1.x; D[5] = q1.y; D[6] = q1.z; D[7] = q1.w;
+  D[8] = q2.x; D[9] = q2.y; D[10] = q2.z; D[11] = q2.w;
+  D[12] = q3.x; D[13] = q3.y; D[14] = q3.z; D[15] = q3.w;
+}
+// guarded form (the stream's last units, k_rescan)
 __device__ __forceinline__ void load_piece(const uint8_t *buf, uint64_t B, uint64_t off, uint32_t (&D)[19]) {
   if (off + EW_PIECE <= B) {
-    const ew_v4u *p = (const ew_v4u *)(buf + off);
-    ew_v4u q0 = __builtin_nontemporal_load(p), q1 = __builtin_nontemporal_load(p + 1),
-           q2 = __builtin_nontemporal_load(p + 2), q3 = __builtin_nontemporal_load(p + 3);
-    D[0] = q0.x; D[1] = q0.y; D[2] = q0.z; D[3] = q0.w;
-    D[4] = q1.x; D[5] = q1.y; D[6] = q1.z; D[7] = q1.w;
-    D[8] = q2.x; D[9] = q2.y; D[10] = q2.z; D[11] = q2.w;
-    D[12] = q3.x; D[13] = q3.y; D[14] = q3.z; D[15] = q3.w;
+    load_piece_fast(buf, off, D);
   } else {
 #pragma unroll
     for (int k = 0; k < 16; ++k) D[k] = (off < B) ? load_word_guarded(buf, B, off + 4 * k) : 0u;
@@ -135,6 +184,15 @@ __device__ __forceinline__ void load_next3(const uint8_t *buf, uint64_t B, uint6
     D[17] = load_word_guarded(buf, B, o + 4);
     D[18] = load_word_guarded(buf, B, o + 8);
   }
+}
+// fast form: DPP wave_shl:1 (lane i reads lane i + 1); lane 63 keeps `old`,
+// the first words of the next unit, loaded with the piece
+#define EW_DPP_WAVE_SHL1 0x130
+typedef uint32_t ew_v3u __attribute__((ext_vector_type(3)));
+__device__ __forceinline__ void next3_fast(const ew_v3u &nxt, uint32_t (&D)[19]) {
+  D[16] = (uint32_t)__builtin_amdgcn_update_dpp((int)nxt.x, (int)D[0], EW_DPP_WAVE_SHL1, 0xf, 0xf, false);
+  D[17] = (uint32_t)__builtin_amdgcn_update_dpp((int)nxt.y, (int)D[1], EW_DPP_WAVE_SHL1, 0xf, 0xf, false);
+  D[18] = (uint32_t)__builtin_amdgcn_update_dpp((int)nxt.z, (int)D[2], EW_DPP_WAVE_SHL1, 0xf, 0xf, false);
 }
 
 // Decoupled look-back (Merrill & Garland) over 64 predecessors per step, for
@@ -210,83 +268,247 @@ __device__ __forceinline__ void lookback(TileDesc *desc, uint32_t t, uint32_t ag
   }
 }
 
-// One HBM pass, no inter-workgroup communication.  Every wave owns 4 KiB
-// units (grid-stride), 64 B per lane: lin(piece) -> v[], frame-start
-// candidates -> up to EW_SLOTS 12-bit offsets per unit, and the unit's
-// aggregate (lin over 4 KiB, candidate count) -> wagg[], wcnt[].  The next
-// unit's bytes are loaded while the current one is processed.
-template <int R>
-__global__ __launch_bounds__(EW_THREADS, 1) void k_stream(StreamArgs a) {
-  __shared__ uint32_t s_slice[4 * 256 * R];     // replicated slicing tables (R copies, lane % R)
-  __shared__ uint32_t s_shift[6 * 1024];        // 24 KiB, S_{2^6}..S_{2^11}
-  const int tid = threadIdx.x, lane = tid & 63;
-  for (int i = tid; i < 4 * 256 * R; i += EW_THREADS) s_slice[i] = a.g_slice[i / R];
-  for (int i = tid; i < 6 * 1024; i += EW_THREADS) s_shift[i] = a.g_shift[EW_LDS_SHIFT0 * 1024 + i];
-  __syncthreads();
-  const int cl = lane & (R - 1);
-  const uint64_t B = a.B;
-  const uint32_t W = gridDim.x * EW_WAVES;
-  uint32_t u = blockIdx.x * EW_WAVES + (tid >> 6);
-  uint32_t D[19], Nx[19];
-  if (u < a.nunits) load_piece(a.buf, B, (uint64_t)u * EW_WAVE_BYTES + lane * EW_PIECE, D);
-  for (; u < a.nunits; u += W) {
-    const uint64_t off = (uint64_t)u * EW_WAVE_BYTES + (uint64_t)lane * EW_PIECE;
-    const uint32_t un = u + W;
-    if (un < a.nunits) load_piece(a.buf, B, (uint64_t)un * EW_WAVE_BYTES + lane * EW_PIECE, Nx);
+// DPP controls (GFX9 family): row_shr:n = 0x110 + n, row_bcast:15 / :31.
+#define EW_DPP_ROW_SHR(n) (0x110 + (n))
+#define EW_DPP_ROW_BCAST15 0x142
+#define EW_DPP_ROW_BCAST31 0x143
+// inclusive wave prefix sum (u32), DPP only
+__device__ __forceinline__ uint32_t wave_incl_sum(uint32_t x) {
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, EW_DPP_ROW_SHR(1), 0xf, 0xf, false);
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, EW_DPP_ROW_SHR(2), 0xf, 0xf, false);
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, EW_DPP_ROW_SHR(4), 0xf, 0xf, false);
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, EW_DPP_ROW_SHR(8), 0xf, 0xf, false);
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, EW_DPP_ROW_BCAST15, 0xa, 0xf, false);
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, EW_DPP_ROW_BCAST31, 0xc, 0xf, false);
+  return x;
+}
 
-    uint32_t c = 0;
-    if (!(a.ablate & 1)) {
+// lin(piece) of NU pieces at once: slicing-by-4 chains, interleaved so the
+// NU dependent chains hide each other's LDS latency.  Each step is 4 v_perm
+// + 4 conflict-free ds_read_b32 + 2 v_bitop3 (the next data word folded in).
+template <int NU>
+__device__ __forceinline__ void crc_pieces(const uint8_t *s_slice, const uint32_t (&Lt)[4],
+                                           const uint32_t (&D)[NU][19], uint32_t (&c)[NU]) {
+  uint32_t x[NU];
 #pragma unroll
-      for (int k = 0; k < 16; ++k) c = lds_step4<R>(s_slice, cl, c ^ D[k]);
-    } else {   // timing-only build path: keep the loads live, skip the CRC
+  for (int i = 0; i < NU; ++i) x[i] = D[i][0];
 #pragma unroll
-      for (int k = 0; k < 16; ++k) c ^= D[k];
-    }
-    __builtin_nontemporal_store(c, a.v + (uint64_t)u * 64 + lane);
+  for (int k = 0; k < 16; ++k)
+#pragma unroll
+    for (int i = 0; i < NU; ++i) x[i] = perm_step(s_slice, Lt, x[i], k < 15 ? D[i][k + 1] : 0u);
+#pragma unroll
+  for (int i = 0; i < NU; ++i) c[i] = x[i];
+}
 
-    uint32_t cnt = 0;
-    if (a.find_cand && !(a.ablate & 2)) {
-      load_next3(a.buf, B, off, D);
-      if (off < B) cnt = count_cands(D, off, B);
-    }
-    // wave reduction of the affine CRC: lane 0 ends with lin(4 KiB)
-    uint32_t r = c;
+// Exact test at every filter hit of a lane's piece; records the first two
+// candidate offsets (12-bit, inside the unit) in registers.
+__device__ __forceinline__ uint32_t find_cands(const uint32_t (&D)[19], uint64_t off, uint64_t B, uint32_t unit_off,
+                                               uint32_t &pa, uint32_t &pb) {
+  uint32_t n = 0;
+#define CAND_ACTION                                                  \
+  {                                                                  \
+    const uint32_t q_ = unit_off + (uint32_t)(p_ - off);             \
+    pb = (n == 1) ? q_ : pb;                                         \
+    pa = (n == 0) ? q_ : pa;                                         \
+    ++n;                                                             \
+  }
+  CAND_TEST(0) CAND_TEST(1) CAND_TEST(2) CAND_TEST(3) CAND_TEST(4) CAND_TEST(5) CAND_TEST(6) CAND_TEST(7)
+  CAND_TEST(8) CAND_TEST(9) CAND_TEST(10) CAND_TEST(11) CAND_TEST(12) CAND_TEST(13) CAND_TEST(14) CAND_TEST(15)
+#undef CAND_ACTION
+  return n;
+}
+
+// 4 x 4 transpose of 16-B chunks across the lane groups g = lane >> 4: on
+// entry register row r (D[4r..4r+3]) of lane (g, m) holds chunk g of piece
+// 16 r + m; on exit D[4c..4c+3] of lane (g, m) holds chunk c of piece
+// 16 g + m, i.e. the lane owns piece `lane`.  Two butterfly stages of the
+// gfx950 lane-swap instructions (v_permlane32_swap: upper half of vdst <->
+// lower half of vsrc; v_permlane16_swap: odd rows of vdst <-> even rows of
+// vsrc), 16 VALU per 4 KiB.
+__device__ __forceinline__ void row_transpose(uint32_t (&D)[19]) {
 #pragma unroll
-    for (int d = 0; d < 6; ++d) {
-      uint32_t o = __shfl_down(r, 1 << d);
-      if ((lane & ((2 << d) - 1)) == 0) r = lds_shift(s_shift, EW_LDS_SHIFT0 + d, r) ^ o;
-    }
-    uint32_t ci = cnt;
-    if (a.find_cand && __ballot(cnt != 0)) {   // wave-uniform: most 4 KiB units hold no frame start
+  for (int d = 0; d < 4; ++d) {
+    auto s02 = __builtin_amdgcn_permlane32_swap(D[d], D[8 + d], false, false);
+    auto s13 = __builtin_amdgcn_permlane32_swap(D[4 + d], D[12 + d], false, false);
+    D[d] = s02[0]; D[8 + d] = s02[1];
+    D[4 + d] = s13[0]; D[12 + d] = s13[1];
+  }
 #pragma unroll
-      for (int d = 0; d < 6; ++d) {
-        uint32_t o = __shfl_up(ci, 1 << d);
-        if (lane >= (1 << d)) ci += o;
-      }
-      if (cnt) slot_cands(D, off, B, ci - cnt, a.slots + (size_t)u * EW_SLOTS, (uint32_t)(lane * EW_PIECE));
-    }
-    if (lane == 0) a.wagg[u] = r;
-    if (lane == 63) a.wcnt[u] = ci;
-#pragma unroll
-    for (int k = 0; k < 16; ++k) D[k] = Nx[k];
+  for (int d = 0; d < 4; ++d) {
+    auto s01 = __builtin_amdgcn_permlane16_swap(D[d], D[4 + d], false, false);
+    auto s23 = __builtin_amdgcn_permlane16_swap(D[8 + d], D[12 + d], false, false);
+    D[d] = s01[0]; D[4 + d] = s01[1];
+    D[8 + d] = s23[0]; D[12 + d] = s23[1];
   }
 }
 
-// Scan of the unit aggregates: 1024 units (4 MiB of stream) per workgroup,
-// wave shuffles + one look-back per workgroup.  Writes pwave[u] = P at the
-// unit's start and cbase[u] = candidates before the unit.
+// NU units (4 KiB each, 64 B per lane) once D[i][0..18] is in registers:
+// lin(piece) -> v[] and frame-start candidates -> slots[] / wcnt[] (the
+// unit's candidate count, from lane 63).  The 4 KiB aggregates are formed
+// from v[] by k_uscan, where one lane per unit does it with every lane busy.
+template <int NU>
+__device__ __forceinline__ void stream_units(const StreamArgs &a, const uint8_t *s_slice, const uint32_t (&Lt)[4],
+                                             const uint32_t (&u)[NU], const uint32_t (&D)[NU][19]) {
+  const int lane = threadIdx.x & 63;
+  const uint64_t B = a.B;
+  // branch-free candidate filter first: independent VALU the scheduler can
+  // place in the CRC chains' LDS shadows
+  uint32_t fm[NU];
+#pragma unroll
+  for (int i = 0; i < NU; ++i) fm[i] = (a.find_cand && !(a.ablate & 2)) ? cand_filter(D[i]) : 0u;
+  uint32_t c[NU];
+  if (!(a.ablate & 1)) {
+    crc_pieces<NU>(s_slice, Lt, D, c);
+  } else {   // timing-only path: keep the loads live, skip the CRC
+#pragma unroll
+    for (int i = 0; i < NU; ++i) {
+      c[i] = 0;
+#pragma unroll
+      for (int k = 0; k < 16; ++k) c[i] ^= D[i][k];
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < NU; ++i)
+    if (!(a.ablate & 4)) __builtin_nontemporal_store(c[i], a.v + (uint64_t)u[i] * 64 + lane);
+#pragma unroll
+  for (int i = 0; i < NU; ++i) {
+    const uint64_t off = (uint64_t)u[i] * EW_WAVE_BYTES + (uint64_t)lane * EW_PIECE;
+    uint32_t cnt = 0, pa = 0, pb = 0;
+    if (fm[i] && off < B) cnt = find_cands(D[i], off, B, (uint32_t)(lane * EW_PIECE), pa, pb);
+    uint32_t ci = 0;
+    if (__ballot(cnt != 0)) {   // wave-uniform: most 4 KiB units hold no frame start
+      ci = wave_incl_sum(cnt);
+      uint16_t *sl = a.slots + (size_t)u[i] * EW_SLOTS;
+      const uint32_t base = ci - cnt;
+      if (cnt > 2) {
+        slot_cands(D[i], off, B, base, sl, (uint32_t)(lane * EW_PIECE));
+      } else {
+        if (cnt >= 1 && base < EW_SLOTS) sl[base] = (uint16_t)pa;
+        if (cnt >= 2 && base + 1 < EW_SLOTS) sl[base + 1] = (uint16_t)pb;
+      }
+    }
+    if (lane == 63) a.wcnt[u[i]] = ci;
+  }
+}
+
+// One HBM pass, no inter-workgroup communication.  Every wave owns 4 KiB
+// units (grid-stride W) and works on two of them at once (u, u + W) so that
+// two independent CRC chains hide each other's LDS latency.  Pairs whose
+// bytes -- plus the 16 bytes after each unit -- lie inside the stream run
+// the unguarded loop: ping-pong register buffers, the next pair (and the 12
+// bytes after each of its units, for lane 63) always loaded while the
+// current one is processed -- the prefetch address is clamped, never
+// predicated, so no wait lands before the use.  The rest take the guarded
+// single-unit path.
+__global__ __launch_bounds__(EW_THREADS, 1) void k_stream(StreamArgs a) {
+  __shared__ __attribute__((aligned(16))) uint8_t s_slice[EW_SLICE_DWORDS * 4];
+  const int tid = threadIdx.x, lane = tid & 63;
+  for (int i = tid; i < EW_SLICE_DWORDS; i += EW_THREADS) ((uint32_t *)s_slice)[i] = a.g_slice[slice_src(i)];
+  __syncthreads();
+  uint32_t Lt[4];
+  lane_regs(lane, Lt);
+  const uint64_t B = a.B;
+  const uint32_t W = gridDim.x * EW_WAVES;
+  const uint32_t wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  uint32_t u = blockIdx.x * EW_WAVES + wv;
+  const uint32_t nsafe = B >= 16 ? (uint32_t)std::min<uint64_t>(a.nunits, (B - 16) / EW_WAVE_BYTES) : 0u;
+  // Unit loads are fully coalesced: load r covers unit bytes [1024 r, 1024 r + 1024)
+  // with lane (g, m) = (lane >> 4, lane & 15) taking chunk g of piece 16 r + m
+  // (a permutation inside the 1 KiB row, measured as fast as the plain order).
+  // row_transpose() then gives every lane the 64 contiguous bytes of piece `lane`.
+  const uint64_t lo = (uint64_t)(64 * (lane & 15) + 16 * (lane >> 4));
+  auto load_pair = [&](uint32_t p, uint32_t (&T)[2][19], ew_v3u (&t3)[2]) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const uint64_t ub = (uint64_t)(p + i * W) * EW_WAVE_BYTES;
+      const ew_v4u *q = (const ew_v4u *)(a.buf + ub + lo);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const ew_v4u w = __builtin_nontemporal_load(q + 64 * r);
+        T[i][4 * r] = w.x; T[i][4 * r + 1] = w.y; T[i][4 * r + 2] = w.z; T[i][4 * r + 3] = w.w;
+      }
+      if (lane == 63 && !(a.ablate & 16)) t3[i] = __builtin_nontemporal_load((const ew_v3u *)(a.buf + ub + EW_WAVE_BYTES));
+    }
+  };
+  auto run_pair = [&](uint32_t p, uint32_t (&T)[2][19], const ew_v3u (&t3)[2]) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      row_transpose(T[i]);
+      next3_fast(t3[i], T[i]);
+    }
+    const uint32_t uu[2] = {p, p + W};
+    stream_units<2>(a, s_slice, Lt, uu, T);
+  };
+  uint32_t DA[2][19], DB[2][19];
+  ew_v3u nA[2] = {{0, 0, 0}, {0, 0, 0}}, nB[2] = {{0, 0, 0}, {0, 0, 0}};
+  if (u + W < nsafe) load_pair(u, DA, nA);
+  for (;;) {   // two pairs per trip: A is current while B loads, then B while A loads
+    if (!(u + W < nsafe)) break;
+    {
+      const uint32_t un = (u + 3 * W < nsafe) ? u + 2 * W : u;   // clamped prefetch
+      load_pair(un, DB, nB);
+      run_pair(u, DA, nA);
+      u += 2 * W;
+    }
+    if (!(u + W < nsafe)) break;
+    {
+      const uint32_t un = (u + 3 * W < nsafe) ? u + 2 * W : u;
+      load_pair(un, DA, nA);
+      run_pair(u, DB, nB);
+      u += 2 * W;
+    }
+  }
+  for (; u < a.nunits; u += W) {
+    const uint64_t off = (uint64_t)u * EW_WAVE_BYTES + (uint64_t)lane * EW_PIECE;
+    uint32_t D1[1][19];
+    load_piece(a.buf, B, off, D1[0]);
+    load_next3(a.buf, B, off, D1[0]);
+    const uint32_t uu[1] = {u};
+    stream_units<1>(a, s_slice, Lt, uu, D1);
+  }
+}
+
+// Scan of the unit aggregates: 1024 units (4 MiB of stream) per workgroup.
+// Each thread first forms its unit's aggregate lin(4 KiB) from the unit's 64
+// piece lins v[] (k_stream): four Horner chains of 16 pieces with S_64
+// (conflict-free perm layout) joined with S_1024.  Then wave shuffles + one
+// look-back per workgroup.  Writes pwave[u] = P at the unit's start and
+// cbase[u] = candidates before the unit.
 __global__ __launch_bounds__(1024, 1) void k_uscan(ScanArgs a) {
-  __shared__ uint32_t s_shift[10 * 1024];   // S_{2^12} .. S_{2^21}
+  __shared__ __attribute__((aligned(16))) uint8_t s_s64[EW_SLICE_DWORDS * 4];   // S_64, 128 KiB
+  __shared__ uint32_t s_shift[6 * 1024];   // S_{2^12} .. S_{2^17}
+  __shared__ uint32_t s_s1k[1024];         // S_1024
   __shared__ uint32_t s_wq[16], s_wc[16], s_base[16];
   __shared__ unsigned long long s_cb[16];
   __shared__ uint32_t s_tile;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  for (int i = tid; i < 10 * 1024; i += 1024) s_shift[i] = a.g_shift[12 * 1024 + i];
+  for (int i = tid; i < EW_SLICE_DWORDS; i += 1024) ((uint32_t *)s_s64)[i] = a.g_shift[shift_src(6, i)];
+  for (int i = tid; i < 6 * 1024; i += 1024) s_shift[i] = a.g_shift[12 * 1024 + i];
+  s_s1k[tid] = a.g_shift[10 * 1024 + tid];
   if (tid == 0) s_tile = atomicAdd(a.ticket, 1u);
   __syncthreads();
   const uint32_t t = s_tile;
   const uint32_t u = t * 1024 + tid;
-  const uint32_t x = u < a.nunits ? a.wagg[u] : 0u;
+  uint32_t x = 0;
+  if (u < a.nunits) {
+    uint32_t Lt[4];
+    lane_regs(lane, Lt);
+    const uint4 *vq = (const uint4 *)(a.v + (size_t)u * 64);
+    uint32_t pv[64];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const uint4 w = vq[q];
+      pv[4 * q] = w.x; pv[4 * q + 1] = w.y; pv[4 * q + 2] = w.z; pv[4 * q + 3] = w.w;
+    }
+    uint32_t h[4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) h[g] = pv[16 * g];
+#pragma unroll
+    for (int j = 1; j < 16; ++j)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) h[g] = perm_step(s_s64, Lt, h[g], pv[16 * g + j]);
+    x = tab_apply(s_s1k, tab_apply(s_s1k, tab_apply(s_s1k, h[0]) ^ h[1]) ^ h[2]) ^ h[3];
+  }
   const uint32_t cx = u < a.nunits ? a.wcnt[u] : 0u;
   // inclusive wave scan (units of 4 KiB -> shift 2^(12+d))
   uint32_t q = x, qc = cx;
@@ -295,7 +517,7 @@ __global__ __launch_bounds__(1024, 1) void k_uscan(ScanArgs a) {
     uint32_t o = __shfl_up(q, 1 << d);
     uint32_t oc = __shfl_up(qc, 1 << d);
     if (lane >= (1 << d)) {
-      q = tab_apply(s_shift + d * 1024, o) ^ q;
+      q = tab_apply(s_shift + d * 1024, o) ^ q;   // S_{2^(12+d)}
       qc += oc;
     }
   }
@@ -309,7 +531,7 @@ __global__ __launch_bounds__(1024, 1) void k_uscan(ScanArgs a) {
     for (int d = 0; d < 4; ++d) {
       uint32_t o = __shfl_up(w, 1 << d), oc = __shfl_up(wc, 1 << d);
       if (lane >= (1 << d) && lane < 16) {
-        w = tab_apply(s_shift + (6 + d) * 1024, o) ^ w;   // waves of 256 KiB -> 2^(18+d)
+        w = tab_apply(a.g_shift + (18 + d) * 1024, o) ^ w;   // waves of 256 KiB -> 2^(18+d)
         wc += oc;
       }
     }
@@ -323,7 +545,7 @@ __global__ __launch_bounds__(1024, 1) void k_uscan(ScanArgs a) {
       uint32_t xs = X;                         // S_{lane * 2^18}(X)
 #pragma unroll
       for (int b = 0; b < 4; ++b)
-        if ((lane >> b) & 1) xs = tab_apply(s_shift + (6 + b) * 1024, xs);
+        if ((lane >> b) & 1) xs = tab_apply(a.g_shift + (18 + b) * 1024, xs);
       s_base[lane] = xs ^ we;
       s_cb[lane] = N + wce;
     }
