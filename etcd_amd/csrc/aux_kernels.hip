@@ -17,10 +17,10 @@ __global__ __launch_bounds__(256) void k_snap(const uint8_t *__restrict__ buf, c
                        const uint32_t *__restrict__ g_shift, SnapDesc *__restrict__ sd,
                        esnap_snapshot *__restrict__ snaps, uint32_t n) {
   __shared__ uint32_t s_t4[1024];
-  __shared__ uint32_t s_s64[1024];
+  __shared__ uint32_t s_svp[1024];   // S_256 (prefix_at's Horner step)
   for (int i = threadIdx.x; i < 1024; i += blockDim.x) {
     s_t4[i] = g_slice[i];
-    s_s64[i] = g_shift[6 * 1024 + i];
+    s_svp[i] = g_shift[EW_VLOG * 1024 + i];
   }
   __syncthreads();
   uint32_t f = blockIdx.x * blockDim.x + threadIdx.x;
@@ -40,8 +40,8 @@ __global__ __launch_bounds__(256) void k_snap(const uint8_t *__restrict__ buf, c
     if (d.dlen == 0) {
       d.computed = 0;
     } else {
-      const uint32_t Ps = prefix_at(d.doff, pwave, v, buf, s_t4, s_s64);
-      const uint32_t Pe = prefix_at(d.doff + d.dlen, pwave, v, buf, s_t4, s_s64);
+      const uint32_t Ps = prefix_at(d.doff, pwave, v, buf, s_t4, s_svp);
+      const uint32_t Pe = prefix_at(d.doff + d.dlen, pwave, v, buf, s_t4, s_svp);
       d.computed = gshift_n(g_shift, d.dlen, 0xffffffffu ^ Ps) ^ Pe ^ 0xffffffffu;
     }
     if (d.computed != d.stored) {

@@ -143,7 +143,7 @@ static int run_stream(ewal_ctx *c, DevTables *tb, const uint8_t *d_buf, uint64_t
   if (nunits64 >= 0xffff0000ull) return EWAL_E_INVAL;
   const uint32_t nunits = (uint32_t)nunits64;
   const uint32_t nstiles = (nunits + 1023) / 1024;
-  EW_CHECK(c->v.ensure((size_t)nunits * 64 * 4));
+  EW_CHECK(c->v.ensure((size_t)nunits * EW_VPU * 4));
   EW_CHECK(c->pwave.ensure((size_t)nunits * 4));
   EW_CHECK(c->wcnt.ensure((size_t)nunits * 4));
   EW_CHECK(c->cbase.ensure((size_t)nunits * 8));

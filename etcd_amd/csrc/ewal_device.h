@@ -6,13 +6,16 @@
 
 #define EW_PIECE 64                      // bytes per lane in the stream pass
 #define EW_WAVE_BYTES 4096               // 64 lanes x 64 B
-#define EW_WAVES 16                      // waves per workgroup (1024 threads)
+#define EW_WAVES 12                      // k_stream waves per workgroup (768 threads, 3 per SIMD)
 #define EW_THREADS (EW_WAVES * 64)
 #define EW_TILE (EW_WAVES * EW_WAVE_BYTES)  // 64 KiB per tile (one look-back step)
 #define EW_TILE_LOG2 16
 #define EW_R 16                          // LDS replicas of each slicing table
 #define EW_NIL 0xFFFFFFFFu
 #define EW_SLOTS 32                      // candidate slots per 4 KiB unit
+#define EW_VLOG 8                        // v[] holds lin of every 2^EW_VLOG = 256-B super-piece
+#define EW_VPIECE (1 << EW_VLOG)
+#define EW_VPU (EW_WAVE_BYTES / EW_VPIECE)  // v[] values per 4 KiB unit (16)
 #define EW_LDS_SHIFT0 6                  // LDS holds S_{2^6} .. S_{2^15}
 #define EW_LDS_SHIFTS 10
 

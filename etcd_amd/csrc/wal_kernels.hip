@@ -104,13 +104,16 @@ __device__ __forceinline__ uint32_t load_word_guarded(const uint8_t *buf, uint64
 // y ^ 10.. = alignbyte(E[J+3], E[J+2], 2) ^ 18..; one bitop3 each for z and
 // for the accumulated zero-byte test.
 __device__ __forceinline__ uint32_t cand_filter(const uint32_t (&D)[19]) {
+  // per dword: 1 xor, 1 alignbyte, 3 bitop3/add (5 VALU)
+  //   z   = e0 | (y ^ 18..)            bitop3 0xF6 (a | (b ^ c))
+  //   acc = ((z - 01..) & ~z) | acc    bitop3 0xBA ((a & ~b) | c)
   uint32_t acc = 0, e0 = D[2] ^ 0x08080808u;
 #pragma unroll
   for (int J = 0; J < 16; ++J) {
     const uint32_t e1 = D[J + 3] ^ 0x08080808u;
-    const uint32_t y = __builtin_amdgcn_alignbyte(e1, e0, 2) ^ 0x18181818u;
-    const uint32_t z = e0 | y;
-    acc |= (z - 0x01010101u) & ~z;
+    const uint32_t y = __builtin_amdgcn_alignbyte(e1, e0, 2);
+    const uint32_t z = __builtin_amdgcn_bitop3_b32(e0, y, 0x18181818u, 0xF6);
+    acc = __builtin_amdgcn_bitop3_b32(z + 0xFEFEFEFFu, z, acc, 0xBA);
     e0 = e1;
   }
   return acc & 0x80808080u;
@@ -188,6 +191,7 @@ __device__ __forceinline__ void load_next3(const uint8_t *buf, uint64_t B, uint6
 // fast form: DPP wave_shl:1 (lane i reads lane i + 1); lane 63 keeps `old`,
 // the first words of the next unit, loaded with the piece
 #define EW_DPP_WAVE_SHL1 0x130
+#define EW_DPP_WAVE_ROL1 0x134
 typedef uint32_t ew_v3u __attribute__((ext_vector_type(3)));
 __device__ __forceinline__ void next3_fast(const ew_v3u &nxt, uint32_t (&D)[19]) {
   D[16] = (uint32_t)__builtin_amdgcn_update_dpp((int)nxt.x, (int)D[0], EW_DPP_WAVE_SHL1, 0xf, 0xf, false);
@@ -343,11 +347,13 @@ __device__ __forceinline__ void row_transpose(uint32_t (&D)[19]) {
 }
 
 // NU units (4 KiB each, 64 B per lane) once D[i][0..18] is in registers:
-// lin(piece) -> v[] and frame-start candidates -> slots[] / wcnt[] (the
-// unit's candidate count, from lane 63).  The 4 KiB aggregates are formed
-// from v[] by k_uscan, where one lane per unit does it with every lane busy.
+// lin of every 256-B super-piece -> v[] (1/64 of the stream bytes) and
+// frame-start candidates -> slots[] / wcnt[] (the unit's candidate count,
+// from lane 63).  The 4 KiB aggregates are formed from v[] by k_uscan, where
+// one lane per unit does it with every lane busy.
 template <int NU>
-__device__ __forceinline__ void stream_units(const StreamArgs &a, const uint8_t *s_slice, const uint32_t (&Lt)[4],
+__device__ __forceinline__ void stream_units(const StreamArgs &a, const uint8_t *s_slice, const uint32_t *s_s64,
+                                             const uint32_t *s_s128, const uint32_t (&Lt)[4],
                                              const uint32_t (&u)[NU], const uint32_t (&D)[NU][19]) {
   const int lane = threadIdx.x & 63;
   const uint64_t B = a.B;
@@ -367,9 +373,26 @@ __device__ __forceinline__ void stream_units(const StreamArgs &a, const uint8_t 
       for (int k = 0; k < 16; ++k) c[i] ^= D[i][k];
     }
   }
+  // lin of every 256-B super-piece (lanes 4m .. 4m+3) by a two-level tree,
+  // branch-free: the lanes that do not combine look up entry 0 (one address,
+  // a broadcast, no extra bank cycles).  Lane 4m+3 ends with the value.
+  //   level 0 (odd lanes):      y = S_64(c[L-1]) ^ c[L]
+  //   level 1 (lanes 3 mod 4):  z = S_128(y[L-2]) ^ y[L]
+  const bool odd = lane & 1, top = (lane & 3) == 3;
 #pragma unroll
-  for (int i = 0; i < NU; ++i)
-    if (!(a.ablate & 4)) __builtin_nontemporal_store(c[i], a.v + (uint64_t)u[i] * 64 + lane);
+  for (int i = 0; i < NU; ++i) {
+    const uint32_t o = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c[i], EW_DPP_ROW_SHR(1), 0xf, 0xf, false);
+    c[i] ^= tab_apply(s_s64, odd ? o : 0u);   // S_64(0) = 0
+  }
+#pragma unroll
+  for (int i = 0; i < NU; ++i) {
+    const uint32_t o = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c[i], EW_DPP_ROW_SHR(2), 0xf, 0xf, false);
+    c[i] ^= tab_apply(s_s128, top ? o : 0u);
+  }
+  if (top && !(a.ablate & 4)) {
+#pragma unroll
+    for (int i = 0; i < NU; ++i) __builtin_nontemporal_store(c[i], a.v + (uint64_t)u[i] * EW_VPU + (lane >> 2));
+  }
 #pragma unroll
   for (int i = 0; i < NU; ++i) {
     const uint64_t off = (uint64_t)u[i] * EW_WAVE_BYTES + (uint64_t)lane * EW_PIECE;
@@ -391,98 +414,118 @@ __device__ __forceinline__ void stream_units(const StreamArgs &a, const uint8_t 
   }
 }
 
-// One HBM pass, no inter-workgroup communication.  Every wave owns 4 KiB
-// units (grid-stride W) and works on two of them at once (u, u + W) so that
-// two independent CRC chains hide each other's LDS latency.  Pairs whose
-// bytes -- plus the 16 bytes after each unit -- lie inside the stream run
-// the unguarded loop: ping-pong register buffers, the next pair (and the 12
-// bytes after each of its units, for lane 63) always loaded while the
-// current one is processed -- the prefetch address is clamped, never
-// predicated, so no wait lands before the use.  The rest take the guarded
-// single-unit path.
+// One HBM pass, no inter-workgroup communication.  Every wave works on PAIRS
+// of adjacent units (8 KiB; pair p = units 2p, 2p + 1, grid-stride over p)
+// so that two independent CRC chains hide each other's LDS latency, the
+// first unit's trailing bytes come from the second unit's registers, and
+// the pair's super-piece lins form one whole 128-B line of v[].  Pairs
+// inside the stream (plus 16 bytes) run the unguarded loop with THREE
+// register buffers: while one pair is processed the next two are in flight
+// (12 waves x 16 KiB = 192 KiB of HBM reads outstanding per CU, what the HBM
+// latency under full load needs).  Loop control is scalar and the loads are
+// raw buffer loads (scalar base, loop-invariant lane offset), so no wait
+// lands before the use.  The last units take the guarded single-unit path.
 __global__ __launch_bounds__(EW_THREADS, 1) void k_stream(StreamArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t s_slice[EW_SLICE_DWORDS * 4];
+  __shared__ uint32_t s_s64[1024], s_s128[1024];   // S_64, S_128 byte tables (super-piece tree)
   const int tid = threadIdx.x, lane = tid & 63;
   for (int i = tid; i < EW_SLICE_DWORDS; i += EW_THREADS) ((uint32_t *)s_slice)[i] = a.g_slice[slice_src(i)];
+  for (int i = tid; i < 1024; i += EW_THREADS) {
+    s_s64[i] = a.g_shift[6 * 1024 + i];
+    s_s128[i] = a.g_shift[7 * 1024 + i];
+  }
   __syncthreads();
   uint32_t Lt[4];
   lane_regs(lane, Lt);
   const uint64_t B = a.B;
   const uint32_t W = gridDim.x * EW_WAVES;
   const uint32_t wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-  uint32_t u = blockIdx.x * EW_WAVES + wv;
+  const uint32_t p0 = blockIdx.x * EW_WAVES + wv;
   const uint32_t nsafe = B >= 16 ? (uint32_t)std::min<uint64_t>(a.nunits, (B - 16) / EW_WAVE_BYTES) : 0u;
+  const uint32_t NP = nsafe / 2;   // pairs whose units are both safe
   // Unit loads are fully coalesced: load r covers unit bytes [1024 r, 1024 r + 1024)
   // with lane (g, m) = (lane >> 4, lane & 15) taking chunk g of piece 16 r + m
   // (a permutation inside the 1 KiB row, measured as fast as the plain order).
   // row_transpose() then gives every lane the 64 contiguous bytes of piece `lane`.
-  const uint64_t lo = (uint64_t)(64 * (lane & 15) + 16 * (lane >> 4));
-  auto load_pair = [&](uint32_t p, uint32_t (&T)[2][19], ew_v3u (&t3)[2]) {
+  const uint32_t lo = (uint32_t)(64 * (lane & 15) + 16 * (lane >> 4));
+  // Raw buffer loads: the pair base lives in the (scalar) buffer resource,
+  // the per-lane offset is a loop-invariant VGPR, so no address VGPR is ever
+  // rewritten while loads are in flight.  Lane 63 also fetches the 12 bytes
+  // after the pair; the other lanes' offset for that load is out of range
+  // (the resource covers 8192 + 12 bytes), which returns 0 and moves no data.
+  const int o3 = lane == 63 ? 2 * EW_WAVE_BYTES : 0x7ffffff0;
+  auto load_pair = [&](uint32_t p, uint32_t (&T)[2][19], ew_v3u &t3) {
+    p = __builtin_amdgcn_readfirstlane(p);
+    const uint8_t *pb = a.buf + (uint64_t)p * (2 * EW_WAVE_BYTES);
+    __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void *)pb, 0, 2 * EW_WAVE_BYTES + 12, 0x00020000);
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
-      const uint64_t ub = (uint64_t)(p + i * W) * EW_WAVE_BYTES;
-      const ew_v4u *q = (const ew_v4u *)(a.buf + ub + lo);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const ew_v4u w = __builtin_nontemporal_load(q + 64 * r);
+        const ew_v4u w = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)lo + EW_WAVE_BYTES * i + 1024 * r, 0, 2 /* nt */);
         T[i][4 * r] = w.x; T[i][4 * r + 1] = w.y; T[i][4 * r + 2] = w.z; T[i][4 * r + 3] = w.w;
       }
-      if (lane == 63 && !(a.ablate & 16)) t3[i] = __builtin_nontemporal_load((const ew_v3u *)(a.buf + ub + EW_WAVE_BYTES));
     }
+    t3 = __builtin_amdgcn_raw_buffer_load_b96(rs, o3, 0, 2);
   };
-  auto run_pair = [&](uint32_t p, uint32_t (&T)[2][19], const ew_v3u (&t3)[2]) {
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      row_transpose(T[i]);
-      next3_fast(t3[i], T[i]);
-    }
-    const uint32_t uu[2] = {p, p + W};
-    stream_units<2>(a, s_slice, Lt, uu, T);
+  auto run_pair = [&](uint32_t p, uint32_t (&T)[2][19], const ew_v3u &t3) {
+    row_transpose(T[0]);
+    row_transpose(T[1]);
+    // unit 0's lane 63 continues into unit 1's piece 0 (lane 0): wave_rol:1
+    ew_v3u f3;
+    f3.x = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)T[1][0], EW_DPP_WAVE_ROL1, 0xf, 0xf, false);
+    f3.y = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)T[1][1], EW_DPP_WAVE_ROL1, 0xf, 0xf, false);
+    f3.z = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)T[1][2], EW_DPP_WAVE_ROL1, 0xf, 0xf, false);
+    next3_fast(f3, T[0]);
+    next3_fast(t3, T[1]);
+    const uint32_t uu[2] = {2 * p, 2 * p + 1};
+    stream_units<2>(a, s_slice, s_s64, s_s128, Lt, uu, T);
   };
-  uint32_t DA[2][19], DB[2][19];
-  ew_v3u nA[2] = {{0, 0, 0}, {0, 0, 0}}, nB[2] = {{0, 0, 0}, {0, 0, 0}};
-  if (u + W < nsafe) load_pair(u, DA, nA);
-  for (;;) {   // two pairs per trip: A is current while B loads, then B while A loads
-    if (!(u + W < nsafe)) break;
-    {
-      const uint32_t un = (u + 3 * W < nsafe) ? u + 2 * W : u;   // clamped prefetch
-      load_pair(un, DB, nB);
-      run_pair(u, DA, nA);
-      u += 2 * W;
-    }
-    if (!(u + W < nsafe)) break;
-    {
-      const uint32_t un = (u + 3 * W < nsafe) ? u + 2 * W : u;
-      load_pair(un, DA, nA);
-      run_pair(u, DB, nB);
-      u += 2 * W;
-    }
+  const uint32_t npairs = p0 < NP ? (NP - 1 - p0) / W + 1 : 0u;
+  auto pair_at = [&](uint32_t k) {   // clamped: a prefetch past the end reloads the last pair
+    return __builtin_amdgcn_readfirstlane(p0 + W * (k < npairs ? k : npairs - 1));
+  };
+  uint32_t DA[2][19], DB[2][19], DC[2][19];
+  ew_v3u nA, nB, nC;
+  if (npairs) {
+    load_pair(pair_at(0), DA, nA);
+    load_pair(pair_at(1), DB, nB);
   }
-  for (; u < a.nunits; u += W) {
+  for (uint32_t k = 0; k < npairs; k += 3) {   // A is processed while B and C load, and so on
+    load_pair(pair_at(k + 2), DC, nC);
+    run_pair(pair_at(k), DA, nA);
+    if (k + 1 >= npairs) break;
+    load_pair(pair_at(k + 3), DA, nA);
+    run_pair(pair_at(k + 1), DB, nB);
+    if (k + 2 >= npairs) break;
+    load_pair(pair_at(k + 4), DB, nB);
+    run_pair(pair_at(k + 2), DC, nC);
+  }
+  for (uint32_t u = 2 * NP + p0; u < a.nunits; u += W) {
     const uint64_t off = (uint64_t)u * EW_WAVE_BYTES + (uint64_t)lane * EW_PIECE;
     uint32_t D1[1][19];
     load_piece(a.buf, B, off, D1[0]);
     load_next3(a.buf, B, off, D1[0]);
     const uint32_t uu[1] = {u};
-    stream_units<1>(a, s_slice, Lt, uu, D1);
+    stream_units<1>(a, s_slice, s_s64, s_s128, Lt, uu, D1);
   }
 }
 
 // Scan of the unit aggregates: 1024 units (4 MiB of stream) per workgroup.
-// Each thread first forms its unit's aggregate lin(4 KiB) from the unit's 64
-// piece lins v[] (k_stream): four Horner chains of 16 pieces with S_64
-// (conflict-free perm layout) joined with S_1024.  Then wave shuffles + one
+// Each thread first forms its unit's aggregate lin(4 KiB) from the unit's 16
+// super-piece lins v[] (k_stream): Horner with S_256 (conflict-free perm
+// layout) joined with S_1024.  Then wave shuffles + one
 // look-back per workgroup.  Writes pwave[u] = P at the unit's start and
 // cbase[u] = candidates before the unit.
 __global__ __launch_bounds__(1024, 1) void k_uscan(ScanArgs a) {
-  __shared__ __attribute__((aligned(16))) uint8_t s_s64[EW_SLICE_DWORDS * 4];   // S_64, 128 KiB
+  __shared__ __attribute__((aligned(16))) uint8_t s_svp[EW_SLICE_DWORDS * 4];   // S_256, 128 KiB
   __shared__ uint32_t s_shift[6 * 1024];   // S_{2^12} .. S_{2^17}
   __shared__ uint32_t s_s1k[1024];         // S_1024
   __shared__ uint32_t s_wq[16], s_wc[16], s_base[16];
   __shared__ unsigned long long s_cb[16];
   __shared__ uint32_t s_tile;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  for (int i = tid; i < EW_SLICE_DWORDS; i += 1024) ((uint32_t *)s_s64)[i] = a.g_shift[shift_src(6, i)];
+  for (int i = tid; i < EW_SLICE_DWORDS; i += 1024) ((uint32_t *)s_svp)[i] = a.g_shift[shift_src(EW_VLOG, i)];
   for (int i = tid; i < 6 * 1024; i += 1024) s_shift[i] = a.g_shift[12 * 1024 + i];
   s_s1k[tid] = a.g_shift[10 * 1024 + tid];
   if (tid == 0) s_tile = atomicAdd(a.ticket, 1u);
@@ -490,23 +533,20 @@ __global__ __launch_bounds__(1024, 1) void k_uscan(ScanArgs a) {
   const uint32_t t = s_tile;
   const uint32_t u = t * 1024 + tid;
   uint32_t x = 0;
-  if (u < a.nunits) {
+  if (u < a.nunits) {   // four Horner chains of four 256-B values, joined with S_1024
     uint32_t Lt[4];
     lane_regs(lane, Lt);
-    const uint4 *vq = (const uint4 *)(a.v + (size_t)u * 64);
-    uint32_t pv[64];
+    const uint4 *vq = (const uint4 *)(a.v + (size_t)u * EW_VPU);
+    uint4 q[4];
 #pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      const uint4 w = vq[q];
-      pv[4 * q] = w.x; pv[4 * q + 1] = w.y; pv[4 * q + 2] = w.z; pv[4 * q + 3] = w.w;
-    }
+    for (int g = 0; g < 4; ++g) q[g] = vq[g];
     uint32_t h[4];
 #pragma unroll
-    for (int g = 0; g < 4; ++g) h[g] = pv[16 * g];
-#pragma unroll
-    for (int j = 1; j < 16; ++j)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) h[g] = perm_step(s_s64, Lt, h[g], pv[16 * g + j]);
+    for (int g = 0; g < 4; ++g) {
+      h[g] = perm_step(s_svp, Lt, q[g].x, q[g].y);
+      h[g] = perm_step(s_svp, Lt, h[g], q[g].z);
+      h[g] = perm_step(s_svp, Lt, h[g], q[g].w);
+    }
     x = tab_apply(s_s1k, tab_apply(s_s1k, tab_apply(s_s1k, h[0]) ^ h[1]) ^ h[2]) ^ h[3];
   }
   const uint32_t cx = u < a.nunits ? a.wcnt[u] : 0u;
@@ -704,36 +744,37 @@ __global__ void k_member(const uint32_t *__restrict__ E, uint32_t R, const uint8
 // ===========================================================================
 
 // Stream prefix P(x) = lin(stream[0..x)) from the per-unit prefix and the
-// per-piece lins of k_stream.  Every load is issued up front (the unit's 64
-// piece lins, 256 B, and the 64-B piece holding x) so the dependent chain
-// that follows runs out of registers: Horner over the whole pieces before x,
-// then slicing-by-4 / byte steps over the bytes of x's piece before x.
+// super-piece lins of k_stream.  Every load is issued up front (the unit's
+// 16 super-piece lins, 64 B, and the 256-B super-piece holding x) so the
+// dependent chain that follows runs out of registers: Horner over the whole
+// super-pieces before x (S_256), then slicing-by-4 / byte steps over the
+// bytes of x's super-piece before x.
 __device__ __forceinline__ uint32_t prefix_at(uint64_t x, const uint32_t *__restrict__ pwave,
                                               const uint32_t *__restrict__ v, const uint8_t *__restrict__ buf,
-                                              const uint32_t *t4, const uint32_t *s64) {
+                                              const uint32_t *t4, const uint32_t *svp) {
   const uint64_t w = x >> 12;
-  const uint64_t x0 = x & ~(uint64_t)(EW_PIECE - 1);
-  const uint32_t k = (uint32_t)((x0 >> 6) & 63);
+  const uint64_t x0 = x & ~(uint64_t)(EW_VPIECE - 1);
+  const uint32_t k = (uint32_t)((x0 >> EW_VLOG) & (EW_VPU - 1));
   const uint32_t tail = (uint32_t)(x - x0);
-  const uint4 *vq = (const uint4 *)(v + (w << 6));
-  uint4 vv[16];
+  const uint4 *vq = (const uint4 *)(v + w * EW_VPU);
+  uint4 vv[EW_VPU / 4];
 #pragma unroll
-  for (int q = 0; q < 16; ++q) vv[q] = (4u * q < k) ? vq[q] : make_uint4(0, 0, 0, 0);
-  uint4 dd[4];
+  for (int q = 0; q < EW_VPU / 4; ++q) vv[q] = (4u * q < k) ? vq[q] : make_uint4(0, 0, 0, 0);
+  uint4 dd[EW_VPIECE / 16];
   const uint4 *dq = (const uint4 *)(buf + x0);
 #pragma unroll
-  for (int q = 0; q < 4; ++q) dd[q] = (16u * q < tail) ? dq[q] : make_uint4(0, 0, 0, 0);
+  for (int q = 0; q < EW_VPIECE / 16; ++q) dd[q] = (16u * q < tail) ? dq[q] : make_uint4(0, 0, 0, 0);
   uint32_t acc = pwave[w];
 #pragma unroll
-  for (int q = 0; q < 16; ++q) {
-    if (4u * q + 0 < k) acc = tab_apply(s64, acc) ^ vv[q].x;
-    if (4u * q + 1 < k) acc = tab_apply(s64, acc) ^ vv[q].y;
-    if (4u * q + 2 < k) acc = tab_apply(s64, acc) ^ vv[q].z;
-    if (4u * q + 3 < k) acc = tab_apply(s64, acc) ^ vv[q].w;
+  for (int q = 0; q < EW_VPU / 4; ++q) {
+    if (4u * q + 0 < k) acc = tab_apply(svp, acc) ^ vv[q].x;
+    if (4u * q + 1 < k) acc = tab_apply(svp, acc) ^ vv[q].y;
+    if (4u * q + 2 < k) acc = tab_apply(svp, acc) ^ vv[q].z;
+    if (4u * q + 3 < k) acc = tab_apply(svp, acc) ^ vv[q].w;
   }
   const uint32_t nd = tail >> 2;
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
+  for (int q = 0; q < EW_VPIECE / 16; ++q) {
     if (4u * q + 0 < nd) acc = step4_flat(t4, acc ^ dd[q].x);
     if (4u * q + 1 < nd) acc = step4_flat(t4, acc ^ dd[q].y);
     if (4u * q + 2 < nd) acc = step4_flat(t4, acc ^ dd[q].z);
@@ -744,7 +785,7 @@ __device__ __forceinline__ uint32_t prefix_at(uint64_t x, const uint32_t *__rest
   if (rem) {
     uint32_t wd = 0;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
+    for (int q = 0; q < EW_VPIECE / 16; ++q) {
       if ((nd >> 2) == (uint32_t)q) {
         const uint32_t s = nd & 3;
         wd = s == 0 ? dd[q].x : s == 1 ? dd[q].y : s == 2 ? dd[q].z : dd[q].w;
@@ -768,10 +809,10 @@ __global__ __launch_bounds__(256) void k_decode(const uint8_t *__restrict__ buf,
                          const uint32_t *__restrict__ g_slice, const uint32_t *__restrict__ g_shift,
                          RecDesc *__restrict__ rd, uint32_t *__restrict__ pf) {
   __shared__ uint32_t s_t4[1024];
-  __shared__ uint32_t s_s64[1024];
+  __shared__ uint32_t s_svp[1024];   // S_256 (prefix_at's Horner step)
   for (int i = threadIdx.x; i < 1024; i += blockDim.x) {
     s_t4[i] = g_slice[i];
-    s_s64[i] = g_shift[6 * 1024 + i];
+    s_svp[i] = g_shift[EW_VLOG * 1024 + i];
   }
   __syncthreads();
   uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
@@ -822,12 +863,12 @@ __global__ __launch_bounds__(256) void k_decode(const uint8_t *__restrict__ buf,
   }
   // P at every frame start (the previous frame's data end, in the canonical
   // layout), and P at this frame's data start from it (header bytes only).
-  const uint32_t Pfo = prefix_at(p, pwave, v, buf, s_t4, s_s64);
+  const uint32_t Pfo = prefix_at(p, pwave, v, buf, s_t4, s_svp);
   pf[n + r] = Pfo;
   if (st == 0 && d.type != 4 && d.dlen > 0) {
     pf[r] = raw_bytes(s_t4, Pfo, buf, p, d.doff);
     if (r == n - 1 || d.doff + d.dlen != p + 8 + (uint64_t)L)
-      d.chained = prefix_at(d.doff + d.dlen, pwave, v, buf, s_t4, s_s64);   // P(data end), used by k_verify
+      d.chained = prefix_at(d.doff + d.dlen, pwave, v, buf, s_t4, s_svp);   // P(data end), used by k_verify
   }
   rd[r] = d;
 }
@@ -979,5 +1020,5 @@ __global__ void k_reverse_u64(const uint64_t *__restrict__ in, uint64_t *__restr
 __global__ void k_prefix_one(const uint8_t *__restrict__ buf, const uint32_t *__restrict__ pwave,
                              const uint32_t *__restrict__ v, const uint32_t *__restrict__ g_slice,
                              const uint32_t *__restrict__ g_shift, uint64_t x, uint32_t *out) {
-  if (threadIdx.x == 0) *out = prefix_at(x, pwave, v, buf, g_slice, g_shift + 6 * 1024);
+  if (threadIdx.x == 0) *out = prefix_at(x, pwave, v, buf, g_slice, g_shift + EW_VLOG * 1024);
 }
