@@ -59,20 +59,6 @@ struct DevBuf {
   }
 };
 
-struct Small {  // per-call device scratch (zeroed / initialised each call)
-  uint32_t ticket;
-  uint32_t errflag;
-  uint32_t novf;
-  uint32_t pad0;
-  unsigned long long total;
-  ChainInfo ci;
-  ReadAllAgg agg;
-  uint32_t nsel;      // hipcub select counts
-  uint32_t nsel2;
-  uint32_t nsel3;
-  uint32_t pad;
-};
-
 }  // namespace
 
 struct ewal_ctx {
@@ -84,9 +70,12 @@ struct ewal_ctx {
   hipEvent_t ev0 = nullptr, ev1 = nullptr, evs0 = nullptr, evs1 = nullptr;
   std::map<uint32_t, DevTables> tables;
   std::map<uint32_t, std::unique_ptr<ewal::CrcTables>> host_tables;
-  DevBuf pf, v, pwave, desc, wcnt, slots, cbase, ovf, cpos, clen, nxt, exc, E, rs, jl, vis, entry, on, rec_cand, rd, opf, ops, kk, kkrev, suf,
+  DevBuf mlist, pf, v, pwave, ux, tagg, tpx, wcnt, slots, cbase, ovf, cpos, clen, nxt, exc, E, rs, jl, vis, entry, on, rec_cand, rd, opf, ops, kk, kkrev, suf,
       ents, recs, tmp, small, sdesc, snaps, hbuf_dev;
-  Small *h_small = nullptr;  // pinned mirror
+  Small *h_small = nullptr;        // host-mapped pinned mirrors (written by k_export_small / k_result)
+  ResultDev *h_res = nullptr;
+  Small *h_small_dev = nullptr;    // their device-side addresses
+  ResultDev *h_res_dev = nullptr;
   // results of the last readall
   uint64_t last_n = 0, last_nents = 0;
   bool last_ok = false;
@@ -122,9 +111,8 @@ static int select_flagged(ewal_ctx *c, const uint8_t *flags, uint32_t n, uint32_
   return 0;
 }
 
-// Run the HBM pass (k_stream) and the unit scan (k_uscan) over d_buf[0..B):
-// fills c->v, c->pwave; with find_cand also the dense, sorted candidate list
-// (k_compact + k_rescan) and returns its size via *K (synchronises).
+// The overflow path of the candidate compaction (the list outgrew ccap):
+// slots -> dense list again (k_compact), then the overflow units (k_rescan).
 static int compact_cands(ewal_ctx *c, const uint8_t *d_buf, uint64_t B, uint32_t nunits, uint64_t ccap) {
   Small *ds = c->small.as<Small>();
   EW_CHECK(hipMemsetAsync(&ds->novf, 0, 4, c->stream));
@@ -137,8 +125,11 @@ static int compact_cands(ewal_ctx *c, const uint8_t *d_buf, uint64_t B, uint32_t
   return 0;
 }
 
-static int run_stream(ewal_ctx *c, DevTables *tb, const uint8_t *d_buf, uint64_t B, int find_cand, uint64_t ccap,
-                      uint64_t *K) {
+// Run the HBM pass (k_stream) and the unit scan (k_uscan) over d_buf[0..B):
+// fills c->v, c->pwave; with find_cand also the dense, position-sorted
+// candidate list cpos[] (k_uscan's epilogue + k_rescan), its size in
+// Small.total.  Asynchronous: nothing waits for the device here.
+static int run_stream(ewal_ctx *c, DevTables *tb, const uint8_t *d_buf, uint64_t B, int find_cand, uint64_t ccap) {
   const uint64_t nunits64 = B / EW_WAVE_BYTES + 1;
   if (nunits64 >= 0xffff0000ull) return EWAL_E_INVAL;
   const uint32_t nunits = (uint32_t)nunits64;
@@ -151,8 +142,9 @@ static int run_stream(ewal_ctx *c, DevTables *tb, const uint8_t *d_buf, uint64_t
     EW_CHECK(c->slots.ensure((size_t)nunits * EW_SLOTS * 2));
     EW_CHECK(c->ovf.ensure((size_t)nunits * 4));
   }
-  EW_CHECK(c->desc.ensure((size_t)nstiles * sizeof(TileDesc)));
-  EW_CHECK(hipMemsetAsync(c->desc.p, 0, (size_t)nstiles * sizeof(TileDesc), c->stream));
+  EW_CHECK(c->ux.ensure((size_t)nunits * 4));
+  EW_CHECK(c->tagg.ensure((size_t)nstiles * 16));
+  EW_CHECK(c->tpx.ensure((size_t)nstiles * 16));
   EW_CHECK(hipMemsetAsync(c->small.p, 0, sizeof(Small), c->stream));
   Small *ds = c->small.as<Small>();
   StreamArgs a;
@@ -166,7 +158,7 @@ static int run_stream(ewal_ctx *c, DevTables *tb, const uint8_t *d_buf, uint64_t
   a.v = c->v.as<uint32_t>();
   a.wcnt = c->wcnt.as<uint32_t>();
   a.slots = find_cand ? c->slots.as<uint16_t>() : nullptr;
-  const unsigned grid = (unsigned)std::min<uint64_t>((nunits + EW_WAVES - 1) / EW_WAVES, (uint64_t)c->num_cu);
+  const unsigned grid = (unsigned)std::min<uint64_t>((nunits + 2 * EW_WAVES - 1) / (2 * EW_WAVES), (uint64_t)c->num_cu);
   EW_CHECK(hipEventRecord(c->evs0, c->stream));
   hipLaunchKernelGGL(k_stream, dim3(grid), dim3(EW_THREADS), 0, c->stream, a);
   EW_CHECK(hipGetLastError());
@@ -179,37 +171,108 @@ static int run_stream(ewal_ctx *c, DevTables *tb, const uint8_t *d_buf, uint64_t
   s.g_shift = tb->shift;
   s.pwave = c->pwave.as<uint32_t>();
   s.cbase = c->cbase.as<unsigned long long>();
-  s.desc = c->desc.as<TileDesc>();
-  s.ticket = &ds->ticket;
-  s.errflag = &ds->errflag;
+  s.ux = c->ux.as<uint32_t>();
+  s.tagg = c->tagg.as<uint32_t>();
+  s.tcnt = s.tagg + nstiles;
+  s.tpx = c->tpx.as<uint32_t>();
+  s.tcb = (unsigned long long *)(c->tpx.as<uint8_t>() + (size_t)nstiles * 8);
   s.total = &ds->total;
-  hipLaunchKernelGGL(k_uscan, dim3(nstiles), dim3(1024), 0, c->stream, s);
+  s.slots = find_cand ? c->slots.as<uint16_t>() : nullptr;
+  s.cpos = find_cand ? c->cpos.as<uint64_t>() : nullptr;
+  s.ccap = ccap;
+  s.ovf = find_cand ? c->ovf.as<uint32_t>() : nullptr;
+  s.novf = &ds->novf;
+  const unsigned sgrid = std::min<uint32_t>(nstiles, 2u * (uint32_t)c->num_cu);   // 2 x 1024 threads per CU
+  hipLaunchKernelGGL(k_uagg, dim3(sgrid), dim3(1024), 0, c->stream, s);
+  hipLaunchKernelGGL(k_tscan, dim3(1), dim3(1024), 0, c->stream, s);
+  hipLaunchKernelGGL(k_uapply, dim3(sgrid), dim3(1024), 0, c->stream, s);
   EW_CHECK(hipGetLastError());
-  if (!find_cand) return 0;
-  int rc = compact_cands(c, d_buf, B, nunits, ccap);
-  if (rc) return rc;
-  EW_CHECK(hipMemcpyAsync(c->h_small, c->small.p, sizeof(Small), hipMemcpyDeviceToHost, c->stream));
+  if (find_cand) {
+    hipLaunchKernelGGL(k_rescan, dim3(64), dim3(256), 0, c->stream, d_buf, B, c->ovf.as<uint32_t>(), &ds->novf,
+                       c->cbase.as<unsigned long long>(), c->cpos.as<uint64_t>(), c->clen.as<uint64_t>(), ccap);
+    EW_CHECK(hipGetLastError());
+  }
+  return 0;
+}
+
+static int sync_small(ewal_ctx *c) {
+  hipLaunchKernelGGL(k_export_small, dim3(1), dim3(64), 0, c->stream, c->small.as<Small>(), c->h_small_dev);
+  EW_CHECK(hipGetLastError());
   EW_CHECK(hipStreamSynchronize(c->stream));
   if (c->h_small->errflag) return EWAL_E_TIMEOUT;
-  *K = c->h_small->total;
   return 0;
 }
 
-static int classify_terminal(ewal_ctx *c, const uint8_t *d_buf, uint64_t B, uint64_t q, int *st) {
-  // decoder.decode at frame start q when q is not a candidate frame
-  // (wal/decoder.go:28-39 + io.ReadFull's EOF/ErrUnexpectedEOF rule).
-  if (q == B) { *st = EWAL_OK; return 0; }
-  if (B - q < 8) { *st = EWAL_ERR_UNEXPECTED_EOF; return 0; }
-  int64_t L = 0;
-  EW_CHECK(hipMemcpyAsync(&L, d_buf + q, 8, hipMemcpyDeviceToHost, c->stream));
-  EW_CHECK(hipStreamSynchronize(c->stream));
+// decoder.decode at frame start q when q is not a frame of the chain
+// (wal/decoder.go:28-39 + io.ReadFull's EOF/ErrUnexpectedEOF rule); L is the
+// int64 at q (valid when q + 8 <= B).
+static int classify_terminal(uint64_t B, uint64_t q, int64_t L) {
+  if (q == B) return EWAL_OK;
+  if (B - q < 8) return EWAL_ERR_UNEXPECTED_EOF;
   const uint64_t rem = B - q - 8;
-  if (L < 0) *st = EWAL_PANIC_NEG_LENGTH;
-  else if ((uint64_t)L > rem) *st = rem == 0 ? EWAL_OK : EWAL_ERR_UNEXPECTED_EOF;
-  else *st = EWAL_UNSUPPORTED_ENCODING;   // a frame that fits but is not canonical
+  if (L < 0) return EWAL_PANIC_NEG_LENGTH;
+  if ((uint64_t)L > rem) return rem == 0 ? EWAL_OK : EWAL_ERR_UNEXPECTED_EOF;
+  return EWAL_UNSUPPORTED_ENCODING;   // a frame that fits but is not canonical
+}
+
+// Framing when the candidates do not form one chain from byte 0: runs of
+// consecutive candidates, pointer jumping over runs, membership (k_runs ..
+// k_member); returns the chain length n (c->rec_cand) and its terminal q.
+static int frame_irregular(ewal_ctx *c, uint64_t K, ewal_result *out, uint64_t *n_out, uint64_t *q_out) {
+  Small *ds = c->small.as<Small>();
+  const uint32_t K32 = (uint32_t)K;
+  EW_CHECK(c->E.ensure((size_t)K * 4));
+  int rc = select_flagged(c, c->exc.as<uint8_t>(), K32, c->E.as<uint32_t>(), &ds->nsel);
+  if (rc) return rc;
+  if ((rc = sync_small(c))) return rc;
+  const uint32_t R = c->h_small->nsel;
+  out->n_runs = R;
+  int top = 0;
+  while ((1ull << top) < R) ++top;
+  EW_CHECK(c->jl.ensure((size_t)R * 4 * (top + 1)));
+  EW_CHECK(c->vis.ensure(R));
+  EW_CHECK(c->entry.ensure((size_t)R * 4));
+  uint32_t *J = c->jl.as<uint32_t>();
+  hipLaunchKernelGGL(k_runs, dim3(grid_for(R, 256)), dim3(256), 0, c->stream, c->E.as<uint32_t>(), R,
+                     c->nxt.as<uint32_t>(), J);
+  for (int k = 1; k <= top; ++k)
+    hipLaunchKernelGGL(k_jump, dim3(grid_for(R, 256)), dim3(256), 0, c->stream, J + (size_t)(k - 1) * R,
+                       J + (size_t)k * R, R);
+  EW_CHECK(hipMemsetAsync(c->vis.p, 0, R, c->stream));
+  EW_CHECK(hipMemsetAsync(c->vis.p, 1, 1, c->stream));
+  for (int k = top; k >= 0; --k)
+    hipLaunchKernelGGL(k_mark, dim3(grid_for(R, 256)), dim3(256), 0, c->stream, J + (size_t)k * R,
+                       c->vis.as<uint8_t>(), R);
+  EW_CHECK(hipMemsetAsync(c->entry.p, 0xff, (size_t)R * 4, c->stream));
+  hipLaunchKernelGGL(k_entry, dim3(grid_for(R, 256)), dim3(256), 0, c->stream, c->E.as<uint32_t>(),
+                     c->nxt.as<uint32_t>(), J, c->vis.as<uint8_t>(), R, c->entry.as<uint32_t>(), &ds->ci);
+  EW_CHECK(c->on.ensure(K));
+  EW_CHECK(c->rec_cand.ensure((size_t)K * 4));
+  hipLaunchKernelGGL(k_member, dim3(grid_for(K, 256)), dim3(256), 0, c->stream, c->E.as<uint32_t>(), R,
+                     c->vis.as<uint8_t>(), c->entry.as<uint32_t>(), K32, c->on.as<uint8_t>());
+  rc = select_flagged(c, c->on.as<uint8_t>(), K32, c->rec_cand.as<uint32_t>(), &ds->nsel2);
+  if (rc) return rc;
+  if ((rc = sync_small(c))) return rc;
+  const uint32_t lc = c->h_small->ci.last_cand;
+  uint64_t pl[2];
+  EW_CHECK(hipMemcpyAsync(&pl[0], c->cpos.as<uint64_t>() + lc, 8, hipMemcpyDeviceToHost, c->stream));
+  EW_CHECK(hipMemcpyAsync(&pl[1], c->clen.as<uint64_t>() + lc, 8, hipMemcpyDeviceToHost, c->stream));
+  EW_CHECK(hipStreamSynchronize(c->stream));
+  *n_out = c->h_small->nsel2;
+  *q_out = pl[0] + 8 + pl[1];
   return 0;
 }
 
+static int read_le64_at(ewal_ctx *c, const uint8_t *d_buf, uint64_t B, uint64_t q, int64_t *L) {
+  *L = 0;
+  if (q + 8 > B) return 0;
+  EW_CHECK(hipMemcpyAsync(L, d_buf + q, 8, hipMemcpyDeviceToHost, c->stream));
+  EW_CHECK(hipStreamSynchronize(c->stream));
+  return 0;
+}
+
+// (*WAL).ReadAll, wal/wal.go:164-216.  Regular case: two host syncs in all
+// (after k_link, and the final result copy).
 static int readall_impl(ewal_ctx *c, const uint8_t *d_buf, uint64_t B, uint64_t ri, ewal_result *out) {
   std::memset(out, 0, sizeof(*out));
   out->fail_record = -1;
@@ -224,125 +287,102 @@ static int readall_impl(ewal_ctx *c, const uint8_t *d_buf, uint64_t B, uint64_t 
   if (rc) return rc;
   EW_CHECK(c->small.ensure(sizeof(Small)));
   EW_CHECK(hipEventRecord(c->ev0, c->stream));
+  Small *ds = c->small.as<Small>();
 
   uint64_t n = 0;          // frames on the chain
   uint64_t q = 0;          // terminal frame offset
   uint64_t K = 0;
+  int64_t qlen = 0;
+  bool regular = false;
   if (B > 0) {
     uint64_t ccap = std::min<uint64_t>(B / 128 + 65536, 0xfffffff0ull);
     EW_CHECK(c->cpos.ensure(ccap * 8));
     EW_CHECK(c->clen.ensure(ccap * 8));
-    rc = run_stream(c, tb, d_buf, B, 1, ccap, &K);
+    EW_CHECK(c->nxt.ensure(ccap * 4));
+    EW_CHECK(c->exc.ensure(ccap));
+    rc = run_stream(c, tb, d_buf, B, 1, ccap);
     if (rc) return rc;
-    if (K > ccap) {   // grow and redo only the compaction (the slots stay valid)
+    const unsigned lgrid = (unsigned)std::max(1, c->num_cu) * 8;
+    hipLaunchKernelGGL(k_link, dim3(lgrid), dim3(256), 0, c->stream, d_buf, B, c->cpos.as<uint64_t>(),
+                       c->clen.as<uint64_t>(), ccap, c->nxt.as<uint32_t>(), c->exc.as<uint8_t>(), ds);
+    EW_CHECK(hipGetLastError());
+    if ((rc = sync_small(c))) return rc;
+    K = c->h_small->total;
+    if (K > ccap) {   // grow and redo the compaction and the links (the slots stay valid)
       if (K >= 0xfffffff0ull) return EWAL_E_NOMEM;
       ccap = K + 1024;
       EW_CHECK(c->cpos.ensure(ccap * 8));
       EW_CHECK(c->clen.ensure(ccap * 8));
+      EW_CHECK(c->nxt.ensure(ccap * 4));
+      EW_CHECK(c->exc.ensure(ccap));
       rc = compact_cands(c, d_buf, B, (uint32_t)(B / EW_WAVE_BYTES + 1), ccap);
       if (rc) return rc;
+      EW_CHECK(hipMemsetAsync(&ds->irregular, 0, 4, c->stream));
+      hipLaunchKernelGGL(k_link, dim3(lgrid), dim3(256), 0, c->stream, d_buf, B, c->cpos.as<uint64_t>(),
+                         c->clen.as<uint64_t>(), ccap, c->nxt.as<uint32_t>(), c->exc.as<uint8_t>(), ds);
+      EW_CHECK(hipGetLastError());
+      if ((rc = sync_small(c))) return rc;
     }
   }
   out->n_candidates = (int64_t)K;
-  uint64_t pos0 = ~0ull;
-  if (K) {
-    EW_CHECK(hipMemcpyAsync(&pos0, c->cpos.p, 8, hipMemcpyDeviceToHost, c->stream));
-    EW_CHECK(hipStreamSynchronize(c->stream));
-  }
-  Small *ds = c->small.as<Small>();
-  if (K && pos0 == 0) {
-    const uint32_t K32 = (uint32_t)K;
-    EW_CHECK(c->nxt.ensure((size_t)K * 4));
-    EW_CHECK(c->exc.ensure((size_t)K));
-    EW_CHECK(c->E.ensure((size_t)K * 4));
-    hipLaunchKernelGGL(k_link, dim3(grid_for(K, 256)), dim3(256), 0, c->stream, c->cpos.as<uint64_t>(),
-                       c->clen.as<uint64_t>(), K32, c->nxt.as<uint32_t>(), c->exc.as<uint8_t>());
-    rc = select_flagged(c, c->exc.as<uint8_t>(), K32, c->E.as<uint32_t>(), &ds->nsel);
+  if (K && c->h_small->pos0 == 0) {
+    if (!c->h_small->irregular) {
+      regular = true;
+      n = K;
+      q = c->h_small->q;
+      qlen = c->h_small->qlen;
+      out->n_runs = 1;
+    } else {
+      rc = frame_irregular(c, K, out, &n, &q);
+      if (rc) return rc;
+      rc = read_le64_at(c, d_buf, B, q, &qlen);
+      if (rc) return rc;
+    }
+  } else {
+    rc = read_le64_at(c, d_buf, B, 0, &qlen);   // frame 0 is not a candidate: the chain is empty
     if (rc) return rc;
-    EW_CHECK(hipMemcpyAsync(c->h_small, ds, sizeof(Small), hipMemcpyDeviceToHost, c->stream));
-    EW_CHECK(hipStreamSynchronize(c->stream));
-    const uint32_t R = c->h_small->nsel;
-    out->n_runs = R;
-    int top = 0;
-    while ((1ull << top) < R) ++top;
-    EW_CHECK(c->jl.ensure((size_t)R * 4 * (top + 1)));
-    EW_CHECK(c->vis.ensure(R));
-    EW_CHECK(c->entry.ensure((size_t)R * 4));
-    uint32_t *J = c->jl.as<uint32_t>();
-    hipLaunchKernelGGL(k_runs, dim3(grid_for(R, 256)), dim3(256), 0, c->stream, c->E.as<uint32_t>(), R,
-                       c->nxt.as<uint32_t>(), J);
-    for (int k = 1; k <= top; ++k)
-      hipLaunchKernelGGL(k_jump, dim3(grid_for(R, 256)), dim3(256), 0, c->stream, J + (size_t)(k - 1) * R,
-                         J + (size_t)k * R, R);
-    EW_CHECK(hipMemsetAsync(c->vis.p, 0, R, c->stream));
-    EW_CHECK(hipMemsetAsync(c->vis.p, 1, 1, c->stream));
-    for (int k = top; k >= 0; --k)
-      hipLaunchKernelGGL(k_mark, dim3(grid_for(R, 256)), dim3(256), 0, c->stream, J + (size_t)k * R,
-                         c->vis.as<uint8_t>(), R);
-    EW_CHECK(hipMemsetAsync(c->entry.p, 0xff, (size_t)R * 4, c->stream));
-    hipLaunchKernelGGL(k_entry, dim3(grid_for(R, 256)), dim3(256), 0, c->stream, c->E.as<uint32_t>(),
-                       c->nxt.as<uint32_t>(), J, c->vis.as<uint8_t>(), R, c->entry.as<uint32_t>(), &ds->ci);
-    EW_CHECK(c->on.ensure(K));
-    EW_CHECK(c->rec_cand.ensure((size_t)K * 4));
-    hipLaunchKernelGGL(k_member, dim3(grid_for(K, 256)), dim3(256), 0, c->stream, c->E.as<uint32_t>(), R,
-                       c->vis.as<uint8_t>(), c->entry.as<uint32_t>(), K32, c->on.as<uint8_t>());
-    rc = select_flagged(c, c->on.as<uint8_t>(), K32, c->rec_cand.as<uint32_t>(), &ds->nsel2);
-    if (rc) return rc;
-    EW_CHECK(hipMemcpyAsync(c->h_small, ds, sizeof(Small), hipMemcpyDeviceToHost, c->stream));
-    EW_CHECK(hipStreamSynchronize(c->stream));
-    n = c->h_small->nsel2;
-    const uint32_t lc = c->h_small->ci.last_cand;
-    uint64_t pl[2];
-    EW_CHECK(hipMemcpyAsync(&pl[0], c->cpos.as<uint64_t>() + lc, 8, hipMemcpyDeviceToHost, c->stream));
-    EW_CHECK(hipMemcpyAsync(&pl[1], c->clen.as<uint64_t>() + lc, 8, hipMemcpyDeviceToHost, c->stream));
-    EW_CHECK(hipStreamSynchronize(c->stream));
-    q = pl[0] + 8 + pl[1];
   }
-  int tst = EWAL_OK;
-  rc = classify_terminal(c, d_buf, B, q, &tst);
-  if (rc) return rc;
+  const int tst = classify_terminal(B, q, qlen);
 
-  ReadAllAgg hagg;
-  hagg.first_fail = ~0ull;
-  hagg.last_entry = -1;
-  hagg.last_state = -1;
-  hagg.first_meta = ~0ull;
-  uint32_t nops = 0;
+  ResultDev res;
+  std::memset(&res, 0, sizeof(res));
+  res.agg.first_fail = ~0ull;
+  res.agg.last_entry = -1;
+  res.agg.last_state = -1;
+  res.agg.first_meta = ~0ull;
   if (n) {
     const uint32_t n32 = (uint32_t)n;
     EW_CHECK(c->rd.ensure((size_t)n * sizeof(RecDesc)));
-    EW_CHECK(hipMemcpyAsync(&ds->agg, &hagg, sizeof(hagg), hipMemcpyHostToDevice, c->stream));
     RecDesc *rd = c->rd.as<RecDesc>();
     EW_CHECK(c->pf.ensure((size_t)n * 8));
-    hipLaunchKernelGGL(k_decode, dim3(grid_for(n, 256)), dim3(256), 0, c->stream, d_buf, c->cpos.as<uint64_t>(),
-                       c->clen.as<uint64_t>(), c->rec_cand.as<uint32_t>(), n32, c->pwave.as<uint32_t>(),
-                       c->v.as<uint32_t>(), tb->slice, tb->shift, rd, c->pf.as<uint32_t>());
-    hipLaunchKernelGGL(k_verify, dim3(grid_for(n, 1024)), dim3(1024), 0, c->stream, d_buf, c->pwave.as<uint32_t>(),
-                       c->v.as<uint32_t>(), tb->slice, tb->shift, rd, n32, c->pf.as<uint32_t>(), &ds->agg);
-    hipLaunchKernelGGL(k_meta, dim3(grid_for(n, 256)), dim3(256), 0, c->stream, d_buf, rd, n32, &ds->agg);
+    hipLaunchKernelGGL(k_decode, dim3(grid_for(n, 256)), dim3(256), 0, c->stream, d_buf, B,
+                       c->cpos.as<uint64_t>(), c->clen.as<uint64_t>(),
+                       regular ? (const uint32_t *)nullptr : c->rec_cand.as<uint32_t>(), n32,
+                       c->pwave.as<uint32_t>(), c->v.as<uint32_t>(), tb->slice, tb->shift, rd, c->pf.as<uint32_t>(),
+                       c->ablate);
     EW_CHECK(c->opf.ensure(n));
     EW_CHECK(c->ops.ensure((size_t)n * 4));
-    hipLaunchKernelGGL(k_opflag, dim3(grid_for(n, 256)), dim3(256), 0, c->stream, rd, n32, ri, c->opf.as<uint8_t>());
+    EW_CHECK(c->mlist.ensure((size_t)n * 4));
+    hipLaunchKernelGGL(k_verify, dim3(grid_for(n, 1024)), dim3(1024), 0, c->stream, tb->shift, rd, n32,
+                       c->pf.as<uint32_t>(), ri, c->opf.as<uint8_t>(), c->mlist.as<uint32_t>(), ds);
+    hipLaunchKernelGGL(k_meta, dim3(64), dim3(256), 0, c->stream, d_buf, rd, c->mlist.as<uint32_t>(), ds);
     rc = select_flagged(c, c->opf.as<uint8_t>(), n32, c->ops.as<uint32_t>(), &ds->nsel3);
     if (rc) return rc;
-    EW_CHECK(hipMemcpyAsync(c->h_small, ds, sizeof(Small), hipMemcpyDeviceToHost, c->stream));
+    EW_CHECK(c->kk.ensure((size_t)n * 8));
+    EW_CHECK(c->ents.ensure((size_t)n * sizeof(ewal_entry)));
+    const unsigned ggrid = (unsigned)std::min<uint64_t>(grid_for(n, 256), (uint64_t)c->num_cu * 8);
+    hipLaunchKernelGGL(k_gap, dim3(ggrid), dim3(256), 0, c->stream, rd, c->ops.as<uint32_t>(), ri,
+                       c->kk.as<uint64_t>(), c->ents.as<ewal_entry>(), ds);
+    hipLaunchKernelGGL(k_result, dim3(1), dim3(64), 0, c->stream, rd, n32, ds, c->h_res_dev);
+    EW_CHECK(hipGetLastError());
     EW_CHECK(hipStreamSynchronize(c->stream));
-    nops = c->h_small->nsel3;
-    if (nops) {
-      EW_CHECK(c->kk.ensure((size_t)nops * 8));
-      hipLaunchKernelGGL(k_gap, dim3(grid_for(nops, 256)), dim3(256), 0, c->stream, rd, c->ops.as<uint32_t>(),
-                         nops, ri, c->kk.as<uint64_t>(), &ds->agg);
-    }
-    EW_CHECK(hipMemcpyAsync(c->h_small, ds, sizeof(Small), hipMemcpyDeviceToHost, c->stream));
-    EW_CHECK(hipStreamSynchronize(c->stream));
-    hagg = c->h_small->agg;
+    std::memcpy(&res, c->h_res, sizeof(ResultDev));
   }
+  const ReadAllAgg &hagg = res.agg;
   out->n_records = (int64_t)n;
 
   if (hagg.first_fail < n) {
-    RecDesc f;
-    EW_CHECK(hipMemcpyAsync(&f, c->rd.as<RecDesc>() + hagg.first_fail, sizeof(f), hipMemcpyDeviceToHost, c->stream));
-    EW_CHECK(hipStreamSynchronize(c->stream));
+    const RecDesc &f = res.fail;
     out->status = f.st;
     out->fail_record = (int64_t)hagg.first_fail;
     out->fail_offset = (int64_t)f.off;
@@ -354,44 +394,30 @@ static int readall_impl(ewal_ctx *c, const uint8_t *d_buf, uint64_t B, uint64_t 
     out->fail_record = (int64_t)n;
     out->fail_offset = (int64_t)q;
   } else {
-    uint64_t enti = 0;
-    if (hagg.last_entry >= 0) {
-      RecDesc e;
-      EW_CHECK(hipMemcpyAsync(&e, c->rd.as<RecDesc>() + hagg.last_entry, sizeof(e), hipMemcpyDeviceToHost, c->stream));
-      EW_CHECK(hipStreamSynchronize(c->stream));
-      enti = e.f1;
-    }
+    const uint64_t enti = hagg.last_entry >= 0 ? res.lastent.f1 : 0;
     out->enti = enti;
     if (enti < ri) {
       out->status = EWAL_ERR_INDEX_NOT_FOUND;
     } else {
       out->status = EWAL_OK;
       if (n) {
-        RecDesc last;
-        EW_CHECK(hipMemcpyAsync(&last, c->rd.as<RecDesc>() + (n - 1), sizeof(last), hipMemcpyDeviceToHost, c->stream));
-        RecDesc md, sd;
-        if (hagg.first_meta != ~0ull)
-          EW_CHECK(hipMemcpyAsync(&md, c->rd.as<RecDesc>() + hagg.first_meta, sizeof(md), hipMemcpyDeviceToHost, c->stream));
-        if (hagg.last_state >= 0)
-          EW_CHECK(hipMemcpyAsync(&sd, c->rd.as<RecDesc>() + hagg.last_state, sizeof(sd), hipMemcpyDeviceToHost, c->stream));
-        uint64_t klast = 0;
-        if (nops) EW_CHECK(hipMemcpyAsync(&klast, c->kk.as<uint64_t>() + (nops - 1), 8, hipMemcpyDeviceToHost, c->stream));
-        EW_CHECK(hipStreamSynchronize(c->stream));
-        out->last_crc = last.chained;
+        out->last_crc = res.last.chained;
         if (hagg.first_meta != ~0ull) {
-          out->metadata_off = (int64_t)md.doff;
-          out->metadata_len = (int64_t)md.dlen;
+          out->metadata_off = (int64_t)res.md.doff;
+          out->metadata_len = (int64_t)res.md.dlen;
         }
         if (hagg.last_state >= 0) {
           out->has_state = 1;
-          out->state_term = sd.f0;
-          out->state_vote = sd.f1;
-          out->state_commit = sd.f2;
+          out->state_term = res.sd.f0;
+          out->state_vote = res.sd.f1;
+          out->state_commit = res.sd.f2;
         }
-        const uint64_t nents = nops ? klast + 1 : 0;
+        const uint32_t nops = res.nops;
+        const uint64_t nents = nops ? res.klast + 1 : 0;
         out->n_ents = (int64_t)nents;
-        if (nents) {
-          // suffix-min over kk via a reversed inclusive min-scan
+        if (nents && res.nonmono) {
+          // index rewinds: op j is ents[k_j] iff every later op has k > k_j
+          // (suffix-min over kk via a reversed inclusive min-scan)
           EW_CHECK(c->kkrev.ensure((size_t)nops * 8));
           EW_CHECK(c->suf.ensure((size_t)nops * 8));
           EW_CHECK(c->ents.ensure((size_t)nents * sizeof(ewal_entry)));
@@ -406,6 +432,7 @@ static int readall_impl(ewal_ctx *c, const uint8_t *d_buf, uint64_t B, uint64_t 
           hipLaunchKernelGGL(k_reverse_u64, dim3(grid_for(nops, 256)), dim3(256), 0, c->stream, sf, kr, nops);
           hipLaunchKernelGGL(k_ents, dim3(grid_for(nops, 256)), dim3(256), 0, c->stream, c->rd.as<RecDesc>(),
                              c->ops.as<uint32_t>(), nops, kk, kr, c->ents.as<ewal_entry>(), nents);
+          EW_CHECK(hipGetLastError());
         }
         c->last_nents = nents;
       }
@@ -451,7 +478,10 @@ int ewal_ctx_create(int device, ewal_ctx **out) {
   EW_CHECK(hipEventCreate(&c->ev1));
   EW_CHECK(hipEventCreate(&c->evs0));
   EW_CHECK(hipEventCreate(&c->evs1));
-  EW_CHECK(hipHostMalloc((void **)&c->h_small, sizeof(Small), hipHostMallocDefault));
+  EW_CHECK(hipHostMalloc((void **)&c->h_small, sizeof(Small), hipHostMallocMapped));
+  EW_CHECK(hipHostMalloc((void **)&c->h_res, sizeof(ResultDev), hipHostMallocMapped));
+  EW_CHECK(hipHostGetDevicePointer((void **)&c->h_small_dev, c->h_small, 0));
+  EW_CHECK(hipHostGetDevicePointer((void **)&c->h_res_dev, c->h_res, 0));
   EW_CHECK(c->small.ensure(sizeof(Small)));
   *out = c;
   return EWAL_OK;
@@ -461,7 +491,7 @@ void ewal_ctx_destroy(ewal_ctx *c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
   (void)hipStreamSynchronize(c->stream);
-  DevBuf *bufs[] = {&c->pf, &c->v, &c->pwave, &c->desc, &c->wcnt, &c->slots, &c->cbase, &c->ovf, &c->cpos, &c->clen, &c->nxt, &c->exc, &c->E, &c->rs, &c->jl,
+  DevBuf *bufs[] = {&c->mlist, &c->pf, &c->v, &c->pwave, &c->ux, &c->tagg, &c->tpx, &c->wcnt, &c->slots, &c->cbase, &c->ovf, &c->cpos, &c->clen, &c->nxt, &c->exc, &c->E, &c->rs, &c->jl,
                     &c->vis, &c->entry, &c->on, &c->rec_cand, &c->rd, &c->opf, &c->ops, &c->kk, &c->kkrev,
                     &c->suf, &c->ents, &c->recs, &c->tmp, &c->small, &c->sdesc, &c->snaps, &c->hbuf_dev};
   for (DevBuf *b : bufs) b->release();
@@ -470,6 +500,7 @@ void ewal_ctx_destroy(ewal_ctx *c) {
     (void)hipFree(kv.second.shift);
   }
   if (c->h_small) (void)hipHostFree(c->h_small);
+  if (c->h_res) (void)hipHostFree(c->h_res);
   (void)hipEventDestroy(c->ev0);
   (void)hipEventDestroy(c->ev1);
   (void)hipEventDestroy(c->evs0);
@@ -576,7 +607,7 @@ int ewal_crc32_update_device(ewal_ctx *c, uint32_t crc, uint32_t poly, const voi
   int rc = get_tables(c, poly, &tb);
   if (rc) return rc;
   EW_CHECK(c->small.ensure(sizeof(Small)));
-  rc = run_stream(c, tb, (const uint8_t *)d_buf, n, 0, 0, nullptr);
+  rc = run_stream(c, tb, (const uint8_t *)d_buf, n, 0, 0);
   if (rc) return rc;
   // P(n) = lin(all n bytes) from the stream prefixes (one thread).
   EW_CHECK(c->sdesc.ensure(sizeof(uint32_t)));
@@ -604,7 +635,7 @@ int esnap_verify_packed(ewal_ctx *c, const void *d_buf, uint64_t buf_len, const 
   EW_CHECK(c->small.ensure(sizeof(Small)));
   EW_CHECK(hipEventRecord(c->ev0, c->stream));
   if (buf_len) {
-    rc = run_stream(c, tb, (const uint8_t *)d_buf, buf_len, 0, 0, nullptr);
+    rc = run_stream(c, tb, (const uint8_t *)d_buf, buf_len, 0, 0);
     if (rc) return rc;
   }
   std::vector<SnapDesc> h(n);

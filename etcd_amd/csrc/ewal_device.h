@@ -8,16 +8,11 @@
 #define EW_WAVE_BYTES 4096               // 64 lanes x 64 B
 #define EW_WAVES 12                      // k_stream waves per workgroup (768 threads, 3 per SIMD)
 #define EW_THREADS (EW_WAVES * 64)
-#define EW_TILE (EW_WAVES * EW_WAVE_BYTES)  // 64 KiB per tile (one look-back step)
-#define EW_TILE_LOG2 16
-#define EW_R 16                          // LDS replicas of each slicing table
 #define EW_NIL 0xFFFFFFFFu
 #define EW_SLOTS 32                      // candidate slots per 4 KiB unit
 #define EW_VLOG 8                        // v[] holds lin of every 2^EW_VLOG = 256-B super-piece
 #define EW_VPIECE (1 << EW_VLOG)
 #define EW_VPU (EW_WAVE_BYTES / EW_VPIECE)  // v[] values per 4 KiB unit (16)
-#define EW_LDS_SHIFT0 6                  // LDS holds S_{2^6} .. S_{2^15}
-#define EW_LDS_SHIFTS 10
 
 // ---- shift operators S_{2^m} -------------------------------------------
 // Byte tables: tb[k*256 + b] = S_{2^m}(b << 8k).
@@ -50,40 +45,27 @@ __device__ __forceinline__ uint32_t raw_bytes(const uint32_t *t, uint32_t c, con
   return c;
 }
 
-// ---- wave helpers ---------------------------------------------------------
-__device__ __forceinline__ uint32_t wave_xor(uint32_t x) {
-#pragma unroll
-  for (int d = 32; d >= 1; d >>= 1) x ^= __shfl_xor(x, d);
-  return x;
-}
-__device__ __forceinline__ unsigned long long wave_sum64(unsigned long long x) {
-#pragma unroll
-  for (int d = 32; d >= 1; d >>= 1) x += __shfl_xor(x, d);
-  return x;
-}
-
-// Tile descriptor for the decoupled look-back (one per 64 KiB tile).
-// agg  : VALID | count << 32 | lin(tile)        (one 8-byte sc1 store)
-// inc  : VALID | prefix lin through this tile   (stored after inc_cnt, drained)
-// inc_cnt: inclusive candidate count
-struct TileDesc {
-  unsigned long long agg, inc, inc_cnt, pad;
+// ---- byte sources for the protobuf walkers --------------------------------
+// A plain global pointer, or WinReader: the first n bytes from an LDS copy
+// (the frame head k_decode loaded with a few vector loads), the rest from
+// global memory.  gptr() is the global address of byte 0 (proto.Skip).
+struct WinReader {
+  const uint8_t *w;   // LDS copy of bytes [0, n)
+  int64_t n;
+  const uint8_t *g;   // the same bytes in global memory
+  __device__ __forceinline__ uint8_t operator[](int64_t i) const { return i < n ? w[i] : g[i]; }
 };
-#define EW_DESC_VALID (1ull << 63)
-
-template <typename T>
-__device__ __forceinline__ T ld_agent(T *p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+__device__ __forceinline__ WinReader operator+(const WinReader &r, int64_t k) {
+  return WinReader{r.w + k, r.n - k, r.g + k};
 }
-template <typename T>
-__device__ __forceinline__ void st_agent(T *p, T v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
+__device__ __forceinline__ const uint8_t *gptr(const uint8_t *p) { return p; }
+__device__ __forceinline__ const uint8_t *gptr(const WinReader &r) { return r.g; }
 
 // ---- Go varint readers (shifts >= width give 0) --------------------------
 // Reads buf[base+i...] while i < l; returns 0 or EWAL_ERR_UNEXPECTED_EOF (2).
 // width 32 keeps Go's uint32/int32 truncation ((uint32(b)&0x7F) << 28 loses bits).
-__device__ __forceinline__ int rd_varint(const uint8_t *p, int64_t &i, int64_t l, uint64_t &v, int width) {
+template <class P>
+__device__ __forceinline__ int rd_varint(const P &p, int64_t &i, int64_t l, uint64_t &v, int width) {
   for (uint32_t shift = 0;; shift += 7) {
     if (i >= l) return 2;
     uint8_t b = p[i++];
@@ -202,8 +184,8 @@ struct PbField {
 };
 __device__ __forceinline__ void pbf_init(PbField &f) { f.v = 0; f.boff = -1; f.blen = 0; }
 
-template <int K>
-__device__ __forceinline__ int pb_field(const uint8_t *p, int64_t &i, int64_t l, int wt, PbField &f, uint64_t *rep,
+template <int K, class P>
+__device__ __forceinline__ int pb_field(const P &p, int64_t &i, int64_t l, int wt, PbField &f, uint64_t *rep,
                                         uint32_t repcap) {
   if (K == PB_BYTES) {
     if (wt != 2) return 7;
@@ -233,8 +215,8 @@ __device__ __forceinline__ int pb_field(const uint8_t *p, int64_t &i, int64_t l,
   }
 }
 
-template <int K1, int K2, int K3, int K4, int K5>
-__device__ inline int pb_walk(const uint8_t *p, int64_t l, PbField &f1, PbField &f2, PbField &f3, PbField &f4,
+template <int K1, int K2, int K3, int K4, int K5, class P>
+__device__ inline int pb_walk(const P &p, int64_t l, PbField &f1, PbField &f2, PbField &f3, PbField &f4,
                               PbField &f5, int &unrec, uint64_t *rep2, uint64_t *rep5, uint32_t repcap) {
   int64_t i = 0;
   unrec = 0;
@@ -260,7 +242,7 @@ __device__ inline int pb_walk(const uint8_t *p, int64_t l, PbField &f1, PbField 
     do { ++sow; w >>= 7; } while (w);
     i -= sow;
     int64_t skippy;
-    st = pb_skip(p + i, l - i, skippy);
+    st = pb_skip(gptr(p) + i, l - i, skippy);
     if (st) return st;
     int64_t hi = (int64_t)((uint64_t)i + (uint64_t)skippy);
     if (hi > l) return 2;

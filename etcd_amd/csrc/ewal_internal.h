@@ -20,14 +20,21 @@ struct StreamArgs {
 };
 
 struct ScanArgs {
-  uint32_t nunits, ntiles;        // ntiles = ceil(nunits / 1024)
-  const uint32_t *v, *wcnt;       // piece lins, candidate counts (k_stream)
+  uint32_t nunits, ntiles;        // ntiles = ceil(nunits / 1024) (4 MiB tiles)
+  const uint32_t *v, *wcnt;       // super-piece lins, candidate counts (k_stream)
   const uint32_t *g_shift;
+  uint32_t *ux;                   // lin of every 4 KiB unit          [nunits]
+  uint32_t *tagg, *tcnt;          // tile aggregates                  [ntiles]
+  uint32_t *tpx;                  // P at every tile start            [ntiles]
+  unsigned long long *tcb;        // candidates before every tile     [ntiles]
   uint32_t *pwave;                // stream prefix at every unit start
   unsigned long long *cbase;      // candidates before every unit
-  TileDesc *desc;                 // [ntiles], zeroed per launch
-  uint32_t *ticket, *errflag;
   unsigned long long *total;      // all candidates
+  // compaction (find_cand only): slots -> dense sorted candidate list
+  const uint16_t *slots;          // nullptr: no compaction
+  uint64_t *cpos;
+  uint64_t ccap;
+  uint32_t *ovf, *novf;           // units with more than EW_SLOTS candidates (k_rescan)
 };
 
 // Per-frame descriptor (device), 96 B.
@@ -63,4 +70,33 @@ struct SnapDesc {
   uint64_t doff, dlen;     // snappb.Snapshot.Data
   uint32_t stored, computed;
   int32_t st, pad;
+};
+
+// Per-call device scratch (zeroed / initialised each call).
+struct Small {
+  uint32_t ticket;
+  uint32_t errflag;
+  uint32_t novf;
+  uint32_t irregular;             // k_link: the candidates do not form one chain from byte 0
+  unsigned long long total;       // candidates (k_uscan)
+  uint64_t pos0;                  // first candidate position (~0: none)
+  uint64_t q;                     // regular chain: offset after the last frame
+  int64_t qlen;                   // the int64 at q when q + 8 <= B
+  ChainInfo ci;
+  ReadAllAgg agg;
+  uint32_t nsel;                  // hipcub select counts
+  uint32_t nsel2;
+  uint32_t nsel3;                 // entry ops
+  uint32_t nonmono;               // k_gap: entry indexes not strictly increasing
+  uint64_t klast;                 // k of the last entry op (len(ents) - 1)
+  uint32_t nmeta;                 // metadata frames listed by k_verify
+  uint32_t pad1;
+};
+
+// Everything the host needs after the frame pass, gathered by k_result.
+struct ResultDev {
+  ReadAllAgg agg;
+  RecDesc fail, lastent, last, md, sd;
+  uint32_t nops, nonmono;
+  uint64_t klast;
 };

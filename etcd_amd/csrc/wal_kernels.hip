@@ -199,78 +199,6 @@ __device__ __forceinline__ void next3_fast(const ew_v3u &nxt, uint32_t (&D)[19])
   D[18] = (uint32_t)__builtin_amdgcn_update_dpp((int)nxt.z, (int)D[2], EW_DPP_WAVE_SHL1, 0xf, 0xf, false);
 }
 
-// Decoupled look-back (Merrill & Garland) over 64 predecessors per step, for
-// tiles of 2^tile_log2 bytes.  Returns (X, N): the stream prefix
-// lin(stream[0 .. t*TILE)) and the candidate count before tile t, and
-// publishes tile t's inclusive values.  Called by one whole wave.
-__device__ __forceinline__ void lookback(TileDesc *desc, uint32_t t, uint32_t agg, uint32_t cnt, int tile_log2,
-                                         const uint32_t *g_shift, uint32_t &X, unsigned long long &N,
-                                         uint32_t *errflag) {
-  const int lane = threadIdx.x & 63;
-  uint32_t accx = 0;
-  unsigned long long accn = 0;
-  if (t > 0) {
-    if (lane == 0) st_agent(&desc[t].agg, EW_DESC_VALID | ((unsigned long long)cnt << 32) | agg);
-    uint64_t acc_tiles = 0;
-    int64_t j = (int64_t)t - 1;
-    uint32_t spins = 0;
-    for (;;) {
-      int64_t idx = j - lane;
-      unsigned long long inc = 0, ag = 0;
-      int st;
-      if (idx < 0) {
-        st = 2;
-      } else {
-        inc = ld_agent(&desc[idx].inc);
-        if (inc & EW_DESC_VALID) {
-          st = 2;
-        } else {
-          ag = ld_agent(&desc[idx].agg);
-          st = (ag & EW_DESC_VALID) ? 1 : 0;
-        }
-      }
-      unsigned long long m2 = __ballot(st == 2), m0 = __ballot(st == 0);
-      int f2 = m2 ? __ffsll((long long)m2) - 1 : 64;
-      int f0 = m0 ? __ffsll((long long)m0) - 1 : 64;
-      if (f2 < f0) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        uint32_t term = 0;
-        unsigned long long tn = 0;
-        if (lane < f2) {
-          term = gshift_n(g_shift, (acc_tiles + lane) << tile_log2, (uint32_t)ag);
-          tn = (ag >> 32) & 0x7fffffffull;
-        } else if (lane == f2 && idx >= 0) {
-          tn = ld_agent(&desc[idx].inc_cnt);
-          term = gshift_n(g_shift, (acc_tiles + lane) << tile_log2, (uint32_t)inc);
-        }
-        accx ^= wave_xor(term);
-        accn += wave_sum64(tn);
-        break;
-      }
-      if (f0 < 64) {
-        if (++spins > (1u << 24)) {
-          if (lane == 0) atomicOr(errflag, 1u);
-          break;
-        }
-        __builtin_amdgcn_s_sleep(1);
-        continue;
-      }
-      uint32_t term = gshift_n(g_shift, (acc_tiles + lane) << tile_log2, (uint32_t)ag);
-      accx ^= wave_xor(term);
-      accn += wave_sum64((ag >> 32) & 0x7fffffffull);
-      acc_tiles += 64;
-      j -= 64;
-    }
-  }
-  X = accx;
-  N = accn;
-  if (lane == 0) {
-    uint32_t I = gshift_pow2(g_shift, tile_log2, accx) ^ agg;
-    st_agent(&desc[t].inc_cnt, accn + cnt);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    st_agent(&desc[t].inc, EW_DESC_VALID | (unsigned long long)I);
-  }
-}
 
 // DPP controls (GFX9 family): row_shr:n = 0x110 + n, row_bcast:15 / :31.
 #define EW_DPP_ROW_SHR(n) (0x110 + (n))
@@ -389,9 +317,10 @@ __device__ __forceinline__ void stream_units(const StreamArgs &a, const uint8_t 
     const uint32_t o = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c[i], EW_DPP_ROW_SHR(2), 0xf, 0xf, false);
     c[i] ^= tab_apply(s_s128, top ? o : 0u);
   }
+  // plain stores (measured a little faster than nontemporal ones here)
   if (top && !(a.ablate & 4)) {
 #pragma unroll
-    for (int i = 0; i < NU; ++i) __builtin_nontemporal_store(c[i], a.v + (uint64_t)u[i] * EW_VPU + (lane >> 2));
+    for (int i = 0; i < NU; ++i) a.v[(uint64_t)u[i] * EW_VPU + (lane >> 2)] = c[i];
   }
 #pragma unroll
   for (int i = 0; i < NU; ++i) {
@@ -511,94 +440,196 @@ __global__ __launch_bounds__(EW_THREADS, 1) void k_stream(StreamArgs a) {
   }
 }
 
-// Scan of the unit aggregates: 1024 units (4 MiB of stream) per workgroup.
-// Each thread first forms its unit's aggregate lin(4 KiB) from the unit's 16
-// super-piece lins v[] (k_stream): Horner with S_256 (conflict-free perm
-// layout) joined with S_1024.  Then wave shuffles + one
-// look-back per workgroup.  Writes pwave[u] = P at the unit's start and
-// cbase[u] = candidates before the unit.
-__global__ __launch_bounds__(1024, 1) void k_uscan(ScanArgs a) {
-  __shared__ __attribute__((aligned(16))) uint8_t s_svp[EW_SLICE_DWORDS * 4];   // S_256, 128 KiB
-  __shared__ uint32_t s_shift[6 * 1024];   // S_{2^12} .. S_{2^17}
-  __shared__ uint32_t s_s1k[1024];         // S_1024
-  __shared__ uint32_t s_wq[16], s_wc[16], s_base[16];
-  __shared__ unsigned long long s_cb[16];
-  __shared__ uint32_t s_tile;
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  for (int i = tid; i < EW_SLICE_DWORDS; i += 1024) ((uint32_t *)s_svp)[i] = a.g_shift[shift_src(EW_VLOG, i)];
-  for (int i = tid; i < 6 * 1024; i += 1024) s_shift[i] = a.g_shift[12 * 1024 + i];
-  s_s1k[tid] = a.g_shift[10 * 1024 + tid];
-  if (tid == 0) s_tile = atomicAdd(a.ticket, 1u);
-  __syncthreads();
-  const uint32_t t = s_tile;
-  const uint32_t u = t * 1024 + tid;
-  uint32_t x = 0;
-  if (u < a.nunits) {   // four Horner chains of four 256-B values, joined with S_1024
-    uint32_t Lt[4];
-    lane_regs(lane, Lt);
-    const uint4 *vq = (const uint4 *)(a.v + (size_t)u * EW_VPU);
-    uint4 q[4];
-#pragma unroll
-    for (int g = 0; g < 4; ++g) q[g] = vq[g];
-    uint32_t h[4];
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      h[g] = perm_step(s_svp, Lt, q[g].x, q[g].y);
-      h[g] = perm_step(s_svp, Lt, h[g], q[g].z);
-      h[g] = perm_step(s_svp, Lt, h[g], q[g].w);
-    }
-    x = tab_apply(s_s1k, tab_apply(s_s1k, tab_apply(s_s1k, h[0]) ^ h[1]) ^ h[2]) ^ h[3];
-  }
-  const uint32_t cx = u < a.nunits ? a.wcnt[u] : 0u;
-  // inclusive wave scan (units of 4 KiB -> shift 2^(12+d))
-  uint32_t q = x, qc = cx;
+// ===========================================================================
+// unit scan: stream prefixes P at every 4 KiB unit, candidate bases, and the
+// dense candidate list -- three launches, no inter-workgroup waiting:
+//   k_uagg   per 4 MiB tile (1024 units, one workgroup): each unit's
+//            aggregate lin(4 KiB) from its 16 super-piece lins v[] (Horner
+//            with S_256 joined with S_1024) -> ux[u]; the tile's affine
+//            aggregate and candidate count -> tagg[t], tcnt[t]
+//   k_tscan  one workgroup scans the tile aggregates -> tpx[t] (P at the
+//            tile start), tcb[t] (candidates before the tile), *total
+//   k_uapply per tile: the in-tile scan of ux / wcnt on top of the tile's
+//            prefix -> pwave[u], cbase[u]; compacts the unit's candidate
+//            slots into cpos[] (units with more than EW_SLOTS: k_rescan)
+// ===========================================================================
+
+// inclusive affine scan over a wave of units (4 KiB each): value q = lin of
+// the lane's span, count qc; tables s + d*1024 = S_{2^(12+d)}
+__device__ __forceinline__ void wave_unit_scan(const uint32_t *s, uint32_t &q, uint32_t &qc) {
+  const int lane = threadIdx.x & 63;
 #pragma unroll
   for (int d = 0; d < 6; ++d) {
-    uint32_t o = __shfl_up(q, 1 << d);
-    uint32_t oc = __shfl_up(qc, 1 << d);
+    const uint32_t o = __shfl_up(q, 1 << d), oc = __shfl_up(qc, 1 << d);
     if (lane >= (1 << d)) {
-      q = tab_apply(s_shift + d * 1024, o) ^ q;   // S_{2^(12+d)}
+      q = tab_apply(s + d * 1024, o) ^ q;
       qc += oc;
     }
   }
-  uint32_t ex = __shfl_up(q, 1), exc = __shfl_up(qc, 1);
-  if (lane == 0) { ex = 0; exc = 0; }
-  if (lane == 63) { s_wq[wv] = q; s_wc[wv] = qc; }
-  __syncthreads();
-  if (wv == 0) {
-    uint32_t w = lane < 16 ? s_wq[lane] : 0u, wc = lane < 16 ? s_wc[lane] : 0u;
+}
+// inclusive scan of the 16 wave totals (256 KiB each) in lanes 0..15 of one
+// wave; tables s + (6 + d)*1024 = S_{2^(18+d)}
+__device__ __forceinline__ void block_wave_scan(const uint32_t *s, uint32_t &w, uint32_t &wc) {
+  const int lane = threadIdx.x & 63;
 #pragma unroll
-    for (int d = 0; d < 4; ++d) {
-      uint32_t o = __shfl_up(w, 1 << d), oc = __shfl_up(wc, 1 << d);
-      if (lane >= (1 << d) && lane < 16) {
-        w = tab_apply(a.g_shift + (18 + d) * 1024, o) ^ w;   // waves of 256 KiB -> 2^(18+d)
-        wc += oc;
+  for (int d = 0; d < 4; ++d) {
+    const uint32_t o = __shfl_up(w, 1 << d), oc = __shfl_up(wc, 1 << d);
+    if (lane >= (1 << d) && lane < 16) {
+      w = tab_apply(s + (6 + d) * 1024, o) ^ w;
+      wc += oc;
+    }
+  }
+}
+
+__global__ __launch_bounds__(1024) void k_uagg(ScanArgs a) {
+  __shared__ uint32_t s_svp[1024], s_s1k[1024];   // S_256, S_1024
+  __shared__ uint32_t s_sh[10 * 1024];            // S_{2^12} .. S_{2^21}
+  __shared__ uint32_t s_wq[16], s_wc[16];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  s_svp[tid] = a.g_shift[EW_VLOG * 1024 + tid];
+  s_s1k[tid] = a.g_shift[10 * 1024 + tid];
+  for (int i = tid; i < 10 * 1024; i += 1024) s_sh[i] = a.g_shift[12 * 1024 + i];
+  __syncthreads();
+  for (uint32_t t = blockIdx.x; t < a.ntiles; t += gridDim.x) {   // persistent: tables staged once
+    const uint32_t u = t * 1024 + tid;
+    uint32_t x = 0, cx = 0;
+    if (u < a.nunits) {   // four Horner chains of four 256-B values, joined with S_1024
+      const uint4 *vq = (const uint4 *)(a.v + (size_t)u * EW_VPU);
+      uint4 q[4];
+  #pragma unroll
+      for (int g = 0; g < 4; ++g) q[g] = vq[g];
+      uint32_t h[4];
+  #pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        h[g] = tab_apply(s_svp, q[g].x) ^ q[g].y;
+        h[g] = tab_apply(s_svp, h[g]) ^ q[g].z;
+        h[g] = tab_apply(s_svp, h[g]) ^ q[g].w;
+      }
+      x = tab_apply(s_s1k, tab_apply(s_s1k, tab_apply(s_s1k, h[0]) ^ h[1]) ^ h[2]) ^ h[3];
+      cx = a.wcnt[u];
+      a.ux[u] = x;
+    }
+    uint32_t q = x, qc = cx;
+    wave_unit_scan(s_sh, q, qc);
+    if (lane == 63) { s_wq[wv] = q; s_wc[wv] = qc; }
+    __syncthreads();
+    if (wv == 0) {
+      uint32_t w = lane < 16 ? s_wq[lane] : 0u, wc = lane < 16 ? s_wc[lane] : 0u;
+      block_wave_scan(s_sh, w, wc);
+      if (lane == 15) { a.tagg[t] = w; a.tcnt[t] = wc; }
+    }
+    __syncthreads();
+  }
+}
+
+// One workgroup: exclusive affine scan of the tile aggregates (4 MiB each),
+// 1024 tiles per round with a carried prefix.
+__global__ __launch_bounds__(1024) void k_tscan(ScanArgs a) {
+  __shared__ uint32_t s_sh[10 * 1024];            // S_{2^22} .. S_{2^31}
+  __shared__ uint32_t s_wq[16], s_wc[16], s_base[16];
+  __shared__ unsigned long long s_cb[16];
+  __shared__ uint32_t s_carry;
+  __shared__ unsigned long long s_ncarry;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  for (int i = tid; i < 10 * 1024; i += 1024) s_sh[i] = a.g_shift[22 * 1024 + i];
+  if (tid == 0) { s_carry = 0; s_ncarry = 0; }
+  __syncthreads();
+  for (uint32_t t0 = 0; t0 < a.ntiles; t0 += 1024) {
+    const uint32_t t = t0 + tid;
+    const uint32_t x = t < a.ntiles ? a.tagg[t] : 0u;
+    const uint32_t cx = t < a.ntiles ? a.tcnt[t] : 0u;
+    uint32_t q = x, qc = cx;
+    wave_unit_scan(s_sh, q, qc);   // tables are S_{2^(22+d)} here
+    uint32_t ex = __shfl_up(q, 1), exc = __shfl_up(qc, 1);
+    if (lane == 0) { ex = 0; exc = 0; }
+    if (lane == 63) { s_wq[wv] = q; s_wc[wv] = qc; }
+    __syncthreads();
+    if (wv == 0) {
+      uint32_t w = lane < 16 ? s_wq[lane] : 0u, wc = lane < 16 ? s_wc[lane] : 0u;
+      block_wave_scan(s_sh, w, wc);   // S_{2^(28+d)}
+      uint32_t we = __shfl_up(w, 1), wce = __shfl_up(wc, 1);
+      if (lane == 0) { we = 0; wce = 0; }
+      const uint32_t X = s_carry;
+      const unsigned long long N = s_ncarry;
+      if (lane < 16) {
+        uint32_t xs = X;                     // S_{lane * 2^28}(X)
+#pragma unroll
+        for (int b = 0; b < 4; ++b)
+          if ((lane >> b) & 1) xs = tab_apply(s_sh + (6 + b) * 1024, xs);
+        s_base[lane] = xs ^ we;
+        s_cb[lane] = N + wce;
+      }
+      const uint32_t tot = __shfl(w, 15), totc = __shfl(wc, 15);
+      if (lane == 0) {   // carry over 1024 tiles = 2^32 bytes
+        s_carry = gshift_pow2(a.g_shift, 32, X) ^ tot;
+        s_ncarry = N + totc;
       }
     }
-    const uint32_t tagg = __shfl(w, 15), tcnt = __shfl(wc, 15);
-    uint32_t we = __shfl_up(w, 1), wce = __shfl_up(wc, 1);
-    if (lane == 0) { we = 0; wce = 0; }
-    uint32_t X;
-    unsigned long long N;
-    lookback(a.desc, t, tagg, tcnt, 22, a.g_shift, X, N, a.errflag);
-    if (lane < 16) {
-      uint32_t xs = X;                         // S_{lane * 2^18}(X)
+    __syncthreads();
+    if (t < a.ntiles) {
+      uint32_t b = s_base[wv];                 // S_{lane * 2^22}(base)
 #pragma unroll
-      for (int b = 0; b < 4; ++b)
-        if ((lane >> b) & 1) xs = tab_apply(a.g_shift + (18 + b) * 1024, xs);
-      s_base[lane] = xs ^ we;
-      s_cb[lane] = N + wce;
+      for (int k = 0; k < 6; ++k)
+        if ((lane >> k) & 1) b = tab_apply(s_sh + k * 1024, b);
+      a.tpx[t] = b ^ ex;
+      a.tcb[t] = s_cb[wv] + exc;
     }
-    if (lane == 0 && t == a.ntiles - 1) *a.total = N + tcnt;
+    __syncthreads();
   }
+  if (tid == 0) *a.total = s_ncarry;
+}
+
+__global__ __launch_bounds__(1024) void k_uapply(ScanArgs a) {
+  __shared__ uint32_t s_sh[10 * 1024];            // S_{2^12} .. S_{2^21}
+  __shared__ uint32_t s_wq[16], s_wc[16], s_base[16];
+  __shared__ unsigned long long s_cb[16];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  for (int i = tid; i < 10 * 1024; i += 1024) s_sh[i] = a.g_shift[12 * 1024 + i];
   __syncthreads();
-  if (u < a.nunits) {
-    uint32_t b = s_base[wv];                   // S_{lane * 4096}(base)
-#pragma unroll
-    for (int k = 0; k < 6; ++k)
-      if ((lane >> k) & 1) b = tab_apply(s_shift + k * 1024, b);
-    a.pwave[u] = b ^ ex;
-    a.cbase[u] = s_cb[wv] + exc;
+  for (uint32_t t = blockIdx.x; t < a.ntiles; t += gridDim.x) {   // persistent: tables staged once
+    const uint32_t u = t * 1024 + tid;
+    const uint32_t x = u < a.nunits ? a.ux[u] : 0u;
+    const uint32_t cx = u < a.nunits ? a.wcnt[u] : 0u;
+    uint32_t q = x, qc = cx;
+    wave_unit_scan(s_sh, q, qc);
+    uint32_t ex = __shfl_up(q, 1), exc = __shfl_up(qc, 1);
+    if (lane == 0) { ex = 0; exc = 0; }
+    if (lane == 63) { s_wq[wv] = q; s_wc[wv] = qc; }
+    __syncthreads();
+    if (wv == 0) {
+      uint32_t w = lane < 16 ? s_wq[lane] : 0u, wc = lane < 16 ? s_wc[lane] : 0u;
+      block_wave_scan(s_sh, w, wc);
+      uint32_t we = __shfl_up(w, 1), wce = __shfl_up(wc, 1);
+      if (lane == 0) { we = 0; wce = 0; }
+      if (lane < 16) {
+        uint32_t xs = a.tpx[t];                  // S_{lane * 2^18}(P at the tile start)
+  #pragma unroll
+        for (int b = 0; b < 4; ++b)
+          if ((lane >> b) & 1) xs = tab_apply(s_sh + (6 + b) * 1024, xs);
+        s_base[lane] = xs ^ we;
+        s_cb[lane] = a.tcb[t] + wce;
+      }
+    }
+    __syncthreads();
+    if (u < a.nunits) {
+      uint32_t b = s_base[wv];                   // S_{lane * 4096}(base)
+  #pragma unroll
+      for (int k = 0; k < 6; ++k)
+        if ((lane >> k) & 1) b = tab_apply(s_sh + k * 1024, b);
+      a.pwave[u] = b ^ ex;
+      const unsigned long long base = s_cb[wv] + exc;
+      a.cbase[u] = base;
+      if (a.slots && cx) {   // compaction: slots -> the dense, position-sorted candidate list
+        if (cx > EW_SLOTS) {
+          a.ovf[atomicAdd(a.novf, 1u)] = u;
+        } else {
+          const uint16_t *sl = a.slots + (size_t)u * EW_SLOTS;
+          for (uint32_t j = 0; j < cx; ++j)
+            if (base + j < a.ccap) a.cpos[base + j] = (uint64_t)u * EW_WAVE_BYTES + sl[j];
+        }
+      }
+    }
+    __syncthreads();
   }
 }
 
@@ -659,27 +690,68 @@ __global__ void k_rescan(const uint8_t *__restrict__ buf, uint64_t B, const uint
 // ===========================================================================
 // framing: candidate links, runs, pointer jumping
 // ===========================================================================
-__global__ void k_link(const uint64_t *__restrict__ pos, const uint64_t *__restrict__ len, uint32_t K,
-                       uint32_t *__restrict__ nxt, uint8_t *__restrict__ exc) {
-  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= K) return;
-  const uint64_t s = pos[i] + 8 + len[i];
-  uint32_t r = EW_NIL;
-  if (i + 1 < K) {
-    const uint64_t p1 = pos[i + 1];
-    if (p1 == s) {
-      r = i + 1;
-    } else if (p1 < s) {
-      uint32_t lo = i + 2, hi = K;
-      while (lo < hi) {
-        uint32_t mid = lo + ((hi - lo) >> 1);
-        if (pos[mid] < s) lo = mid + 1; else hi = mid;
-      }
-      if (lo < K && pos[lo] == s) r = lo;
-    }
+// little-endian int64 at byte offset p of the stream (buf 8-B aligned);
+// never reads at or beyond B
+__device__ __forceinline__ uint64_t ld_le64_b(const uint8_t *buf, uint64_t B, uint64_t p) {
+  const uint64_t al = p & ~7ull;
+  if (al + 16 <= B) {
+    const uint64_t lo = *(const uint64_t *)(buf + al), hi = *(const uint64_t *)(buf + al + 8);
+    const uint32_t sh = (uint32_t)(p & 7) * 8;
+    return sh ? (lo >> sh) | (hi << (64 - sh)) : lo;
   }
-  nxt[i] = r;
-  exc[i] = (r != i + 1);
+  uint64_t v = 0;
+  for (int i = 0; i < 8; ++i)
+    if (p + i < B) v |= (uint64_t)buf[p + i] << (8 * i);
+  return v;
+}
+
+// Candidate i -> its length L (the int64 prefix) and successor candidate
+// (pos + 8 + L), grid-stride over the K candidates counted on the device.
+// Also decides whether the candidates form ONE chain from byte 0 (the
+// normal case: nxt[i] == i + 1 everywhere), so the pointer-jumping framing
+// can be skipped, and records that chain's terminal offset q and the int64
+// there; initialises the ReadAll reductions.
+__global__ __launch_bounds__(256) void k_link(const uint8_t *__restrict__ buf, uint64_t B,
+                                              const uint64_t *__restrict__ pos, uint64_t *__restrict__ len,
+                                              uint64_t ccap, uint32_t *__restrict__ nxt, uint8_t *__restrict__ exc,
+                                              Small *ds) {
+  const uint64_t K = ds->total < ccap ? ds->total : ccap;
+  const uint64_t g0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, stride = (uint64_t)gridDim.x * blockDim.x;
+  if (g0 == 0) {
+    ds->agg.first_fail = ~0ull;
+    ds->agg.last_entry = -1;
+    ds->agg.last_state = -1;
+    ds->agg.first_meta = ~0ull;
+    ds->pos0 = K ? pos[0] : ~0ull;
+  }
+  uint32_t irr = 0;
+  for (uint64_t i = g0; i < K; i += stride) {
+    const uint64_t p = pos[i];
+    const uint64_t L = ld_le64_b(buf, B, p);
+    len[i] = L;
+    const uint64_t s = p + 8 + L;
+    uint32_t r = EW_NIL;
+    if (i + 1 < K) {
+      const uint64_t p1 = pos[i + 1];
+      if (p1 == s) {
+        r = (uint32_t)(i + 1);
+      } else if (p1 < s) {
+        uint64_t lo = i + 2, hi = K;
+        while (lo < hi) {
+          const uint64_t mid = lo + ((hi - lo) >> 1);
+          if (pos[mid] < s) lo = mid + 1; else hi = mid;
+        }
+        if (lo < K && pos[lo] == s) r = (uint32_t)lo;
+      }
+      if (r != i + 1) irr = 1;
+    } else {   // the last candidate: terminal of the regular chain
+      ds->q = s;
+      ds->qlen = (s <= B && B - s >= 8) ? (int64_t)ld_le64_b(buf, B, s) : 0;
+    }
+    nxt[i] = r;
+    exc[i] = (r != i + 1);
+  }
+  if (__ballot(irr) && (threadIdx.x & 63) == 0) atomicOr(&ds->irregular, 1u);
 }
 
 __device__ __forceinline__ uint32_t lower_bound_u32(const uint32_t *E, uint32_t R, uint32_t x) {
@@ -802,14 +874,20 @@ __device__ __forceinline__ uint32_t prefix_at(uint64_t x, const uint32_t *__rest
 // k_decode: parse frame r, and P at its frame start and data start:
 //   Pd[r] = P(doff) = raw(P(off), frame header bytes)
 // plus, for the last frame, P at its data end (the frame after it is not on
-// the chain).
-__global__ __launch_bounds__(256) void k_decode(const uint8_t *__restrict__ buf, const uint64_t *__restrict__ pos,
-                         const uint64_t *__restrict__ len, const uint32_t *__restrict__ rec_cand, uint32_t n,
+// the chain).  The frame head (80 bytes from the 16-B boundary below the
+// frame start) is fetched with five vector loads, issued together with
+// prefix_at's loads, and parsed out of LDS: a canonical Record + Entry head
+// is at most ~50 bytes, so the walkers' byte reads do not go to HBM.
+// rec_cand == nullptr: frame r is candidate r (the regular chain).
+__global__ __launch_bounds__(256) void k_decode(const uint8_t *__restrict__ buf, uint64_t B,
+                         const uint64_t *__restrict__ pos, const uint64_t *__restrict__ len,
+                         const uint32_t *__restrict__ rec_cand, uint32_t n,
                          const uint32_t *__restrict__ pwave, const uint32_t *__restrict__ v,
                          const uint32_t *__restrict__ g_slice, const uint32_t *__restrict__ g_shift,
-                         RecDesc *__restrict__ rd, uint32_t *__restrict__ pf) {
+                         RecDesc *__restrict__ rd, uint32_t *__restrict__ pf, int dbg) {
   __shared__ uint32_t s_t4[1024];
   __shared__ uint32_t s_svp[1024];   // S_256 (prefix_at's Horner step)
+  __shared__ uint4 s_win[256][5];
   for (int i = threadIdx.x; i < 1024; i += blockDim.x) {
     s_t4[i] = g_slice[i];
     s_svp[i] = g_shift[EW_VLOG * 1024 + i];
@@ -817,9 +895,25 @@ __global__ __launch_bounds__(256) void k_decode(const uint8_t *__restrict__ buf,
   __syncthreads();
   uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= n) return;
-  const uint32_t i = rec_cand[r];
+  const uint32_t i = rec_cand ? rec_cand[r] : r;
   const uint64_t p = pos[i];
   const int64_t L = (int64_t)len[i];
+  const uint64_t p16 = p & ~15ull;
+#pragma unroll
+  for (int k = 0; k < 5; ++k) {
+    const uint64_t o = p16 + 16 * k;
+    uint4 w;
+    if (o + 16 <= B) {
+      w = *(const uint4 *)(buf + o);
+    } else {
+      uint32_t x[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) x[j] = load_word_guarded(buf, B, o + 4 * j);
+      w = make_uint4(x[0], x[1], x[2], x[3]);
+    }
+    s_win[threadIdx.x][k] = w;
+  }
+  const WinReader R{(const uint8_t *)&s_win[threadIdx.x][0] + (p - p16), (int64_t)(80 - (p - p16)), buf + p};
   RecDesc d;
   d.off = p;
   d.type = 0; d.crc = 0; d.chained = 0; d.st = 0; d.sub_st = 0;
@@ -828,15 +922,15 @@ __global__ __launch_bounds__(256) void k_decode(const uint8_t *__restrict__ buf,
   PbField a1, a2, a3, a4, a5;
   pbf_init(a1); pbf_init(a2); pbf_init(a3); pbf_init(a4); pbf_init(a5);
   int unrec;
-  int st = pb_walk<PB_VAR64, PB_VAR32, PB_BYTES, PB_NONE, PB_NONE>(buf + p + 8, L, a1, a2, a3, a4, a5, unrec,
+  int st = (dbg & 256) ? 0 : pb_walk<PB_VAR64, PB_VAR32, PB_BYTES, PB_NONE, PB_NONE>(R + 8, L, a1, a2, a3, a4, a5, unrec,
                                                                      nullptr, nullptr, 0);
   d.type = (int64_t)a1.v;
   d.crc = (uint32_t)a2.v;
   if (a3.blen > 0) { d.doff = p + 8 + a3.boff; d.dlen = a3.blen; d.dnil = 0; }
   d.st = st;
   if (st == 0) {
-    const uint8_t *dp = buf + d.doff;
-    if (d.type == 2) {           // entryType: mustUnmarshalEntry
+    const WinReader dp = R + (int64_t)(d.doff - p);
+    if (d.type == 2 && !(dbg & 512)) {           // entryType: mustUnmarshalEntry
       PbField e1, e2, e3, e4, e5;
       pbf_init(e1); pbf_init(e2); pbf_init(e3); pbf_init(e4); pbf_init(e5);
       int s2 = 0, ur = 0;
@@ -863,28 +957,42 @@ __global__ __launch_bounds__(256) void k_decode(const uint8_t *__restrict__ buf,
   }
   // P at every frame start (the previous frame's data end, in the canonical
   // layout), and P at this frame's data start from it (header bytes only).
-  const uint32_t Pfo = prefix_at(p, pwave, v, buf, s_t4, s_svp);
+  const uint32_t Pfo = (dbg & 1024) ? 0u : prefix_at(p, pwave, v, buf, s_t4, s_svp);
   pf[n + r] = Pfo;
   if (st == 0 && d.type != 4 && d.dlen > 0) {
-    pf[r] = raw_bytes(s_t4, Pfo, buf, p, d.doff);
+    uint32_t c = Pfo;
+    const int64_t nh = (int64_t)(d.doff - p);
+    for (int64_t j = 0; j < nh; ++j) c = s_t4[(c ^ R[j]) & 0xff] ^ (c >> 8);
+    pf[r] = c;
     if (r == n - 1 || d.doff + d.dlen != p + 8 + (uint64_t)L)
       d.chained = prefix_at(d.doff + d.dlen, pwave, v, buf, s_t4, s_svp);   // P(data end), used by k_verify
   }
   rd[r] = d;
 }
 
-__global__ __launch_bounds__(1024) void k_verify(const uint8_t *__restrict__ buf, const uint32_t *__restrict__ pwave,
-                         const uint32_t *__restrict__ v, const uint32_t *__restrict__ g_slice,
-                         const uint32_t *__restrict__ g_shift, RecDesc *__restrict__ rd, uint32_t n,
-                         const uint32_t *__restrict__ pf, ReadAllAgg *agg) {
+// k_verify: the chained-CRC check of every frame (== the reference's running
+// CRC up to its first failure), the Entry/HardState verdicts, ReadAll's
+// reductions (first failure, last entry / state, first metadata), the
+// entry-op flags (Index >= ri) and the list of metadata frames k_meta checks.
+__global__ __launch_bounds__(1024) void k_verify(const uint32_t *__restrict__ g_shift, RecDesc *__restrict__ rd,
+                         uint32_t n, const uint32_t *__restrict__ pf, uint64_t ri, uint8_t *__restrict__ opf,
+                         uint32_t *__restrict__ mlist, Small *ds) {
+  ReadAllAgg *agg = &ds->agg;
   __shared__ uint32_t s_sh[17 * 1024];   // S_{2^0} .. S_{2^16}
+  __shared__ uint32_t s_red[4];          // block: last entry + 1, last state + 1, first metadata, first failure
   for (int i = threadIdx.x; i < 17 * 1024; i += blockDim.x) s_sh[i] = g_shift[i];
+  if (threadIdx.x == 0) { s_red[0] = 0; s_red[1] = 0; s_red[2] = 0xffffffffu; s_red[3] = 0xffffffffu; }
   __syncthreads();
-  uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
-  if (r >= n) return;
-  RecDesc &d = rd[r];
-  int st = d.st;
+  const uint32_t rt = blockIdx.x * blockDim.x + threadIdx.x;
+  const bool live = rt < n;
+  const uint32_t r = live ? rt : n - 1;   // the whole block reaches the barrier below; writes masked
+  // every load up front: the frame, its neighbours' CRC / offset, the prefixes
+  const RecDesc d = rd[r];
   const uint32_t seed = r ? rd[r - 1].crc : 0u;
+  const uint64_t noff = r + 1 < n ? rd[r + 1].off : ~0ull;
+  const uint32_t ps = pf[r];
+  const uint32_t pn = r + 1 < n ? pf[n + r + 1] : 0u;
+  int st = d.st;
   uint32_t chained = seed;
   if (st == 0) {
     if (d.type == 4) {                      // crcType: ReadAll's check, wal/wal.go:184-192
@@ -898,8 +1006,8 @@ __global__ __launch_bounds__(1024) void k_verify(const uint8_t *__restrict__ buf
         const uint64_t e = d.doff + d.dlen;
         // P(data end) = P(next frame start) in the canonical layout (pf[n+r+1]),
         // else k_decode left it in d.chained.  U(seed, D) = S_n(seed ^ ~0 ^ P(s)) ^ P(e) ^ ~0
-        const uint32_t Pe = (r + 1 < n && rd[r + 1].off == e) ? pf[n + r + 1] : d.chained;
-        uint32_t x = seed ^ 0xffffffffu ^ pf[r];
+        const uint32_t Pe = noff == e ? pn : d.chained;
+        uint32_t x = seed ^ 0xffffffffu ^ ps;
         uint64_t m = d.dlen;
         for (int lvl = 0; m; ++lvl, m >>= 1) {
           if (m & 1) x = lvl <= 16 ? tab_apply(s_sh + lvl * 1024, x) : gshift_pow2(g_shift, lvl, x);
@@ -922,58 +1030,115 @@ __global__ __launch_bounds__(1024) void k_verify(const uint8_t *__restrict__ buf
       }
     }
   }
-  d.st = st;
-  d.chained = chained;
-  if (st != 0) atomicMin(&agg->first_fail, (unsigned long long)r);
-  if (d.type == 2) atomicMax(&agg->last_entry, (long long)r);
-  if (d.type == 3) atomicMax(&agg->last_state, (long long)r);
-  if (d.type == 1 && d.dlen > 0) atomicMin(&agg->first_meta, (unsigned long long)r);
-}
-
-// metadata: `metadata != nil && !reflect.DeepEqual(metadata, rec.Data)`, wal/wal.go:178-183
-__global__ void k_meta(const uint8_t *__restrict__ buf, RecDesc *__restrict__ rd, uint32_t n, ReadAllAgg *agg) {
-  uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
-  if (r >= n) return;
-  const unsigned long long fm = agg->first_meta;
-  if (fm == ~0ull || r <= fm) return;
-  RecDesc &d = rd[r];
-  if (d.type != 1 || d.st != 0) return;
-  const RecDesc &m = rd[fm];
-  bool eq = (d.dlen == m.dlen);
-  for (uint64_t k = 0; eq && k < d.dlen; ++k) eq = buf[d.doff + k] == buf[m.doff + k];
-  if (!eq) {
-    d.st = EWAL_ERR_METADATA_CONFLICT;
-    atomicMin(&agg->first_fail, (unsigned long long)r);
+  if (live) {
+    rd[r].st = st;
+    rd[r].chained = chained;
+    opf[r] = (d.type == 2 && st == 0 && d.f1 >= ri) ? 1 : 0;
+    if (d.type == 1 && st == 0) mlist[atomicAdd(&ds->nmeta, 1u)] = r;   // rare: one per WAL file
+  }
+  // One atomic per WORKGROUP and quantity (same-address atomics from every
+  // wave serialise at the memory side): r grows with the lane and the wave,
+  // so a wave's max is its highest set lane and its min its lowest.
+  const int lane = threadIdx.x & 63;
+  const unsigned long long me = __ballot(live && d.type == 2), ms = __ballot(live && d.type == 3),
+                           mm = __ballot(live && d.type == 1 && d.dlen > 0), mf = __ballot(live && st != 0);
+  const uint32_t r0 = r - lane;
+  if (lane == 0) {
+    if (mf) atomicMin(&s_red[3], r0 + (uint32_t)(__ffsll((long long)mf) - 1));
+    if (me) atomicMax(&s_red[0], r0 + (uint32_t)(63 - __clzll((long long)me)) + 1u);
+    if (ms) atomicMax(&s_red[1], r0 + (uint32_t)(63 - __clzll((long long)ms)) + 1u);
+    if (mm) atomicMin(&s_red[2], r0 + (uint32_t)(__ffsll((long long)mm) - 1));
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    if (s_red[0]) atomicMax(&agg->last_entry, (long long)(s_red[0] - 1));
+    if (s_red[1]) atomicMax(&agg->last_state, (long long)(s_red[1] - 1));
+    if (s_red[2] != 0xffffffffu) atomicMin(&agg->first_meta, (unsigned long long)s_red[2]);
+    if (s_red[3] != 0xffffffffu) atomicMin(&agg->first_fail, (unsigned long long)s_red[3]);
   }
 }
 
-// entry ops: entries with Index >= ri (the `ents = append(ents[:Index-ri], e)` steps)
-__global__ void k_opflag(const RecDesc *__restrict__ rd, uint32_t n, uint64_t ri, uint8_t *__restrict__ f) {
-  uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
-  if (r >= n) return;
-  const RecDesc &d = rd[r];
-  f[r] = (d.type == 2 && d.st == 0 && d.f1 >= ri) ? 1 : 0;
+// metadata: `metadata != nil && !reflect.DeepEqual(metadata, rec.Data)`,
+// wal/wal.go:178-183, over the metadata frames k_verify listed
+__global__ void k_meta(const uint8_t *__restrict__ buf, RecDesc *__restrict__ rd, const uint32_t *__restrict__ mlist,
+                       Small *ds) {
+  const uint32_t nm = ds->nmeta;
+  const unsigned long long fm = ds->agg.first_meta;
+  if (fm == ~0ull) return;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nm; i += gridDim.x * blockDim.x) {
+    const uint32_t r = mlist[i];
+    if (r <= fm) continue;
+    RecDesc &d = rd[r];
+    const RecDesc &m = rd[fm];
+    bool eq = (d.dlen == m.dlen);
+    for (uint64_t k = 0; eq && k < d.dlen; ++k) eq = buf[d.doff + k] == buf[m.doff + k];
+    if (!eq) {
+      d.st = EWAL_ERR_METADATA_CONFLICT;
+      atomicMin(&ds->agg.first_fail, (unsigned long long)r);
+    }
+  }
 }
 
-// gap check: op j needs k_j <= len(ents) = k_{j-1} + 1 (wal/wal.go:173)
-__global__ void k_gap(RecDesc *__restrict__ rd, const uint32_t *__restrict__ ops, uint32_t nops, uint64_t ri,
-                      uint64_t *__restrict__ kk, ReadAllAgg *agg) {
-  uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= nops) return;
-  const uint32_t r = ops[j];
-  const uint64_t k = rd[r].f1 - ri;
-  kk[j] = k;
-  bool gap;
-  if (j == 0) {
-    gap = k > 0;
-  } else {
-    const uint64_t kp = rd[ops[j - 1]].f1 - ri;
-    gap = (k > kp) && (k - kp > 1);
+// gap check: op j needs k_j <= len(ents) = k_{j-1} + 1 (wal/wal.go:173).
+// Grid-stride over the device-side op count; also flags whether the ops'
+// k are strictly increasing, records the last k (len(ents) - 1) and writes
+// ents[j] = op j.
+__global__ void k_gap(RecDesc *__restrict__ rd, const uint32_t *__restrict__ ops, uint64_t ri,
+                      uint64_t *__restrict__ kk, ewal_entry *__restrict__ ents, Small *ds) {
+  const uint32_t nops = ds->nsel3;
+  uint32_t nm = 0;
+  for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < nops; j += gridDim.x * blockDim.x) {
+    const uint32_t r = ops[j];
+    const RecDesc d = rd[r];
+    const uint64_t k = d.f1 - ri;
+    kk[j] = k;
+    bool gap;
+    if (j == 0) {
+      gap = k > 0;
+    } else {
+      const uint64_t kp = rd[ops[j - 1]].f1 - ri;
+      gap = (k > kp) && (k - kp > 1);
+      if (k <= kp) nm = 1;
+    }
+    if (gap) {
+      rd[r].st = EWAL_PANIC_INDEX_GAP;
+      atomicMin(&ds->agg.first_fail, (unsigned long long)r);
+    }
+    if (j == nops - 1) ds->klast = k;
+    // ents[j] = op j; exact when the ops' k are strictly increasing and
+    // gap-free (k_j = j), otherwise the host's survivor pass rewrites ents
+    ewal_entry e;
+    e.term = d.f0;
+    e.index = d.f1;
+    e.data_off = d.edoff;
+    e.data_len = d.edlen;
+    e.type = d.etype;
+    e.data_nil = d.enil;
+    ents[j] = e;
   }
-  if (gap) {
-    rd[r].st = EWAL_PANIC_INDEX_GAP;
-    atomicMin(&agg->first_fail, (unsigned long long)r);
-  }
+  if (__ballot(nm) && (threadIdx.x & 63) == 0) atomicOr(&ds->nonmono, 1u);
+}
+
+// Small -> host-mapped pinned memory: a one-thread kernel is far cheaper
+// than a device-to-host copy of a few hundred bytes.
+__global__ void k_export_small(const Small *ds, Small *h) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) *h = *ds;
+}
+
+// the handful of frames the host result needs, in one struct, written
+// straight into host-mapped pinned memory
+__global__ void k_result(const RecDesc *__restrict__ rd, uint32_t n, const Small *ds, ResultDev *o) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  const ReadAllAgg g = ds->agg;
+  o->agg = g;
+  o->nops = ds->nsel3;
+  o->nonmono = ds->nonmono;
+  o->klast = ds->klast;
+  if (g.first_fail < n) o->fail = rd[g.first_fail];
+  if (g.last_entry >= 0) o->lastent = rd[g.last_entry];
+  if (n) o->last = rd[n - 1];
+  if (g.first_meta != ~0ull) o->md = rd[g.first_meta];
+  if (g.last_state >= 0) o->sd = rd[g.last_state];
 }
 
 // survivors: op j is ents[k_j] iff every later op has k > k_j
