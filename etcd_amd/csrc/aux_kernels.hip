@@ -18,10 +18,8 @@ __global__ __launch_bounds__(256) void k_snap(const uint8_t *__restrict__ buf, c
                        esnap_snapshot *__restrict__ snaps, uint32_t n) {
   __shared__ uint32_t s_t4[1024];
   __shared__ uint32_t s_svp[1024];   // S_256 (prefix_at's Horner step)
-  for (int i = threadIdx.x; i < 1024; i += blockDim.x) {
-    s_t4[i] = g_slice[i];
-    s_svp[i] = g_shift[EW_VLOG * 1024 + i];
-  }
+  stage_lds<256>(s_t4, 1024, [&](int i) { return g_slice[i]; });
+  stage_lds<256>(s_svp, 1024, [&](int i) { return g_shift[EW_VLOG * 1024 + i]; });
   __syncthreads();
   uint32_t f = blockIdx.x * blockDim.x + threadIdx.x;
   if (f >= n) return;

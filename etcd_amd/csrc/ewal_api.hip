@@ -70,7 +70,7 @@ struct ewal_ctx {
   hipEvent_t ev0 = nullptr, ev1 = nullptr, evs0 = nullptr, evs1 = nullptr;
   std::map<uint32_t, DevTables> tables;
   std::map<uint32_t, std::unique_ptr<ewal::CrcTables>> host_tables;
-  DevBuf mlist, pf, v, pwave, ux, tagg, tpx, wcnt, slots, cbase, ovf, cpos, clen, nxt, exc, E, rs, jl, vis, entry, on, rec_cand, rd, opf, ops, kk, kkrev, suf,
+  DevBuf slow, mlist, pf, v, pwave, ux, tagg, tpx, wcnt, slots, cbase, ovf, cpos, clen, nxt, exc, E, rs, jl, vis, entry, on, rec_cand, rd, opf, ops, kk, kkrev, suf,
       ents, recs, tmp, small, sdesc, snaps, hbuf_dev;
   Small *h_small = nullptr;        // host-mapped pinned mirrors (written by k_export_small / k_result)
   ResultDev *h_res = nullptr;
@@ -78,6 +78,8 @@ struct ewal_ctx {
   ResultDev *h_res_dev = nullptr;
   // results of the last readall
   uint64_t last_n = 0, last_nents = 0;
+  uint64_t last_k = 0;     // candidates of the previous call (sizes k_frame's descriptors)
+  uint64_t pfcap = 0;      // pf = [P at data starts | P at frame starts], pfcap each
   bool last_ok = false;
 };
 
@@ -182,10 +184,11 @@ static int run_stream(ewal_ctx *c, DevTables *tb, const uint8_t *d_buf, uint64_t
   s.ccap = ccap;
   s.ovf = find_cand ? c->ovf.as<uint32_t>() : nullptr;
   s.novf = &ds->novf;
-  const unsigned sgrid = std::min<uint32_t>(nstiles, 2u * (uint32_t)c->num_cu);   // 2 x 1024 threads per CU
-  hipLaunchKernelGGL(k_uagg, dim3(sgrid), dim3(1024), 0, c->stream, s);
+  // one wave per 4 MiB tile, four waves per workgroup
+  const unsigned sgrid = std::min<uint32_t>((nstiles + 3) / 4, 4u * (uint32_t)c->num_cu);
+  hipLaunchKernelGGL(k_uagg, dim3(sgrid), dim3(256), 0, c->stream, s);
   hipLaunchKernelGGL(k_tscan, dim3(1), dim3(1024), 0, c->stream, s);
-  hipLaunchKernelGGL(k_uapply, dim3(sgrid), dim3(1024), 0, c->stream, s);
+  hipLaunchKernelGGL(k_uapply, dim3(sgrid), dim3(256), 0, c->stream, s);
   EW_CHECK(hipGetLastError());
   if (find_cand) {
     hipLaunchKernelGGL(k_rescan, dim3(64), dim3(256), 0, c->stream, d_buf, B, c->ovf.as<uint32_t>(), &ds->novf,
@@ -294,29 +297,51 @@ static int readall_impl(ewal_ctx *c, const uint8_t *d_buf, uint64_t B, uint64_t 
   uint64_t K = 0;
   int64_t qlen = 0;
   bool regular = false;
+  bool decoded = false;    // k_frame's speculative decode holds
   if (B > 0) {
     uint64_t ccap = std::min<uint64_t>(B / 128 + 65536, 0xfffffff0ull);
     EW_CHECK(c->cpos.ensure(ccap * 8));
     EW_CHECK(c->clen.ensure(ccap * 8));
     EW_CHECK(c->nxt.ensure(ccap * 4));
     EW_CHECK(c->exc.ensure(ccap));
+    // descriptor capacity of the speculative frame pass: the previous call's
+    // frame count with headroom, at least one frame per 4 KiB
+    const uint64_t rdcap = std::min<uint64_t>(ccap, std::max<uint64_t>(c->last_k + c->last_k / 8 + 1024,
+                                                                       B / 4096 + 1024));
+    EW_CHECK(c->rd.ensure(rdcap * sizeof(RecDesc)));
+    EW_CHECK(c->pf.ensure(rdcap * 8));
+    EW_CHECK(c->slow.ensure(rdcap * 4));
+    c->pfcap = rdcap;
     rc = run_stream(c, tb, d_buf, B, 1, ccap);
     if (rc) return rc;
-    const unsigned lgrid = (unsigned)std::max(1, c->num_cu) * 8;
-    hipLaunchKernelGGL(k_link, dim3(lgrid), dim3(256), 0, c->stream, d_buf, B, c->cpos.as<uint64_t>(),
-                       c->clen.as<uint64_t>(), ccap, c->nxt.as<uint32_t>(), c->exc.as<uint8_t>(), ds);
+    uint32_t *pf = c->pf.as<uint32_t>();
+    const unsigned fgrid = (unsigned)std::max(1, c->num_cu) * 8;
+    hipLaunchKernelGGL(k_frame, dim3(fgrid), dim3(256), 0, c->stream, d_buf, B, c->cpos.as<uint64_t>(), ccap, rdcap,
+                       c->pwave.as<uint32_t>(), c->v.as<uint32_t>(), tb->slice, tb->shift, c->rd.as<RecDesc>(), pf,
+                       pf + rdcap, c->slow.as<uint32_t>(), ds);
+    hipLaunchKernelGGL(k_decode_slow, dim3(64), dim3(256), 0, c->stream, d_buf, B, c->cpos.as<uint64_t>(),
+                       (const uint32_t *)nullptr, c->slow.as<uint32_t>(), ds, c->pwave.as<uint32_t>(),
+                       c->v.as<uint32_t>(), tb->slice, tb->shift, c->rd.as<RecDesc>(), pf, pf + rdcap, 0u);
     EW_CHECK(hipGetLastError());
     if ((rc = sync_small(c))) return rc;
     K = c->h_small->total;
-    if (K > ccap) {   // grow and redo the compaction and the links (the slots stay valid)
-      if (K >= 0xfffffff0ull) return EWAL_E_NOMEM;
-      ccap = K + 1024;
-      EW_CHECK(c->cpos.ensure(ccap * 8));
-      EW_CHECK(c->clen.ensure(ccap * 8));
-      EW_CHECK(c->nxt.ensure(ccap * 4));
-      EW_CHECK(c->exc.ensure(ccap));
-      rc = compact_cands(c, d_buf, B, (uint32_t)(B / EW_WAVE_BYTES + 1), ccap);
-      if (rc) return rc;
+    c->last_k = K;
+    if (K && K <= ccap && K <= rdcap && c->h_small->pos0 == 0 && !c->h_small->irregular) {
+      decoded = true;
+    } else {
+      // the speculation failed: frame by candidate links (k_link), growing
+      // the candidate list first if it overflowed
+      const unsigned lgrid = (unsigned)std::max(1, c->num_cu) * 8;
+      if (K > ccap) {   // grow and redo the compaction (the slots stay valid)
+        if (K >= 0xfffffff0ull) return EWAL_E_NOMEM;
+        ccap = K + 1024;
+        EW_CHECK(c->cpos.ensure(ccap * 8));
+        EW_CHECK(c->clen.ensure(ccap * 8));
+        EW_CHECK(c->nxt.ensure(ccap * 4));
+        EW_CHECK(c->exc.ensure(ccap));
+        rc = compact_cands(c, d_buf, B, (uint32_t)(B / EW_WAVE_BYTES + 1), ccap);
+        if (rc) return rc;
+      }
       EW_CHECK(hipMemsetAsync(&ds->irregular, 0, 4, c->stream));
       hipLaunchKernelGGL(k_link, dim3(lgrid), dim3(256), 0, c->stream, d_buf, B, c->cpos.as<uint64_t>(),
                          c->clen.as<uint64_t>(), ccap, c->nxt.as<uint32_t>(), c->exc.as<uint8_t>(), ds);
@@ -352,19 +377,31 @@ static int readall_impl(ewal_ctx *c, const uint8_t *d_buf, uint64_t B, uint64_t 
   res.agg.first_meta = ~0ull;
   if (n) {
     const uint32_t n32 = (uint32_t)n;
-    EW_CHECK(c->rd.ensure((size_t)n * sizeof(RecDesc)));
+    if (!decoded) {
+      if (n > c->pfcap) {
+        EW_CHECK(c->rd.ensure((size_t)n * sizeof(RecDesc)));
+        EW_CHECK(c->pf.ensure((size_t)n * 8));
+        EW_CHECK(c->slow.ensure((size_t)n * 4));
+        c->pfcap = n;
+      }
+      uint32_t *pf = c->pf.as<uint32_t>();
+      const uint32_t *rc_list = regular ? (const uint32_t *)nullptr : c->rec_cand.as<uint32_t>();
+      EW_CHECK(hipMemsetAsync(&ds->nslow, 0, 4, c->stream));
+      hipLaunchKernelGGL(k_decode, dim3(grid_for(n, 256)), dim3(256), 0, c->stream, d_buf, B,
+                         c->cpos.as<uint64_t>(), rc_list, n32, c->pwave.as<uint32_t>(), c->v.as<uint32_t>(),
+                         tb->slice, tb->shift, c->rd.as<RecDesc>(), pf, pf + c->pfcap, c->slow.as<uint32_t>(), ds);
+      hipLaunchKernelGGL(k_decode_slow, dim3(std::min<uint64_t>(grid_for(n, 256), 64)), dim3(256), 0, c->stream,
+                         d_buf, B, c->cpos.as<uint64_t>(), rc_list, c->slow.as<uint32_t>(), ds,
+                         c->pwave.as<uint32_t>(), c->v.as<uint32_t>(), tb->slice, tb->shift, c->rd.as<RecDesc>(), pf,
+                         pf + c->pfcap, n32);
+    }
     RecDesc *rd = c->rd.as<RecDesc>();
-    EW_CHECK(c->pf.ensure((size_t)n * 8));
-    hipLaunchKernelGGL(k_decode, dim3(grid_for(n, 256)), dim3(256), 0, c->stream, d_buf, B,
-                       c->cpos.as<uint64_t>(), c->clen.as<uint64_t>(),
-                       regular ? (const uint32_t *)nullptr : c->rec_cand.as<uint32_t>(), n32,
-                       c->pwave.as<uint32_t>(), c->v.as<uint32_t>(), tb->slice, tb->shift, rd, c->pf.as<uint32_t>(),
-                       c->ablate);
+    const uint32_t *pfd = c->pf.as<uint32_t>(), *pfo = pfd + c->pfcap;
     EW_CHECK(c->opf.ensure(n));
     EW_CHECK(c->ops.ensure((size_t)n * 4));
     EW_CHECK(c->mlist.ensure((size_t)n * 4));
     hipLaunchKernelGGL(k_verify, dim3(grid_for(n, 1024)), dim3(1024), 0, c->stream, tb->shift, rd, n32,
-                       c->pf.as<uint32_t>(), ri, c->opf.as<uint8_t>(), c->mlist.as<uint32_t>(), ds);
+                       pfd, pfo, ri, c->opf.as<uint8_t>(), c->mlist.as<uint32_t>(), ds);
     hipLaunchKernelGGL(k_meta, dim3(64), dim3(256), 0, c->stream, d_buf, rd, c->mlist.as<uint32_t>(), ds);
     rc = select_flagged(c, c->opf.as<uint8_t>(), n32, c->ops.as<uint32_t>(), &ds->nsel3);
     if (rc) return rc;
@@ -491,7 +528,7 @@ void ewal_ctx_destroy(ewal_ctx *c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
   (void)hipStreamSynchronize(c->stream);
-  DevBuf *bufs[] = {&c->mlist, &c->pf, &c->v, &c->pwave, &c->ux, &c->tagg, &c->tpx, &c->wcnt, &c->slots, &c->cbase, &c->ovf, &c->cpos, &c->clen, &c->nxt, &c->exc, &c->E, &c->rs, &c->jl,
+  DevBuf *bufs[] = {&c->slow, &c->mlist, &c->pf, &c->v, &c->pwave, &c->ux, &c->tagg, &c->tpx, &c->wcnt, &c->slots, &c->cbase, &c->ovf, &c->cpos, &c->clen, &c->nxt, &c->exc, &c->E, &c->rs, &c->jl,
                     &c->vis, &c->entry, &c->on, &c->rec_cand, &c->rd, &c->opf, &c->ops, &c->kk, &c->kkrev,
                     &c->suf, &c->ents, &c->recs, &c->tmp, &c->small, &c->sdesc, &c->snaps, &c->hbuf_dev};
   for (DevBuf *b : bufs) b->release();

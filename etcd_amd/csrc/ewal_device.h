@@ -32,6 +32,28 @@ __device__ __forceinline__ uint32_t gshift_n(const uint32_t *g, uint64_t n, uint
   return x;
 }
 
+// Copy n dwords into LDS: dst[i] = src(i).  Every thread issues 16 loads
+// before its first store (a plain strided copy loop waits on each load in
+// turn, one L2 round trip per iteration).  Indices past n load a clamped
+// address and are not stored.
+template <int NT, class F>
+__device__ __forceinline__ void stage_lds(uint32_t *dst, int n, F src) {
+  const int tid = threadIdx.x;
+  for (int i0 = 0; i0 < n; i0 += 16 * NT) {
+    uint32_t r[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const int i = i0 + k * NT + tid;
+      r[k] = src(i < n ? i : n - 1);
+    }
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const int i = i0 + k * NT + tid;
+      if (i < n) dst[i] = r[k];
+    }
+  }
+}
+
 // Slicing-by-4 step on a register already XORed with the next data word;
 // tables t[4][256] (t[0] = MakeTable(poly)), non-replicated layout.
 __device__ __forceinline__ uint32_t step4_flat(const uint32_t *t, uint32_t c) {

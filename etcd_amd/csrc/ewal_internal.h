@@ -90,7 +90,7 @@ struct Small {
   uint32_t nonmono;               // k_gap: entry indexes not strictly increasing
   uint64_t klast;                 // k of the last entry op (len(ents) - 1)
   uint32_t nmeta;                 // metadata frames listed by k_verify
-  uint32_t pad1;
+  uint32_t nslow;                 // frames k_decode left to k_decode_slow (non-canonical encodings)
 };
 
 // Everything the host needs after the frame pass, gathered by k_result.

@@ -358,11 +358,9 @@ __global__ __launch_bounds__(EW_THREADS, 1) void k_stream(StreamArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t s_slice[EW_SLICE_DWORDS * 4];
   __shared__ uint32_t s_s64[1024], s_s128[1024];   // S_64, S_128 byte tables (super-piece tree)
   const int tid = threadIdx.x, lane = tid & 63;
-  for (int i = tid; i < EW_SLICE_DWORDS; i += EW_THREADS) ((uint32_t *)s_slice)[i] = a.g_slice[slice_src(i)];
-  for (int i = tid; i < 1024; i += EW_THREADS) {
-    s_s64[i] = a.g_shift[6 * 1024 + i];
-    s_s128[i] = a.g_shift[7 * 1024 + i];
-  }
+  stage_lds<EW_THREADS>((uint32_t *)s_slice, EW_SLICE_DWORDS, [&](int i) { return a.g_slice[slice_src(i)]; });
+  stage_lds<EW_THREADS>(s_s64, 1024, [&](int i) { return a.g_shift[6 * 1024 + i]; });
+  stage_lds<EW_THREADS>(s_s128, 1024, [&](int i) { return a.g_shift[7 * 1024 + i]; });
   __syncthreads();
   uint32_t Lt[4];
   lane_regs(lane, Lt);
@@ -454,182 +452,247 @@ __global__ __launch_bounds__(EW_THREADS, 1) void k_stream(StreamArgs a) {
 //            slots into cpos[] (units with more than EW_SLOTS: k_rescan)
 // ===========================================================================
 
-// inclusive affine scan over a wave of units (4 KiB each): value q = lin of
-// the lane's span, count qc; tables s + d*1024 = S_{2^(12+d)}
-__device__ __forceinline__ void wave_unit_scan(const uint32_t *s, uint32_t &q, uint32_t &qc) {
-  const int lane = threadIdx.x & 63;
+// The unit scan turns the per-unit lins into the stream prefix P at every
+// unit start.  Three kernels, one WAVE per 4 MiB tile (1024 units) so no
+// workgroup barrier sits on the critical path:
+//   k_uagg   per-unit lin x (from the 16 super-piece lins) and per-tile
+//            aggregate, via the linear form  agg = XOR_u S_{4096 (1023-u)}(x_u);
+//   k_tscan  exclusive affine scan of the tile aggregates (one workgroup);
+//   k_uapply lane-serial Horner over 16 consecutive units, one wave scan of
+//            the 64 lane spans, replay -> P and candidate base per unit, and
+//            the candidate-list compaction.
+// Tables live in LDS; tab_apply(S_m) costs four random ds_read_b32.
+
+// lin of one 4 KiB unit from its 16 super-piece lins: four Horner chains of
+// four 256-B values (S_256), joined with S_1024
+__device__ __forceinline__ uint32_t unit_lin(const uint4 (&q)[4], const uint32_t *svp, const uint32_t *s1k) {
+  uint32_t h[4];
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    h[g] = tab_apply(svp, q[g].x) ^ q[g].y;
+    h[g] = tab_apply(svp, h[g]) ^ q[g].z;
+    h[g] = tab_apply(svp, h[g]) ^ q[g].w;
+  }
+  return tab_apply(s1k, tab_apply(s1k, tab_apply(s1k, h[0]) ^ h[1]) ^ h[2]) ^ h[3];
+}
+
+// Lane l of a wave reads units 64 i + l (i = 0..15: coalesced 4 KiB rows of
+// v), folds them with h = S_{2^18}(h) ^ x (S_{2^18} = 64 units), shifts the
+// fold by the units after it in its row (S_{4096 (63-l)}) and XOR-reduces.
+__global__ __launch_bounds__(256) void k_uagg(ScanArgs a) {
+  __shared__ uint32_t s_svp[1024], s_s1k[1024];   // S_256, S_1024
+  __shared__ uint32_t s_sh[7 * 1024];             // S_{2^12} .. S_{2^18}
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  stage_lds<256>(s_svp, 1024, [&](int i) { return a.g_shift[EW_VLOG * 1024 + i]; });
+  stage_lds<256>(s_s1k, 1024, [&](int i) { return a.g_shift[10 * 1024 + i]; });
+  stage_lds<256>(s_sh, 7 * 1024, [&](int i) { return a.g_shift[12 * 1024 + i]; });
+  __syncthreads();
+  for (uint32_t t = blockIdx.x * 4 + wv; t < a.ntiles; t += gridDim.x * 4) {
+    const uint32_t u0 = t * 1024 + lane;
+    uint32_t h = 0, cnt = 0;
+    for (int i0 = 0; i0 < 16; i0 += 4) {
+      uint4 q[4][4];
+      uint32_t c[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {   // every load of the four rows up front
+        const uint32_t u = u0 + 64 * (i0 + r);
+        const bool in = u < a.nunits;
+        const uint4 *vq = (const uint4 *)(a.v + (size_t)(in ? u : 0) * EW_VPU);
+#pragma unroll
+        for (int g = 0; g < 4; ++g) q[r][g] = in ? vq[g] : make_uint4(0, 0, 0, 0);
+        c[r] = in ? a.wcnt[u] : 0u;
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const uint32_t u = u0 + 64 * (i0 + r);
+        const uint32_t x = unit_lin(q[r], s_svp, s_s1k);
+        if (u < a.nunits) a.ux[u] = x;
+        h = tab_apply(s_sh + 6 * 1024, h) ^ x;
+        cnt += c[r];
+      }
+    }
+    const uint32_t after = 63 - lane;
+#pragma unroll
+    for (int k = 0; k < 6; ++k)
+      if ((after >> k) & 1) h = tab_apply(s_sh + k * 1024, h);
+#pragma unroll
+    for (int o = 32; o; o >>= 1) {
+      h ^= __shfl_xor(h, o);
+      cnt += __shfl_xor(cnt, o);
+    }
+    if (lane == 0) { a.tagg[t] = h; a.tcnt[t] = cnt; }
+  }
+}
+
+// One workgroup of 1024 threads; thread T owns tiles [T k, T k + k), k = 2^e
+// the smallest power of two with 1024 k >= ntiles: lane Horner (S_{2^22} per
+// tile), wave and workgroup scans of the thread spans (S_{2^(22+e+d)}), replay.
+__global__ __launch_bounds__(1024) void k_tscan(ScanArgs a) {
+  __shared__ uint32_t s_t1[1024];                 // S_{2^22}: one tile
+  __shared__ uint32_t s_sh[10 * 1024];            // S_{2^(22+e+d)}, d = 0..9
+  __shared__ uint32_t s_wq[16];
+  __shared__ unsigned long long s_wc[16];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  int e = 0;
+  while ((1024ull << e) < a.ntiles) ++e;
+  const uint32_t k = 1u << e;
+  s_t1[tid] = a.g_shift[22 * 1024 + tid];
+  stage_lds<1024>(s_sh, 10 * 1024, [&](int i) { return a.g_shift[(22 + e) * 1024 + i]; });
+  __syncthreads();
+  const uint64_t t0 = (uint64_t)tid * k;
+  uint32_t h = 0;
+  unsigned long long cs = 0;
+  for (uint32_t j = 0; j < k; ++j) {
+    const uint64_t t = t0 + j;
+    const uint32_t x = t < a.ntiles ? a.tagg[t] : 0u;
+    h = tab_apply(s_t1, h) ^ x;
+    cs += t < a.ntiles ? a.tcnt[t] : 0u;
+  }
+  uint32_t q = h;
+  unsigned long long qc = cs;
 #pragma unroll
   for (int d = 0; d < 6; ++d) {
-    const uint32_t o = __shfl_up(q, 1 << d), oc = __shfl_up(qc, 1 << d);
-    if (lane >= (1 << d)) {
-      q = tab_apply(s + d * 1024, o) ^ q;
-      qc += oc;
-    }
+    const uint32_t o = __shfl_up(q, 1 << d);
+    const unsigned long long oc = __shfl_up(qc, 1 << d);
+    if (lane >= (1 << d)) { q = tab_apply(s_sh + d * 1024, o) ^ q; qc += oc; }
   }
-}
-// inclusive scan of the 16 wave totals (256 KiB each) in lanes 0..15 of one
-// wave; tables s + (6 + d)*1024 = S_{2^(18+d)}
-__device__ __forceinline__ void block_wave_scan(const uint32_t *s, uint32_t &w, uint32_t &wc) {
-  const int lane = threadIdx.x & 63;
+  uint32_t ex = __shfl_up(q, 1);
+  unsigned long long exc = __shfl_up(qc, 1);
+  if (lane == 0) { ex = 0; exc = 0; }
+  if (lane == 63) { s_wq[wv] = q; s_wc[wv] = qc; }
+  __syncthreads();
+  if (wv == 0) {   // scan of the 16 wave spans, in place (exclusive)
+    uint32_t w = lane < 16 ? s_wq[lane] : 0u;
+    unsigned long long wc = lane < 16 ? s_wc[lane] : 0ull;
 #pragma unroll
-  for (int d = 0; d < 4; ++d) {
-    const uint32_t o = __shfl_up(w, 1 << d), oc = __shfl_up(wc, 1 << d);
-    if (lane >= (1 << d) && lane < 16) {
-      w = tab_apply(s + (6 + d) * 1024, o) ^ w;
-      wc += oc;
+    for (int d = 0; d < 4; ++d) {
+      const uint32_t o = __shfl_up(w, 1 << d);
+      const unsigned long long oc = __shfl_up(wc, 1 << d);
+      if (lane >= (1 << d) && lane < 16) { w = tab_apply(s_sh + (6 + d) * 1024, o) ^ w; wc += oc; }
     }
+    uint32_t we = __shfl_up(w, 1);
+    unsigned long long wce = __shfl_up(wc, 1);
+    if (lane == 0) { we = 0; wce = 0; }
+    if (lane == 15) *a.total = wc;
+    if (lane < 16) { s_wq[lane] = we; s_wc[lane] = wce; }
+  }
+  __syncthreads();
+  uint32_t cur = s_wq[wv];                        // S_{span * lane}(wave start) ^ lane prefix
+#pragma unroll
+  for (int b = 0; b < 6; ++b)
+    if ((lane >> b) & 1) cur = tab_apply(s_sh + b * 1024, cur);
+  cur ^= ex;
+  unsigned long long cb = s_wc[wv] + exc;
+  for (uint32_t j = 0; j < k; ++j) {
+    const uint64_t t = t0 + j;
+    if (t >= a.ntiles) break;
+    a.tpx[t] = cur;
+    a.tcb[t] = cb;
+    cur = tab_apply(s_t1, cur) ^ a.tagg[t];
+    cb += a.tcnt[t];
   }
 }
 
-__global__ __launch_bounds__(1024) void k_uagg(ScanArgs a) {
-  __shared__ uint32_t s_svp[1024], s_s1k[1024];   // S_256, S_1024
-  __shared__ uint32_t s_sh[10 * 1024];            // S_{2^12} .. S_{2^21}
-  __shared__ uint32_t s_wq[16], s_wc[16];
+// Lane l owns units 16 l .. 16 l + 15 of the wave's tile: Horner over them
+// (S_4096), wave scan of the 64 lane spans (S_{2^(16+d)}), lane start =
+// S_{2^16 l}(P at the tile start) ^ exclusive span, replay.
+__global__ __launch_bounds__(256) void k_uapply(ScanArgs a) {
+  __shared__ uint32_t s_s12[1024];                // S_4096
+  __shared__ uint32_t s_sh[6 * 1024];             // S_{2^16} .. S_{2^21}
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  s_svp[tid] = a.g_shift[EW_VLOG * 1024 + tid];
-  s_s1k[tid] = a.g_shift[10 * 1024 + tid];
-  for (int i = tid; i < 10 * 1024; i += 1024) s_sh[i] = a.g_shift[12 * 1024 + i];
+  stage_lds<256>(s_s12, 1024, [&](int i) { return a.g_shift[12 * 1024 + i]; });
+  stage_lds<256>(s_sh, 6 * 1024, [&](int i) { return a.g_shift[16 * 1024 + i]; });
   __syncthreads();
-  for (uint32_t t = blockIdx.x; t < a.ntiles; t += gridDim.x) {   // persistent: tables staged once
-    const uint32_t u = t * 1024 + tid;
-    uint32_t x = 0, cx = 0;
-    if (u < a.nunits) {   // four Horner chains of four 256-B values, joined with S_1024
-      const uint4 *vq = (const uint4 *)(a.v + (size_t)u * EW_VPU);
-      uint4 q[4];
-  #pragma unroll
-      for (int g = 0; g < 4; ++g) q[g] = vq[g];
-      uint32_t h[4];
-  #pragma unroll
+  for (uint32_t t = blockIdx.x * 4 + wv; t < a.ntiles; t += gridDim.x * 4) {
+    const uint32_t u0 = t * 1024 + 16 * lane;
+    uint32_t x[16], c[16];
+    if (u0 + 16 <= a.nunits) {
+#pragma unroll
       for (int g = 0; g < 4; ++g) {
-        h[g] = tab_apply(s_svp, q[g].x) ^ q[g].y;
-        h[g] = tab_apply(s_svp, h[g]) ^ q[g].z;
-        h[g] = tab_apply(s_svp, h[g]) ^ q[g].w;
+        const uint4 xv = ((const uint4 *)(a.ux + u0))[g], cv = ((const uint4 *)(a.wcnt + u0))[g];
+        x[4 * g] = xv.x; x[4 * g + 1] = xv.y; x[4 * g + 2] = xv.z; x[4 * g + 3] = xv.w;
+        c[4 * g] = cv.x; c[4 * g + 1] = cv.y; c[4 * g + 2] = cv.z; c[4 * g + 3] = cv.w;
       }
-      x = tab_apply(s_s1k, tab_apply(s_s1k, tab_apply(s_s1k, h[0]) ^ h[1]) ^ h[2]) ^ h[3];
-      cx = a.wcnt[u];
-      a.ux[u] = x;
+    } else {
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const bool in = u0 + j < a.nunits;
+        x[j] = in ? a.ux[u0 + j] : 0u;
+        c[j] = in ? a.wcnt[u0 + j] : 0u;
+      }
     }
-    uint32_t q = x, qc = cx;
-    wave_unit_scan(s_sh, q, qc);
-    if (lane == 63) { s_wq[wv] = q; s_wc[wv] = qc; }
-    __syncthreads();
-    if (wv == 0) {
-      uint32_t w = lane < 16 ? s_wq[lane] : 0u, wc = lane < 16 ? s_wc[lane] : 0u;
-      block_wave_scan(s_sh, w, wc);
-      if (lane == 15) { a.tagg[t] = w; a.tcnt[t] = wc; }
+    // the tile's P / base and the first 8 candidate slots of every unit with
+    // candidates, issued before the arithmetic so the wave waits once
+    const uint32_t tp = a.tpx[t];
+    const unsigned long long tcb = a.tcb[t];
+    uint4 sv[16];
+    if (a.slots) {
+#pragma unroll
+      for (int j = 0; j < 16; ++j)
+        sv[j] = c[j] ? *(const uint4 *)(a.slots + (size_t)(u0 + j) * EW_SLOTS) : make_uint4(0, 0, 0, 0);
     }
-    __syncthreads();
-  }
-}
-
-// One workgroup: exclusive affine scan of the tile aggregates (4 MiB each),
-// 1024 tiles per round with a carried prefix.
-__global__ __launch_bounds__(1024) void k_tscan(ScanArgs a) {
-  __shared__ uint32_t s_sh[10 * 1024];            // S_{2^22} .. S_{2^31}
-  __shared__ uint32_t s_wq[16], s_wc[16], s_base[16];
-  __shared__ unsigned long long s_cb[16];
-  __shared__ uint32_t s_carry;
-  __shared__ unsigned long long s_ncarry;
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  for (int i = tid; i < 10 * 1024; i += 1024) s_sh[i] = a.g_shift[22 * 1024 + i];
-  if (tid == 0) { s_carry = 0; s_ncarry = 0; }
-  __syncthreads();
-  for (uint32_t t0 = 0; t0 < a.ntiles; t0 += 1024) {
-    const uint32_t t = t0 + tid;
-    const uint32_t x = t < a.ntiles ? a.tagg[t] : 0u;
-    const uint32_t cx = t < a.ntiles ? a.tcnt[t] : 0u;
-    uint32_t q = x, qc = cx;
-    wave_unit_scan(s_sh, q, qc);   // tables are S_{2^(22+d)} here
+    uint32_t q = 0, qc = 0;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) { q = tab_apply(s_s12, q) ^ x[j]; qc += c[j]; }
+#pragma unroll
+    for (int d = 0; d < 6; ++d) {
+      const uint32_t o = __shfl_up(q, 1 << d), oc = __shfl_up(qc, 1 << d);
+      if (lane >= (1 << d)) { q = tab_apply(s_sh + d * 1024, o) ^ q; qc += oc; }
+    }
     uint32_t ex = __shfl_up(q, 1), exc = __shfl_up(qc, 1);
     if (lane == 0) { ex = 0; exc = 0; }
-    if (lane == 63) { s_wq[wv] = q; s_wc[wv] = qc; }
-    __syncthreads();
-    if (wv == 0) {
-      uint32_t w = lane < 16 ? s_wq[lane] : 0u, wc = lane < 16 ? s_wc[lane] : 0u;
-      block_wave_scan(s_sh, w, wc);   // S_{2^(28+d)}
-      uint32_t we = __shfl_up(w, 1), wce = __shfl_up(wc, 1);
-      if (lane == 0) { we = 0; wce = 0; }
-      const uint32_t X = s_carry;
-      const unsigned long long N = s_ncarry;
-      if (lane < 16) {
-        uint32_t xs = X;                     // S_{lane * 2^28}(X)
+    uint32_t cur = tp;
 #pragma unroll
-        for (int b = 0; b < 4; ++b)
-          if ((lane >> b) & 1) xs = tab_apply(s_sh + (6 + b) * 1024, xs);
-        s_base[lane] = xs ^ we;
-        s_cb[lane] = N + wce;
-      }
-      const uint32_t tot = __shfl(w, 15), totc = __shfl(wc, 15);
-      if (lane == 0) {   // carry over 1024 tiles = 2^32 bytes
-        s_carry = gshift_pow2(a.g_shift, 32, X) ^ tot;
-        s_ncarry = N + totc;
-      }
-    }
-    __syncthreads();
-    if (t < a.ntiles) {
-      uint32_t b = s_base[wv];                 // S_{lane * 2^22}(base)
+    for (int b = 0; b < 6; ++b)
+      if ((lane >> b) & 1) cur = tab_apply(s_sh + b * 1024, cur);
+    cur ^= ex;
+    unsigned long long cb = tcb + exc;
+    uint32_t pw[16];
+    unsigned long long cbs[16];
 #pragma unroll
-      for (int k = 0; k < 6; ++k)
-        if ((lane >> k) & 1) b = tab_apply(s_sh + k * 1024, b);
-      a.tpx[t] = b ^ ex;
-      a.tcb[t] = s_cb[wv] + exc;
+    for (int j = 0; j < 16; ++j) {
+      pw[j] = cur;
+      cbs[j] = cb;
+      cur = tab_apply(s_s12, cur) ^ x[j];
+      cb += c[j];
     }
-    __syncthreads();
-  }
-  if (tid == 0) *a.total = s_ncarry;
-}
-
-__global__ __launch_bounds__(1024) void k_uapply(ScanArgs a) {
-  __shared__ uint32_t s_sh[10 * 1024];            // S_{2^12} .. S_{2^21}
-  __shared__ uint32_t s_wq[16], s_wc[16], s_base[16];
-  __shared__ unsigned long long s_cb[16];
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  for (int i = tid; i < 10 * 1024; i += 1024) s_sh[i] = a.g_shift[12 * 1024 + i];
-  __syncthreads();
-  for (uint32_t t = blockIdx.x; t < a.ntiles; t += gridDim.x) {   // persistent: tables staged once
-    const uint32_t u = t * 1024 + tid;
-    const uint32_t x = u < a.nunits ? a.ux[u] : 0u;
-    const uint32_t cx = u < a.nunits ? a.wcnt[u] : 0u;
-    uint32_t q = x, qc = cx;
-    wave_unit_scan(s_sh, q, qc);
-    uint32_t ex = __shfl_up(q, 1), exc = __shfl_up(qc, 1);
-    if (lane == 0) { ex = 0; exc = 0; }
-    if (lane == 63) { s_wq[wv] = q; s_wc[wv] = qc; }
-    __syncthreads();
-    if (wv == 0) {
-      uint32_t w = lane < 16 ? s_wq[lane] : 0u, wc = lane < 16 ? s_wc[lane] : 0u;
-      block_wave_scan(s_sh, w, wc);
-      uint32_t we = __shfl_up(w, 1), wce = __shfl_up(wc, 1);
-      if (lane == 0) { we = 0; wce = 0; }
-      if (lane < 16) {
-        uint32_t xs = a.tpx[t];                  // S_{lane * 2^18}(P at the tile start)
-  #pragma unroll
-        for (int b = 0; b < 4; ++b)
-          if ((lane >> b) & 1) xs = tab_apply(s_sh + (6 + b) * 1024, xs);
-        s_base[lane] = xs ^ we;
-        s_cb[lane] = a.tcb[t] + wce;
+    if (u0 + 16 <= a.nunits) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        ((uint4 *)(a.pwave + u0))[g] = make_uint4(pw[4 * g], pw[4 * g + 1], pw[4 * g + 2], pw[4 * g + 3]);
+#pragma unroll
+      for (int g = 0; g < 8; ++g) {
+        ulonglong2 w;
+        w.x = cbs[2 * g];
+        w.y = cbs[2 * g + 1];
+        ((ulonglong2 *)(a.cbase + u0))[g] = w;
       }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 16; ++j)
+        if (u0 + j < a.nunits) { a.pwave[u0 + j] = pw[j]; a.cbase[u0 + j] = cbs[j]; }
     }
-    __syncthreads();
-    if (u < a.nunits) {
-      uint32_t b = s_base[wv];                   // S_{lane * 4096}(base)
-  #pragma unroll
-      for (int k = 0; k < 6; ++k)
-        if ((lane >> k) & 1) b = tab_apply(s_sh + k * 1024, b);
-      a.pwave[u] = b ^ ex;
-      const unsigned long long base = s_cb[wv] + exc;
-      a.cbase[u] = base;
-      if (a.slots && cx) {   // compaction: slots -> the dense, position-sorted candidate list
+    if (a.slots) {   // compaction: slots -> the dense, position-sorted candidate list
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const uint32_t u = u0 + j, cx = c[j];
+        if (!cx) continue;
         if (cx > EW_SLOTS) {
           a.ovf[atomicAdd(a.novf, 1u)] = u;
         } else {
-          const uint16_t *sl = a.slots + (size_t)u * EW_SLOTS;
-          for (uint32_t j = 0; j < cx; ++j)
-            if (base + j < a.ccap) a.cpos[base + j] = (uint64_t)u * EW_WAVE_BYTES + sl[j];
+          const uint64_t ub = (uint64_t)u * EW_WAVE_BYTES;
+          const uint32_t w4[4] = {sv[j].x, sv[j].y, sv[j].z, sv[j].w};
+#pragma unroll
+          for (uint32_t m = 0; m < 8; ++m)
+            if (m < cx && cbs[j] + m < a.ccap) a.cpos[cbs[j] + m] = ub + ((w4[m >> 1] >> (16 * (m & 1))) & 0xffffu);
+          if (cx > 8) {   // rare: more than 8 candidates in 4 KiB
+            const uint16_t *sl = a.slots + (size_t)u * EW_SLOTS;
+            for (uint32_t m = 8; m < cx; ++m)
+              if (cbs[j] + m < a.ccap) a.cpos[cbs[j] + m] = ub + sl[m];
+          }
         }
       }
     }
-    __syncthreads();
   }
 }
 
@@ -816,41 +879,48 @@ __global__ void k_member(const uint32_t *__restrict__ E, uint32_t R, const uint8
 // ===========================================================================
 
 // Stream prefix P(x) = lin(stream[0..x)) from the per-unit prefix and the
-// super-piece lins of k_stream.  Every load is issued up front (the unit's
-// 16 super-piece lins, 64 B, and the 256-B super-piece holding x) so the
-// dependent chain that follows runs out of registers: Horner over the whole
-// super-pieces before x (S_256), then slicing-by-4 / byte steps over the
-// bytes of x's super-piece before x.
-__device__ __forceinline__ uint32_t prefix_at(uint64_t x, const uint32_t *__restrict__ pwave,
-                                              const uint32_t *__restrict__ v, const uint8_t *__restrict__ buf,
-                                              const uint32_t *t4, const uint32_t *svp) {
+// super-piece lins of k_stream, in two phases so a caller can issue the loads
+// (the unit's prefix, its 16 super-piece lins, the 256-B super-piece holding
+// x) together with its own and do the arithmetic later: Horner over the whole
+// super-pieces before x (S_256), then slicing-by-4 / byte steps over the bytes
+// of x's super-piece before x.
+struct PrefixIn {
+  uint32_t pw, k, tail;
+  uint4 vv[EW_VPU / 4];
+  uint4 dd[EW_VPIECE / 16];
+};
+__device__ __forceinline__ void prefix_load(uint64_t x, const uint32_t *__restrict__ pwave,
+                                            const uint32_t *__restrict__ v, const uint8_t *__restrict__ buf,
+                                            PrefixIn &in) {
   const uint64_t w = x >> 12;
   const uint64_t x0 = x & ~(uint64_t)(EW_VPIECE - 1);
-  const uint32_t k = (uint32_t)((x0 >> EW_VLOG) & (EW_VPU - 1));
-  const uint32_t tail = (uint32_t)(x - x0);
+  in.k = (uint32_t)((x0 >> EW_VLOG) & (EW_VPU - 1));
+  in.tail = (uint32_t)(x - x0);
   const uint4 *vq = (const uint4 *)(v + w * EW_VPU);
-  uint4 vv[EW_VPU / 4];
 #pragma unroll
-  for (int q = 0; q < EW_VPU / 4; ++q) vv[q] = (4u * q < k) ? vq[q] : make_uint4(0, 0, 0, 0);
-  uint4 dd[EW_VPIECE / 16];
+  for (int q = 0; q < EW_VPU / 4; ++q) in.vv[q] = (4u * q < in.k) ? vq[q] : make_uint4(0, 0, 0, 0);
   const uint4 *dq = (const uint4 *)(buf + x0);
 #pragma unroll
-  for (int q = 0; q < EW_VPIECE / 16; ++q) dd[q] = (16u * q < tail) ? dq[q] : make_uint4(0, 0, 0, 0);
-  uint32_t acc = pwave[w];
+  for (int q = 0; q < EW_VPIECE / 16; ++q) in.dd[q] = (16u * q < in.tail) ? dq[q] : make_uint4(0, 0, 0, 0);
+  in.pw = pwave[w];
+}
+__device__ __forceinline__ uint32_t prefix_finish(const PrefixIn &in, const uint32_t *t4, const uint32_t *svp) {
+  const uint32_t k = in.k, tail = in.tail;
+  uint32_t acc = in.pw;
 #pragma unroll
   for (int q = 0; q < EW_VPU / 4; ++q) {
-    if (4u * q + 0 < k) acc = tab_apply(svp, acc) ^ vv[q].x;
-    if (4u * q + 1 < k) acc = tab_apply(svp, acc) ^ vv[q].y;
-    if (4u * q + 2 < k) acc = tab_apply(svp, acc) ^ vv[q].z;
-    if (4u * q + 3 < k) acc = tab_apply(svp, acc) ^ vv[q].w;
+    if (4u * q + 0 < k) acc = tab_apply(svp, acc) ^ in.vv[q].x;
+    if (4u * q + 1 < k) acc = tab_apply(svp, acc) ^ in.vv[q].y;
+    if (4u * q + 2 < k) acc = tab_apply(svp, acc) ^ in.vv[q].z;
+    if (4u * q + 3 < k) acc = tab_apply(svp, acc) ^ in.vv[q].w;
   }
   const uint32_t nd = tail >> 2;
 #pragma unroll
   for (int q = 0; q < EW_VPIECE / 16; ++q) {
-    if (4u * q + 0 < nd) acc = step4_flat(t4, acc ^ dd[q].x);
-    if (4u * q + 1 < nd) acc = step4_flat(t4, acc ^ dd[q].y);
-    if (4u * q + 2 < nd) acc = step4_flat(t4, acc ^ dd[q].z);
-    if (4u * q + 3 < nd) acc = step4_flat(t4, acc ^ dd[q].w);
+    if (4u * q + 0 < nd) acc = step4_flat(t4, acc ^ in.dd[q].x);
+    if (4u * q + 1 < nd) acc = step4_flat(t4, acc ^ in.dd[q].y);
+    if (4u * q + 2 < nd) acc = step4_flat(t4, acc ^ in.dd[q].z);
+    if (4u * q + 3 < nd) acc = step4_flat(t4, acc ^ in.dd[q].w);
   }
   // remaining 0..3 bytes live in dword nd
   const uint32_t rem = tail & 3;
@@ -860,7 +930,7 @@ __device__ __forceinline__ uint32_t prefix_at(uint64_t x, const uint32_t *__rest
     for (int q = 0; q < EW_VPIECE / 16; ++q) {
       if ((nd >> 2) == (uint32_t)q) {
         const uint32_t s = nd & 3;
-        wd = s == 0 ? dd[q].x : s == 1 ? dd[q].y : s == 2 ? dd[q].z : dd[q].w;
+        wd = s == 0 ? in.dd[q].x : s == 1 ? in.dd[q].y : s == 2 ? in.dd[q].z : in.dd[q].w;
       }
     }
     for (uint32_t b = 0; b < rem; ++b) {
@@ -870,34 +940,26 @@ __device__ __forceinline__ uint32_t prefix_at(uint64_t x, const uint32_t *__rest
   }
   return acc;
 }
+__device__ __forceinline__ uint32_t prefix_at(uint64_t x, const uint32_t *__restrict__ pwave,
+                                              const uint32_t *__restrict__ v, const uint8_t *__restrict__ buf,
+                                              const uint32_t *t4, const uint32_t *svp) {
+  PrefixIn in;
+  prefix_load(x, pwave, v, buf, in);
+  return prefix_finish(in, t4, svp);
+}
 
-// k_decode: parse frame r, and P at its frame start and data start:
+// General decode of frame r (any encoding the reference accepts): the
+// gogoprotobuf walkers over an LDS copy of the frame head, and P at its frame
+// start and data start:
 //   Pd[r] = P(doff) = raw(P(off), frame header bytes)
 // plus, for the last frame, P at its data end (the frame after it is not on
 // the chain).  The frame head (80 bytes from the 16-B boundary below the
-// frame start) is fetched with five vector loads, issued together with
-// prefix_at's loads, and parsed out of LDS: a canonical Record + Entry head
-// is at most ~50 bytes, so the walkers' byte reads do not go to HBM.
-// rec_cand == nullptr: frame r is candidate r (the regular chain).
-__global__ __launch_bounds__(256) void k_decode(const uint8_t *__restrict__ buf, uint64_t B,
-                         const uint64_t *__restrict__ pos, const uint64_t *__restrict__ len,
-                         const uint32_t *__restrict__ rec_cand, uint32_t n,
-                         const uint32_t *__restrict__ pwave, const uint32_t *__restrict__ v,
-                         const uint32_t *__restrict__ g_slice, const uint32_t *__restrict__ g_shift,
-                         RecDesc *__restrict__ rd, uint32_t *__restrict__ pf, int dbg) {
-  __shared__ uint32_t s_t4[1024];
-  __shared__ uint32_t s_svp[1024];   // S_256 (prefix_at's Horner step)
-  __shared__ uint4 s_win[256][5];
-  for (int i = threadIdx.x; i < 1024; i += blockDim.x) {
-    s_t4[i] = g_slice[i];
-    s_svp[i] = g_shift[EW_VLOG * 1024 + i];
-  }
-  __syncthreads();
-  uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
-  if (r >= n) return;
-  const uint32_t i = rec_cand ? rec_cand[r] : r;
-  const uint64_t p = pos[i];
-  const int64_t L = (int64_t)len[i];
+// frame start) is fetched with five vector loads and parsed out of LDS.
+__device__ __forceinline__ void decode_general(const uint8_t *__restrict__ buf, uint64_t B, uint64_t p, int64_t L,
+                                               uint32_t r, uint32_t n, const uint32_t *__restrict__ pwave,
+                                               const uint32_t *__restrict__ v, const uint32_t *s_t4,
+                                               const uint32_t *s_svp, uint4 (&win)[5], RecDesc *__restrict__ rd,
+                                               uint32_t *__restrict__ pfd, uint32_t *__restrict__ pfo) {
   const uint64_t p16 = p & ~15ull;
 #pragma unroll
   for (int k = 0; k < 5; ++k) {
@@ -911,9 +973,9 @@ __global__ __launch_bounds__(256) void k_decode(const uint8_t *__restrict__ buf,
       for (int j = 0; j < 4; ++j) x[j] = load_word_guarded(buf, B, o + 4 * j);
       w = make_uint4(x[0], x[1], x[2], x[3]);
     }
-    s_win[threadIdx.x][k] = w;
+    win[k] = w;
   }
-  const WinReader R{(const uint8_t *)&s_win[threadIdx.x][0] + (p - p16), (int64_t)(80 - (p - p16)), buf + p};
+  const WinReader R{(const uint8_t *)&win[0] + (p - p16), (int64_t)(80 - (p - p16)), buf + p};
   RecDesc d;
   d.off = p;
   d.type = 0; d.crc = 0; d.chained = 0; d.st = 0; d.sub_st = 0;
@@ -922,15 +984,15 @@ __global__ __launch_bounds__(256) void k_decode(const uint8_t *__restrict__ buf,
   PbField a1, a2, a3, a4, a5;
   pbf_init(a1); pbf_init(a2); pbf_init(a3); pbf_init(a4); pbf_init(a5);
   int unrec;
-  int st = (dbg & 256) ? 0 : pb_walk<PB_VAR64, PB_VAR32, PB_BYTES, PB_NONE, PB_NONE>(R + 8, L, a1, a2, a3, a4, a5, unrec,
-                                                                     nullptr, nullptr, 0);
+  int st = pb_walk<PB_VAR64, PB_VAR32, PB_BYTES, PB_NONE, PB_NONE>(R + 8, L, a1, a2, a3, a4, a5, unrec,
+                                                                   nullptr, nullptr, 0);
   d.type = (int64_t)a1.v;
   d.crc = (uint32_t)a2.v;
   if (a3.blen > 0) { d.doff = p + 8 + a3.boff; d.dlen = a3.blen; d.dnil = 0; }
   d.st = st;
   if (st == 0) {
     const WinReader dp = R + (int64_t)(d.doff - p);
-    if (d.type == 2 && !(dbg & 512)) {           // entryType: mustUnmarshalEntry
+    if (d.type == 2) {           // entryType: mustUnmarshalEntry
       PbField e1, e2, e3, e4, e5;
       pbf_init(e1); pbf_init(e2); pbf_init(e3); pbf_init(e4); pbf_init(e5);
       int s2 = 0, ur = 0;
@@ -957,17 +1019,237 @@ __global__ __launch_bounds__(256) void k_decode(const uint8_t *__restrict__ buf,
   }
   // P at every frame start (the previous frame's data end, in the canonical
   // layout), and P at this frame's data start from it (header bytes only).
-  const uint32_t Pfo = (dbg & 1024) ? 0u : prefix_at(p, pwave, v, buf, s_t4, s_svp);
-  pf[n + r] = Pfo;
+  const uint32_t Pfo = prefix_at(p, pwave, v, buf, s_t4, s_svp);
+  pfo[r] = Pfo;
   if (st == 0 && d.type != 4 && d.dlen > 0) {
     uint32_t c = Pfo;
     const int64_t nh = (int64_t)(d.doff - p);
     for (int64_t j = 0; j < nh; ++j) c = s_t4[(c ^ R[j]) & 0xff] ^ (c >> 8);
-    pf[r] = c;
+    pfd[r] = c;
     if (r == n - 1 || d.doff + d.dlen != p + 8 + (uint64_t)L)
       d.chained = prefix_at(d.doff + d.dlen, pwave, v, buf, s_t4, s_svp);   // P(data end), used by k_verify
   }
   rd[r] = d;
+}
+
+// The frames the canonical parser declined, grid-stride over the device-side
+// count (rec_cand == nullptr: frame r is candidate r).
+__global__ __launch_bounds__(256) void k_decode_slow(const uint8_t *__restrict__ buf, uint64_t B,
+                         const uint64_t *__restrict__ pos, const uint32_t *__restrict__ rec_cand,
+                         const uint32_t *__restrict__ slow, const Small *ds, const uint32_t *__restrict__ pwave,
+                         const uint32_t *__restrict__ v, const uint32_t *__restrict__ g_slice,
+                         const uint32_t *__restrict__ g_shift, RecDesc *__restrict__ rd, uint32_t *__restrict__ pfd,
+                         uint32_t *__restrict__ pfo, uint32_t n_host) {
+  const uint32_t ns = ds->nslow;
+  if (ns == 0) return;
+  // frames on the chain: the host's count, or the device's candidate count (k_frame)
+  const uint32_t n = n_host ? n_host : (uint32_t)ds->total;
+  __shared__ uint32_t s_t4[1024];
+  __shared__ uint32_t s_svp[1024];
+  __shared__ uint4 s_win[256][5];
+  stage_lds<256>(s_t4, 1024, [&](int i) { return g_slice[i]; });
+  stage_lds<256>(s_svp, 1024, [&](int i) { return g_shift[EW_VLOG * 1024 + i]; });
+  __syncthreads();
+  for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < ns; j += gridDim.x * blockDim.x) {
+    const uint32_t r = slow[j];
+    const uint64_t p = pos[rec_cand ? rec_cand[r] : r];
+    decode_general(buf, B, p, (int64_t)ld_le64_b(buf, B, p), r, n, pwave, v, s_t4, s_svp, s_win[threadIdx.x], rd,
+                   pfd, pfo);
+  }
+}
+
+// ---- canonical fast path ---------------------------------------------------
+// The frame head (80 bytes from the 16-B boundary below the frame start) in
+// LDS, TRANSPOSED: dword k of thread t at w[k * 256] (w = s_win + t), so the
+// bank of every read is t & 31 whatever offset each lane reads.
+__device__ __forceinline__ uint32_t win4(const uint32_t *w, int o) {
+  const int k = o >> 2;
+  return __builtin_amdgcn_alignbyte(w[(k + 1) * 256], w[k * 256], (uint32_t)(o & 3));
+}
+__device__ __forceinline__ uint64_t win8(const uint32_t *w, int o) {
+  const int k = o >> 2;
+  const uint32_t a = w[k * 256], b = w[(k + 1) * 256], c = w[(k + 2) * 256];
+  const uint32_t sh = (uint32_t)(o & 3);
+  return ((uint64_t)__builtin_amdgcn_alignbyte(c, b, sh) << 32) | __builtin_amdgcn_alignbyte(b, a, sh);
+}
+// tag byte + varint of at most 7 bytes at window offset o: returns the offset
+// after the field, clears ok on a different tag, a longer varint or a field
+// outside the window (the general walker then takes the frame).
+__device__ __forceinline__ int pb_field_fast(const uint32_t *w, int o, uint32_t tag, uint64_t &v, bool &ok) {
+  const int oc = o <= 71 ? o : 71;
+  const uint64_t x = win8(w, oc);
+  const uint64_t t = ~(x >> 8) & 0x0080808080808080ull;   // terminators among the 7 bytes after the tag
+  const int nb = t ? (__builtin_ctzll(t) >> 3) + 1 : 8;
+  uint64_t y = (x >> 8) & (nb >= 8 ? 0x00ffffffffffffffull : ((1ull << (8 * nb)) - 1));
+  y = ((y & 0x7f007f007f007f00ull) >> 1) | (y & 0x007f007f007f007full);
+  y = ((y & 0x3fff00003fff0000ull) >> 2) | (y & 0x00003fff00003fffull);
+  y = ((y & 0x0fffffff00000000ull) >> 4) | (y & 0x000000000fffffffull);
+  v = y;
+  ok = ok && o <= 71 && (uint32_t)(x & 0xff) == tag && nb < 8;
+  return o + 1 + nb;
+}
+
+// Canonical fast decode of frame r at p (int64 length L read from the
+// window, so no earlier pass has to fetch it): canonical encodings -- Record
+// {08 type 10 crc [1a len Data]}, Entry {08 type 10 term 18 index [22 len
+// Data]}, HardState {08 term 10 vote 18 commit}, every varint at most 7
+// bytes, the last field ending exactly at the message end -- are parsed with
+// word operations; any other frame goes to the slow list (k_decode_slow: the
+// general walkers, exact gogoprotobuf semantics).  Then P at the frame start
+// and at the data start.  The frame head and prefix_at's operands are loaded
+// together, one memory round trip.  Returns L.
+__device__ __forceinline__ int64_t decode_fast(const uint8_t *__restrict__ buf, uint64_t B, uint64_t p, uint32_t r,
+                                               bool last, const uint32_t *__restrict__ pwave,
+                                               const uint32_t *__restrict__ v, const uint32_t *s_t4,
+                                               const uint32_t *s_svp, uint32_t *w, RecDesc *__restrict__ rd,
+                                               uint32_t *__restrict__ pfd, uint32_t *__restrict__ pfo,
+                                               uint32_t *__restrict__ slow, Small *ds) {
+  const uint64_t p16 = p & ~15ull;
+  uint4 hq[5];
+#pragma unroll
+  for (int k = 0; k < 5; ++k) {
+    const uint64_t o = p16 + 16 * k;
+    if (o + 16 <= B) {
+      hq[k] = *(const uint4 *)(buf + o);
+    } else {
+      uint32_t x[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) x[j] = load_word_guarded(buf, B, o + 4 * j);
+      hq[k] = make_uint4(x[0], x[1], x[2], x[3]);
+    }
+  }
+  PrefixIn pin;
+  prefix_load(p, pwave, v, buf, pin);
+#pragma unroll
+  for (int k = 0; k < 5; ++k) {
+    w[(4 * k) * 256] = hq[k].x; w[(4 * k + 1) * 256] = hq[k].y;
+    w[(4 * k + 2) * 256] = hq[k].z; w[(4 * k + 3) * 256] = hq[k].w;
+  }
+  const int base = (int)(p - p16);
+  const int64_t L = (int64_t)win8(w, base);
+  const int64_t end = 8 + L;          // message end, relative to p
+  bool ok = L >= 0 && L < (1ll << 40);
+  uint64_t ty = 0, cr = 0, dl = 0;
+  int o = pb_field_fast(w, base + 8, 0x08, ty, ok);
+  o = pb_field_fast(w, o, 0x10, cr, ok);
+  const bool hasd = ok && (int64_t)(o - base) < end;
+  if (hasd) o = pb_field_fast(w, o, 0x1a, dl, ok);
+  ok = ok && (hasd ? (end - (int64_t)(o - base) == (int64_t)dl) : ((int64_t)(o - base) == end));
+  RecDesc d;
+  d.off = p;
+  d.type = (int64_t)ty;
+  d.crc = (uint32_t)cr;
+  d.chained = 0; d.st = 0; d.sub_st = 0;
+  d.doff = p + 8; d.dlen = 0; d.dnil = 1;
+  d.f0 = d.f1 = d.f2 = 0; d.edoff = 0; d.edlen = 0; d.enil = 1; d.etype = 0;
+  const int ho = o;                   // window offset of the data start
+  if (hasd && dl > 0) { d.doff = p + (uint64_t)(o - base); d.dlen = dl; d.dnil = 0; }
+  if (ok && !d.dnil && (d.type == 2 || d.type == 3)) {
+    const int64_t eend = (int64_t)(ho - base) + (int64_t)dl;
+    uint64_t f0 = 0, f1 = 0, f2 = 0;
+    int e = pb_field_fast(w, ho, 0x08, f0, ok);
+    e = pb_field_fast(w, e, 0x10, f1, ok);
+    e = pb_field_fast(w, e, 0x18, f2, ok);
+    if (d.type == 2) {                // Entry: Type, Term, Index [, Data]
+      const bool hase = ok && (int64_t)(e - base) < eend;
+      uint64_t el = 0;
+      if (hase) e = pb_field_fast(w, e, 0x22, el, ok);
+      ok = ok && (hase ? (eend - (int64_t)(e - base) == (int64_t)el) : ((int64_t)(e - base) == eend));
+      d.etype = (int32_t)(uint32_t)f0;
+      d.f0 = f1;
+      d.f1 = f2;
+      if (hase && el > 0) { d.edoff = p + (uint64_t)(e - base); d.edlen = el; d.enil = 0; }
+    } else {                          // HardState: Term, Vote, Commit
+      ok = ok && (int64_t)(e - base) == eend;
+      d.f0 = f0; d.f1 = f1; d.f2 = f2;
+    }
+  }
+  if (!ok) {
+    slow[atomicAdd(&ds->nslow, 1u)] = r;
+    return L;
+  }
+  const uint32_t Pfo = prefix_finish(pin, s_t4, s_svp);
+  pfo[r] = Pfo;
+  if (d.type != 4 && d.dlen > 0) {    // P(data start): the header bytes after P(frame start)
+    uint32_t c = Pfo;
+    const int nh = ho - base;
+    int j = 0;
+    for (; j + 4 <= nh; j += 4) c = step4_flat(s_t4, c ^ win4(w, base + j));
+    uint32_t t = win4(w, base + j);
+    for (; j < nh; ++j, t >>= 8) c = s_t4[(c ^ t) & 0xff] ^ (c >> 8);
+    pfd[r] = c;
+    if (last) d.chained = prefix_at(d.doff + d.dlen, pwave, v, buf, s_t4, s_svp);   // P(data end)
+  }
+  rd[r] = d;
+  return L;
+}
+
+// k_decode: the frames of a chain the host framed (frame r = candidate
+// rec_cand[r], or candidate r when rec_cand is null).
+__global__ __launch_bounds__(256) void k_decode(const uint8_t *__restrict__ buf, uint64_t B,
+                         const uint64_t *__restrict__ pos, const uint32_t *__restrict__ rec_cand, uint32_t n,
+                         const uint32_t *__restrict__ pwave, const uint32_t *__restrict__ v,
+                         const uint32_t *__restrict__ g_slice, const uint32_t *__restrict__ g_shift,
+                         RecDesc *__restrict__ rd, uint32_t *__restrict__ pfd, uint32_t *__restrict__ pfo,
+                         uint32_t *__restrict__ slow, Small *ds) {
+  __shared__ uint32_t s_t4[1024];
+  __shared__ uint32_t s_svp[1024];   // S_256 (prefix_at's Horner step)
+  __shared__ uint32_t s_win[20 * 256];
+  stage_lds<256>(s_t4, 1024, [&](int i) { return g_slice[i]; });
+  stage_lds<256>(s_svp, 1024, [&](int i) { return g_shift[EW_VLOG * 1024 + i]; });
+  __syncthreads();
+  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= n) return;
+  decode_fast(buf, B, pos[rec_cand ? rec_cand[r] : r], r, r == n - 1, pwave, v, s_t4, s_svp, s_win + threadIdx.x, rd, pfd, pfo,
+              slow, ds);
+}
+
+// k_frame: framing and decode in one pass, speculating that the candidates
+// form ONE chain from byte 0 (frame r = candidate r; the normal case).  Per
+// candidate: its int64 length L (from the frame head it decodes anyway), the
+// check that the next candidate starts at p + 8 + L (else the chain is
+// irregular and the host redoes the framing by pointer jumping), the chain's
+// terminal q and the int64 there, and the decode of the frame.  Grid-stride
+// over the device-side candidate count; also initialises ReadAll's
+// reductions.  Frames past rdcap (the descriptor capacity) are left to the
+// host's retry with larger buffers.
+__global__ __launch_bounds__(256) void k_frame(const uint8_t *__restrict__ buf, uint64_t B,
+                         const uint64_t *__restrict__ pos, uint64_t ccap, uint64_t rdcap,
+                         const uint32_t *__restrict__ pwave, const uint32_t *__restrict__ v,
+                         const uint32_t *__restrict__ g_slice, const uint32_t *__restrict__ g_shift,
+                         RecDesc *__restrict__ rd, uint32_t *__restrict__ pfd, uint32_t *__restrict__ pfo,
+                         uint32_t *__restrict__ slow, Small *ds) {
+  __shared__ uint32_t s_t4[1024];
+  __shared__ uint32_t s_svp[1024];
+  __shared__ uint32_t s_win[20 * 256];
+  uint64_t K = ds->total;
+  const uint64_t g0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, stride = (uint64_t)gridDim.x * blockDim.x;
+  if (g0 == 0) {
+    ds->agg.first_fail = ~0ull;
+    ds->agg.last_entry = -1;
+    ds->agg.last_state = -1;
+    ds->agg.first_meta = ~0ull;
+    ds->pos0 = K ? pos[0] : ~0ull;
+  }
+  if (K > ccap || K > rdcap) return;   // the host retries with larger buffers
+  stage_lds<256>(s_t4, 1024, [&](int i) { return g_slice[i]; });
+  stage_lds<256>(s_svp, 1024, [&](int i) { return g_shift[EW_VLOG * 1024 + i]; });
+  __syncthreads();
+  uint32_t irr = 0;
+  for (uint64_t r = g0; r < K; r += stride) {
+    const uint64_t p = pos[r];
+    const uint64_t pn = r + 1 < K ? pos[r + 1] : 0;
+    const int64_t L = decode_fast(buf, B, p, (uint32_t)r, r + 1 == K, pwave, v, s_t4, s_svp, s_win + threadIdx.x, rd,
+                                  pfd, pfo, slow, ds);
+    const uint64_t s = p + 8 + (uint64_t)L;
+    if (r + 1 < K) {
+      irr |= pn != s;
+    } else {   // the last candidate: terminal of the regular chain
+      ds->q = s;
+      ds->qlen = (s <= B && B - s >= 8) ? (int64_t)ld_le64_b(buf, B, s) : 0;
+    }
+  }
+  if (__ballot(irr) && (threadIdx.x & 63) == 0) atomicOr(&ds->irregular, 1u);
 }
 
 // k_verify: the chained-CRC check of every frame (== the reference's running
@@ -975,12 +1257,13 @@ __global__ __launch_bounds__(256) void k_decode(const uint8_t *__restrict__ buf,
 // reductions (first failure, last entry / state, first metadata), the
 // entry-op flags (Index >= ri) and the list of metadata frames k_meta checks.
 __global__ __launch_bounds__(1024) void k_verify(const uint32_t *__restrict__ g_shift, RecDesc *__restrict__ rd,
-                         uint32_t n, const uint32_t *__restrict__ pf, uint64_t ri, uint8_t *__restrict__ opf,
+                         uint32_t n, const uint32_t *__restrict__ pfd, const uint32_t *__restrict__ pfo, uint64_t ri,
+                         uint8_t *__restrict__ opf,
                          uint32_t *__restrict__ mlist, Small *ds) {
   ReadAllAgg *agg = &ds->agg;
   __shared__ uint32_t s_sh[17 * 1024];   // S_{2^0} .. S_{2^16}
   __shared__ uint32_t s_red[4];          // block: last entry + 1, last state + 1, first metadata, first failure
-  for (int i = threadIdx.x; i < 17 * 1024; i += blockDim.x) s_sh[i] = g_shift[i];
+  stage_lds<1024>(s_sh, 17 * 1024, [&](int i) { return g_shift[i]; });
   if (threadIdx.x == 0) { s_red[0] = 0; s_red[1] = 0; s_red[2] = 0xffffffffu; s_red[3] = 0xffffffffu; }
   __syncthreads();
   const uint32_t rt = blockIdx.x * blockDim.x + threadIdx.x;
@@ -990,8 +1273,8 @@ __global__ __launch_bounds__(1024) void k_verify(const uint32_t *__restrict__ g_
   const RecDesc d = rd[r];
   const uint32_t seed = r ? rd[r - 1].crc : 0u;
   const uint64_t noff = r + 1 < n ? rd[r + 1].off : ~0ull;
-  const uint32_t ps = pf[r];
-  const uint32_t pn = r + 1 < n ? pf[n + r + 1] : 0u;
+  const uint32_t ps = pfd[r];
+  const uint32_t pn = r + 1 < n ? pfo[r + 1] : 0u;
   int st = d.st;
   uint32_t chained = seed;
   if (st == 0) {
@@ -1004,7 +1287,7 @@ __global__ __launch_bounds__(1024) void k_verify(const uint32_t *__restrict__ g_
         computed = seed;
       } else {
         const uint64_t e = d.doff + d.dlen;
-        // P(data end) = P(next frame start) in the canonical layout (pf[n+r+1]),
+        // P(data end) = P(next frame start) in the canonical layout (pfo[r+1]),
         // else k_decode left it in d.chained.  U(seed, D) = S_n(seed ^ ~0 ^ P(s)) ^ P(e) ^ ~0
         const uint32_t Pe = noff == e ? pn : d.chained;
         uint32_t x = seed ^ 0xffffffffu ^ ps;
