@@ -58,7 +58,7 @@ class Result(C.Structure):
     _fields_ = [("status", C.c_int32), ("flags", C.c_int32), ("detail", C.c_int64), ("fail_record", C.c_int64),
                 ("fail_offset", C.c_int64), ("n_records", C.c_int64), ("last_crc", C.c_uint32),
                 ("reserved0", C.c_uint32), ("enti", C.c_uint64), ("metadata_off", C.c_int64),
-                ("metadata_len", C.c_int64), ("has_state", C.c_int32), ("reserved1", C.c_int32),
+                ("metadata_len", C.c_int64), ("has_state", C.c_int32), ("n_slow", C.c_int32),
                 ("state_term", C.c_uint64), ("state_vote", C.c_uint64), ("state_commit", C.c_uint64),
                 ("n_ents", C.c_int64), ("n_candidates", C.c_int64), ("n_runs", C.c_int64), ("device_ms", C.c_double),
                 ("stream_ms", C.c_double)]

@@ -26,6 +26,7 @@ namespace ewal {
 struct CrcTables {
   uint32_t poly = 0;
   uint32_t slice[4][256];
+  uint32_t slice16[16][256];    // slicing-by-16 (slice16[t] = slice[t] for t < 4): the device table
   std::vector<uint32_t> shift;  // EW_SHIFT_LEVELS * 4 * 256
 
   explicit CrcTables(uint32_t p) : poly(p), shift((size_t)EW_SHIFT_LEVELS * 1024) {
@@ -37,6 +38,10 @@ struct CrcTables {
     for (int t = 1; t < 4; t++)
       for (uint32_t i = 0; i < 256; i++)
         slice[t][i] = (slice[t - 1][i] >> 8) ^ slice[0][slice[t - 1][i] & 0xff];
+    std::memcpy(slice16, slice, sizeof(slice));
+    for (int t = 4; t < 16; t++)
+      for (uint32_t i = 0; i < 256; i++)
+        slice16[t][i] = (slice16[t - 1][i] >> 8) ^ slice[0][slice16[t - 1][i] & 0xff];
     // S_1 as a GF(2) matrix (column j = S_1(1 << j)), then repeated squaring.
     uint32_t m[32], sq[32];
     for (int j = 0; j < 32; j++) {

@@ -33,7 +33,7 @@
 namespace {
 
 struct DevTables {
-  uint32_t *slice = nullptr;  // [4][256]
+  uint32_t *slice = nullptr;  // [16][256] slicing-by-16 (the first 4 tables: slicing-by-4)
   uint32_t *shift = nullptr;  // [48][4][256]
 };
 
@@ -70,7 +70,7 @@ struct ewal_ctx {
   hipEvent_t ev0 = nullptr, ev1 = nullptr, evs0 = nullptr, evs1 = nullptr;
   std::map<uint32_t, DevTables> tables;
   std::map<uint32_t, std::unique_ptr<ewal::CrcTables>> host_tables;
-  DevBuf slow, mlist, pf, v, pwave, ux, tagg, tpx, wcnt, slots, cbase, ovf, cpos, clen, nxt, exc, E, rs, jl, vis, entry, on, rec_cand, rd, opf, ops, kk, kkrev, suf,
+  DevBuf gagg, slow, mlist, pf, v, pwave, ux, tagg, tpx, wcnt, slots, cbase, ovf, cpos, clen, nxt, exc, E, rs, jl, vis, entry, on, rec_cand, rd, opf, ops, kk, kkrev, suf,
       ents, recs, tmp, small, sdesc, snaps, hbuf_dev;
   Small *h_small = nullptr;        // host-mapped pinned mirrors (written by k_export_small / k_result)
   ResultDev *h_res = nullptr;
@@ -91,9 +91,9 @@ static int get_tables(ewal_ctx *c, uint32_t poly, DevTables **out) {
   }
   auto ht = std::make_unique<ewal::CrcTables>(poly);
   DevTables t;
-  EW_CHECK(hipMalloc(&t.slice, sizeof(ht->slice)));
+  EW_CHECK(hipMalloc(&t.slice, sizeof(ht->slice16)));
   EW_CHECK(hipMalloc(&t.shift, ht->shift.size() * sizeof(uint32_t)));
-  EW_CHECK(hipMemcpy(t.slice, ht->slice, sizeof(ht->slice), hipMemcpyHostToDevice));
+  EW_CHECK(hipMemcpy(t.slice, ht->slice16, sizeof(ht->slice16), hipMemcpyHostToDevice));
   EW_CHECK(hipMemcpy(t.shift, ht->shift.data(), ht->shift.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
   c->host_tables[poly] = std::move(ht);
   c->tables[poly] = t;
@@ -135,7 +135,7 @@ static int run_stream(ewal_ctx *c, DevTables *tb, const uint8_t *d_buf, uint64_t
   const uint64_t nunits64 = B / EW_WAVE_BYTES + 1;
   if (nunits64 >= 0xffff0000ull) return EWAL_E_INVAL;
   const uint32_t nunits = (uint32_t)nunits64;
-  const uint32_t nstiles = (nunits + 1023) / 1024;
+  const uint32_t nstiles = (nunits + EW_TILE_UNITS - 1) / EW_TILE_UNITS;
   EW_CHECK(c->v.ensure((size_t)nunits * EW_VPU * 4));
   EW_CHECK(c->pwave.ensure((size_t)nunits * 4));
   EW_CHECK(c->wcnt.ensure((size_t)nunits * 4));
@@ -147,6 +147,7 @@ static int run_stream(ewal_ctx *c, DevTables *tb, const uint8_t *d_buf, uint64_t
   EW_CHECK(c->ux.ensure((size_t)nunits * 4));
   EW_CHECK(c->tagg.ensure((size_t)nstiles * 16));
   EW_CHECK(c->tpx.ensure((size_t)nstiles * 16));
+  EW_CHECK(c->gagg.ensure((size_t)((nstiles + 1023) / 1024) * 16));
   EW_CHECK(hipMemsetAsync(c->small.p, 0, sizeof(Small), c->stream));
   Small *ds = c->small.as<Small>();
   StreamArgs a;
@@ -178,16 +179,23 @@ static int run_stream(ewal_ctx *c, DevTables *tb, const uint8_t *d_buf, uint64_t
   s.tcnt = s.tagg + nstiles;
   s.tpx = c->tpx.as<uint32_t>();
   s.tcb = (unsigned long long *)(c->tpx.as<uint8_t>() + (size_t)nstiles * 8);
+  s.gcnt = c->gagg.as<unsigned long long>();
+  s.gagg = (uint32_t *)(s.gcnt + (nstiles + 1023) / 1024);
   s.total = &ds->total;
   s.slots = find_cand ? c->slots.as<uint16_t>() : nullptr;
   s.cpos = find_cand ? c->cpos.as<uint64_t>() : nullptr;
   s.ccap = ccap;
   s.ovf = find_cand ? c->ovf.as<uint32_t>() : nullptr;
   s.novf = &ds->novf;
-  // one wave per 4 MiB tile, four waves per workgroup
-  const unsigned sgrid = std::min<uint32_t>((nstiles + 3) / 4, 4u * (uint32_t)c->num_cu);
-  hipLaunchKernelGGL(k_uagg, dim3(sgrid), dim3(256), 0, c->stream, s);
-  hipLaunchKernelGGL(k_tscan, dim3(1), dim3(1024), 0, c->stream, s);
+  // one wave per 1 MiB tile: k_uagg one 16-wave workgroup per CU (its S_256
+  // table fills the LDS), k_uapply four waves per workgroup
+  const unsigned agrid = std::min<uint32_t>((nstiles + 15) / 16, (uint32_t)c->num_cu);
+  const unsigned sgrid = std::min<uint32_t>((nstiles + 3) / 4, 8u * (uint32_t)c->num_cu);
+  hipLaunchKernelGGL(k_uagg, dim3(agrid), dim3(1024), 0, c->stream, s);
+  const uint32_t ngroups = (nstiles + 1023) / 1024;
+  if (ngroups > 1024) return EWAL_E_INVAL;   // k_tfix: at most 1024 tile groups (1 TiB)
+  hipLaunchKernelGGL(k_tscan, dim3(ngroups), dim3(1024), 0, c->stream, s);
+  hipLaunchKernelGGL(k_tfix, dim3(ngroups), dim3(1024), 0, c->stream, s, ngroups);
   hipLaunchKernelGGL(k_uapply, dim3(sgrid), dim3(256), 0, c->stream, s);
   EW_CHECK(hipGetLastError());
   if (find_cand) {
@@ -318,7 +326,7 @@ static int readall_impl(ewal_ctx *c, const uint8_t *d_buf, uint64_t B, uint64_t 
     const unsigned fgrid = (unsigned)std::max(1, c->num_cu) * 8;
     hipLaunchKernelGGL(k_frame, dim3(fgrid), dim3(256), 0, c->stream, d_buf, B, c->cpos.as<uint64_t>(), ccap, rdcap,
                        c->pwave.as<uint32_t>(), c->v.as<uint32_t>(), tb->slice, tb->shift, c->rd.as<RecDesc>(), pf,
-                       pf + rdcap, c->slow.as<uint32_t>(), ds);
+                       pf + rdcap, c->slow.as<uint32_t>(), ds, c->ablate);
     hipLaunchKernelGGL(k_decode_slow, dim3(64), dim3(256), 0, c->stream, d_buf, B, c->cpos.as<uint64_t>(),
                        (const uint32_t *)nullptr, c->slow.as<uint32_t>(), ds, c->pwave.as<uint32_t>(),
                        c->v.as<uint32_t>(), tb->slice, tb->shift, c->rd.as<RecDesc>(), pf, pf + rdcap, 0u);
@@ -414,6 +422,7 @@ static int readall_impl(ewal_ctx *c, const uint8_t *d_buf, uint64_t B, uint64_t 
     EW_CHECK(hipGetLastError());
     EW_CHECK(hipStreamSynchronize(c->stream));
     std::memcpy(&res, c->h_res, sizeof(ResultDev));
+    out->n_slow = (int32_t)res.nslow;
   }
   const ReadAllAgg &hagg = res.agg;
   out->n_records = (int64_t)n;
@@ -528,7 +537,7 @@ void ewal_ctx_destroy(ewal_ctx *c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
   (void)hipStreamSynchronize(c->stream);
-  DevBuf *bufs[] = {&c->slow, &c->mlist, &c->pf, &c->v, &c->pwave, &c->ux, &c->tagg, &c->tpx, &c->wcnt, &c->slots, &c->cbase, &c->ovf, &c->cpos, &c->clen, &c->nxt, &c->exc, &c->E, &c->rs, &c->jl,
+  DevBuf *bufs[] = {&c->gagg, &c->slow, &c->mlist, &c->pf, &c->v, &c->pwave, &c->ux, &c->tagg, &c->tpx, &c->wcnt, &c->slots, &c->cbase, &c->ovf, &c->cpos, &c->clen, &c->nxt, &c->exc, &c->E, &c->rs, &c->jl,
                     &c->vis, &c->entry, &c->on, &c->rec_cand, &c->rd, &c->opf, &c->ops, &c->kk, &c->kkrev,
                     &c->suf, &c->ents, &c->recs, &c->tmp, &c->small, &c->sdesc, &c->snaps, &c->hbuf_dev};
   for (DevBuf *b : bufs) b->release();

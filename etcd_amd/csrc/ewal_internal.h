@@ -20,12 +20,14 @@ struct StreamArgs {
 };
 
 struct ScanArgs {
-  uint32_t nunits, ntiles;        // ntiles = ceil(nunits / 1024) (4 MiB tiles)
+  uint32_t nunits, ntiles;        // ntiles = ceil(nunits / EW_TILE_UNITS) (1 MiB tiles)
   const uint32_t *v, *wcnt;       // super-piece lins, candidate counts (k_stream)
   const uint32_t *g_shift;
   uint32_t *ux;                   // lin of every 4 KiB unit          [nunits]
   uint32_t *tagg, *tcnt;          // tile aggregates                  [ntiles]
   uint32_t *tpx;                  // P at every tile start            [ntiles]
+  uint32_t *gagg;                 // tile-group (1024 tiles) aggregates [ngroups]
+  unsigned long long *gcnt;       // candidates per tile group        [ngroups]
   unsigned long long *tcb;        // candidates before every tile     [ntiles]
   uint32_t *pwave;                // stream prefix at every unit start
   unsigned long long *cbase;      // candidates before every unit
@@ -99,4 +101,5 @@ struct ResultDev {
   RecDesc fail, lastent, last, md, sd;
   uint32_t nops, nonmono;
   uint64_t klast;
+  uint32_t nslow, pad;
 };

@@ -453,63 +453,62 @@ __global__ __launch_bounds__(EW_THREADS, 1) void k_stream(StreamArgs a) {
 // ===========================================================================
 
 // The unit scan turns the per-unit lins into the stream prefix P at every
-// unit start.  Three kernels, one WAVE per 4 MiB tile (1024 units) so no
-// workgroup barrier sits on the critical path:
+// unit start.  Three kernels, one WAVE per 1 MiB tile (EW_TILE_UNITS = 256
+// units) so no workgroup barrier sits on the critical path:
 //   k_uagg   per-unit lin x (from the 16 super-piece lins) and per-tile
-//            aggregate, via the linear form  agg = XOR_u S_{4096 (1023-u)}(x_u);
+//            aggregate, via the linear form  agg = XOR_u S_{4096 (255-u)}(x_u);
 //   k_tscan  exclusive affine scan of the tile aggregates (one workgroup);
-//   k_uapply lane-serial Horner over 16 consecutive units, one wave scan of
+//   k_uapply lane-serial Horner over 4 consecutive units, one wave scan of
 //            the 64 lane spans, replay -> P and candidate base per unit, and
 //            the candidate-list compaction.
-// Tables live in LDS; tab_apply(S_m) costs four random ds_read_b32.
+#define EW_TILE_UNITS 256
+#define EW_TILE_LOG 20                            // 1 MiB
 
-// lin of one 4 KiB unit from its 16 super-piece lins: four Horner chains of
-// four 256-B values (S_256), joined with S_1024
-__device__ __forceinline__ uint32_t unit_lin(const uint4 (&q)[4], const uint32_t *svp, const uint32_t *s1k) {
-  uint32_t h[4];
-#pragma unroll
-  for (int g = 0; g < 4; ++g) {
-    h[g] = tab_apply(svp, q[g].x) ^ q[g].y;
-    h[g] = tab_apply(svp, h[g]) ^ q[g].z;
-    h[g] = tab_apply(svp, h[g]) ^ q[g].w;
-  }
-  return tab_apply(s1k, tab_apply(s1k, tab_apply(s1k, h[0]) ^ h[1]) ^ h[2]) ^ h[3];
-}
-
-// Lane l of a wave reads units 64 i + l (i = 0..15: coalesced 4 KiB rows of
-// v), folds them with h = S_{2^18}(h) ^ x (S_{2^18} = 64 units), shifts the
-// fold by the units after it in its row (S_{4096 (63-l)}) and XOR-reduces.
-__global__ __launch_bounds__(256) void k_uagg(ScanArgs a) {
-  __shared__ uint32_t s_svp[1024], s_s1k[1024];   // S_256, S_1024
+// Lane l of a wave reads units 64 i + l (i = 0..3: coalesced 4 KiB rows of
+// v), forms x with 15 S_256 steps through the conflict-free perm-layout table
+// (the k_stream layout: 128 KiB, bank = lane & 31), folds its 4 units with
+// h = S_{2^18}(h) ^ x (S_{2^18} = 64 units), shifts the fold by the units
+// after it in its row (S_{4096 (63-l)}) and XOR-reduces.  One workgroup of
+// 16 waves per CU, persistent over the tiles.
+__global__ __launch_bounds__(1024, 1) void k_uagg(ScanArgs a) {
+  __shared__ __attribute__((aligned(16))) uint8_t s_s256[EW_SLICE_DWORDS * 4];   // S_256, perm layout
   __shared__ uint32_t s_sh[7 * 1024];             // S_{2^12} .. S_{2^18}
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  stage_lds<256>(s_svp, 1024, [&](int i) { return a.g_shift[EW_VLOG * 1024 + i]; });
-  stage_lds<256>(s_s1k, 1024, [&](int i) { return a.g_shift[10 * 1024 + i]; });
-  stage_lds<256>(s_sh, 7 * 1024, [&](int i) { return a.g_shift[12 * 1024 + i]; });
+  stage_lds<1024>((uint32_t *)s_s256, EW_SLICE_DWORDS, [&](int i) { return a.g_shift[shift_src(EW_VLOG, i)]; });
+  stage_lds<1024>(s_sh, 7 * 1024, [&](int i) { return a.g_shift[12 * 1024 + i]; });
   __syncthreads();
-  for (uint32_t t = blockIdx.x * 4 + wv; t < a.ntiles; t += gridDim.x * 4) {
-    const uint32_t u0 = t * 1024 + lane;
-    uint32_t h = 0, cnt = 0;
-    for (int i0 = 0; i0 < 16; i0 += 4) {
-      uint4 q[4][4];
-      uint32_t c[4];
+  uint32_t Lt[4];
+  lane_regs(lane, Lt);
+  for (uint32_t t = blockIdx.x * 16 + wv; t < a.ntiles; t += gridDim.x * 16) {
+    const uint32_t u0 = t * EW_TILE_UNITS + lane;
+    uint4 q[4][4];
+    uint32_t c[4];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {   // every load of the four rows up front
-        const uint32_t u = u0 + 64 * (i0 + r);
-        const bool in = u < a.nunits;
-        const uint4 *vq = (const uint4 *)(a.v + (size_t)(in ? u : 0) * EW_VPU);
+    for (int r = 0; r < 4; ++r) {   // every load of the tile up front
+      const uint32_t u = u0 + 64 * r;
+      const bool in = u < a.nunits;
+      const uint4 *vq = (const uint4 *)(a.v + (size_t)(in ? u : 0) * EW_VPU);
 #pragma unroll
-        for (int g = 0; g < 4; ++g) q[r][g] = in ? vq[g] : make_uint4(0, 0, 0, 0);
-        c[r] = in ? a.wcnt[u] : 0u;
-      }
+      for (int g = 0; g < 4; ++g) q[r][g] = in ? vq[g] : make_uint4(0, 0, 0, 0);
+      c[r] = in ? a.wcnt[u] : 0u;
+    }
+    uint32_t x[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) x[r] = q[r][0].x;
+#pragma unroll
+    for (int k = 1; k < 16; ++k)   // four independent Horner chains
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const uint32_t u = u0 + 64 * (i0 + r);
-        const uint32_t x = unit_lin(q[r], s_svp, s_s1k);
-        if (u < a.nunits) a.ux[u] = x;
-        h = tab_apply(s_sh + 6 * 1024, h) ^ x;
-        cnt += c[r];
+        const uint4 &g = q[r][k >> 2];
+        const uint32_t d = (k & 3) == 0 ? g.x : (k & 3) == 1 ? g.y : (k & 3) == 2 ? g.z : g.w;
+        x[r] = perm_step(s_s256, Lt, x[r], d);
       }
+    uint32_t h = 0, cnt = 0;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      if (u0 + 64 * r < a.nunits) a.ux[u0 + 64 * r] = x[r];
+      h = tab_apply(s_sh + 6 * 1024, h) ^ x[r];
+      cnt += c[r];
     }
     const uint32_t after = 63 - lane;
 #pragma unroll
@@ -524,32 +523,24 @@ __global__ __launch_bounds__(256) void k_uagg(ScanArgs a) {
   }
 }
 
-// One workgroup of 1024 threads; thread T owns tiles [T k, T k + k), k = 2^e
-// the smallest power of two with 1024 k >= ntiles: lane Horner (S_{2^22} per
-// tile), wave and workgroup scans of the thread spans (S_{2^(22+e+d)}), replay.
+// Tile scan in two launches of one workgroup per 1024 tiles (1 GiB):
+//   k_tscan  thread T <- tile 1024 b + T: wave and workgroup scans of the tile
+//            aggregates (S_{2^(20+d)}), the exclusive in-group prefix -> tpx,
+//            tcb, the group aggregate -> gagg[b], gcnt[b];
+//   k_tfix   P at the group start from the groups before it, via the linear
+//            form XOR_i S_{2^30 (b-1-i)}(gagg[i]) (thread i, workgroup XOR), then
+//            tpx[t] = S_{2^20 T}(P at the group start) ^ tpx[t].
 __global__ __launch_bounds__(1024) void k_tscan(ScanArgs a) {
-  __shared__ uint32_t s_t1[1024];                 // S_{2^22}: one tile
-  __shared__ uint32_t s_sh[10 * 1024];            // S_{2^(22+e+d)}, d = 0..9
+  __shared__ uint32_t s_sh[10 * 1024];            // S_{2^20} .. S_{2^29}
   __shared__ uint32_t s_wq[16];
   __shared__ unsigned long long s_wc[16];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  int e = 0;
-  while ((1024ull << e) < a.ntiles) ++e;
-  const uint32_t k = 1u << e;
-  s_t1[tid] = a.g_shift[22 * 1024 + tid];
-  stage_lds<1024>(s_sh, 10 * 1024, [&](int i) { return a.g_shift[(22 + e) * 1024 + i]; });
+  stage_lds<1024>(s_sh, 10 * 1024, [&](int i) { return a.g_shift[EW_TILE_LOG * 1024 + i]; });
   __syncthreads();
-  const uint64_t t0 = (uint64_t)tid * k;
-  uint32_t h = 0;
-  unsigned long long cs = 0;
-  for (uint32_t j = 0; j < k; ++j) {
-    const uint64_t t = t0 + j;
-    const uint32_t x = t < a.ntiles ? a.tagg[t] : 0u;
-    h = tab_apply(s_t1, h) ^ x;
-    cs += t < a.ntiles ? a.tcnt[t] : 0u;
-  }
-  uint32_t q = h;
-  unsigned long long qc = cs;
+  const uint32_t t = blockIdx.x * 1024 + tid;
+  const bool in = t < a.ntiles;
+  uint32_t q = in ? a.tagg[t] : 0u;
+  unsigned long long qc = in ? a.tcnt[t] : 0u;
 #pragma unroll
   for (int d = 0; d < 6; ++d) {
     const uint32_t o = __shfl_up(q, 1 << d);
@@ -573,49 +564,87 @@ __global__ __launch_bounds__(1024) void k_tscan(ScanArgs a) {
     uint32_t we = __shfl_up(w, 1);
     unsigned long long wce = __shfl_up(wc, 1);
     if (lane == 0) { we = 0; wce = 0; }
-    if (lane == 15) *a.total = wc;
+    if (lane == 15) { a.gagg[blockIdx.x] = w; a.gcnt[blockIdx.x] = wc; }
     if (lane < 16) { s_wq[lane] = we; s_wc[lane] = wce; }
   }
   __syncthreads();
-  uint32_t cur = s_wq[wv];                        // S_{span * lane}(wave start) ^ lane prefix
+  uint32_t cur = s_wq[wv];                        // S_{2^20 lane}(wave start) ^ lane prefix
 #pragma unroll
   for (int b = 0; b < 6; ++b)
     if ((lane >> b) & 1) cur = tab_apply(s_sh + b * 1024, cur);
-  cur ^= ex;
-  unsigned long long cb = s_wc[wv] + exc;
-  for (uint32_t j = 0; j < k; ++j) {
-    const uint64_t t = t0 + j;
-    if (t >= a.ntiles) break;
-    a.tpx[t] = cur;
-    a.tcb[t] = cb;
-    cur = tab_apply(s_t1, cur) ^ a.tagg[t];
-    cb += a.tcnt[t];
+  if (in) {
+    a.tpx[t] = cur ^ ex;
+    a.tcb[t] = s_wc[wv] + exc;
   }
 }
 
-// Lane l owns units 16 l .. 16 l + 15 of the wave's tile: Horner over them
-// (S_4096), wave scan of the 64 lane spans (S_{2^(16+d)}), lane start =
-// S_{2^16 l}(P at the tile start) ^ exclusive span, replay.
+__global__ __launch_bounds__(1024) void k_tfix(ScanArgs a, uint32_t ngroups) {
+  __shared__ uint32_t s_sh[20 * 1024];            // S_{2^20} .. S_{2^39}
+  __shared__ uint32_t s_x[16];
+  __shared__ unsigned long long s_c[16];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const uint32_t b = blockIdx.x;
+  if (b == 0 && ngroups == 1) {
+    if (tid == 0) *a.total = a.gcnt[0];
+    return;                                       // one group: tpx is final
+  }
+  stage_lds<1024>(s_sh, 20 * 1024, [&](int i) { return a.g_shift[EW_TILE_LOG * 1024 + i]; });
+  __syncthreads();
+  // group i < b contributes S_{2^30 (b - 1 - i)}(gagg[i]); groups <= 1024
+  uint32_t x = 0;
+  unsigned long long cnt = 0;
+  if ((uint32_t)tid < b) {
+    x = a.gagg[tid];
+    cnt = a.gcnt[tid];
+    const uint32_t m = b - 1 - tid;
+#pragma unroll
+    for (int k = 0; k < 10; ++k)
+      if ((m >> k) & 1) x = tab_apply(s_sh + (10 + k) * 1024, x);
+  }
+#pragma unroll
+  for (int o = 32; o; o >>= 1) {
+    x ^= __shfl_xor(x, o);
+    cnt += __shfl_xor(cnt, o);
+  }
+  if (lane == 0) { s_x[wv] = x; s_c[wv] = cnt; }
+  __syncthreads();
+  uint32_t P = 0;
+  unsigned long long C = 0;
+#pragma unroll
+  for (int w = 0; w < 16; ++w) { P ^= s_x[w]; C += s_c[w]; }
+  if (b == ngroups - 1 && tid == 0) *a.total = C + a.gcnt[b];
+  if (b == 0) return;                             // P = 0 at the stream start
+  const uint32_t t = b * 1024 + tid;
+  if (t < a.ntiles) {
+#pragma unroll
+    for (int k = 0; k < 10; ++k)
+      if ((tid >> k) & 1) P = tab_apply(s_sh + k * 1024, P);
+    a.tpx[t] ^= P;
+    a.tcb[t] += C;
+  }
+}
+
+// Lane l owns units 4 l .. 4 l + 3 of the wave's tile: Horner over them
+// (S_4096), wave scan of the 64 lane spans (S_{2^(14+d)}), lane start =
+// S_{2^14 l}(P at the tile start) ^ exclusive span, replay.
 __global__ __launch_bounds__(256) void k_uapply(ScanArgs a) {
   __shared__ uint32_t s_s12[1024];                // S_4096
-  __shared__ uint32_t s_sh[6 * 1024];             // S_{2^16} .. S_{2^21}
+  __shared__ uint32_t s_sh[6 * 1024];             // S_{2^14} .. S_{2^19}
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   stage_lds<256>(s_s12, 1024, [&](int i) { return a.g_shift[12 * 1024 + i]; });
-  stage_lds<256>(s_sh, 6 * 1024, [&](int i) { return a.g_shift[16 * 1024 + i]; });
+  stage_lds<256>(s_sh, 6 * 1024, [&](int i) { return a.g_shift[14 * 1024 + i]; });
   __syncthreads();
   for (uint32_t t = blockIdx.x * 4 + wv; t < a.ntiles; t += gridDim.x * 4) {
-    const uint32_t u0 = t * 1024 + 16 * lane;
-    uint32_t x[16], c[16];
-    if (u0 + 16 <= a.nunits) {
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const uint4 xv = ((const uint4 *)(a.ux + u0))[g], cv = ((const uint4 *)(a.wcnt + u0))[g];
-        x[4 * g] = xv.x; x[4 * g + 1] = xv.y; x[4 * g + 2] = xv.z; x[4 * g + 3] = xv.w;
-        c[4 * g] = cv.x; c[4 * g + 1] = cv.y; c[4 * g + 2] = cv.z; c[4 * g + 3] = cv.w;
-      }
+    const uint32_t u0 = t * EW_TILE_UNITS + 4 * lane;
+    const bool full = u0 + 4 <= a.nunits;
+    uint32_t x[4], c[4];
+    if (full) {
+      const uint4 xv = *(const uint4 *)(a.ux + u0), cv = *(const uint4 *)(a.wcnt + u0);
+      x[0] = xv.x; x[1] = xv.y; x[2] = xv.z; x[3] = xv.w;
+      c[0] = cv.x; c[1] = cv.y; c[2] = cv.z; c[3] = cv.w;
     } else {
 #pragma unroll
-      for (int j = 0; j < 16; ++j) {
+      for (int j = 0; j < 4; ++j) {
         const bool in = u0 + j < a.nunits;
         x[j] = in ? a.ux[u0 + j] : 0u;
         c[j] = in ? a.wcnt[u0 + j] : 0u;
@@ -625,15 +654,15 @@ __global__ __launch_bounds__(256) void k_uapply(ScanArgs a) {
     // candidates, issued before the arithmetic so the wave waits once
     const uint32_t tp = a.tpx[t];
     const unsigned long long tcb = a.tcb[t];
-    uint4 sv[16];
+    uint4 sv[4];
     if (a.slots) {
 #pragma unroll
-      for (int j = 0; j < 16; ++j)
+      for (int j = 0; j < 4; ++j)
         sv[j] = c[j] ? *(const uint4 *)(a.slots + (size_t)(u0 + j) * EW_SLOTS) : make_uint4(0, 0, 0, 0);
     }
     uint32_t q = 0, qc = 0;
 #pragma unroll
-    for (int j = 0; j < 16; ++j) { q = tab_apply(s_s12, q) ^ x[j]; qc += c[j]; }
+    for (int j = 0; j < 4; ++j) { q = tab_apply(s_s12, q) ^ x[j]; qc += c[j]; }
 #pragma unroll
     for (int d = 0; d < 6; ++d) {
       const uint32_t o = __shfl_up(q, 1 << d), oc = __shfl_up(qc, 1 << d);
@@ -647,34 +676,29 @@ __global__ __launch_bounds__(256) void k_uapply(ScanArgs a) {
       if ((lane >> b) & 1) cur = tab_apply(s_sh + b * 1024, cur);
     cur ^= ex;
     unsigned long long cb = tcb + exc;
-    uint32_t pw[16];
-    unsigned long long cbs[16];
+    uint32_t pw[4];
+    unsigned long long cbs[4];
 #pragma unroll
-    for (int j = 0; j < 16; ++j) {
+    for (int j = 0; j < 4; ++j) {
       pw[j] = cur;
       cbs[j] = cb;
       cur = tab_apply(s_s12, cur) ^ x[j];
       cb += c[j];
     }
-    if (u0 + 16 <= a.nunits) {
-#pragma unroll
-      for (int g = 0; g < 4; ++g)
-        ((uint4 *)(a.pwave + u0))[g] = make_uint4(pw[4 * g], pw[4 * g + 1], pw[4 * g + 2], pw[4 * g + 3]);
-#pragma unroll
-      for (int g = 0; g < 8; ++g) {
-        ulonglong2 w;
-        w.x = cbs[2 * g];
-        w.y = cbs[2 * g + 1];
-        ((ulonglong2 *)(a.cbase + u0))[g] = w;
-      }
+    if (full) {
+      *(uint4 *)(a.pwave + u0) = make_uint4(pw[0], pw[1], pw[2], pw[3]);
+      ulonglong2 w0, w1;
+      w0.x = cbs[0]; w0.y = cbs[1]; w1.x = cbs[2]; w1.y = cbs[3];
+      ((ulonglong2 *)(a.cbase + u0))[0] = w0;
+      ((ulonglong2 *)(a.cbase + u0))[1] = w1;
     } else {
 #pragma unroll
-      for (int j = 0; j < 16; ++j)
+      for (int j = 0; j < 4; ++j)
         if (u0 + j < a.nunits) { a.pwave[u0 + j] = pw[j]; a.cbase[u0 + j] = cbs[j]; }
     }
     if (a.slots) {   // compaction: slots -> the dense, position-sorted candidate list
 #pragma unroll
-      for (int j = 0; j < 16; ++j) {
+      for (int j = 0; j < 4; ++j) {
         const uint32_t u = u0 + j, cx = c[j];
         if (!cx) continue;
         if (cx > EW_SLOTS) {
@@ -940,6 +964,48 @@ __device__ __forceinline__ uint32_t prefix_finish(const PrefixIn &in, const uint
   }
   return acc;
 }
+// Slicing-by-16 step over one 16-B chunk (t = 16 tables, t[k] = byte then k
+// zero bytes): only the first dword's four lookups depend on c, so the
+// dependent chain is one lookup level per 16 bytes.
+__device__ __forceinline__ uint32_t step16(const uint32_t *t, uint32_t c, const uint4 &d) {
+  const uint32_t x = c ^ d.x;
+  const uint32_t a = t[15 * 256 + (x & 0xff)] ^ t[14 * 256 + ((x >> 8) & 0xff)] ^ t[13 * 256 + ((x >> 16) & 0xff)] ^
+                     t[12 * 256 + (x >> 24)];
+  const uint32_t b = t[11 * 256 + (d.y & 0xff)] ^ t[10 * 256 + ((d.y >> 8) & 0xff)] ^
+                     t[9 * 256 + ((d.y >> 16) & 0xff)] ^ t[8 * 256 + (d.y >> 24)];
+  const uint32_t e = t[7 * 256 + (d.z & 0xff)] ^ t[6 * 256 + ((d.z >> 8) & 0xff)] ^
+                     t[5 * 256 + ((d.z >> 16) & 0xff)] ^ t[4 * 256 + (d.z >> 24)];
+  const uint32_t f = t[3 * 256 + (d.w & 0xff)] ^ t[2 * 256 + ((d.w >> 8) & 0xff)] ^
+                     t[1 * 256 + ((d.w >> 16) & 0xff)] ^ t[d.w >> 24];
+  return a ^ b ^ e ^ f;
+}
+// prefix_finish with the slicing-by-16 tables t16 (the first 1024 entries are
+// the slicing-by-4 tables)
+__device__ __forceinline__ uint32_t prefix_finish16(const PrefixIn &in, const uint32_t *t16, const uint32_t *svp) {
+  const uint32_t k = in.k, tail = in.tail;
+  uint32_t acc = in.pw;
+#pragma unroll
+  for (int q = 0; q < EW_VPU / 4; ++q) {
+    if (4u * q + 0 < k) acc = tab_apply(svp, acc) ^ in.vv[q].x;
+    if (4u * q + 1 < k) acc = tab_apply(svp, acc) ^ in.vv[q].y;
+    if (4u * q + 2 < k) acc = tab_apply(svp, acc) ^ in.vv[q].z;
+    if (4u * q + 3 < k) acc = tab_apply(svp, acc) ^ in.vv[q].w;
+  }
+  const uint32_t nq = tail >> 4;
+  uint4 pc = in.dd[0];
+#pragma unroll
+  for (int q = 0; q < EW_VPIECE / 16; ++q) {
+    if ((uint32_t)q < nq) acc = step16(t16, acc, in.dd[q]);
+    if (q && (uint32_t)q == nq) pc = in.dd[q];
+  }
+  const uint32_t nd = (tail & 15) >> 2;
+  if (nd > 0) acc = step4_flat(t16, acc ^ pc.x);
+  if (nd > 1) acc = step4_flat(t16, acc ^ pc.y);
+  if (nd > 2) acc = step4_flat(t16, acc ^ pc.z);
+  uint32_t wd = nd == 0 ? pc.x : nd == 1 ? pc.y : nd == 2 ? pc.z : pc.w;
+  for (uint32_t b = 0; b < (tail & 3); ++b, wd >>= 8) acc = t16[(acc ^ wd) & 0xff] ^ (acc >> 8);
+  return acc;
+}
 __device__ __forceinline__ uint32_t prefix_at(uint64_t x, const uint32_t *__restrict__ pwave,
                                               const uint32_t *__restrict__ v, const uint8_t *__restrict__ buf,
                                               const uint32_t *t4, const uint32_t *svp) {
@@ -1103,7 +1169,7 @@ __device__ __forceinline__ int64_t decode_fast(const uint8_t *__restrict__ buf, 
                                                const uint32_t *__restrict__ v, const uint32_t *s_t4,
                                                const uint32_t *s_svp, uint32_t *w, RecDesc *__restrict__ rd,
                                                uint32_t *__restrict__ pfd, uint32_t *__restrict__ pfo,
-                                               uint32_t *__restrict__ slow, Small *ds) {
+                                               uint32_t *__restrict__ slow, Small *ds, int dbg = 0) {
   const uint64_t p16 = p & ~15ull;
   uint4 hq[5];
 #pragma unroll
@@ -1119,7 +1185,7 @@ __device__ __forceinline__ int64_t decode_fast(const uint8_t *__restrict__ buf, 
     }
   }
   PrefixIn pin;
-  prefix_load(p, pwave, v, buf, pin);
+  prefix_load((dbg & 256) ? (p & ~255ull) : (dbg & 512) ? (p & ~4095ull) + (p & 255) : p, pwave, v, buf, pin);
 #pragma unroll
   for (int k = 0; k < 5; ++k) {
     w[(4 * k) * 256] = hq[k].x; w[(4 * k + 1) * 256] = hq[k].y;
@@ -1168,7 +1234,8 @@ __device__ __forceinline__ int64_t decode_fast(const uint8_t *__restrict__ buf, 
     slow[atomicAdd(&ds->nslow, 1u)] = r;
     return L;
   }
-  const uint32_t Pfo = prefix_finish(pin, s_t4, s_svp);
+  const uint32_t Pfo = prefix_finish16(pin, s_t4, s_svp);
+  if (dbg & 1024) { if (Pfo == 0x12345678u) rd[r] = d; return L; }
   pfo[r] = Pfo;
   if (d.type != 4 && d.dlen > 0) {    // P(data start): the header bytes after P(frame start)
     uint32_t c = Pfo;
@@ -1192,10 +1259,10 @@ __global__ __launch_bounds__(256) void k_decode(const uint8_t *__restrict__ buf,
                          const uint32_t *__restrict__ g_slice, const uint32_t *__restrict__ g_shift,
                          RecDesc *__restrict__ rd, uint32_t *__restrict__ pfd, uint32_t *__restrict__ pfo,
                          uint32_t *__restrict__ slow, Small *ds) {
-  __shared__ uint32_t s_t4[1024];
+  __shared__ uint32_t s_t4[16 * 256];   // slicing-by-16
   __shared__ uint32_t s_svp[1024];   // S_256 (prefix_at's Horner step)
   __shared__ uint32_t s_win[20 * 256];
-  stage_lds<256>(s_t4, 1024, [&](int i) { return g_slice[i]; });
+  stage_lds<256>(s_t4, 16 * 256, [&](int i) { return g_slice[i]; });
   stage_lds<256>(s_svp, 1024, [&](int i) { return g_shift[EW_VLOG * 1024 + i]; });
   __syncthreads();
   const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1218,8 +1285,8 @@ __global__ __launch_bounds__(256) void k_frame(const uint8_t *__restrict__ buf, 
                          const uint32_t *__restrict__ pwave, const uint32_t *__restrict__ v,
                          const uint32_t *__restrict__ g_slice, const uint32_t *__restrict__ g_shift,
                          RecDesc *__restrict__ rd, uint32_t *__restrict__ pfd, uint32_t *__restrict__ pfo,
-                         uint32_t *__restrict__ slow, Small *ds) {
-  __shared__ uint32_t s_t4[1024];
+                         uint32_t *__restrict__ slow, Small *ds, int dbg) {
+  __shared__ uint32_t s_t4[16 * 256];   // slicing-by-16
   __shared__ uint32_t s_svp[1024];
   __shared__ uint32_t s_win[20 * 256];
   uint64_t K = ds->total;
@@ -1232,7 +1299,7 @@ __global__ __launch_bounds__(256) void k_frame(const uint8_t *__restrict__ buf, 
     ds->pos0 = K ? pos[0] : ~0ull;
   }
   if (K > ccap || K > rdcap) return;   // the host retries with larger buffers
-  stage_lds<256>(s_t4, 1024, [&](int i) { return g_slice[i]; });
+  stage_lds<256>(s_t4, 16 * 256, [&](int i) { return g_slice[i]; });
   stage_lds<256>(s_svp, 1024, [&](int i) { return g_shift[EW_VLOG * 1024 + i]; });
   __syncthreads();
   uint32_t irr = 0;
@@ -1240,7 +1307,7 @@ __global__ __launch_bounds__(256) void k_frame(const uint8_t *__restrict__ buf, 
     const uint64_t p = pos[r];
     const uint64_t pn = r + 1 < K ? pos[r + 1] : 0;
     const int64_t L = decode_fast(buf, B, p, (uint32_t)r, r + 1 == K, pwave, v, s_t4, s_svp, s_win + threadIdx.x, rd,
-                                  pfd, pfo, slow, ds);
+                                  pfd, pfo, slow, ds, dbg);
     const uint64_t s = p + 8 + (uint64_t)L;
     if (r + 1 < K) {
       irr |= pn != s;
@@ -1417,6 +1484,7 @@ __global__ void k_result(const RecDesc *__restrict__ rd, uint32_t n, const Small
   o->nops = ds->nsel3;
   o->nonmono = ds->nonmono;
   o->klast = ds->klast;
+  o->nslow = ds->nslow;
   if (g.first_fail < n) o->fail = rd[g.first_fail];
   if (g.last_entry >= 0) o->lastent = rd[g.last_entry];
   if (n) o->last = rd[n - 1];

@@ -130,6 +130,7 @@ class ReadAllResult:
     n_runs: int = 0
     device_ms: float = 0.0
     stream_ms: float = 0.0
+    n_slow: int = 0           # frames decoded by the general (non-canonical) walker
 
     def as_dict(self):
         return dict(status=self.status, detail=self.detail, fail_record=self.fail_record,
@@ -154,7 +155,7 @@ def _collect(ctx, r, buf_view, with_ents=True):
             data = None if e.data_nil else bytes(buf_view[e.data_off:e.data_off + e.data_len])
             ents.append(Entry(e.type, e.term, e.index, data))
     return ReadAllResult(r.status, r.detail, r.fail_record, r.fail_offset, r.n_records, r.last_crc if ok else 0,
-                         r.enti, md, st, ents, r.n_candidates, r.n_runs, r.device_ms, r.stream_ms)
+                         r.enti, md, st, ents, r.n_candidates, r.n_runs, r.device_ms, r.stream_ms, r.n_slow)
 
 
 def readall_bytes(buf: bytes, ri: int = 0, ctx: Context = None, with_ents=True) -> ReadAllResult:

@@ -76,7 +76,7 @@ typedef struct ewal_result {
   int64_t metadata_off;    /* metadata []byte as (offset,len) into the stream; -1 == nil */
   int64_t metadata_len;
   int32_t has_state;       /* 0 -> HardState{} */
-  int32_t reserved1;
+  int32_t n_slow;          /* diagnostics: frames decoded by the general (non-canonical) walker */
   uint64_t state_term, state_vote, state_commit;
   int64_t n_ents;          /* len(ents); fetch with ewal_copy_entries */
   int64_t n_candidates;    /* diagnostics: frame-start candidates found */
