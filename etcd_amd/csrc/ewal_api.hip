@@ -2,8 +2,9 @@
 //
 // Implements include/ewal.h's compute entry points.  The pipeline for
 // (*WAL).ReadAll (wal/wal.go:164-216) is:
-//   k_stream (one HBM pass) -> framing (k_link, runs, pointer jumping) ->
-//   k_decode -> k_verify -> k_meta -> entry ops (k_opflag, k_gap, k_ents)
+//   k_stream (one HBM pass) -> unit scan -> k_frame (speculative framing +
+//   decode; fallback: k_link, runs, pointer jumping, k_decode) -> k_check ->
+//   k_meta (k_check also places the entry ops; rare: k_gap, k_ents)
 // and the host only classifies the chain's terminal frame and assembles the
 // ewal_result from a few device reductions.  No CPU decoding or CRC happens
 // on this path; without a GPU every call returns EWAL_E_NODEVICE.
@@ -70,7 +71,7 @@ struct ewal_ctx {
   hipEvent_t ev0 = nullptr, ev1 = nullptr, evs0 = nullptr, evs1 = nullptr;
   std::map<uint32_t, DevTables> tables;
   std::map<uint32_t, std::unique_ptr<ewal::CrcTables>> host_tables;
-  DevBuf gagg, slow, mlist, pf, v, pwave, ux, tagg, tpx, wcnt, slots, cbase, ovf, cpos, clen, nxt, exc, E, rs, jl, vis, entry, on, rec_cand, rd, opf, ops, kk, kkrev, suf,
+  DevBuf lbstat, gagg, slow, mlist, pf, v, pwave, ux, tagg, tpx, wcnt, slots, cbase, ovf, cpos, clen, nxt, exc, E, rs, jl, vis, entry, on, rec_cand, rd, opf, ops, kk, kkrev, suf,
       ents, recs, tmp, small, sdesc, snaps, hbuf_dev;
   Small *h_small = nullptr;        // host-mapped pinned mirrors (written by k_export_small / k_result)
   ResultDev *h_res = nullptr;
@@ -79,6 +80,7 @@ struct ewal_ctx {
   // results of the last readall
   uint64_t last_n = 0, last_nents = 0;
   uint64_t last_k = 0;     // candidates of the previous call (sizes k_frame's descriptors)
+  uint32_t epoch = 0;      // k_check look-back epoch (24 bits)
   uint64_t pfcap = 0;      // pf = [P at data starts | P at frame starts], pfcap each
   bool last_ok = false;
 };
@@ -405,23 +407,38 @@ static int readall_impl(ewal_ctx *c, const uint8_t *d_buf, uint64_t B, uint64_t 
     }
     RecDesc *rd = c->rd.as<RecDesc>();
     const uint32_t *pfd = c->pf.as<uint32_t>(), *pfo = pfd + c->pfcap;
-    EW_CHECK(c->opf.ensure(n));
+    const uint32_t nb = grid_for(n, 1024);
+    // look-back status words of k_check: zeroed when (re)allocated and when
+    // the 24-bit epoch wraps; otherwise the epoch tells old words apart
+    const size_t had = c->lbstat.cap;
+    EW_CHECK(c->lbstat.ensure((size_t)nb * 8));
+    c->epoch = (c->epoch + 1) & 0xffffffu;
+    if (c->lbstat.cap != had || c->epoch == 0) {
+      EW_CHECK(hipMemsetAsync(c->lbstat.p, 0, c->lbstat.cap, c->stream));
+      if (c->epoch == 0) c->epoch = 1;
+    }
     EW_CHECK(c->ops.ensure((size_t)n * 4));
     EW_CHECK(c->mlist.ensure((size_t)n * 4));
-    hipLaunchKernelGGL(k_verify, dim3(grid_for(n, 1024)), dim3(1024), 0, c->stream, tb->shift, rd, n32,
-                       pfd, pfo, ri, c->opf.as<uint8_t>(), c->mlist.as<uint32_t>(), ds);
-    hipLaunchKernelGGL(k_meta, dim3(64), dim3(256), 0, c->stream, d_buf, rd, c->mlist.as<uint32_t>(), ds);
-    rc = select_flagged(c, c->opf.as<uint8_t>(), n32, c->ops.as<uint32_t>(), &ds->nsel3);
-    if (rc) return rc;
     EW_CHECK(c->kk.ensure((size_t)n * 8));
     EW_CHECK(c->ents.ensure((size_t)n * sizeof(ewal_entry)));
-    const unsigned ggrid = (unsigned)std::min<uint64_t>(grid_for(n, 256), (uint64_t)c->num_cu * 8);
-    hipLaunchKernelGGL(k_gap, dim3(ggrid), dim3(256), 0, c->stream, rd, c->ops.as<uint32_t>(), ri,
-                       c->kk.as<uint64_t>(), c->ents.as<ewal_entry>(), ds);
-    hipLaunchKernelGGL(k_result, dim3(1), dim3(64), 0, c->stream, rd, n32, ds, c->h_res_dev);
+    hipLaunchKernelGGL(k_check, dim3(nb), dim3(1024), 0, c->stream, tb->shift, rd, n32, pfd, pfo, ri,
+                       c->lbstat.as<unsigned long long>(), c->epoch, c->ops.as<uint32_t>(), c->kk.as<uint64_t>(),
+                       c->ents.as<ewal_entry>(), c->mlist.as<uint32_t>(), ds);
+    hipLaunchKernelGGL(k_meta, dim3(64), dim3(256), 0, c->stream, d_buf, rd, c->mlist.as<uint32_t>(), ds);
+    hipLaunchKernelGGL(k_result, dim3(1), dim3(64), 0, c->stream, rd, n32, ri, ds, c->h_res_dev);
     EW_CHECK(hipGetLastError());
     EW_CHECK(hipStreamSynchronize(c->stream));
     std::memcpy(&res, c->h_res, sizeof(ResultDev));
+    if (res.errflag) return EWAL_E_TIMEOUT;
+    if (res.gapslow) {   // an op's predecessor lay too far back for k_check: list-based gap pass
+      const unsigned ggrid = (unsigned)std::min<uint64_t>(grid_for(n, 256), (uint64_t)c->num_cu * 8);
+      hipLaunchKernelGGL(k_gap, dim3(ggrid), dim3(256), 0, c->stream, rd, c->ops.as<uint32_t>(),
+                         c->kk.as<uint64_t>(), ds);
+      hipLaunchKernelGGL(k_result, dim3(1), dim3(64), 0, c->stream, rd, n32, ri, ds, c->h_res_dev);
+      EW_CHECK(hipGetLastError());
+      EW_CHECK(hipStreamSynchronize(c->stream));
+      std::memcpy(&res, c->h_res, sizeof(ResultDev));
+    }
     out->n_slow = (int32_t)res.nslow;
   }
   const ReadAllAgg &hagg = res.agg;
@@ -537,7 +554,7 @@ void ewal_ctx_destroy(ewal_ctx *c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
   (void)hipStreamSynchronize(c->stream);
-  DevBuf *bufs[] = {&c->gagg, &c->slow, &c->mlist, &c->pf, &c->v, &c->pwave, &c->ux, &c->tagg, &c->tpx, &c->wcnt, &c->slots, &c->cbase, &c->ovf, &c->cpos, &c->clen, &c->nxt, &c->exc, &c->E, &c->rs, &c->jl,
+  DevBuf *bufs[] = {&c->lbstat, &c->gagg, &c->slow, &c->mlist, &c->pf, &c->v, &c->pwave, &c->ux, &c->tagg, &c->tpx, &c->wcnt, &c->slots, &c->cbase, &c->ovf, &c->cpos, &c->clen, &c->nxt, &c->exc, &c->E, &c->rs, &c->jl,
                     &c->vis, &c->entry, &c->on, &c->rec_cand, &c->rd, &c->opf, &c->ops, &c->kk, &c->kkrev,
                     &c->suf, &c->ents, &c->recs, &c->tmp, &c->small, &c->sdesc, &c->snaps, &c->hbuf_dev};
   for (DevBuf *b : bufs) b->release();

@@ -90,9 +90,10 @@ struct Small {
   uint32_t nsel2;
   uint32_t nsel3;                 // entry ops
   uint32_t nonmono;               // k_gap: entry indexes not strictly increasing
-  uint64_t klast;                 // k of the last entry op (len(ents) - 1)
-  uint32_t nmeta;                 // metadata frames listed by k_verify
+  uint32_t nmeta;                 // metadata frames listed by k_check
   uint32_t nslow;                 // frames k_decode left to k_decode_slow (non-canonical encodings)
+  uint32_t lastop;                // k_check: 1 + the last entry op's frame (0: none)
+  uint32_t gapslow;               // k_check: an op's predecessor lies too far back (list-based k_gap)
 };
 
 // Everything the host needs after the frame pass, gathered by k_result.
@@ -101,5 +102,6 @@ struct ResultDev {
   RecDesc fail, lastent, last, md, sd;
   uint32_t nops, nonmono;
   uint64_t klast;
-  uint32_t nslow, pad;
+  uint32_t nslow, gapslow;
+  uint32_t errflag, pad;
 };

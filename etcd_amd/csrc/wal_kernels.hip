@@ -8,21 +8,27 @@
 //   raft/raftpb/raft.pb.go:170-277,618-704  -- Entry / HardState Unmarshal
 //
 // Kernels (one HBM pass over the WAL bytes, then per-frame work):
-//   k_stream   fused: per-lane CRC (slicing-by-4, LDS tables), frame-start
-//              candidate detection, wave/tile affine CRC reduction and the
-//              device-wide decoupled look-back that turns tile CRCs into
-//              stream prefixes P(x) = lin(stream[0..x)) at every 4 KiB, plus
-//              the ordered candidate list.
-//   k_link     candidate -> successor candidate (pos + 8 + len).
-//   k_runs / k_jump / k_mark / k_entry / k_member
-//              framing: the true frame chain from byte 0 by pointer jumping
-//              over runs of consecutive candidates.
-//   k_decode   walpb.Record / raftpb.Entry / HardState decode per frame.
-//   k_verify   chained CRC check per frame against its predecessor's stored
+//   k_stream   per-lane CRC of every 64-B piece (slicing-by-4, conflict-free
+//              LDS tables), lin of every 256-B super-piece -> v[], frame-start
+//              candidates -> per-unit slots.
+//   k_uagg / k_tscan / k_tfix / k_uapply
+//              unit scan: stream prefixes P(x) = lin(stream[0..x)) at every
+//              4 KiB unit, candidate bases, the dense sorted candidate list.
+//   k_frame    speculative framing + decode: candidate r is frame r when the
+//              candidates chain from byte 0 (checked here); canonical
+//              Record / Entry / HardState parse; P at frame and data starts.
+//   k_decode_slow  the general gogoprotobuf walkers for the frames k_frame
+//              declined.
+//   k_link, k_runs / k_jump / k_mark / k_entry / k_member, k_decode
+//              the fallback framing by pointer jumping over runs of
+//              consecutive candidates (false candidates, torn tails).
+//   k_check    chained CRC check per frame against its predecessor's stored
 //              CRC (== the reference's running CRC up to the first failure),
 //              using the stream prefixes: Update(seed, D[s,e)) =
-//              S_n(seed ^ ~0 ^ P(s)) ^ P(e) ^ ~0.
-//   k_meta / k_ops / k_gap / k_ents: ReadAll's metadata / ents semantics.
+//              S_n(seed ^ ~0 ^ P(s)) ^ P(e) ^ ~0; Entry / HardState verdicts,
+//              the index-gap panic, ReadAll's reductions.
+//   k_meta / k_opscan / k_opents (k_gap, k_ents): ReadAll's metadata and
+//              ents semantics.
 #include "ewal_device.h"
 #include "ewal_internal.h"
 
@@ -1093,7 +1099,7 @@ __device__ __forceinline__ void decode_general(const uint8_t *__restrict__ buf, 
     for (int64_t j = 0; j < nh; ++j) c = s_t4[(c ^ R[j]) & 0xff] ^ (c >> 8);
     pfd[r] = c;
     if (r == n - 1 || d.doff + d.dlen != p + 8 + (uint64_t)L)
-      d.chained = prefix_at(d.doff + d.dlen, pwave, v, buf, s_t4, s_svp);   // P(data end), used by k_verify
+      d.chained = prefix_at(d.doff + d.dlen, pwave, v, buf, s_t4, s_svp);   // P(data end), used by k_check
   }
   rd[r] = d;
 }
@@ -1319,19 +1325,78 @@ __global__ __launch_bounds__(256) void k_frame(const uint8_t *__restrict__ buf, 
   if (__ballot(irr) && (threadIdx.x & 63) == 0) atomicOr(&ds->irregular, 1u);
 }
 
-// k_verify: the chained-CRC check of every frame (== the reference's running
-// CRC up to its first failure), the Entry/HardState verdicts, ReadAll's
-// reductions (first failure, last entry / state, first metadata), the
-// entry-op flags (Index >= ri) and the list of metadata frames k_meta checks.
-__global__ __launch_bounds__(1024) void k_verify(const uint32_t *__restrict__ g_shift, RecDesc *__restrict__ rd,
+// k_check: the chained-CRC check of every frame (== the reference's running
+// CRC up to its first failure), the Entry/HardState verdicts, the entry-op
+// index-gap panic, ReadAll's reductions (first failure, last entry / state /
+// op, first metadata), the per-workgroup op counts (k_opscan / k_opents) and
+// the list of metadata frames k_meta checks.
+#define EW_GAP_BACK 16
+
+// Decoupled look-back over per-workgroup counts (one wave): workgroup b
+// publishes its count, then sums its predecessors' counts 64 at a time until
+// it meets a published inclusive prefix, and publishes its own.  status[b] =
+// epoch << 40 | flag << 32 | value (flag 1: the workgroup's count, 2: the
+// inclusive prefix through it); an entry from an earlier call has another
+// epoch and reads as not yet published.  Workgroups are dispatched in order
+// (per XCD), so the lowest unfinished one is always resident and the waits
+// drain; a spin budget reports EWAL_E_TIMEOUT instead of hanging.
+__device__ __forceinline__ uint32_t lookback_count(unsigned long long *status, uint32_t b, uint32_t cnt,
+                                                   uint32_t epoch, uint32_t *errflag) {
+  const int lane = threadIdx.x & 63;
+  const unsigned long long tag = (unsigned long long)(epoch & 0xffffffu) << 40;
+  if (b == 0) {
+    if (lane == 0) __hip_atomic_store(&status[0], tag | (2ull << 32) | cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return 0;
+  }
+  if (lane == 0) __hip_atomic_store(&status[b], tag | (1ull << 32) | cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  uint32_t acc = 0;
+  int64_t j = (int64_t)b - 1;
+  uint32_t spins = 0;
+  for (;;) {
+    const int64_t idx = j - lane;
+    unsigned long long sv = 0;
+    int f = 2;                          // before workgroup 0: an inclusive prefix of 0
+    if (idx >= 0) {
+      sv = __hip_atomic_load(&status[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      f = ((sv >> 40) == (unsigned long long)(epoch & 0xffffffu)) ? (int)((sv >> 32) & 3) : 0;
+    }
+    const unsigned long long m2 = __ballot(f == 2), m0 = __ballot(f == 0);
+    const int f2 = m2 ? __ffsll((long long)m2) - 1 : 64, f0 = m0 ? __ffsll((long long)m0) - 1 : 64;
+    if (f2 < f0) {                      // lanes below f2 hold counts, lane f2 the inclusive prefix
+      acc += __shfl(wave_incl_sum(lane <= f2 ? (uint32_t)sv : 0u), 63);
+      break;
+    }
+    if (f0 < 64) {
+      if (++spins > (1u << 22)) {
+        if (lane == 0) atomicOr(errflag, 1u);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+      continue;
+    }
+    acc += __shfl(wave_incl_sum((uint32_t)sv), 63);
+    j -= 64;
+  }
+  if (lane == 0)
+    __hip_atomic_store(&status[b], tag | (2ull << 32) | (uint32_t)(acc + cnt), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  return acc;
+}
+__global__ __launch_bounds__(1024) void k_check(const uint32_t *__restrict__ g_shift, RecDesc *__restrict__ rd,
                          uint32_t n, const uint32_t *__restrict__ pfd, const uint32_t *__restrict__ pfo, uint64_t ri,
-                         uint8_t *__restrict__ opf,
-                         uint32_t *__restrict__ mlist, Small *ds) {
+                         unsigned long long *__restrict__ status, uint32_t epoch, uint32_t *__restrict__ ops,
+                         uint64_t *__restrict__ kk, ewal_entry *__restrict__ ents, uint32_t *__restrict__ mlist,
+                         Small *ds) {
   ReadAllAgg *agg = &ds->agg;
+  __shared__ uint32_t s_wo[16];          // ops per wave
+  __shared__ uint32_t s_base;            // ops before the workgroup
   __shared__ uint32_t s_sh[17 * 1024];   // S_{2^0} .. S_{2^16}
-  __shared__ uint32_t s_red[4];          // block: last entry + 1, last state + 1, first metadata, first failure
+  __shared__ uint32_t s_red[5];          // block: last entry + 1, last state + 1, first metadata, first failure,
+                                         //        last op + 1
   stage_lds<1024>(s_sh, 17 * 1024, [&](int i) { return g_shift[i]; });
-  if (threadIdx.x == 0) { s_red[0] = 0; s_red[1] = 0; s_red[2] = 0xffffffffu; s_red[3] = 0xffffffffu; }
+  if (threadIdx.x == 0) {
+    s_red[0] = 0; s_red[1] = 0; s_red[2] = 0xffffffffu; s_red[3] = 0xffffffffu; s_red[4] = 0;
+  }
   __syncthreads();
   const uint32_t rt = blockIdx.x * blockDim.x + threadIdx.x;
   const bool live = rt < n;
@@ -1380,16 +1445,47 @@ __global__ __launch_bounds__(1024) void k_verify(const uint32_t *__restrict__ g_
       }
     }
   }
+  // ReadAll's entry ops (wal/wal.go:170-176): an entry with Index >= ri is
+  // appended at k = Index - ri, and ents[:k] panics when k > len(ents) =
+  // k_prev + 1 (k_prev: the previous op's k; none: len 0).  Decided from the
+  // decoded fields alone, as if every earlier frame verified: when one did
+  // not, ReadAll stopped there and this frame's verdict is not the first
+  // failure.  The previous op is found among the wave's lanes (ballot), else
+  // by reading back at most EW_GAP_BACK earlier frames; farther -> the host's
+  // list-based gap pass (ds->gapslow).
+  const int lane = threadIdx.x & 63;
+  const bool op = live && d.type == 2 && d.f1 >= ri;
+  const unsigned long long mo = __ballot(op);
+  const unsigned long long below = mo & ((1ull << lane) - 1ull);
+  const uint64_t fprev = __shfl(d.f1, below ? 63 - __clzll((long long)below) : lane);   // every lane takes part
+  if (op) {
+    const uint64_t k = d.f1 - ri;
+    bool has = below != 0;
+    uint64_t kp = fprev - ri;
+    if (!has) {
+      uint32_t s2 = r - lane;   // the frames before the wave
+      for (int back = 0; back < EW_GAP_BACK && s2 > 0; ++back) {
+        --s2;
+        const int64_t t2 = rd[s2].type;
+        const uint64_t i2 = rd[s2].f1;
+        if (t2 == 2 && i2 >= ri) { kp = i2 - ri; has = true; break; }
+      }
+      if (!has && s2 > 0) atomicOr(&ds->gapslow, 1u);   // unresolved: k_gap decides
+    }
+    if (has || (r - lane) <= EW_GAP_BACK) {
+      if (has && k <= kp) atomicOr(&ds->nonmono, 1u);
+      const bool gap = has ? (k > kp && k - kp > 1) : (k > 0);
+      if (st == 0 && gap) st = EWAL_PANIC_INDEX_GAP;
+    }
+  }
   if (live) {
     rd[r].st = st;
     rd[r].chained = chained;
-    opf[r] = (d.type == 2 && st == 0 && d.f1 >= ri) ? 1 : 0;
     if (d.type == 1 && st == 0) mlist[atomicAdd(&ds->nmeta, 1u)] = r;   // rare: one per WAL file
   }
   // One atomic per WORKGROUP and quantity (same-address atomics from every
   // wave serialise at the memory side): r grows with the lane and the wave,
   // so a wave's max is its highest set lane and its min its lowest.
-  const int lane = threadIdx.x & 63;
   const unsigned long long me = __ballot(live && d.type == 2), ms = __ballot(live && d.type == 3),
                            mm = __ballot(live && d.type == 1 && d.dlen > 0), mf = __ballot(live && st != 0);
   const uint32_t r0 = r - lane;
@@ -1398,18 +1494,47 @@ __global__ __launch_bounds__(1024) void k_verify(const uint32_t *__restrict__ g_
     if (me) atomicMax(&s_red[0], r0 + (uint32_t)(63 - __clzll((long long)me)) + 1u);
     if (ms) atomicMax(&s_red[1], r0 + (uint32_t)(63 - __clzll((long long)ms)) + 1u);
     if (mm) atomicMin(&s_red[2], r0 + (uint32_t)(__ffsll((long long)mm) - 1));
+    if (mo) atomicMax(&s_red[4], r0 + (uint32_t)(63 - __clzll((long long)mo)) + 1u);
+    s_wo[threadIdx.x >> 6] = (uint32_t)__popcll(mo);
   }
   __syncthreads();
-  if (threadIdx.x == 0) {
-    if (s_red[0]) atomicMax(&agg->last_entry, (long long)(s_red[0] - 1));
-    if (s_red[1]) atomicMax(&agg->last_state, (long long)(s_red[1] - 1));
-    if (s_red[2] != 0xffffffffu) atomicMin(&agg->first_meta, (unsigned long long)s_red[2]);
-    if (s_red[3] != 0xffffffffu) atomicMin(&agg->first_fail, (unsigned long long)s_red[3]);
+  if (threadIdx.x < 64) {   // wave 0: the workgroup's op base by decoupled look-back
+    uint32_t cnt = 0;
+#pragma unroll
+    for (int w = 0; w < 16; ++w) cnt += s_wo[w];
+    const uint32_t base = lookback_count(status, blockIdx.x, cnt, epoch, &ds->errflag);
+    if (threadIdx.x == 0) {
+      s_base = base;
+      if (blockIdx.x == gridDim.x - 1) ds->nsel3 = base + cnt;
+      if (s_red[0]) atomicMax(&agg->last_entry, (long long)(s_red[0] - 1));
+      if (s_red[1]) atomicMax(&agg->last_state, (long long)(s_red[1] - 1));
+      if (s_red[2] != 0xffffffffu) atomicMin(&agg->first_meta, (unsigned long long)s_red[2]);
+      if (s_red[3] != 0xffffffffu) atomicMin(&agg->first_fail, (unsigned long long)s_red[3]);
+      if (s_red[4]) atomicMax(&ds->lastop, s_red[4]);
+    }
+  }
+  __syncthreads();
+  if (op) {   // ents[j] = op j (exact when the ops' k are strictly increasing and gap-free,
+              // otherwise the host's survivor pass rewrites ents), ops[j] = its frame, kk[j] = its k
+    uint32_t j = s_base + (uint32_t)__popcll(below);
+    const int wv = threadIdx.x >> 6;
+#pragma unroll
+    for (int w = 0; w < 16; ++w) j += (w < wv) ? s_wo[w] : 0u;
+    ewal_entry e;
+    e.term = d.f0;
+    e.index = d.f1;
+    e.data_off = d.edoff;
+    e.data_len = d.edlen;
+    e.type = d.etype;
+    e.data_nil = d.enil;
+    ents[j] = e;
+    ops[j] = r;
+    kk[j] = d.f1 - ri;
   }
 }
 
 // metadata: `metadata != nil && !reflect.DeepEqual(metadata, rec.Data)`,
-// wal/wal.go:178-183, over the metadata frames k_verify listed
+// wal/wal.go:178-183, over the metadata frames k_check listed
 __global__ void k_meta(const uint8_t *__restrict__ buf, RecDesc *__restrict__ rd, const uint32_t *__restrict__ mlist,
                        Small *ds) {
   const uint32_t nm = ds->nmeta;
@@ -1429,42 +1554,29 @@ __global__ void k_meta(const uint8_t *__restrict__ buf, RecDesc *__restrict__ rd
   }
 }
 
-// gap check: op j needs k_j <= len(ents) = k_{j-1} + 1 (wal/wal.go:173).
-// Grid-stride over the device-side op count; also flags whether the ops'
-// k are strictly increasing, records the last k (len(ents) - 1) and writes
-// ents[j] = op j.
-__global__ void k_gap(RecDesc *__restrict__ rd, const uint32_t *__restrict__ ops, uint64_t ri,
-                      uint64_t *__restrict__ kk, ewal_entry *__restrict__ ents, Small *ds) {
+// List-based gap check (the rare case where k_check could not find an op's
+// predecessor nearby): op j needs k_j <= len(ents) = k_{j-1} + 1
+// (wal/wal.go:173), over the op list k_opents wrote; frames k_check already
+// failed keep their verdict.  Also flags k not strictly increasing.
+__global__ void k_gap(RecDesc *__restrict__ rd, const uint32_t *__restrict__ ops, const uint64_t *__restrict__ kk,
+                      Small *ds) {
   const uint32_t nops = ds->nsel3;
   uint32_t nm = 0;
   for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < nops; j += gridDim.x * blockDim.x) {
     const uint32_t r = ops[j];
-    const RecDesc d = rd[r];
-    const uint64_t k = d.f1 - ri;
-    kk[j] = k;
+    const uint64_t k = kk[j];
     bool gap;
     if (j == 0) {
       gap = k > 0;
     } else {
-      const uint64_t kp = rd[ops[j - 1]].f1 - ri;
+      const uint64_t kp = kk[j - 1];
       gap = (k > kp) && (k - kp > 1);
       if (k <= kp) nm = 1;
     }
-    if (gap) {
+    if (gap && rd[r].st == 0) {
       rd[r].st = EWAL_PANIC_INDEX_GAP;
       atomicMin(&ds->agg.first_fail, (unsigned long long)r);
     }
-    if (j == nops - 1) ds->klast = k;
-    // ents[j] = op j; exact when the ops' k are strictly increasing and
-    // gap-free (k_j = j), otherwise the host's survivor pass rewrites ents
-    ewal_entry e;
-    e.term = d.f0;
-    e.index = d.f1;
-    e.data_off = d.edoff;
-    e.data_len = d.edlen;
-    e.type = d.etype;
-    e.data_nil = d.enil;
-    ents[j] = e;
   }
   if (__ballot(nm) && (threadIdx.x & 63) == 0) atomicOr(&ds->nonmono, 1u);
 }
@@ -1477,14 +1589,16 @@ __global__ void k_export_small(const Small *ds, Small *h) {
 
 // the handful of frames the host result needs, in one struct, written
 // straight into host-mapped pinned memory
-__global__ void k_result(const RecDesc *__restrict__ rd, uint32_t n, const Small *ds, ResultDev *o) {
+__global__ void k_result(const RecDesc *__restrict__ rd, uint32_t n, uint64_t ri, const Small *ds, ResultDev *o) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   const ReadAllAgg g = ds->agg;
   o->agg = g;
   o->nops = ds->nsel3;
   o->nonmono = ds->nonmono;
-  o->klast = ds->klast;
+  o->klast = ds->lastop ? rd[ds->lastop - 1].f1 - ri : 0;   // len(ents) - 1
   o->nslow = ds->nslow;
+  o->gapslow = ds->gapslow;
+  o->errflag = ds->errflag;
   if (g.first_fail < n) o->fail = rd[g.first_fail];
   if (g.last_entry >= 0) o->lastent = rd[g.last_entry];
   if (n) o->last = rd[n - 1];
