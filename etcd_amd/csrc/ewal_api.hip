@@ -329,15 +329,19 @@ static int readall_impl(ewal_ctx *c, const uint8_t *d_buf, uint64_t B, uint64_t 
     hipLaunchKernelGGL(k_frame, dim3(fgrid), dim3(256), 0, c->stream, d_buf, B, c->cpos.as<uint64_t>(), ccap, rdcap,
                        c->pwave.as<uint32_t>(), c->v.as<uint32_t>(), tb->slice, tb->shift, c->rd.as<RecDesc>(), pf,
                        pf + rdcap, c->slow.as<uint32_t>(), ds, c->ablate);
-    hipLaunchKernelGGL(k_decode_slow, dim3(64), dim3(256), 0, c->stream, d_buf, B, c->cpos.as<uint64_t>(),
-                       (const uint32_t *)nullptr, c->slow.as<uint32_t>(), ds, c->pwave.as<uint32_t>(),
-                       c->v.as<uint32_t>(), tb->slice, tb->shift, c->rd.as<RecDesc>(), pf, pf + rdcap, 0u);
     EW_CHECK(hipGetLastError());
     if ((rc = sync_small(c))) return rc;
     K = c->h_small->total;
     c->last_k = K;
     if (K && K <= ccap && K <= rdcap && c->h_small->pos0 == 0 && !c->h_small->irregular) {
       decoded = true;
+      if (c->h_small->nslow) {   // frames the canonical parser declined (a launch only when there are any)
+        hipLaunchKernelGGL(k_decode_slow, dim3(std::min<uint64_t>(grid_for(c->h_small->nslow, 256), 1024)),
+                           dim3(256), 0, c->stream, d_buf, B, c->cpos.as<uint64_t>(), (const uint32_t *)nullptr,
+                           c->slow.as<uint32_t>(), ds, c->pwave.as<uint32_t>(), c->v.as<uint32_t>(), tb->slice,
+                           tb->shift, c->rd.as<RecDesc>(), pf, pf + rdcap, 0u);
+        EW_CHECK(hipGetLastError());
+      }
     } else {
       // the speculation failed: frame by candidate links (k_link), growing
       // the candidate list first if it overflowed
