@@ -10,7 +10,9 @@ import os
 import re
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libewal.so")
+# EWAL_LIB_PATH: an alternative build of the same library (A/B timing runs
+# in tools/ only); the default is the in-tree build.
+LIB_PATH = os.environ.get("EWAL_LIB_PATH") or os.path.join(_HERE, "libewal.so")
 HEADER = os.path.join(os.path.dirname(_HERE), "include", "ewal.h")
 
 if not os.path.exists(LIB_PATH):

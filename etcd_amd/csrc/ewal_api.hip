@@ -165,7 +165,10 @@ static int run_stream(ewal_ctx *c, DevTables *tb, const uint8_t *d_buf, uint64_t
   a.slots = find_cand ? c->slots.as<uint16_t>() : nullptr;
   const unsigned grid = (unsigned)std::min<uint64_t>((nunits + 2 * EW_WAVES - 1) / (2 * EW_WAVES), (uint64_t)c->num_cu);
   EW_CHECK(hipEventRecord(c->evs0, c->stream));
-  hipLaunchKernelGGL(k_stream, dim3(grid), dim3(EW_THREADS), 0, c->stream, a);
+  if (find_cand)
+    hipLaunchKernelGGL(k_stream<true>, dim3(grid), dim3(EW_THREADS), 0, c->stream, a);
+  else
+    hipLaunchKernelGGL(k_stream<false>, dim3(grid), dim3(EW_THREADS), 0, c->stream, a);
   EW_CHECK(hipGetLastError());
   EW_CHECK(hipEventRecord(c->evs1, c->stream));
   ScanArgs s;

@@ -10,8 +10,7 @@ struct StreamArgs {
   uint64_t B;              // byte count
   uint32_t nunits;         // B / 4096 + 1 (P is read at x == B)
   int find_cand;           // 1: WAL framing candidates, 0: CRC prefixes only
-  int ablate;              // timing-only ablations (EWAL_STREAM_ABLATE): 1 no CRC, 2 no candidates,
-                           // 4 no v store, 16 no lane-63 tail load
+  int ablate;              // unused by k_stream (EWAL_STREAM_ABLATE timing hooks live in k_frame only)
   const uint32_t *g_slice; // [4][256]
   const uint32_t *g_shift; // [48][4][256]
   uint32_t *v;             // lin of every 64-B piece        [nunits*64]

@@ -113,14 +113,13 @@ __device__ __forceinline__ uint32_t cand_filter(const uint32_t (&D)[19]) {
   // per dword: 1 xor, 1 alignbyte, 3 bitop3/add (5 VALU)
   //   z   = e0 | (y ^ 18..)            bitop3 0xF6 (a | (b ^ c))
   //   acc = ((z - 01..) & ~z) | acc    bitop3 0xBA ((a & ~b) | c)
-  uint32_t acc = 0, e0 = D[2] ^ 0x08080808u;
+  uint32_t acc = 0;
 #pragma unroll
   for (int J = 0; J < 16; ++J) {
-    const uint32_t e1 = D[J + 3] ^ 0x08080808u;
-    const uint32_t y = __builtin_amdgcn_alignbyte(e1, e0, 2);
-    const uint32_t z = __builtin_amdgcn_bitop3_b32(e0, y, 0x18181818u, 0xF6);
+    const uint32_t e = D[J + 2] ^ 0x08080808u;                            // x ^ 08..
+    const uint32_t y = __builtin_amdgcn_alignbyte(D[J + 3], D[J + 2], 2);   // raw: no xor to carry
+    const uint32_t z = __builtin_amdgcn_bitop3_b32(e, y, 0x10101010u, 0xF6);
     acc = __builtin_amdgcn_bitop3_b32(z + 0xFEFEFEFFu, z, acc, 0xBA);
-    e0 = e1;
   }
   return acc & 0x80808080u;
 }
@@ -285,7 +284,7 @@ __device__ __forceinline__ void row_transpose(uint32_t (&D)[19]) {
 // frame-start candidates -> slots[] / wcnt[] (the unit's candidate count,
 // from lane 63).  The 4 KiB aggregates are formed from v[] by k_uscan, where
 // one lane per unit does it with every lane busy.
-template <int NU>
+template <int NU, bool FIND>
 __device__ __forceinline__ void stream_units(const StreamArgs &a, const uint8_t *s_slice, const uint32_t *s_s64,
                                              const uint32_t *s_s128, const uint32_t (&Lt)[4],
                                              const uint32_t (&u)[NU], const uint32_t (&D)[NU][19]) {
@@ -295,18 +294,9 @@ __device__ __forceinline__ void stream_units(const StreamArgs &a, const uint8_t 
   // place in the CRC chains' LDS shadows
   uint32_t fm[NU];
 #pragma unroll
-  for (int i = 0; i < NU; ++i) fm[i] = (a.find_cand && !(a.ablate & 2)) ? cand_filter(D[i]) : 0u;
+  for (int i = 0; i < NU; ++i) fm[i] = FIND ? cand_filter(D[i]) : 0u;
   uint32_t c[NU];
-  if (!(a.ablate & 1)) {
-    crc_pieces<NU>(s_slice, Lt, D, c);
-  } else {   // timing-only path: keep the loads live, skip the CRC
-#pragma unroll
-    for (int i = 0; i < NU; ++i) {
-      c[i] = 0;
-#pragma unroll
-      for (int k = 0; k < 16; ++k) c[i] ^= D[i][k];
-    }
-  }
+  crc_pieces<NU>(s_slice, Lt, D, c);
   // lin of every 256-B super-piece (lanes 4m .. 4m+3) by a two-level tree,
   // branch-free: the lanes that do not combine look up entry 0 (one address,
   // a broadcast, no extra bank cycles).  Lane 4m+3 ends with the value.
@@ -324,10 +314,11 @@ __device__ __forceinline__ void stream_units(const StreamArgs &a, const uint8_t 
     c[i] ^= tab_apply(s_s128, top ? o : 0u);
   }
   // plain stores (measured a little faster than nontemporal ones here)
-  if (top && !(a.ablate & 4)) {
+  if (top) {
 #pragma unroll
     for (int i = 0; i < NU; ++i) a.v[(uint64_t)u[i] * EW_VPU + (lane >> 2)] = c[i];
   }
+  if (!FIND) return;
 #pragma unroll
   for (int i = 0; i < NU; ++i) {
     const uint64_t off = (uint64_t)u[i] * EW_WAVE_BYTES + (uint64_t)lane * EW_PIECE;
@@ -360,6 +351,7 @@ __device__ __forceinline__ void stream_units(const StreamArgs &a, const uint8_t 
 // latency under full load needs).  Loop control is scalar and the loads are
 // raw buffer loads (scalar base, loop-invariant lane offset), so no wait
 // lands before the use.  The last units take the guarded single-unit path.
+template <bool FIND>
 __global__ __launch_bounds__(EW_THREADS, 1) void k_stream(StreamArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t s_slice[EW_SLICE_DWORDS * 4];
   __shared__ uint32_t s_s64[1024], s_s128[1024];   // S_64, S_128 byte tables (super-piece tree)
@@ -412,7 +404,7 @@ __global__ __launch_bounds__(EW_THREADS, 1) void k_stream(StreamArgs a) {
     next3_fast(f3, T[0]);
     next3_fast(t3, T[1]);
     const uint32_t uu[2] = {2 * p, 2 * p + 1};
-    stream_units<2>(a, s_slice, s_s64, s_s128, Lt, uu, T);
+    stream_units<2, FIND>(a, s_slice, s_s64, s_s128, Lt, uu, T);
   };
   const uint32_t npairs = p0 < NP ? (NP - 1 - p0) / W + 1 : 0u;
   auto pair_at = [&](uint32_t k) {   // clamped: a prefetch past the end reloads the last pair
@@ -424,14 +416,18 @@ __global__ __launch_bounds__(EW_THREADS, 1) void k_stream(StreamArgs a) {
     load_pair(pair_at(0), DA, nA);
     load_pair(pair_at(1), DB, nB);
   }
+  // sched_barrier: each batch of loads stays ahead of the previous pair's arithmetic
   for (uint32_t k = 0; k < npairs; k += 3) {   // A is processed while B and C load, and so on
     load_pair(pair_at(k + 2), DC, nC);
+    __builtin_amdgcn_sched_barrier(0);
     run_pair(pair_at(k), DA, nA);
     if (k + 1 >= npairs) break;
     load_pair(pair_at(k + 3), DA, nA);
+    __builtin_amdgcn_sched_barrier(0);
     run_pair(pair_at(k + 1), DB, nB);
     if (k + 2 >= npairs) break;
     load_pair(pair_at(k + 4), DB, nB);
+    __builtin_amdgcn_sched_barrier(0);
     run_pair(pair_at(k + 2), DC, nC);
   }
   for (uint32_t u = 2 * NP + p0; u < a.nunits; u += W) {
@@ -440,7 +436,7 @@ __global__ __launch_bounds__(EW_THREADS, 1) void k_stream(StreamArgs a) {
     load_piece(a.buf, B, off, D1[0]);
     load_next3(a.buf, B, off, D1[0]);
     const uint32_t uu[1] = {u};
-    stream_units<1>(a, s_slice, s_s64, s_s128, Lt, uu, D1);
+    stream_units<1, FIND>(a, s_slice, s_s64, s_s128, Lt, uu, D1);
   }
 }
 
