@@ -23,7 +23,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 import torch  # noqa: E402  (first: its HIP runtime is the one libewal.so binds to)
-from etcd_amd import wal as W, _lib as L  # noqa: E402
+from etcd_amd import wal as W, _lib as L, shard  # noqa: E402
 
 HBM_PEAK_GBPS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
 
@@ -105,13 +105,8 @@ def main():
         r = W.readall_device(dbuf, nb, 1)
         stream_ms.append(r.stream_ms)
         dev_ms.append(r.device_ms)
-        if dist is not None:
-            key = (rank << 40) | r.fail_record if r.fail_record >= 0 else (1 << 62)
-            summary[0] = key
-            dist.all_reduce(summary[0:1], op=dist.ReduceOp.MIN)
-            summary[1] = r.fail_record if r.fail_record >= 0 else r.n_records
-            summary[2] = 1 if r.status != L.OK else 0
-            dist.all_reduce(summary[1:3], op=dist.ReduceOp.SUM)
+        if dist is not None:   # one all-reduce of the shard verdicts (etcd_amd/shard.py)
+            shard.combine(dist, rank, r.fail_record, r.n_records, r.status != L.OK, out=summary)
     torch.cuda.synchronize()
     barrier()
     elapsed = time.perf_counter() - t0

@@ -1,0 +1,64 @@
+"""Multi-GPU combination of per-shard ReadAll results.
+
+WAL replay shards with no data-path exchange: per-raft-group WAL directories
+are independent, and inside one WAL every file starts with a crcType record
+holding the running CRC at the cut (wal/wal.go:93, 232-234), so files verify
+independently.  What crosses ranks is small:
+
+* `combine`   -- one all-reduce of {MIN first-corrupt key, SUM frames, SUM
+  failing shards}; key = shard << 40 | frame, so the minimum names the first
+  corrupt record of the lowest failing shard.
+* `seam_check` -- for ONE WAL whose files were verified on different ranks:
+  the only cross-file rule of ReadAll (wal/wal.go:184-192): file k+1's leading
+  crcType record must carry file k's final running CRC whenever that CRC is
+  non-zero (otherwise wal.ErrCRCMismatch).  One all-gather of two words per
+  rank.
+
+Backend-agnostic (torch.distributed: "nccl" = RCCL on the GPU box, "gloo" in
+the CPU tests); tensors live on `device`.
+"""
+import torch
+
+NO_FAILURE = 1 << 62
+
+
+def failure_key(shard: int, fail_record: int) -> int:
+    """shard << 40 | frame for a failing shard, NO_FAILURE otherwise."""
+    return (shard << 40) | fail_record if fail_record >= 0 else NO_FAILURE
+
+
+def combine(dist, shard: int, fail_record: int, n_records: int, failed: bool, device="cpu", out=None):
+    """All-reduce one shard's verdict.  Returns (min key, total frames
+    verified, failing shards); frames of a failing shard count up to its first
+    failure, as ReadAll's n_records does."""
+    t = out if out is not None else torch.zeros(3, dtype=torch.int64, device=device)
+    t[0] = failure_key(shard, fail_record)
+    t[1] = fail_record if fail_record >= 0 else n_records
+    t[2] = 1 if failed else 0
+    dist.all_reduce(t[0:1], op=dist.ReduceOp.MIN)
+    dist.all_reduce(t[1:3], op=dist.ReduceOp.SUM)
+    return int(t[0].item()), int(t[1].item()), int(t[2].item())
+
+
+def decode_key(key: int):
+    """(shard, frame) of a combined key, or None when no shard failed."""
+    if key >= NO_FAILURE:
+        return None
+    return key >> 40, key & ((1 << 40) - 1)
+
+
+def seam_check(dist, world: int, rank: int, first_crc_record: int, last_crc: int, device="cpu"):
+    """Rank r verified file r of one WAL (files in sequence order).
+    first_crc_record: the Crc of the file's leading crcType record (-1 when
+    the file does not start with one); last_crc: decoder.lastCRC() after the
+    file.  Returns the index of the first file whose seam fails (wal.go:188:
+    running != 0 and stored != running), or -1."""
+    mine = torch.tensor([first_crc_record, last_crc], dtype=torch.int64, device=device)
+    allv = [torch.zeros(2, dtype=torch.int64, device=device) for _ in range(world)]
+    dist.all_gather(allv, mine)
+    for k in range(1, world):
+        running = int(allv[k - 1][1].item())
+        stored = int(allv[k][0].item())
+        if stored >= 0 and running != 0 and stored != running:
+            return k
+    return -1
