@@ -150,8 +150,7 @@ static int run_stream(ewal_ctx *c, DevTables *tb, const uint8_t *d_buf, uint64_t
   EW_CHECK(c->tagg.ensure((size_t)nstiles * 16));
   EW_CHECK(c->tpx.ensure((size_t)nstiles * 16));
   EW_CHECK(c->gagg.ensure((size_t)((nstiles + 1023) / 1024) * 16));
-  EW_CHECK(hipMemsetAsync(c->small.p, 0, sizeof(Small), c->stream));
-  Small *ds = c->small.as<Small>();
+  Small *ds = c->small.as<Small>();   // zeroed by k_stream (workgroup 0), the first kernel of every call
   StreamArgs a;
   a.buf = d_buf;
   a.B = B;
@@ -163,6 +162,7 @@ static int run_stream(ewal_ctx *c, DevTables *tb, const uint8_t *d_buf, uint64_t
   a.v = c->v.as<uint32_t>();
   a.wcnt = c->wcnt.as<uint32_t>();
   a.slots = find_cand ? c->slots.as<uint16_t>() : nullptr;
+  a.small = ds;
   const unsigned grid = (unsigned)std::min<uint64_t>((nunits + 2 * EW_WAVES - 1) / (2 * EW_WAVES), (uint64_t)c->num_cu);
   EW_CHECK(hipEventRecord(c->evs0, c->stream));
   if (find_cand)

@@ -5,6 +5,7 @@
 
 struct TileDesc;
 
+struct Small;
 struct StreamArgs {
   const uint8_t *buf;      // WAL bytes (device, 16-B aligned)
   uint64_t B;              // byte count
@@ -16,6 +17,7 @@ struct StreamArgs {
   uint32_t *v;             // lin of every 64-B piece        [nunits*64]
   uint32_t *wcnt;          // candidates in the unit         [nunits]
   uint16_t *slots;         // first EW_SLOTS candidate offsets per unit
+  Small *small;            // the call's device scratch, zeroed by k_stream's workgroup 0
 };
 
 struct ScanArgs {

@@ -356,6 +356,8 @@ __global__ __launch_bounds__(EW_THREADS, 1) void k_stream(StreamArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t s_slice[EW_SLICE_DWORDS * 4];
   __shared__ uint32_t s_s64[1024], s_s128[1024];   // S_64, S_128 byte tables (super-piece tree)
   const int tid = threadIdx.x, lane = tid & 63;
+  static_assert(sizeof(Small) % 4 == 0 && sizeof(Small) / 4 <= EW_THREADS, "Small is zeroed by one workgroup");
+  if (blockIdx.x == 0 && tid < (int)(sizeof(Small) / 4)) ((uint32_t *)a.small)[tid] = 0u;   // the call's scratch
   stage_lds<EW_THREADS>((uint32_t *)s_slice, EW_SLICE_DWORDS, [&](int i) { return a.g_slice[slice_src(i)]; });
   stage_lds<EW_THREADS>(s_s64, 1024, [&](int i) { return a.g_shift[6 * 1024 + i]; });
   stage_lds<EW_THREADS>(s_s128, 1024, [&](int i) { return a.g_shift[7 * 1024 + i]; });
