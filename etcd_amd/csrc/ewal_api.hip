@@ -4,7 +4,7 @@
 // (*WAL).ReadAll (wal/wal.go:164-216) is:
 //   k_stream (one HBM pass) -> unit scan -> k_frame (speculative framing +
 //   decode; fallback: k_link, runs, pointer jumping, k_decode) -> k_check ->
-//   k_meta (k_check also places the entry ops; rare: k_gap, k_ents)
+//   k_result (k_check also places the entry ops; rare: k_gap, k_ents)
 // and the host only classifies the chain's terminal frame and assembles the
 // ewal_result from a few device reductions.  No CPU decoding or CRC happens
 // on this path; without a GPU every call returns EWAL_E_NODEVICE.
@@ -129,9 +129,10 @@ static int compact_cands(ewal_ctx *c, const uint8_t *d_buf, uint64_t B, uint32_t
   return 0;
 }
 
-// Run the HBM pass (k_stream) and the unit scan (k_uscan) over d_buf[0..B):
-// fills c->v, c->pwave; with find_cand also the dense, position-sorted
-// candidate list cpos[] (k_uscan's epilogue + k_rescan), its size in
+// Run the HBM pass (k_stream) and the unit scan over d_buf[0..B): fills
+// c->v, c->pwave; with find_cand also the dense, position-sorted candidate
+// list cpos[] (k_uapply's epilogue; units with more than EW_SLOTS candidates
+// are counted in Small.novf and filled in by k_rescan later), its size in
 // Small.total.  Asynchronous: nothing waits for the device here.
 static int run_stream(ewal_ctx *c, DevTables *tb, const uint8_t *d_buf, uint64_t B, int find_cand, uint64_t ccap) {
   const uint64_t nunits64 = B / EW_WAVE_BYTES + 1;
@@ -203,11 +204,8 @@ static int run_stream(ewal_ctx *c, DevTables *tb, const uint8_t *d_buf, uint64_t
   hipLaunchKernelGGL(k_tfix, dim3(ngroups), dim3(1024), 0, c->stream, s, ngroups);
   hipLaunchKernelGGL(k_uapply, dim3(sgrid), dim3(256), 0, c->stream, s);
   EW_CHECK(hipGetLastError());
-  if (find_cand) {
-    hipLaunchKernelGGL(k_rescan, dim3(64), dim3(256), 0, c->stream, d_buf, B, c->ovf.as<uint32_t>(), &ds->novf,
-                       c->cbase.as<unsigned long long>(), c->cpos.as<uint64_t>(), c->clen.as<uint64_t>(), ccap);
-    EW_CHECK(hipGetLastError());
-  }
+  // units with more than EW_SLOTS candidates (ds->novf) are left out of cpos
+  // here: k_frame then declines to speculate and the host runs k_rescan
   return 0;
 }
 
@@ -336,7 +334,7 @@ static int readall_impl(ewal_ctx *c, const uint8_t *d_buf, uint64_t B, uint64_t 
     if ((rc = sync_small(c))) return rc;
     K = c->h_small->total;
     c->last_k = K;
-    if (K && K <= ccap && K <= rdcap && c->h_small->pos0 == 0 && !c->h_small->irregular) {
+    if (K && K <= ccap && K <= rdcap && !c->h_small->novf && c->h_small->pos0 == 0 && !c->h_small->irregular) {
       decoded = true;
       if (c->h_small->nslow) {   // frames the canonical parser declined (a launch only when there are any)
         hipLaunchKernelGGL(k_decode_slow, dim3(std::min<uint64_t>(grid_for(c->h_small->nslow, 256), 1024)),
@@ -349,6 +347,11 @@ static int readall_impl(ewal_ctx *c, const uint8_t *d_buf, uint64_t B, uint64_t 
       // the speculation failed: frame by candidate links (k_link), growing
       // the candidate list first if it overflowed
       const unsigned lgrid = (unsigned)std::max(1, c->num_cu) * 8;
+      if (K <= ccap && c->h_small->novf) {   // candidates of the overflow units
+        hipLaunchKernelGGL(k_rescan, dim3(64), dim3(256), 0, c->stream, d_buf, B, c->ovf.as<uint32_t>(), &ds->novf,
+                           c->cbase.as<unsigned long long>(), c->cpos.as<uint64_t>(), c->clen.as<uint64_t>(), ccap);
+        EW_CHECK(hipGetLastError());
+      }
       if (K > ccap) {   // grow and redo the compaction (the slots stay valid)
         if (K >= 0xfffffff0ull) return EWAL_E_NOMEM;
         ccap = K + 1024;
@@ -431,8 +434,8 @@ static int readall_impl(ewal_ctx *c, const uint8_t *d_buf, uint64_t B, uint64_t 
     hipLaunchKernelGGL(k_check, dim3(nb), dim3(1024), 0, c->stream, tb->shift, rd, n32, pfd, pfo, ri,
                        c->lbstat.as<unsigned long long>(), c->epoch, c->ops.as<uint32_t>(), c->kk.as<uint64_t>(),
                        c->ents.as<ewal_entry>(), c->mlist.as<uint32_t>(), ds);
-    hipLaunchKernelGGL(k_meta, dim3(64), dim3(256), 0, c->stream, d_buf, rd, c->mlist.as<uint32_t>(), ds);
-    hipLaunchKernelGGL(k_result, dim3(1), dim3(64), 0, c->stream, rd, n32, ri, ds, c->h_res_dev);
+    hipLaunchKernelGGL(k_result, dim3(1), dim3(256), 0, c->stream, d_buf, rd, c->mlist.as<uint32_t>(), n32, ri, ds,
+                       c->h_res_dev);
     EW_CHECK(hipGetLastError());
     EW_CHECK(hipStreamSynchronize(c->stream));
     std::memcpy(&res, c->h_res, sizeof(ResultDev));
@@ -441,7 +444,8 @@ static int readall_impl(ewal_ctx *c, const uint8_t *d_buf, uint64_t B, uint64_t 
       const unsigned ggrid = (unsigned)std::min<uint64_t>(grid_for(n, 256), (uint64_t)c->num_cu * 8);
       hipLaunchKernelGGL(k_gap, dim3(ggrid), dim3(256), 0, c->stream, rd, c->ops.as<uint32_t>(),
                          c->kk.as<uint64_t>(), ds);
-      hipLaunchKernelGGL(k_result, dim3(1), dim3(64), 0, c->stream, rd, n32, ri, ds, c->h_res_dev);
+      hipLaunchKernelGGL(k_result, dim3(1), dim3(256), 0, c->stream, d_buf, rd, c->mlist.as<uint32_t>(), n32, ri, ds,
+                       c->h_res_dev);
       EW_CHECK(hipGetLastError());
       EW_CHECK(hipStreamSynchronize(c->stream));
       std::memcpy(&res, c->h_res, sizeof(ResultDev));

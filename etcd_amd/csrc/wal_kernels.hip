@@ -27,8 +27,8 @@
 //              using the stream prefixes: Update(seed, D[s,e)) =
 //              S_n(seed ^ ~0 ^ P(s)) ^ P(e) ^ ~0; Entry / HardState verdicts,
 //              the index-gap panic, ReadAll's reductions.
-//   k_meta / k_opscan / k_opents (k_gap, k_ents): ReadAll's metadata and
-//              ents semantics.
+//   k_result   ReadAll's metadata rule and the result gather (rare: k_gap,
+//              k_ents for index gaps far back / index rewinds).
 #include "ewal_device.h"
 #include "ewal_internal.h"
 
@@ -1302,7 +1302,7 @@ __global__ __launch_bounds__(256) void k_frame(const uint8_t *__restrict__ buf, 
     ds->agg.first_meta = ~0ull;
     ds->pos0 = K ? pos[0] : ~0ull;
   }
-  if (K > ccap || K > rdcap) return;   // the host retries with larger buffers
+  if (K > ccap || K > rdcap || ds->novf) return;   // the host frames the slow way (larger buffers, k_rescan)
   stage_lds<256>(s_t4, 16 * 256, [&](int i) { return g_slice[i]; });
   stage_lds<256>(s_svp, 1024, [&](int i) { return g_shift[EW_VLOG * 1024 + i]; });
   __syncthreads();
@@ -1327,7 +1327,7 @@ __global__ __launch_bounds__(256) void k_frame(const uint8_t *__restrict__ buf, 
 // CRC up to its first failure), the Entry/HardState verdicts, the entry-op
 // index-gap panic, ReadAll's reductions (first failure, last entry / state /
 // op, first metadata), the per-workgroup op counts (k_opscan / k_opents) and
-// the list of metadata frames k_meta checks.
+// the list of metadata frames k_result checks.
 #define EW_GAP_BACK 16
 
 // Decoupled look-back over per-workgroup counts (one wave): workgroup b
@@ -1531,27 +1531,6 @@ __global__ __launch_bounds__(1024) void k_check(const uint32_t *__restrict__ g_s
   }
 }
 
-// metadata: `metadata != nil && !reflect.DeepEqual(metadata, rec.Data)`,
-// wal/wal.go:178-183, over the metadata frames k_check listed
-__global__ void k_meta(const uint8_t *__restrict__ buf, RecDesc *__restrict__ rd, const uint32_t *__restrict__ mlist,
-                       Small *ds) {
-  const uint32_t nm = ds->nmeta;
-  const unsigned long long fm = ds->agg.first_meta;
-  if (fm == ~0ull) return;
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nm; i += gridDim.x * blockDim.x) {
-    const uint32_t r = mlist[i];
-    if (r <= fm) continue;
-    RecDesc &d = rd[r];
-    const RecDesc &m = rd[fm];
-    bool eq = (d.dlen == m.dlen);
-    for (uint64_t k = 0; eq && k < d.dlen; ++k) eq = buf[d.doff + k] == buf[m.doff + k];
-    if (!eq) {
-      d.st = EWAL_ERR_METADATA_CONFLICT;
-      atomicMin(&ds->agg.first_fail, (unsigned long long)r);
-    }
-  }
-}
-
 // List-based gap check (the rare case where k_check could not find an op's
 // predecessor nearby): op j needs k_j <= len(ents) = k_{j-1} + 1
 // (wal/wal.go:173), over the op list k_opents wrote; frames k_check already
@@ -1587,8 +1566,32 @@ __global__ void k_export_small(const Small *ds, Small *h) {
 
 // the handful of frames the host result needs, in one struct, written
 // straight into host-mapped pinned memory
-__global__ void k_result(const RecDesc *__restrict__ rd, uint32_t n, uint64_t ri, const Small *ds, ResultDev *o) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+// One workgroup: first ReadAll's metadata rule, `metadata != nil &&
+// !reflect.DeepEqual(metadata, rec.Data)` (wal/wal.go:178-183), over the
+// metadata frames k_check listed (usually one per WAL file), then thread 0
+// gathers the result.
+__global__ __launch_bounds__(256) void k_result(const uint8_t *__restrict__ buf, RecDesc *__restrict__ rd,
+                                                const uint32_t *__restrict__ mlist, uint32_t n, uint64_t ri, Small *ds,
+                                                ResultDev *o) {
+  const uint32_t nm = ds->nmeta;
+  const unsigned long long fm = ds->agg.first_meta;
+  if (fm != ~0ull) {
+    for (uint32_t i = threadIdx.x; i < nm; i += blockDim.x) {
+      const uint32_t r = mlist[i];
+      if (r <= fm) continue;
+      RecDesc &d = rd[r];
+      const RecDesc &m = rd[fm];
+      bool eq = (d.dlen == m.dlen);
+      for (uint64_t k = 0; eq && k < d.dlen; ++k) eq = buf[d.doff + k] == buf[m.doff + k];
+      if (!eq) {
+        d.st = EWAL_ERR_METADATA_CONFLICT;
+        atomicMin(&ds->agg.first_fail, (unsigned long long)r);
+      }
+    }
+  }
+  __threadfence();
+  __syncthreads();
+  if (threadIdx.x != 0) return;
   const ReadAllAgg g = ds->agg;
   o->agg = g;
   o->nops = ds->nsel3;
