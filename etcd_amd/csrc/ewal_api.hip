@@ -326,7 +326,7 @@ static int readall_impl(ewal_ctx *c, const uint8_t *d_buf, uint64_t B, uint64_t 
     rc = run_stream(c, tb, d_buf, B, 1, ccap);
     if (rc) return rc;
     uint32_t *pf = c->pf.as<uint32_t>();
-    const unsigned fgrid = (unsigned)std::max(1, c->num_cu) * 8;
+    const unsigned fgrid = (unsigned)std::max(1, c->num_cu) * 3;   // persistent: 3 resident workgroups per CU
     hipLaunchKernelGGL(k_frame, dim3(fgrid), dim3(256), 0, c->stream, d_buf, B, c->cpos.as<uint64_t>(), ccap, rdcap,
                        c->pwave.as<uint32_t>(), c->v.as<uint32_t>(), tb->slice, tb->shift, c->rd.as<RecDesc>(), pf,
                        pf + rdcap, c->slow.as<uint32_t>(), ds, c->ablate);
