@@ -428,18 +428,22 @@ static int readall_impl(ewal_ctx *c, const uint8_t *d_buf, uint64_t B, uint64_t 
       if (c->epoch == 0) c->epoch = 1;
     }
     EW_CHECK(c->ops.ensure((size_t)n * 4));
+    EW_CHECK(c->opf.ensure((size_t)nb * 4));   // k_check's per-workgroup op bases
     EW_CHECK(c->mlist.ensure((size_t)n * 4));
     EW_CHECK(c->kk.ensure((size_t)n * 8));
     EW_CHECK(c->ents.ensure((size_t)n * sizeof(ewal_entry)));
     hipLaunchKernelGGL(k_check, dim3(nb), dim3(1024), 0, c->stream, tb->shift, rd, n32, pfd, pfo, ri,
-                       c->lbstat.as<unsigned long long>(), c->epoch, c->ops.as<uint32_t>(), c->kk.as<uint64_t>(),
-                       c->ents.as<ewal_entry>(), c->mlist.as<uint32_t>(), ds);
+                       c->lbstat.as<unsigned long long>(), c->epoch, c->opf.as<uint32_t>(), c->ents.as<ewal_entry>(),
+                       c->mlist.as<uint32_t>(), ds);
     hipLaunchKernelGGL(k_result, dim3(1), dim3(256), 0, c->stream, d_buf, rd, c->mlist.as<uint32_t>(), n32, ri, ds,
                        c->h_res_dev);
     EW_CHECK(hipGetLastError());
     EW_CHECK(hipStreamSynchronize(c->stream));
     std::memcpy(&res, c->h_res, sizeof(ResultDev));
     if (res.errflag) return EWAL_E_TIMEOUT;
+    if (res.gapslow || res.nonmono)   // the rare paths work on the op list
+      hipLaunchKernelGGL(k_opslist, dim3(nb), dim3(1024), 0, c->stream, rd, n32, ri, c->opf.as<uint32_t>(),
+                         c->ops.as<uint32_t>(), c->kk.as<uint64_t>());
     if (res.gapslow) {   // an op's predecessor lay too far back for k_check: list-based gap pass
       const unsigned ggrid = (unsigned)std::min<uint64_t>(grid_for(n, 256), (uint64_t)c->num_cu * 8);
       hipLaunchKernelGGL(k_gap, dim3(ggrid), dim3(256), 0, c->stream, rd, c->ops.as<uint32_t>(),

@@ -1382,9 +1382,8 @@ __device__ __forceinline__ uint32_t lookback_count(unsigned long long *status, u
 }
 __global__ __launch_bounds__(1024) void k_check(const uint32_t *__restrict__ g_shift, RecDesc *__restrict__ rd,
                          uint32_t n, const uint32_t *__restrict__ pfd, const uint32_t *__restrict__ pfo, uint64_t ri,
-                         unsigned long long *__restrict__ status, uint32_t epoch, uint32_t *__restrict__ ops,
-                         uint64_t *__restrict__ kk, ewal_entry *__restrict__ ents, uint32_t *__restrict__ mlist,
-                         Small *ds) {
+                         unsigned long long *__restrict__ status, uint32_t epoch, uint32_t *__restrict__ wbase,
+                         ewal_entry *__restrict__ ents, uint32_t *__restrict__ mlist, Small *ds) {
   ReadAllAgg *agg = &ds->agg;
   __shared__ uint32_t s_wo[16];          // ops per wave
   __shared__ uint32_t s_base;            // ops before the workgroup
@@ -1503,6 +1502,7 @@ __global__ __launch_bounds__(1024) void k_check(const uint32_t *__restrict__ g_s
     const uint32_t base = lookback_count(status, blockIdx.x, cnt, epoch, &ds->errflag);
     if (threadIdx.x == 0) {
       s_base = base;
+      wbase[blockIdx.x] = base;   // k_opslist (rare paths) rebuilds ops / kk from it
       if (blockIdx.x == gridDim.x - 1) ds->nsel3 = base + cnt;
       if (s_red[0]) atomicMax(&agg->last_entry, (long long)(s_red[0] - 1));
       if (s_red[1]) atomicMax(&agg->last_state, (long long)(s_red[1] - 1));
@@ -1513,7 +1513,7 @@ __global__ __launch_bounds__(1024) void k_check(const uint32_t *__restrict__ g_s
   }
   __syncthreads();
   if (op) {   // ents[j] = op j (exact when the ops' k are strictly increasing and gap-free,
-              // otherwise the host's survivor pass rewrites ents), ops[j] = its frame, kk[j] = its k
+              // otherwise the host's survivor pass rewrites ents)
     uint32_t j = s_base + (uint32_t)__popcll(below);
     const int wv = threadIdx.x >> 6;
 #pragma unroll
@@ -1526,9 +1526,30 @@ __global__ __launch_bounds__(1024) void k_check(const uint32_t *__restrict__ g_s
     e.type = d.etype;
     e.data_nil = d.enil;
     ents[j] = e;
-    ops[j] = r;
-    kk[j] = d.f1 - ri;
   }
+}
+
+// ops[j] = frame of op j, kk[j] = its k, from k_check's workgroup bases (the
+// rare paths only: index gaps found far back, index rewinds).
+__global__ __launch_bounds__(1024) void k_opslist(const RecDesc *__restrict__ rd, uint32_t n, uint64_t ri,
+                                                  const uint32_t *__restrict__ wbase, uint32_t *__restrict__ ops,
+                                                  uint64_t *__restrict__ kk) {
+  __shared__ uint32_t s_w[16];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const uint32_t r = blockIdx.x * 1024 + tid;
+  const bool live = r < n;
+  const int64_t ty = live ? rd[r].type : 0;
+  const uint64_t f1 = live ? rd[r].f1 : 0;
+  const bool op = live && ty == 2 && f1 >= ri;
+  const unsigned long long mo = __ballot(op);
+  if (lane == 0) s_w[wv] = (uint32_t)__popcll(mo);
+  __syncthreads();
+  if (!op) return;
+  uint32_t j = wbase[blockIdx.x] + (uint32_t)__popcll(mo & ((1ull << lane) - 1ull));
+#pragma unroll
+  for (int w = 0; w < 16; ++w) j += (w < wv) ? s_w[w] : 0u;
+  ops[j] = r;
+  kk[j] = f1 - ri;
 }
 
 // List-based gap check (the rare case where k_check could not find an op's
