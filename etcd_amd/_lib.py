@@ -120,6 +120,8 @@ _SIGS = {
     "ewal_encoder_free": (None, [vp]),
     "ewal_synth_wal": (C.c_int64, [C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint32, C.c_int64, vp, C.c_uint64,
                                    C.POINTER(C.c_int64)]),
+    "ewal_encode_entries_device": (C.c_int, [vp, vp, C.c_uint64, vp, C.c_uint64, C.c_uint32, vp, C.c_uint64,
+                                             C.POINTER(C.c_uint64), C.POINTER(C.c_uint32)]),
     "ewal_crc32_update_device": (C.c_int, [vp, C.c_uint32, C.c_uint32, vp, C.c_uint64, C.POINTER(C.c_uint32)]),
     "ewal_crc32_update_host": (C.c_uint32, [C.c_uint32, C.c_uint32, C.c_char_p, C.c_uint64]),
     "ewal_crc32_combine": (C.c_uint32, [C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint64]),

@@ -118,3 +118,152 @@ __global__ void k_commit(uint64_t G, const uint64_t *__restrict__ match, const u
   changed[g] = chg;
   status[g] = st;
 }
+
+// ===========================================================================
+// Batched encoder.encode of entries (wal/wal.go:248-263 SaveEntry,
+// wal/encoder.go:25-37): frame_i = int64 LE len || walpb.Record{Type: 2, Crc:
+// c_i, Data: E_i}, E_i = raftpb.Entry.Marshal() (raft/raftpb/raft.pb.go:
+// 921-943), c_i = crc32.Update(c_{i-1}, Castagnoli, E_i).  The CRC chain
+// runs over the contiguous "data-only" stream E_0 || E_1 || ... (frame
+// headers are not in it), so ONE stream pass gives every c_i:
+// c_i = ~P(end of E_i) once the stream's first 4 bytes are XORed with
+// ~c_{-1} (a reflected CRC register started at r equals one started at 0 over
+// the message whose first 4 bytes are XORed with r).
+// ===========================================================================
+__device__ __forceinline__ uint32_t sov64(uint64_t x) {
+  uint32_t n = 1;
+  while (x >= 0x80) { x >>= 7; ++n; }
+  return n;
+}
+__device__ __forceinline__ uint32_t put_varint_dev(uint8_t *o, uint64_t v) {
+  uint32_t n = 0;
+  while (v >= 0x80) { o[n++] = (uint8_t)(v | 0x80); v >>= 7; }
+  o[n++] = (uint8_t)v;
+  return n;
+}
+// Entry header 08 v(type) 10 v(term) 18 v(index) 22 v(len) into h (<= 44 B)
+__device__ __forceinline__ uint32_t entry_head(uint8_t *h, const ewal_entry &e) {
+  uint32_t o = 0;
+  h[o++] = 0x08; o += put_varint_dev(h + o, (uint64_t)(int64_t)e.type);
+  h[o++] = 0x10; o += put_varint_dev(h + o, e.term);
+  h[o++] = 0x18; o += put_varint_dev(h + o, e.index);
+  h[o++] = 0x22; o += put_varint_dev(h + o, e.data_len);
+  return o;
+}
+
+// Wave-cooperative copy of n bytes src -> dst (any alignment): byte stores for
+// the unaligned head and tail of dst, dword stores in between (two aligned
+// source dwords and v_alignbyte per output dword).  Source reads stay inside
+// [src_base, src_base + src_len).
+__device__ __forceinline__ void wave_copy(uint8_t *__restrict__ dst, const uint8_t *__restrict__ src, uint64_t n,
+                                          const uint8_t *src_base, uint64_t src_len) {
+  const int lane = threadIdx.x & 63;
+  const uint64_t head = std::min<uint64_t>(n, (4 - ((uintptr_t)dst & 3)) & 3);
+  if ((uint64_t)lane < head) dst[lane] = src[lane];
+  const uint64_t m = (n - head) >> 2;                     // whole output dwords
+  uint32_t *d32 = (uint32_t *)(dst + head);
+  const uint8_t *s = src + head;
+  const uintptr_t send = (uintptr_t)(src_base + src_len);
+  for (uint64_t k = lane; k < m; k += 64) {
+    const uint8_t *p = s + 4 * k;
+    const uintptr_t a = (uintptr_t)p & ~(uintptr_t)3;
+    const uint32_t sh = (uint32_t)((uintptr_t)p & 3);
+    uint32_t w;
+    if (sh == 0) {
+      w = *(const uint32_t *)a;
+    } else if (a + 8 <= send) {
+      w = __builtin_amdgcn_alignbyte(((const uint32_t *)a)[1], ((const uint32_t *)a)[0], sh);
+    } else {
+      w = (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+    }
+    d32[k] = w;
+  }
+  const uint64_t t0 = head + 4 * m;
+  if ((uint64_t)lane < n - t0) dst[t0 + lane] = src[t0 + lane];
+}
+
+// esz[i] = |E_i|
+__global__ void k_enc_sizes(const ewal_entry *__restrict__ ents, uint64_t n, uint64_t data_len,
+                            uint64_t *__restrict__ esz, uint32_t *__restrict__ errflag) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const ewal_entry e = ents[i];
+  if (e.data_len > data_len || e.data_off > data_len - e.data_len) atomicOr(errflag, 1u);   // outside d_data
+  esz[i] = 4 + sov64((uint64_t)(int64_t)e.type) + sov64(e.term) + sov64(e.index) + sov64(e.data_len) + e.data_len;
+}
+
+// E_i at xoff[i] of the data-only stream; one wave per entry (grid-stride)
+__global__ __launch_bounds__(256) void k_enc_body(const uint8_t *__restrict__ data, uint64_t data_len,
+                                                  const ewal_entry *__restrict__ ents, uint64_t n,
+                                                  const uint64_t *__restrict__ xoff, uint8_t *__restrict__ es) {
+  const int lane = threadIdx.x & 63;
+  const uint64_t nw = (uint64_t)gridDim.x * (blockDim.x >> 6);
+  for (uint64_t i = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); i < n; i += nw) {
+    const ewal_entry e = ents[i];
+    uint8_t h[48];
+    const uint32_t hl = entry_head(h, e);
+    uint8_t *o = es + xoff[i];
+    if ((uint32_t)lane < hl) {
+      uint8_t b = 0;
+#pragma unroll
+      for (int k = 0; k < 48; ++k) b = (k == lane) ? h[k] : b;
+      o[lane] = b;
+    }
+    if (e.data_len) wave_copy(o + hl, data + e.data_off, e.data_len, data, data_len);
+  }
+}
+
+// XOR the data-only stream's first 4 bytes with r (and back)
+__global__ void k_enc_xor4(uint8_t *es, uint32_t r) {
+  if (threadIdx.x < 4) es[threadIdx.x] ^= (uint8_t)(r >> (8 * threadIdx.x));
+}
+
+// c_i = ~P(end of E_i); frame size fsz[i] = 8 + |Record|
+__global__ __launch_bounds__(256) void k_enc_crc(const uint8_t *__restrict__ es, const uint64_t *__restrict__ xoff,
+                                                 const uint64_t *__restrict__ esz, uint64_t n,
+                                                 const uint32_t *__restrict__ pwave, const uint32_t *__restrict__ v,
+                                                 const uint32_t *__restrict__ g_slice,
+                                                 const uint32_t *__restrict__ g_shift, uint32_t *__restrict__ crc,
+                                                 uint64_t *__restrict__ fsz) {
+  __shared__ uint32_t s_t4[1024];
+  __shared__ uint32_t s_svp[1024];
+  stage_lds<256>(s_t4, 1024, [&](int i) { return g_slice[i]; });
+  stage_lds<256>(s_svp, 1024, [&](int i) { return g_shift[EW_VLOG * 1024 + i]; });
+  __syncthreads();
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t L = esz[i];
+  const uint32_t c = ~prefix_at(xoff[i] + L, pwave, v, es, s_t4, s_svp);
+  crc[i] = c;
+  fsz[i] = 8 + 1 + 1 + 1 + sov64(c) + 1 + sov64(L) + L;   // 08 02 10 v(c) 1a v(L) E
+}
+
+// frame_i at foff[i]: int64 len, 08 02 10 v(c) 1a v(|E_i|), E_i; one wave per entry
+__global__ __launch_bounds__(256) void k_enc_frame(const uint8_t *__restrict__ es, uint64_t es_len,
+                                                   const uint64_t *__restrict__ xoff,
+                                                   const uint64_t *__restrict__ esz, const uint32_t *__restrict__ crc,
+                                                   const uint64_t *__restrict__ foff, uint64_t n,
+                                                   uint8_t *__restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const uint64_t nw = (uint64_t)gridDim.x * (blockDim.x >> 6);
+  for (uint64_t i = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); i < n; i += nw) {
+    const uint64_t L = esz[i];
+    const uint32_t c = crc[i];
+    uint8_t h[32];
+    uint32_t o = 8;
+    h[o++] = 0x08; h[o++] = 0x02;
+    h[o++] = 0x10; o += put_varint_dev(h + o, c);
+    h[o++] = 0x1a; o += put_varint_dev(h + o, L);
+    const uint64_t rec = (uint64_t)(o - 8) + L;             // the int64 length prefix
+#pragma unroll
+    for (int k = 0; k < 8; ++k) h[k] = (uint8_t)(rec >> (8 * k));
+    uint8_t *dst = out + foff[i];
+    if ((uint32_t)lane < o) {
+      uint8_t b = 0;
+#pragma unroll
+      for (int k = 0; k < 32; ++k) b = (k == lane) ? h[k] : b;
+      dst[lane] = b;
+    }
+    wave_copy(dst + o, es + xoff[i], L, es, es_len);
+  }
+}

@@ -71,7 +71,7 @@ struct ewal_ctx {
   hipEvent_t ev0 = nullptr, ev1 = nullptr, evs0 = nullptr, evs1 = nullptr;
   std::map<uint32_t, DevTables> tables;
   std::map<uint32_t, std::unique_ptr<ewal::CrcTables>> host_tables;
-  DevBuf lbstat, gagg, slow, mlist, pf, v, pwave, ux, tagg, tpx, wcnt, slots, cbase, ovf, cpos, clen, nxt, exc, E, rs, jl, vis, entry, on, rec_cand, rd, opf, ops, kk, kkrev, suf,
+  DevBuf encw, encs, lbstat, gagg, slow, mlist, pf, v, pwave, ux, tagg, tpx, wcnt, slots, cbase, ovf, cpos, clen, nxt, exc, E, rs, jl, vis, entry, on, rec_cand, rd, opf, ops, kk, kkrev, suf,
       ents, recs, tmp, small, sdesc, snaps, hbuf_dev;
   Small *h_small = nullptr;        // host-mapped pinned mirrors (written by k_export_small / k_result)
   ResultDev *h_res = nullptr;
@@ -569,7 +569,7 @@ void ewal_ctx_destroy(ewal_ctx *c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
   (void)hipStreamSynchronize(c->stream);
-  DevBuf *bufs[] = {&c->lbstat, &c->gagg, &c->slow, &c->mlist, &c->pf, &c->v, &c->pwave, &c->ux, &c->tagg, &c->tpx, &c->wcnt, &c->slots, &c->cbase, &c->ovf, &c->cpos, &c->clen, &c->nxt, &c->exc, &c->E, &c->rs, &c->jl,
+  DevBuf *bufs[] = {&c->encw, &c->encs, &c->lbstat, &c->gagg, &c->slow, &c->mlist, &c->pf, &c->v, &c->pwave, &c->ux, &c->tagg, &c->tpx, &c->wcnt, &c->slots, &c->cbase, &c->ovf, &c->cpos, &c->clen, &c->nxt, &c->exc, &c->E, &c->rs, &c->jl,
                     &c->vis, &c->entry, &c->on, &c->rec_cand, &c->rd, &c->opf, &c->ops, &c->kk, &c->kkrev,
                     &c->suf, &c->ents, &c->recs, &c->tmp, &c->small, &c->sdesc, &c->snaps, &c->hbuf_dev};
   for (DevBuf *b : bufs) b->release();
@@ -674,6 +674,69 @@ int64_t ewal_copy_records(ewal_ctx *c, ewal_record *out, int64_t cap) {
     EW_CHECK(hipStreamSynchronize(c->stream));
   }
   return n;
+}
+
+int ewal_encode_entries_device(ewal_ctx *c, const void *d_data, uint64_t data_len_total, const ewal_entry *d_ents,
+                               uint64_t n, uint32_t prev_crc, void *d_out, uint64_t cap, uint64_t *out_len,
+                               uint32_t *last_crc) {
+  if (!c || !out_len || !last_crc || (n && (!d_ents || !d_out)) || (data_len_total && !d_data)) return EWAL_E_INVAL;
+  *out_len = 0;
+  *last_crc = prev_crc;
+  if (n == 0) return EWAL_OK;
+  if (n >= 0x7fffffffull) return EWAL_E_INVAL;
+  EW_CHECK(hipSetDevice(c->device));
+  DevTables *tb;
+  int rc = get_tables(c, 0x82F63B78u, &tb);
+  if (rc) return rc;
+  EW_CHECK(c->small.ensure(sizeof(Small)));
+  Small *ds = c->small.as<Small>();
+  EW_CHECK(hipMemsetAsync(&ds->errflag, 0, 4, c->stream));
+  // per-entry scratch: esz, xoff, fsz, foff (u64) + crc (u32)
+  EW_CHECK(c->encw.ensure((size_t)n * 36 + 64));
+  uint64_t *esz = c->encw.as<uint64_t>(), *xoff = esz + n, *fsz = xoff + n, *foff = fsz + n;
+  uint32_t *crc = (uint32_t *)(foff + n);
+  hipLaunchKernelGGL(k_enc_sizes, dim3(grid_for(n, 256)), dim3(256), 0, c->stream, d_ents, n, data_len_total, esz,
+                     &ds->errflag);
+  size_t tbytes = 0;
+  EW_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, tbytes, esz, xoff, (int)n, c->stream));
+  EW_CHECK(c->tmp.ensure(tbytes));
+  EW_CHECK(hipcub::DeviceScan::ExclusiveSum(c->tmp.p, tbytes, esz, xoff, (int)n, c->stream));
+  uint64_t tail[2];
+  uint32_t bad = 0;
+  EW_CHECK(hipMemcpyAsync(&tail[0], xoff + n - 1, 8, hipMemcpyDeviceToHost, c->stream));
+  EW_CHECK(hipMemcpyAsync(&tail[1], esz + n - 1, 8, hipMemcpyDeviceToHost, c->stream));
+  EW_CHECK(hipMemcpyAsync(&bad, &ds->errflag, 4, hipMemcpyDeviceToHost, c->stream));
+  EW_CHECK(hipStreamSynchronize(c->stream));
+  if (bad) return EWAL_E_INVAL;
+  const uint64_t E = tail[0] + tail[1];                 // bytes of the data-only stream
+  EW_CHECK(c->encs.ensure(E + 64));
+  uint8_t *es = c->encs.as<uint8_t>();
+  const unsigned wgrid = (unsigned)std::min<uint64_t>(grid_for(n, 4), (uint64_t)c->num_cu * 8);
+  hipLaunchKernelGGL(k_enc_body, dim3(wgrid), dim3(256), 0, c->stream, (const uint8_t *)d_data, data_len_total,
+                     d_ents, n, xoff, es);
+  hipLaunchKernelGGL(k_enc_xor4, dim3(1), dim3(64), 0, c->stream, es, ~prev_crc);
+  rc = run_stream(c, tb, es, E, 0, 0);
+  if (rc) return rc;
+  hipLaunchKernelGGL(k_enc_crc, dim3(grid_for(n, 256)), dim3(256), 0, c->stream, es, xoff, esz, n,
+                     c->pwave.as<uint32_t>(), c->v.as<uint32_t>(), tb->slice, tb->shift, crc, fsz);
+  hipLaunchKernelGGL(k_enc_xor4, dim3(1), dim3(64), 0, c->stream, es, ~prev_crc);   // the bytes back
+  EW_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, tbytes, fsz, foff, (int)n, c->stream));
+  EW_CHECK(c->tmp.ensure(tbytes));
+  EW_CHECK(hipcub::DeviceScan::ExclusiveSum(c->tmp.p, tbytes, fsz, foff, (int)n, c->stream));
+  uint32_t lc = 0;
+  EW_CHECK(hipMemcpyAsync(&tail[0], foff + n - 1, 8, hipMemcpyDeviceToHost, c->stream));
+  EW_CHECK(hipMemcpyAsync(&tail[1], fsz + n - 1, 8, hipMemcpyDeviceToHost, c->stream));
+  EW_CHECK(hipMemcpyAsync(&lc, crc + n - 1, 4, hipMemcpyDeviceToHost, c->stream));
+  EW_CHECK(hipStreamSynchronize(c->stream));
+  const uint64_t total = tail[0] + tail[1];
+  if (total > cap) return EWAL_E_NOMEM;
+  hipLaunchKernelGGL(k_enc_frame, dim3(wgrid), dim3(256), 0, c->stream, es, E, xoff, esz, crc, foff, n,
+                     (uint8_t *)d_out);
+  EW_CHECK(hipGetLastError());
+  EW_CHECK(hipStreamSynchronize(c->stream));
+  *out_len = total;
+  *last_crc = lc;
+  return EWAL_OK;
 }
 
 int ewal_crc32_update_device(ewal_ctx *c, uint32_t crc, uint32_t poly, const void *d_buf, uint64_t n, uint32_t *out) {

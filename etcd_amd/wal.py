@@ -304,6 +304,35 @@ class Encoder:
             pass
 
 
+def encode_entries_device(ctx: Context, entries, prev_crc: int = 0):
+    """SaveEntry for every entry, in order, on the GPU (encoder.encode,
+    wal/wal.go:248-263, wal/encoder.go:25-37): returns (frame bytes, the
+    chained CRC after the last entry) -- byte-identical to Encoder.save_entry
+    in a loop."""
+    payload = b"".join((e.Data or b"") for e in entries)
+    n = len(entries)
+    arr = (L.EntryDesc * max(1, n))()
+    off = 0
+    for i, e in enumerate(entries):
+        d = e.Data or b""
+        arr[i].term, arr[i].index, arr[i].data_off, arr[i].data_len = e.Term, e.Index, off, len(d)
+        arr[i].type, arr[i].data_nil = e.Type, int(e.Data is None)
+        off += len(d)
+    cap = len(payload) + 80 * n + 64
+    dd, de, do = ctx.alloc(len(payload) + 64), ctx.alloc(C.sizeof(arr)), ctx.alloc(cap)
+    try:
+        if payload:
+            dd.upload(payload)
+        de.upload(bytes(arr))
+        out_len, crc = C.c_uint64(), C.c_uint32()
+        check(lib.ewal_encode_entries_device(ctx.handle, dd.ptr, len(payload), de.ptr, n, prev_crc, do.ptr, cap,
+                                             C.byref(out_len), C.byref(crc)))
+        return (do.download(out_len.value) if out_len.value else b""), crc.value
+    finally:
+        for b in (dd, de, do):
+            b.free()
+
+
 def synth_wal(target_bytes, min_data=64, max_data=65536, seed=2, corrupt_record=-1):
     """Synthetic WAL (bench/test input); returns (bytearray, n_records)."""
     cap = target_bytes + max_data * 2 + (1 << 20)

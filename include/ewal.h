@@ -176,6 +176,20 @@ void ewal_encoder_free(ewal_encoder *e);
 int64_t ewal_synth_wal(uint64_t seed, uint64_t target_bytes, uint32_t min_data, uint32_t max_data,
                        int64_t corrupt_record, uint8_t *out, uint64_t cap, int64_t *n_records);
 
+/* ---- batched write path: (*WAL).SaveEntry / encoder.encode on the GPU ---- */
+/* encoder.encode(&walpb.Record{Type: entryType, Data: pbutil.MustMarshal(e)})
+ * for n entries in order (wal/wal.go:248-263, wal/encoder.go:25-37): the
+ * frames, byte-identical to the reference's encoder, and the chained CRC
+ * (c_i = crc32.Update(c_{i-1}, Castagnoli, Entry_i bytes), c_{-1} = prev_crc).
+ * d_data: the entries' payloads on the device (d_ents[i].data_off/data_len
+ * index it, data_len_total bytes); d_ents: n ewal_entry on the device.
+ * d_out: device buffer of cap bytes.  *out_len = bytes written, *last_crc =
+ * c_{n-1} (prev_crc when n == 0).  EWAL_E_NOMEM when the frames exceed cap,
+ * EWAL_E_INVAL when an entry's payload lies outside d_data. */
+int ewal_encode_entries_device(ewal_ctx *ctx, const void *d_data, uint64_t data_len_total, const ewal_entry *d_ents,
+                               uint64_t n, uint32_t prev_crc, void *d_out, uint64_t cap, uint64_t *out_len,
+                               uint32_t *last_crc);
+
 /* ---- CRC primitives (pkg/crc, pkg/crc/crc.go:23-41) ---------------------- */
 /* crc32.Update(crc, MakeTable(poly), p) on a DEVICE buffer. */
 int ewal_crc32_update_device(ewal_ctx *ctx, uint32_t crc, uint32_t poly, const void *d_buf, uint64_t n,
