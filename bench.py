@@ -39,6 +39,11 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
+    ap.add_argument("--workload", choices=["wal", "shards", "snap", "commit"], default="wal",
+                    help="wal = configs[1] (the headline, default); shards = configs[2] (4096 x 64 MiB per-group "
+                         "WALs over the node, 512 per GPU); snap = configs[3]; commit = configs[4]")
+    ap.add_argument("--shards-per-gpu", type=int, default=512)
+    ap.add_argument("--shard-mib", type=int, default=64)
     return ap.parse_args()
 
 
@@ -50,6 +55,264 @@ def load_traffic():
         return d.get("hbm_bytes_per_launch")
     except Exception:
         return None
+
+
+METRIC = "WAL verify GB/s (and records/s) per GPU + 8-GPU node, % of HBM roofline"
+
+
+def timed(dist, steps, fn):
+    """barrier + sync, K steps, sync + barrier; the max over ranks (s)."""
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        fn()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    return elapsed
+
+
+def run_shards(a, dist, rank, world, local):
+    """configs[2]: 4096 per-raft-group WAL shards x 64 MiB over the node --
+    each GPU replays its 512 (at N=8) in ONE batched ReadAll
+    (ewal_readall_batch_device); entries 128 B - 4 KiB log-uniform, seed =
+    global shard id; one corrupt record in global shard 2749 mod (512 N).
+    The verdicts cross ranks in one all-reduce (etcd_amd/shard.py)."""
+    nsh, smib = a.shards_per_gpu, a.shard_mib
+    first = rank * nsh
+    bad_shard = 2749 % (nsh * world)
+    t = time.time()
+    blob, lens, nrec = W.synth_shards([first + i for i in range(nsh)], smib << 20, 128, 4096,
+                                      corrupt={bad_shard - first: 1000} if first <= bad_shard < first + nsh else {})
+    gen_s = time.time() - t
+    nb = len(blob)
+    ctx = W.Context(local)
+    dbuf = ctx.alloc(nb + 64)
+    dbuf.upload_ptr(C.addressof((C.c_char * nb).from_buffer(blob)), nb)
+    ris = [1] * nsh
+    res = None
+    for _ in range(max(a.warmup, 1)):
+        res = W.readall_batch_device(dbuf, lens, ris)
+    for i, r in enumerate(res):
+        want = (L.ERR_RECORD_CRC, 1000) if first + i == bad_shard else (L.OK, -1)
+        assert (r.status, r.fail_record) == want and not (r.flags & L.FLAG_SHARD_FALLBACK), (i, r.status, r.flags)
+        assert r.status != L.OK or r.n_records == nrec[i]
+    summary = torch.zeros(3, dtype=torch.int64, device="cuda") if dist is not None else None
+    last = {}
+
+    def step():
+        rr = W.readall_batch_device(dbuf, lens, ris)
+        last["r"] = rr
+        if dist is not None:
+            fails = [(i, x.fail_record) for i, x in enumerate(rr) if x.status != L.OK]
+            i0, fr = fails[0] if fails else (0, -1)
+            shard.combine(dist, first + i0, fr, sum(x.n_records for x in rr), len(fails) > 0, out=summary)
+
+    elapsed = timed(dist, a.steps, step)
+    ms = elapsed / a.steps * 1e3
+    r0 = last["r"][0]
+    frames = sum(nrec)
+    if rank == 0:
+        out = {
+            "metric": METRIC, "value": round(world * nb / (ms / 1e3) / 1e9, 3), "unit": "GB/s", "n_gpus": world,
+            "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(ms, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
+            "config": {"workload": "configs[2]: %d per-raft-group WAL shards x %d MiB per GPU (%d on 8 GPUs), entry "
+                                   "Data log-uniform 128 B-4 KiB, seed = shard id, one corrupt record in shard %d; one "
+                                   "batched ReadAll per GPU per step" % (nsh, smib, nsh * 8, bad_shard),
+                       "wal_bytes_per_gpu": nb, "frames_per_gpu": frames, "shards_per_gpu": nsh, "ri": 1,
+                       "parallelism": "dp%d (independent shards, one all-reduce of verdicts)" % world},
+            "records_per_s": round(world * frames / (ms / 1e3), 1),
+            "roofline": {"bound": "hbm", "achieved": round(nb / (r0.stream_ms / 1e3) / 1e9, 2),
+                         "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                         "frac": round(nb / (r0.stream_ms / 1e3) / 1e9 / HBM_PEAK_GBPS, 4), "traffic": None,
+                         "kernel": "k_stream", "kernel_ms": round(r0.stream_ms, 4),
+                         "algorithmic_bytes_per_launch": nb},
+            "pipeline_device_ms": round(r0.device_ms, 4),
+            "cpu_baseline": None,
+            "gen_seconds": round(gen_s, 2),
+        }
+        print(json.dumps(out), flush=True)
+    dbuf.free()
+    ctx.close()
+
+
+def run_snap(a, dist, rank, world, local):
+    """configs[3]: batch verification of snap/snapshotter snapshot files
+    (loadSnap's CRC, snap/snapshotter.go:76-111): sizes log-uniform 1-256 MiB
+    (seed 4), ~1 % corrupt (seed 5, at least one).  The 10k-file set is
+    ~450 GiB, more than one GPU holds: each GPU verifies a resident batch of
+    --size-gib (default 16 GiB) per step in ONE esnap_verify_packed call (8
+    GPUs: ~56 GiB each)."""
+    import math
+    import random
+    import numpy as np
+    from etcd_amd import snap as S
+    rng, crng = random.Random(4 + 7919 * rank), random.Random(5 + 7919 * rank)
+    budget = int((a.size_gib if a.size_gib != 8.0 else 16.0) * (1 << 30))
+    t = time.time()
+    pool = np.random.default_rng(4 + rank).integers(0, 256, size=(256 << 20) + 4096, dtype=np.uint8).tobytes()
+    files, bad, total = [], [], 0
+    while total < budget:
+        n = int(math.exp(rng.uniform(math.log(1 << 20), math.log(256 << 20))))
+        st = rng.randrange(0, len(pool) - n)
+        f = bytearray(S.snap_file(S.snapshot_marshal(pool[st:st + n], (1, 2, 3), len(files) + 1, 1)))
+        if crng.random() < 0.01 or (not bad and total + len(f) >= budget):
+            f[len(f) // 2] ^= 0x10      # inside Data: snap.ErrCRCMismatch
+            bad.append(len(files))
+        files.append(bytes(f))
+        total += len(f)
+    lens = [len(f) for f in files]
+    offs = [0]
+    for x in lens[:-1]:
+        offs.append(offs[-1] + x)
+    blob = b"".join(files)
+    del files
+    gen_s = time.time() - t
+    nb = len(blob)
+    ctx = W.Context(local)
+    dbuf = ctx.alloc(nb + 64)
+    dbuf.upload(blob)
+    for _ in range(max(a.warmup, 1)):
+        stt, _, _ = S.verify_packed(dbuf, nb, offs, lens)
+    assert [i for i, x in enumerate(stt) if x != L.OK] == bad and all(stt[i] == L.ERR_SNAP_CRC for i in bad), bad
+    elapsed = timed(dist, a.steps, lambda: S.verify_packed(dbuf, nb, offs, lens))
+    ms = elapsed / a.steps * 1e3
+    kms = float(L.lib.ewal_last_stream_ms(ctx.handle))
+    dev_ms = float(L.lib.ewal_last_device_ms(ctx.handle))
+    cpu = None
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        from oracle import oracle as O   # baseline only
+        small = sorted(range(len(lens)), key=lambda i: lens[i])
+        pick, acc = [], 0
+        for i in small:
+            if acc >= (1 << 30):
+                break
+            pick.append(i)
+            acc += lens[i]
+        views = [blob[offs[i]:offs[i] + lens[i]] for i in pick]
+        it, t2 = 0, time.perf_counter()
+        while True:
+            for v in views:
+                O.loadsnap(v)
+            it += 1
+            if time.perf_counter() - t2 >= a.cpu_seconds:
+                break
+        cs = time.perf_counter() - t2
+        cpu = {"value": round(acc * it / cs / 1e9, 4), "unit": "GB/s", "cores": 1, "kind": "port",
+               "sample": "oracle/ or_loadsnap (snappb + raftpb.Snapshot Unmarshal, crc32.Update, 1 thread) over "
+                         "%d of the files (%.2f GiB), %d passes, %.1f s" % (len(pick), acc / (1 << 30), it, cs)}
+    if rank == 0:
+        print(json.dumps({
+            "metric": METRIC, "value": round(world * nb / (ms / 1e3) / 1e9, 3), "unit": "GB/s", "n_gpus": world,
+            "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(ms, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
+            "config": {"workload": "configs[3]: snapshot batch verify, %d files per GPU (%.2f GiB resident), sizes "
+                                   "log-uniform 1-256 MiB, %d corrupt (snap.ErrCRCMismatch)" %
+                                   (len(lens), nb / (1 << 30), len(bad)),
+                       "snapshot_bytes_per_gpu": nb, "files_per_gpu": len(lens),
+                       "parallelism": "dp%d (independent files)" % world},
+            "files_per_s": round(world * len(lens) / (ms / 1e3), 1),
+            "roofline": {"bound": "hbm", "achieved": round(nb / (kms / 1e3) / 1e9, 2), "peak": HBM_PEAK_GBPS,
+                         "unit": "GB/s", "frac": round(nb / (kms / 1e3) / 1e9 / HBM_PEAK_GBPS, 4), "traffic": None,
+                         "kernel": "k_stream<false>", "kernel_ms": round(kms, 4),
+                         "algorithmic_bytes_per_launch": nb},
+            "pipeline_device_ms": round(dev_ms, 4),
+            "cpu_baseline": cpu, "gen_seconds": round(gen_s, 2)}), flush=True)
+    dbuf.free()
+    ctx.close()
+
+
+def run_commit(a, dist, rank, world, local):
+    """configs[4]: batched raft.maybeCommit (raft/raft.go:248-258 +
+    raft/log.go:148-154) over 1M raft groups per GPU, 5 or 7 voters (seed 6),
+    SoA matchIndex, a 16-entry log-term window per group; one
+    ecommit_batch_device launch per step (committed reset from a copy
+    first, so every step does the same work)."""
+    import numpy as np
+    G = 1 << 20
+    rng = np.random.default_rng(6 + rank)
+    nv = np.where(rng.random(G) < 0.5, 5, 7).astype(np.uint8)
+    committed0 = rng.integers(0, 1 << 20, size=G, dtype=np.uint64)
+    match = (committed0[None, :] + rng.integers(0, 24, size=(7, G), dtype=np.uint64)
+             - np.uint64(4)).astype(np.uint64)
+    term = rng.integers(1, 4, size=G, dtype=np.uint64)
+    log_offset = committed0 + np.uint64(1) - rng.integers(0, 3, size=G, dtype=np.uint64)
+    log_ptr = (np.arange(G + 1, dtype=np.uint64) * np.uint64(16))
+    log_terms = np.sort(rng.integers(1, 4, size=(G, 16), dtype=np.uint64), axis=1).reshape(-1)
+    dev = torch.device("cuda", local)
+    T = lambda x: torch.from_numpy(x.view(np.int64) if x.dtype == np.uint64 else x).to(dev)   # noqa: E731
+    d_match, d_nv, d_term, d_c0 = T(match.reshape(-1)), T(nv), T(term), T(committed0)
+    d_off, d_ptr, d_lt = T(log_offset), T(log_ptr), T(log_terms)
+    d_c = d_c0.clone()
+    d_ch = torch.zeros(G, dtype=torch.uint8, device=dev)
+    d_st = torch.zeros(G, dtype=torch.uint8, device=dev)
+    ctx = W.Context(local)
+    ctx.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+    dms = C.c_double(0)
+    kms = []
+
+    def step():
+        d_c.copy_(d_c0)
+        rc = L.lib.ecommit_batch_device(ctx.handle, G, C.c_void_p(d_match.data_ptr()), C.c_void_p(d_nv.data_ptr()),
+                                        C.c_void_p(d_term.data_ptr()), C.c_void_p(d_c.data_ptr()),
+                                        C.c_void_p(d_off.data_ptr()), C.c_void_p(d_ptr.data_ptr()),
+                                        C.c_void_p(d_lt.data_ptr()), C.c_void_p(d_ch.data_ptr()),
+                                        C.c_void_p(d_st.data_ptr()), C.byref(dms))
+        assert rc == 0, rc
+        kms.append(dms.value)
+
+    for _ in range(max(a.warmup, 1)):
+        step()
+    new = d_c.cpu().numpy().view(np.uint64)
+    ch = d_ch.cpu().numpy()
+    assert (new >= committed0).all() and ((new != committed0) == (ch == 1)).all() and not d_st.cpu().numpy().any()
+    nchanged = int(ch.sum())
+    kms.clear()
+    elapsed = timed(dist, a.steps, step)
+    ms = elapsed / a.steps * 1e3
+    k_avg = sum(kms) / len(kms)
+    # algorithmic bytes: nvoters 1 + n match words + term, committed (r+w), log_offset, 2 log_ptr, the term gather,
+    # changed + status
+    abytes = int(G + 8 * int(nv.astype(np.int64).sum()) + G * (8 + 16 + 8 + 16 + 8 + 2))
+    cpu = None
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        from oracle import oracle as O   # baseline only
+        c = committed0.copy()
+        chc, stc = np.zeros(G, np.uint8), np.zeros(G, np.uint8)
+        it, t2 = 0, time.perf_counter()
+        while True:
+            c[:] = committed0
+            O.maybe_commit_batch(G, match.reshape(-1), nv, term, c, log_offset, log_ptr, log_terms, chc, stc)
+            it += 1
+            if time.perf_counter() - t2 >= a.cpu_seconds:
+                break
+        cs = time.perf_counter() - t2
+        cpu = {"value": round(G * it / cs, 1), "unit": "groups/s", "cores": 1, "kind": "port",
+               "sample": "oracle/ or_maybe_commit_batch (insertion sort + q-th largest + term check per group, 1 "
+                         "thread) over all %d groups, %d passes, %.1f s" % (G, it, cs)}
+    if rank == 0:
+        print(json.dumps({
+            "metric": "maybeCommit groups/s (configs[4]); WAL verify GB/s is the headline metric",
+            "value": round(world * G / (ms / 1e3), 1), "unit": "groups/s", "n_gpus": world, "steps": a.steps,
+            "warmup": a.warmup, "ms_per_step": round(ms, 4), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "u64", "data": "synthetic",
+            "config": {"workload": "configs[4]: maybeCommit over %d raft groups per GPU, 5/7 voters (50/50), 16-entry "
+                                   "log-term window; %d groups advance commit" % (G, nchanged),
+                       "groups_per_gpu": G, "parallelism": "dp%d (group ranges)" % world},
+            "roofline": {"bound": "hbm", "achieved": round(abytes / (k_avg / 1e3) / 1e9, 2), "peak": HBM_PEAK_GBPS,
+                         "unit": "GB/s", "frac": round(abytes / (k_avg / 1e3) / 1e9 / HBM_PEAK_GBPS, 4),
+                         "traffic": None, "kernel": "k_commit", "kernel_ms": round(k_avg, 4),
+                         "algorithmic_bytes_per_launch": abytes},
+            "cpu_baseline": cpu}), flush=True)
+    ctx.close()
 
 
 def main():
@@ -67,6 +330,12 @@ def main():
     def barrier():
         if dist is not None:
             dist.barrier()
+
+    if a.workload != "wal":
+        {"shards": run_shards, "snap": run_snap, "commit": run_commit}[a.workload](a, dist, rank, world, local)
+        if dist is not None:
+            dist.destroy_process_group()
+        return
 
     # ---- input: an independent synthetic WAL shard per rank ----------------
     size = int(a.size_gib * (1 << 30))

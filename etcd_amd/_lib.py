@@ -53,6 +53,8 @@ NONTERMINATING = 37
 UNSUPPORTED_ENCODING = 48
 E_HIP, E_INVAL, E_NOMEM, E_NODEVICE, E_TIMEOUT, E_IO = -1, -2, -3, -4, -5, -6
 
+FLAG_SHARD_FALLBACK = 1   # ewal_readall_batch_device verified this shard on its own
+
 CASTAGNOLI, IEEE, KOOPMAN = 0x82F63B78, 0xEDB88320, 0xEB31D82E
 
 
@@ -99,6 +101,10 @@ _SIGS = {
     "ewal_stage_to_device": (C.c_int, [vp, vp, C.c_uint64, C.POINTER(vp)]),
     "ewal_readall_host": (C.c_int, [vp, vp, C.c_uint64, C.c_uint64, C.POINTER(Result)]),
     "ewal_copy_entries": (C.c_int64, [vp, C.POINTER(EntryDesc), C.c_int64]),
+    "ewal_last_stream_ms": (C.c_float, [vp]),
+    "ewal_readall_batch_device": (C.c_int, [vp, vp, C.c_uint64, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64),
+                                            C.POINTER(Result)]),
+    "ewal_batch_copy_entries": (C.c_int64, [vp, C.c_uint64, C.POINTER(EntryDesc), C.c_int64]),
     "ewal_copy_records": (C.c_int64, [vp, C.POINTER(RecordDesc), C.c_int64]),
     "ewal_open_at_index": (C.c_int, [C.c_char_p, C.c_uint64, C.POINTER(vp)]),
     "ewal_wal_readall": (C.c_int, [vp, vp, C.POINTER(Result)]),

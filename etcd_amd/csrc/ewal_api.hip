@@ -73,6 +73,9 @@ struct ewal_ctx {
   std::map<uint32_t, std::unique_ptr<ewal::CrcTables>> host_tables;
   DevBuf encw, encs, lbstat, gagg, slow, mlist, pf, v, pwave, ux, tagg, tpx, wcnt, slots, cbase, ovf, cpos, clen, nxt, exc, E, rs, jl, vis, entry, on, rec_cand, rd, opf, ops, kk, kkrev, suf,
       ents, recs, tmp, small, sdesc, snaps, hbuf_dev;
+  // batched ReadAll (ewal_readall_batch_device): shard tables, results, ents
+  DevBuf bfs, bsoff, bri, bsagg, bres, bef, bents, bshard;
+  std::vector<uint64_t> bent_first, bnents;   // per shard: first ent in bents, count
   Small *h_small = nullptr;        // host-mapped pinned mirrors (written by k_export_small / k_result)
   ResultDev *h_res = nullptr;
   Small *h_small_dev = nullptr;    // their device-side addresses
@@ -432,9 +435,9 @@ static int readall_impl(ewal_ctx *c, const uint8_t *d_buf, uint64_t B, uint64_t 
     EW_CHECK(c->mlist.ensure((size_t)n * 4));
     EW_CHECK(c->kk.ensure((size_t)n * 8));
     EW_CHECK(c->ents.ensure((size_t)n * sizeof(ewal_entry)));
-    hipLaunchKernelGGL(k_check, dim3(nb), dim3(1024), 0, c->stream, tb->shift, rd, n32, pfd, pfo, ri,
+    hipLaunchKernelGGL(k_check<false>, dim3(nb), dim3(1024), 0, c->stream, tb->shift, rd, n32, pfd, pfo, ri,
                        c->lbstat.as<unsigned long long>(), c->epoch, c->opf.as<uint32_t>(), c->ents.as<ewal_entry>(),
-                       c->mlist.as<uint32_t>(), ds);
+                       c->mlist.as<uint32_t>(), ds, SegArgs{});
     hipLaunchKernelGGL(k_result, dim3(1), dim3(256), 0, c->stream, d_buf, rd, c->mlist.as<uint32_t>(), n32, ri, ds,
                        c->h_res_dev);
     EW_CHECK(hipGetLastError());
@@ -530,6 +533,201 @@ static int readall_impl(ewal_ctx *c, const uint8_t *d_buf, uint64_t B, uint64_t 
   return out->status;
 }
 
+// Grow-only device buffer that keeps its first `keep` bytes.
+static hipError_t grow_keep(DevBuf &b, size_t need, size_t keep, hipStream_t st) {
+  if (need <= b.cap) return hipSuccess;
+  DevBuf nb;
+  hipError_t e = nb.ensure(std::max(need, b.cap * 2));
+  if (e != hipSuccess) return e;
+  if (keep) {
+    e = hipMemcpyAsync(nb.p, b.p, keep, hipMemcpyDeviceToDevice, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (e != hipSuccess) {
+      nb.release();
+      return e;
+    }
+  }
+  b.release();
+  b = nb;
+  return hipSuccess;
+}
+
+// Batched ReadAll over many independent WALs (per-raft-group shards, SURVEY
+// §8(d) C3) laid end to end in one device buffer: ONE stream pass, ONE frame
+// pass and ONE segmented check (k_check<true>) for the whole batch, two host
+// syncs in all, instead of a pipeline per shard.  The batch's frame chain runs
+// through every shard when each ends on a frame boundary; when it does not
+// (a torn or corrupt frame boundary), or on the rare op-list paths (index
+// rewinds, far-back gap predecessors), the shards are verified one by one
+// through readall_impl (result flag EWAL_FLAG_SHARD_FALLBACK).
+static int readall_batch_impl(ewal_ctx *c, const uint8_t *d_buf, uint32_t ns, const uint64_t *lens,
+                              const uint64_t *ris, ewal_result *out) {
+  std::vector<uint64_t> soff(ns + 1, 0);
+  for (uint32_t i = 0; i < ns; ++i) {
+    soff[i + 1] = soff[i] + lens[i];
+    if (soff[i + 1] < soff[i]) return EWAL_E_INVAL;
+  }
+  const uint64_t B = soff[ns];
+  if (((uintptr_t)d_buf & 15) != 0 && B) return EWAL_E_INVAL;
+  c->bent_first.assign(ns, 0);
+  c->bnents.assign(ns, 0);
+  c->last_ok = false;
+  c->last_n = 0;
+  c->last_nents = 0;
+  DevTables *tb;
+  int rc = get_tables(c, 0x82F63B78u, &tb);
+  if (rc) return rc;
+  EW_CHECK(c->small.ensure(sizeof(Small)));
+  Small *ds = c->small.as<Small>();
+  bool fast = B > 0 && ns > 0;
+  float dev_ms = 0, str_ms = 0;
+  if (fast) {
+    EW_CHECK(hipEventRecord(c->ev0, c->stream));
+    const uint64_t ccap = std::min<uint64_t>(B / 128 + 65536, 0xfffffff0ull);
+    EW_CHECK(c->cpos.ensure(ccap * 8));
+    EW_CHECK(c->clen.ensure(ccap * 8));
+    EW_CHECK(c->nxt.ensure(ccap * 4));
+    EW_CHECK(c->exc.ensure(ccap));
+    uint64_t rdcap = std::min<uint64_t>(ccap, std::max<uint64_t>(c->last_k + c->last_k / 8 + 1024,
+                                                                 B / 1024 + 1024));
+    rc = run_stream(c, tb, d_buf, B, 1, ccap);
+    if (rc) return rc;
+    uint32_t *pf = nullptr;
+    bool rescanned = false;
+    for (int pass = 0; pass < 3; ++pass) {
+      EW_CHECK(c->rd.ensure(rdcap * sizeof(RecDesc)));
+      EW_CHECK(c->pf.ensure(rdcap * 8));
+      EW_CHECK(c->slow.ensure(rdcap * 4));
+      c->pfcap = rdcap;
+      pf = c->pf.as<uint32_t>();
+      const unsigned fgrid = (unsigned)std::max(1, c->num_cu) * 3;
+      hipLaunchKernelGGL(k_frame, dim3(fgrid), dim3(256), 0, c->stream, d_buf, B, c->cpos.as<uint64_t>(), ccap,
+                         rdcap, c->pwave.as<uint32_t>(), c->v.as<uint32_t>(), tb->slice, tb->shift,
+                         c->rd.as<RecDesc>(), pf, pf + rdcap, c->slow.as<uint32_t>(), ds, c->ablate);
+      EW_CHECK(hipGetLastError());
+      if ((rc = sync_small(c))) return rc;
+      // k_frame declined before decoding anything when there were more
+      // candidates than descriptors or units with more than EW_SLOTS
+      // candidates (small records): grow / k_rescan, and run it again
+      const uint64_t Kf = c->h_small->total;
+      const bool grow = Kf > rdcap && Kf <= ccap;
+      const bool resc = c->h_small->novf && Kf <= ccap && !rescanned;
+      if (!grow && !resc) break;
+      if (resc) {
+        hipLaunchKernelGGL(k_rescan, dim3(64), dim3(256), 0, c->stream, d_buf, B, c->ovf.as<uint32_t>(), &ds->novf,
+                           c->cbase.as<unsigned long long>(), c->cpos.as<uint64_t>(), c->clen.as<uint64_t>(), ccap);
+        EW_CHECK(hipGetLastError());
+        EW_CHECK(hipMemsetAsync(&ds->novf, 0, 4, c->stream));
+        rescanned = true;
+      }
+      if (grow) rdcap = Kf + Kf / 8 + 1024;
+    }
+    const uint64_t K = c->h_small->total;
+    c->last_k = K;
+    fast = K && K <= ccap && K <= rdcap && !c->h_small->novf && c->h_small->pos0 == 0 && !c->h_small->irregular &&
+           c->h_small->q == B;
+    if (!fast && std::getenv("EWAL_DEBUG"))
+      std::fprintf(stderr, "ewal batch: one by one (K %llu ccap %llu rdcap %llu novf %u pos0 %llu irr %u q %llu B %llu)\n",
+                   (unsigned long long)K, (unsigned long long)ccap, (unsigned long long)rdcap, c->h_small->novf,
+                   (unsigned long long)c->h_small->pos0, c->h_small->irregular, (unsigned long long)c->h_small->q,
+                   (unsigned long long)B);
+    if (fast) {
+      const uint32_t n32 = (uint32_t)K;
+      if (c->h_small->nslow) {
+        hipLaunchKernelGGL(k_decode_slow, dim3(std::min<uint64_t>(grid_for(c->h_small->nslow, 256), 1024)),
+                           dim3(256), 0, c->stream, d_buf, B, c->cpos.as<uint64_t>(), (const uint32_t *)nullptr,
+                           c->slow.as<uint32_t>(), ds, c->pwave.as<uint32_t>(), c->v.as<uint32_t>(), tb->slice,
+                           tb->shift, c->rd.as<RecDesc>(), pf, pf + rdcap, 0u);
+        EW_CHECK(hipGetLastError());
+      }
+      EW_CHECK(c->bsoff.ensure((size_t)(ns + 1) * 8));
+      EW_CHECK(c->bri.ensure((size_t)ns * 8));
+      EW_CHECK(c->bfs.ensure((size_t)(ns + 1) * 4));
+      EW_CHECK(c->bsagg.ensure((size_t)ns * sizeof(ShardAgg)));
+      EW_CHECK(c->bres.ensure((size_t)ns * sizeof(ewal_result)));
+      EW_CHECK(c->bef.ensure((size_t)ns * 8));
+      EW_CHECK(hipMemcpyAsync(c->bsoff.p, soff.data(), (size_t)(ns + 1) * 8, hipMemcpyHostToDevice, c->stream));
+      EW_CHECK(hipMemcpyAsync(c->bri.p, ris, (size_t)ns * 8, hipMemcpyHostToDevice, c->stream));
+      RecDesc *rd = c->rd.as<RecDesc>();
+      hipLaunchKernelGGL(k_shard_start, dim3(grid_for(ns + 1, 256)), dim3(256), 0, c->stream, rd, n32,
+                         c->bsoff.as<uint64_t>(), ns, c->bfs.as<uint32_t>(), c->bsagg.as<ShardAgg>(), ds);
+      const uint32_t nb = grid_for(K, 1024);
+      const size_t had = c->lbstat.cap;
+      EW_CHECK(c->lbstat.ensure((size_t)nb * 8));
+      c->epoch = (c->epoch + 1) & 0xffffffu;
+      if (c->lbstat.cap != had || c->epoch == 0) {
+        EW_CHECK(hipMemsetAsync(c->lbstat.p, 0, c->lbstat.cap, c->stream));
+        if (c->epoch == 0) c->epoch = 1;
+      }
+      EW_CHECK(c->opf.ensure((size_t)nb * 4));
+      EW_CHECK(c->mlist.ensure((size_t)K * 4));
+      EW_CHECK(grow_keep(c->bents, (size_t)K * sizeof(ewal_entry), 0, c->stream));
+      SegArgs sg;
+      sg.fs = c->bfs.as<uint32_t>();
+      sg.ns = ns;
+      sg.ri = c->bri.as<uint64_t>();
+      sg.soff = c->bsoff.as<uint64_t>();
+      sg.sagg = c->bsagg.as<ShardAgg>();
+      hipLaunchKernelGGL(k_check<true>, dim3(nb), dim3(1024), 0, c->stream, tb->shift, rd, n32, pf, pf + rdcap, 0ull,
+                         c->lbstat.as<unsigned long long>(), c->epoch, c->opf.as<uint32_t>(),
+                         c->bents.as<ewal_entry>(), c->mlist.as<uint32_t>(), ds, sg);
+      hipLaunchKernelGGL(k_meta_batch, dim3(64), dim3(256), 0, c->stream, d_buf, rd, c->mlist.as<uint32_t>(), ds, sg);
+      hipLaunchKernelGGL(k_result_batch, dim3(grid_for(ns, 256)), dim3(256), 0, c->stream, rd, sg,
+                         c->bres.as<ewal_result>(), c->bef.as<unsigned long long>());
+      EW_CHECK(hipGetLastError());
+      EW_CHECK(hipMemcpyAsync(out, c->bres.p, (size_t)ns * sizeof(ewal_result), hipMemcpyDeviceToHost, c->stream));
+      EW_CHECK(hipMemcpyAsync(c->bent_first.data(), c->bef.p, (size_t)ns * 8, hipMemcpyDeviceToHost, c->stream));
+      EW_CHECK(hipEventRecord(c->ev1, c->stream));
+      if ((rc = sync_small(c))) return rc;
+      fast = !c->h_small->segbad && !c->h_small->gapslow && !c->h_small->nonmono;
+      if (!fast && std::getenv("EWAL_DEBUG"))
+        std::fprintf(stderr, "ewal batch: one by one (segbad %u gapslow %u nonmono %u)\n", c->h_small->segbad,
+                     c->h_small->gapslow, c->h_small->nonmono);
+      if (fast) {
+        EW_CHECK(hipEventElapsedTime(&dev_ms, c->ev0, c->ev1));
+        EW_CHECK(hipEventElapsedTime(&str_ms, c->evs0, c->evs1));
+        for (uint32_t i = 0; i < ns; ++i) {
+          out[i].device_ms = dev_ms;
+          out[i].stream_ms = str_ms;
+          out[i].n_slow = (int32_t)c->h_small->nslow;
+          c->bnents[i] = (uint64_t)out[i].n_ents;
+          if (!out[i].n_ents) c->bent_first[i] = 0;
+        }
+        return 0;
+      }
+    }
+  }
+  // one shard at a time (a shard's bytes are copied to an aligned scratch
+  // buffer: the stream pass reads 16-B aligned)
+  c->bent_first.assign(ns, 0);
+  c->bnents.assign(ns, 0);
+  uint64_t have = 0;
+  for (uint32_t i = 0; i < ns; ++i) {
+    const uint8_t *p = d_buf;
+    if (lens[i]) {
+      EW_CHECK(c->bshard.ensure(lens[i] + 64));
+      EW_CHECK(hipMemcpyAsync(c->bshard.p, d_buf + soff[i], lens[i], hipMemcpyDeviceToDevice, c->stream));
+      p = c->bshard.as<uint8_t>();
+    }
+    rc = readall_impl(c, p, lens[i], ris[i], &out[i]);
+    if (rc < 0) return rc;
+    out[i].flags |= EWAL_FLAG_SHARD_FALLBACK;
+    const uint64_t ne = out[i].status == EWAL_OK ? (uint64_t)out[i].n_ents : 0;
+    if (ne) {
+      EW_CHECK(grow_keep(c->bents, (size_t)(have + ne) * sizeof(ewal_entry), (size_t)have * sizeof(ewal_entry),
+                         c->stream));
+      EW_CHECK(hipMemcpyAsync(c->bents.as<ewal_entry>() + have, c->ents.p, (size_t)ne * sizeof(ewal_entry),
+                              hipMemcpyDeviceToDevice, c->stream));
+      c->bent_first[i] = have;
+      c->bnents[i] = ne;
+      have += ne;
+    }
+  }
+  EW_CHECK(hipStreamSynchronize(c->stream));
+  c->last_ok = false;
+  return 0;
+}
+
 extern "C" {
 
 int ewal_device_count(void) {
@@ -605,6 +803,24 @@ int ewal_readall_device(ewal_ctx *c, const void *d_buf, uint64_t len, uint64_t r
   if (!c || !out || (!d_buf && len)) return EWAL_E_INVAL;
   EW_CHECK(hipSetDevice(c->device));
   return readall_impl(c, (const uint8_t *)d_buf, len, ri, out);
+}
+
+int ewal_readall_batch_device(ewal_ctx *c, const void *d_buf, uint64_t n_shards, const uint64_t *lens,
+                              const uint64_t *ri, ewal_result *out) {
+  if (!c || (n_shards && (!lens || !ri || !out)) || n_shards >= 0x7fffffffull) return EWAL_E_INVAL;
+  EW_CHECK(hipSetDevice(c->device));
+  return readall_batch_impl(c, (const uint8_t *)d_buf, (uint32_t)n_shards, lens, ri, out);
+}
+
+int64_t ewal_batch_copy_entries(ewal_ctx *c, uint64_t shard, ewal_entry *out, int64_t cap) {
+  if (!c || (!out && cap) || shard >= c->bnents.size()) return EWAL_E_INVAL;
+  const int64_t n = std::min<int64_t>(cap, (int64_t)c->bnents[shard]);
+  if (n > 0) {
+    EW_CHECK(hipMemcpyAsync(out, c->bents.as<ewal_entry>() + c->bent_first[shard], (size_t)n * sizeof(ewal_entry),
+                            hipMemcpyDeviceToHost, c->stream));
+    EW_CHECK(hipStreamSynchronize(c->stream));
+  }
+  return n;
 }
 
 int ewal_device_alloc(ewal_ctx *c, uint64_t len, void **d_out) {
@@ -813,6 +1029,12 @@ int esnap_copy_snapshot(ewal_ctx *c, uint32_t i, esnap_snapshot *out) {
 float ewal_last_device_ms(ewal_ctx *c) {
   float ms = 0;
   if (hipEventElapsedTime(&ms, c->ev0, c->ev1) != hipSuccess) return -1.f;
+  return ms;
+}
+
+float ewal_last_stream_ms(ewal_ctx *c) {
+  float ms = 0;
+  if (hipEventElapsedTime(&ms, c->evs0, c->evs1) != hipSuccess) return -1.f;
   return ms;
 }
 

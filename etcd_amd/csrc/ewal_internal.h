@@ -67,6 +67,26 @@ struct ReadAllAgg {
   unsigned long long first_meta;  // min ordinal of a non-empty metadata frame
 };
 
+// Batched ReadAll over concatenated shards (ewal_readall_batch_device): the
+// per-shard reductions of k_check<true>, frame ordinals in the batch.
+struct ShardAgg {
+  unsigned long long first_fail;  // min frame with st != 0 (~0: none)
+  long long last_entry;           // max entry frame (-1)
+  long long last_state;           // max state frame (-1)
+  unsigned long long first_meta;  // min non-empty metadata frame (~0)
+  unsigned long long ent_first;   // global op index of the shard's first entry op (~0)
+  uint32_t lastop;                // 1 + the shard's last entry-op frame (0: none)
+  uint32_t pad;
+};
+
+struct SegArgs {
+  const uint32_t *fs;      // first frame of every shard [ns + 1], fs[ns] = n
+  uint32_t ns;
+  const uint64_t *ri;      // w.ri of every shard [ns]
+  const uint64_t *soff;    // byte offset of every shard in the batch [ns + 1]
+  ShardAgg *sagg;          // [ns]
+};
+
 // Snapshot verify per-file descriptor.
 struct SnapDesc {
   uint64_t off, len;       // file within the packed buffer
@@ -95,6 +115,8 @@ struct Small {
   uint32_t nslow;                 // frames k_decode left to k_decode_slow (non-canonical encodings)
   uint32_t lastop;                // k_check: 1 + the last entry op's frame (0: none)
   uint32_t gapslow;               // k_check: an op's predecessor lies too far back (list-based k_gap)
+  uint32_t segbad;                // k_shard_start: a shard does not start on a frame of the chain
+  uint32_t pad_s;
 };
 
 // Everything the host needs after the frame pass, gathered by k_result.

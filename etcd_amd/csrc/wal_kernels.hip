@@ -1380,10 +1380,17 @@ __device__ __forceinline__ uint32_t lookback_count(unsigned long long *status, u
                        __HIP_MEMORY_SCOPE_AGENT);
   return acc;
 }
+// SEG (ewal_readall_batch_device): the frames are the concatenation of many
+// independent WALs (shards); frame r belongs to the last shard s with
+// fs[s] <= r, every rule restarts at the shard's first frame (the running CRC
+// at 0, the op list empty, ri = sg.ri[s]) and the reductions go to
+// sg.sagg[s].  ents[j] keeps the global op order (a shard's ops are
+// contiguous), with Data offsets relative to the shard.
+template <bool SEG>
 __global__ __launch_bounds__(1024) void k_check(const uint32_t *__restrict__ g_shift, RecDesc *__restrict__ rd,
                          uint32_t n, const uint32_t *__restrict__ pfd, const uint32_t *__restrict__ pfo, uint64_t ri,
                          unsigned long long *__restrict__ status, uint32_t epoch, uint32_t *__restrict__ wbase,
-                         ewal_entry *__restrict__ ents, uint32_t *__restrict__ mlist, Small *ds) {
+                         ewal_entry *__restrict__ ents, uint32_t *__restrict__ mlist, Small *ds, SegArgs sg) {
   ReadAllAgg *agg = &ds->agg;
   __shared__ uint32_t s_wo[16];          // ops per wave
   __shared__ uint32_t s_base;            // ops before the workgroup
@@ -1400,7 +1407,18 @@ __global__ __launch_bounds__(1024) void k_check(const uint32_t *__restrict__ g_s
   const uint32_t r = live ? rt : n - 1;   // the whole block reaches the barrier below; writes masked
   // every load up front: the frame, its neighbours' CRC / offset, the prefixes
   const RecDesc d = rd[r];
-  const uint32_t seed = r ? rd[r - 1].crc : 0u;
+  uint32_t sh = 0, lo = 0;                // the frame's shard and its first frame
+  if (SEG) {
+    uint32_t a = 0, b = sg.ns;            // last s with fs[s] <= r (fs[0] == 0)
+    while (b - a > 1) {
+      const uint32_t m = (a + b) >> 1;
+      if (sg.fs[m] <= r) a = m; else b = m;
+    }
+    sh = a;
+    lo = sg.fs[a];
+    ri = sg.ri[a];
+  }
+  const uint32_t seed = r > lo ? rd[r - 1].crc : 0u;
   const uint64_t noff = r + 1 < n ? rd[r + 1].off : ~0ull;
   const uint32_t ps = pfd[r];
   const uint32_t pn = r + 1 < n ? pfo[r + 1] : 0u;
@@ -1451,25 +1469,31 @@ __global__ __launch_bounds__(1024) void k_check(const uint32_t *__restrict__ g_s
   // by reading back at most EW_GAP_BACK earlier frames; farther -> the host's
   // list-based gap pass (ds->gapslow).
   const int lane = threadIdx.x & 63;
+  const uint32_t r0 = blockIdx.x * blockDim.x + (threadIdx.x & ~63u);   // the wave's first frame
   const bool op = live && d.type == 2 && d.f1 >= ri;
   const unsigned long long mo = __ballot(op);
   const unsigned long long below = mo & ((1ull << lane) - 1ull);
-  const uint64_t fprev = __shfl(d.f1, below ? 63 - __clzll((long long)below) : lane);   // every lane takes part
+  unsigned long long bsh = below;         // ops below in the same shard
+  if (SEG && lo > r0) bsh = (lo - r0 >= 64) ? 0ull : below & ~((1ull << (lo - r0)) - 1ull);
+  const uint64_t fprev = __shfl(d.f1, bsh ? 63 - __clzll((long long)bsh) : lane);   // every lane takes part
   if (op) {
     const uint64_t k = d.f1 - ri;
-    bool has = below != 0;
+    bool has = bsh != 0;
     uint64_t kp = fprev - ri;
+    uint32_t s2 = r0;           // the frames before the wave, back to the shard's first
     if (!has) {
-      uint32_t s2 = r - lane;   // the frames before the wave
-      for (int back = 0; back < EW_GAP_BACK && s2 > 0; ++back) {
+      // SEG: a shard's first op usually follows its replayed-past entries
+      // (Index < ri), so look back further before giving up (rare lanes)
+      const int nback = SEG ? (1 << 16) : EW_GAP_BACK;
+      for (int back = 0; back < nback && s2 > lo; ++back) {
         --s2;
         const int64_t t2 = rd[s2].type;
         const uint64_t i2 = rd[s2].f1;
         if (t2 == 2 && i2 >= ri) { kp = i2 - ri; has = true; break; }
       }
-      if (!has && s2 > 0) atomicOr(&ds->gapslow, 1u);   // unresolved: k_gap decides
+      if (!has && s2 > lo) atomicOr(&ds->gapslow, 1u);   // unresolved: k_gap decides
     }
-    if (has || (r - lane) <= EW_GAP_BACK) {
+    if (has || s2 <= lo) {
       if (has && k <= kp) atomicOr(&ds->nonmono, 1u);
       const bool gap = has ? (k > kp && k - kp > 1) : (k > 0);
       if (st == 0 && gap) st = EWAL_PANIC_INDEX_GAP;
@@ -1485,7 +1509,26 @@ __global__ __launch_bounds__(1024) void k_check(const uint32_t *__restrict__ g_s
   // so a wave's max is its highest set lane and its min its lowest.
   const unsigned long long me = __ballot(live && d.type == 2), ms = __ballot(live && d.type == 3),
                            mm = __ballot(live && d.type == 1 && d.dlen > 0), mf = __ballot(live && st != 0);
-  const uint32_t r0 = r - lane;
+  if (SEG) {   // per-shard reductions: one atomic per wave and quantity when the wave lies in one shard
+    const uint32_t s0 = __shfl(sh, 0);
+    ShardAgg *A = sg.sagg + s0;
+    if (__ballot(live && sh != s0) == 0) {
+      if (lane == 0) {
+        if (mf) atomicMin(&A->first_fail, (unsigned long long)(r0 + (uint32_t)(__ffsll((long long)mf) - 1)));
+        if (me) atomicMax(&A->last_entry, (long long)(r0 + (uint32_t)(63 - __clzll((long long)me))));
+        if (ms) atomicMax(&A->last_state, (long long)(r0 + (uint32_t)(63 - __clzll((long long)ms))));
+        if (mm) atomicMin(&A->first_meta, (unsigned long long)(r0 + (uint32_t)(__ffsll((long long)mm) - 1)));
+        if (mo) atomicMax(&A->lastop, r0 + (uint32_t)(63 - __clzll((long long)mo)) + 1u);
+      }
+    } else if (live) {   // a shard boundary inside the wave (rare): lane by lane
+      A = sg.sagg + sh;
+      if (st != 0) atomicMin(&A->first_fail, (unsigned long long)r);
+      if (d.type == 2) atomicMax(&A->last_entry, (long long)r);
+      if (d.type == 3) atomicMax(&A->last_state, (long long)r);
+      if (d.type == 1 && d.dlen > 0) atomicMin(&A->first_meta, (unsigned long long)r);
+      if (op) atomicMax(&A->lastop, r + 1u);
+    }
+  }
   if (lane == 0) {
     if (mf) atomicMin(&s_red[3], r0 + (uint32_t)(__ffsll((long long)mf) - 1));
     if (me) atomicMax(&s_red[0], r0 + (uint32_t)(63 - __clzll((long long)me)) + 1u);
@@ -1521,11 +1564,12 @@ __global__ __launch_bounds__(1024) void k_check(const uint32_t *__restrict__ g_s
     ewal_entry e;
     e.term = d.f0;
     e.index = d.f1;
-    e.data_off = d.edoff;
+    e.data_off = SEG ? d.edoff - sg.soff[sh] : d.edoff;
     e.data_len = d.edlen;
     e.type = d.etype;
     e.data_nil = d.enil;
     ents[j] = e;
+    if (SEG && bsh == 0) atomicMin(&sg.sagg[sh].ent_first, (unsigned long long)j);   // the shard's first op in the wave
   }
 }
 
@@ -1626,6 +1670,127 @@ __global__ __launch_bounds__(256) void k_result(const uint8_t *__restrict__ buf,
   if (n) o->last = rd[n - 1];
   if (g.first_meta != ~0ull) o->md = rd[g.first_meta];
   if (g.last_state >= 0) o->sd = rd[g.last_state];
+}
+
+// ---- batched ReadAll over concatenated shards (ewal_readall_batch_device) --
+// Every shard is an independent WAL byte stream (one raft group's
+// names[nameIndex:], wal/wal.go:126-134) and the batch is their
+// concatenation, so the frame chain of the batch runs through every shard
+// when each one ends on a frame boundary -- which k_shard_start confirms
+// (otherwise the host verifies the shards one by one).
+
+__device__ __forceinline__ uint32_t shard_of(const uint32_t *__restrict__ fs, uint32_t ns, uint32_t r) {
+  uint32_t a = 0, b = ns;   // last s with fs[s] <= r
+  while (b - a > 1) {
+    const uint32_t m = (a + b) >> 1;
+    if (fs[m] <= r) a = m; else b = m;
+  }
+  return a;
+}
+
+// fs[s] = first frame at or after the shard's first byte; a non-empty shard
+// must start exactly on a frame.  Also initialises the per-shard reductions.
+__global__ void k_shard_start(const RecDesc *__restrict__ rd, uint32_t n, const uint64_t *__restrict__ soff,
+                              uint32_t ns, uint32_t *__restrict__ fs, ShardAgg *__restrict__ sagg, Small *ds) {
+  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s > ns) return;
+  if (s == ns) {
+    fs[ns] = n;
+    return;
+  }
+  const uint64_t o = soff[s];
+  uint32_t a = 0, b = n;
+  while (a < b) {
+    const uint32_t m = (a + b) >> 1;
+    if (rd[m].off < o) a = m + 1; else b = m;
+  }
+  fs[s] = a;
+  if (soff[s + 1] > o && (a >= n || rd[a].off != o)) atomicOr(&ds->segbad, 1u);
+  ShardAgg g;
+  g.first_fail = ~0ull;
+  g.last_entry = -1;
+  g.last_state = -1;
+  g.first_meta = ~0ull;
+  g.ent_first = ~0ull;
+  g.lastop = 0;
+  g.pad = 0;
+  sagg[s] = g;
+}
+
+// ReadAll's metadata rule per shard (wal/wal.go:178-183), over the metadata
+// frames k_check<true> listed.
+__global__ void k_meta_batch(const uint8_t *__restrict__ buf, RecDesc *__restrict__ rd,
+                             const uint32_t *__restrict__ mlist, const Small *ds, SegArgs sg) {
+  const uint32_t nm = ds->nmeta;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nm; i += gridDim.x * blockDim.x) {
+    const uint32_t r = mlist[i];
+    const uint32_t s = shard_of(sg.fs, sg.ns, r);
+    const unsigned long long fm = sg.sagg[s].first_meta;
+    if (fm == ~0ull || r <= fm) continue;
+    RecDesc &d = rd[r];
+    const RecDesc &m = rd[fm];
+    bool eq = (d.dlen == m.dlen);
+    for (uint64_t k = 0; eq && k < d.dlen; ++k) eq = buf[d.doff + k] == buf[m.doff + k];
+    if (!eq) {
+      d.st = EWAL_ERR_METADATA_CONFLICT;
+      atomicMin(&sg.sagg[s].first_fail, (unsigned long long)r);
+    }
+  }
+}
+
+// One thread per shard: its ReadAll result (the same assembly as the host's
+// for one WAL, ewal_api.hip readall_impl), ordinals and offsets relative to
+// the shard.  Every shard ends on a frame boundary here (k_shard_start), so
+// its terminal is a clean io.EOF.
+__global__ void k_result_batch(const RecDesc *__restrict__ rd, SegArgs sg, ewal_result *__restrict__ out,
+                               unsigned long long *__restrict__ ent_first) {
+  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= sg.ns) return;
+  const ShardAgg A = sg.sagg[s];
+  const uint32_t f0 = sg.fs[s], f1 = sg.fs[s + 1];
+  const uint64_t so = sg.soff[s], ri = sg.ri[s];
+  ewal_result o;
+  memset(&o, 0, sizeof(o));
+  o.fail_record = -1;
+  o.fail_offset = -1;
+  o.metadata_off = -1;
+  o.n_records = (int64_t)(f1 - f0);
+  o.n_candidates = (int64_t)(f1 - f0);
+  o.n_runs = 1;
+  unsigned long long ef = 0;
+  if (A.first_fail != ~0ull) {
+    const RecDesc &f = rd[A.first_fail];
+    o.status = f.st;
+    o.fail_record = (int64_t)(A.first_fail - f0);
+    o.fail_offset = (int64_t)(f.off - so);
+    o.n_records = o.fail_record;
+    if (f.st == EWAL_ERR_UNEXPECTED_TYPE) o.detail = f.type;
+    if (f.st == EWAL_PANIC_INDEX_GAP) o.detail = (int64_t)f.f1;
+  } else {
+    const uint64_t enti = A.last_entry >= 0 ? rd[A.last_entry].f1 : 0;
+    o.enti = enti;
+    if (enti < ri) {
+      o.status = EWAL_ERR_INDEX_NOT_FOUND;
+    } else if (f1 > f0) {
+      o.last_crc = rd[f1 - 1].chained;
+      if (A.first_meta != ~0ull) {
+        o.metadata_off = (int64_t)(rd[A.first_meta].doff - so);
+        o.metadata_len = (int64_t)rd[A.first_meta].dlen;
+      }
+      if (A.last_state >= 0) {
+        const RecDesc &sd = rd[A.last_state];
+        o.has_state = 1;
+        o.state_term = sd.f0;
+        o.state_vote = sd.f1;
+        o.state_commit = sd.f2;
+      }
+      // ops strictly increasing and gap-free here (else the host falls back)
+      o.n_ents = A.lastop ? (int64_t)(rd[A.lastop - 1].f1 - ri + 1) : 0;
+      ef = o.n_ents ? A.ent_first : 0;
+    }
+  }
+  out[s] = o;
+  ent_first[s] = ef;
 }
 
 // survivors: op j is ents[k_j] iff every later op has k > k_j

@@ -72,6 +72,10 @@ class Context:
         except Exception:
             pass
 
+    def set_stream(self, hip_stream):
+        """Run this ctx's work on a caller-owned hipStream_t (e.g. torch's)."""
+        check(lib.ewal_ctx_set_stream(self._p, C.c_void_p(hip_stream)))
+
     def alloc(self, n):
         d = C.c_void_p()
         check(lib.ewal_device_alloc(self._p, n, C.byref(d)))
@@ -131,6 +135,7 @@ class ReadAllResult:
     device_ms: float = 0.0
     stream_ms: float = 0.0
     n_slow: int = 0           # frames decoded by the general (non-canonical) walker
+    flags: int = 0            # FLAG_SHARD_FALLBACK: a batched shard verified on its own
 
     def as_dict(self):
         return dict(status=self.status, detail=self.detail, fail_record=self.fail_record,
@@ -140,7 +145,7 @@ class ReadAllResult:
                     ents=[dict(type=e.Type, term=e.Term, index=e.Index, data=e.Data) for e in self.ents])
 
 
-def _collect(ctx, r, buf_view, with_ents=True):
+def _collect(ctx, r, buf_view, with_ents=True, shard=None):
     ok = r.status == L.OK
     md = None
     if ok and r.metadata_off >= 0:
@@ -149,13 +154,17 @@ def _collect(ctx, r, buf_view, with_ents=True):
     ents = []
     if ok and with_ents and r.n_ents:
         arr = (L.EntryDesc * r.n_ents)()
-        n = lib.ewal_copy_entries(ctx.handle, arr, r.n_ents)
+        if shard is None:
+            n = lib.ewal_copy_entries(ctx.handle, arr, r.n_ents)
+        else:
+            n = lib.ewal_batch_copy_entries(ctx.handle, shard, arr, r.n_ents)
         check(0 if n >= 0 else int(n))
         for e in arr[:n]:
             data = None if e.data_nil else bytes(buf_view[e.data_off:e.data_off + e.data_len])
             ents.append(Entry(e.type, e.term, e.index, data))
     return ReadAllResult(r.status, r.detail, r.fail_record, r.fail_offset, r.n_records, r.last_crc if ok else 0,
-                         r.enti, md, st, ents, r.n_candidates, r.n_runs, r.device_ms, r.stream_ms, r.n_slow)
+                         r.enti, md, st, ents, r.n_candidates, r.n_runs, r.device_ms, r.stream_ms, r.n_slow,
+                         r.flags)
 
 
 def readall_bytes(buf: bytes, ri: int = 0, ctx: Context = None, with_ents=True) -> ReadAllResult:
@@ -176,6 +185,37 @@ def readall_device(dbuf: DeviceBuffer, n: int, ri: int = 0, host_view=None, with
     if rc < 0:
         check(rc)
     return _collect(dbuf.ctx, r, host_view if host_view is not None else b"", with_ents and host_view is not None)
+
+
+def readall_batch_device(dbuf: DeviceBuffer, lens, ris, host_views=None, with_ents=False) -> List[ReadAllResult]:
+    """ReadAll of every shard of a batch resident in HBM: shard s is the
+    lens[s] bytes after shards 0..s-1 (ewal_readall_batch_device); one
+    result per shard, as if each were replayed alone with w.ri = ris[s]."""
+    ns = len(lens)
+    out = (L.Result * max(ns, 1))()
+    rc = lib.ewal_readall_batch_device(dbuf.ctx.handle, dbuf.ptr, ns, (C.c_uint64 * max(ns, 1))(*lens),
+                                       (C.c_uint64 * max(ns, 1))(*ris), out)
+    if rc < 0:
+        check(rc)
+    res = []
+    for s in range(ns):
+        hv = host_views[s] if host_views is not None else b""
+        res.append(_collect(dbuf.ctx, out[s], hv, with_ents and host_views is not None, shard=s))
+    return res
+
+
+def readall_batch_bytes(shards, ris, ctx: Context = None, with_ents=True) -> List[ReadAllResult]:
+    """Batched ReadAll over host byte strings (concatenated, staged to HBM)."""
+    ctx = ctx or default_context()
+    blob = b"".join(bytes(x) for x in shards)
+    d = ctx.alloc(len(blob) + 64)
+    try:
+        if blob:
+            d.upload(blob)
+        return readall_batch_device(d, [len(x) for x in shards], ris, [memoryview(bytes(x)) for x in shards],
+                                    with_ents)
+    finally:
+        d.free()
 
 
 def records(ctx: Context, n: int):
@@ -344,3 +384,27 @@ def synth_wal(target_bytes, min_data=64, max_data=65536, seed=2, corrupt_record=
         check(int(n))
     del out[n:]
     return out, nrec.value
+
+
+def synth_shards(seeds, target_bytes, min_data, max_data, corrupt=None):
+    """Per-raft-group WAL shards laid end to end (bench/test input for the
+    batched ReadAll): shard i = synth_wal(target_bytes, seed=seeds[i]),
+    corrupt = {shard index: record ordinal}.  Returns (bytearray, lens,
+    n_records)."""
+    corrupt = corrupt or {}
+    per = target_bytes + max_data * 2 + (1 << 20)
+    out = bytearray(per * len(seeds))
+    base = C.addressof((C.c_char * len(out)).from_buffer(out))
+    lens, nrec, pos = [], [], 0
+    for i, sd in enumerate(seeds):
+        nr = C.c_int64(0)
+        n = lib.ewal_synth_wal(sd, target_bytes, min_data, max_data, corrupt.get(i, -1), C.c_void_p(base + pos),
+                               per, C.byref(nr))
+        if n < 0:
+            check(int(n))
+        lens.append(n)
+        nrec.append(nr.value)
+        pos += n
+    del out[pos:]
+    return out, lens, nrec
+

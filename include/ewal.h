@@ -114,6 +114,8 @@ int ewal_ctx_set_stream(ewal_ctx *ctx, void *hip_stream);
 const char *ewal_status_string(int status);
 /* Device time (ms) of the last pipeline call on this ctx (HIP events). */
 float ewal_last_device_ms(ewal_ctx *ctx);
+/* Device time (ms) of the last call's k_stream HBM pass (HIP events). */
+float ewal_last_stream_ms(ewal_ctx *ctx);
 int ewal_device_count(void);
 
 /* ---- WAL replay/verify -------------------------------------------------- */
@@ -121,6 +123,23 @@ int ewal_device_count(void);
  * names[nameIndex:] (wal/wal.go:126-134, MultiReadCloser semantics), with
  * w.ri = ri.  d_buf is DEVICE memory, 16-byte aligned, len bytes. */
 int ewal_readall_device(ewal_ctx *ctx, const void *d_buf, uint64_t len, uint64_t ri, ewal_result *out);
+/* Batched ReadAll over n_shards independent WALs (one raft group's
+ * names[nameIndex:] each) laid end to end in ONE device
+ * buffer: shard s is the lens[s] bytes after shards 0..s-1; out[s] is exactly
+ * ewal_readall_device's result for that shard alone with w.ri = ri[s]
+ * (ordinals and offsets relative to the shard; device_ms / stream_ms are the
+ * whole batch's).  One stream pass, one frame pass and one segmented check
+ * cover the batch; shards that do not end on a frame boundary (torn or
+ * corrupt framing) or need the rare op-list paths send the batch through the
+ * one-by-one path (flags |= EWAL_FLAG_SHARD_FALLBACK).  Returns 0 or a
+ * negative infrastructure error; per-shard verdicts are in out[].  Replaces,
+ * per shard, wal.OpenAtIndex(...).ReadAll() (wal/wal.go:108,164). */
+#define EWAL_FLAG_SHARD_FALLBACK 1
+int ewal_readall_batch_device(ewal_ctx *ctx, const void *d_buf, uint64_t n_shards, const uint64_t *lens,
+                              const uint64_t *ri, ewal_result *out);
+/* After ewal_readall_batch_device: shard s's ents (Data offsets relative to
+ * the shard).  Returns the number copied (<= cap) or a negative error. */
+int64_t ewal_batch_copy_entries(ewal_ctx *ctx, uint64_t shard, ewal_entry *out, int64_t cap);
 /* Copy host bytes into ctx-owned device memory (16-B aligned; valid until
  * the next staging call on this ctx). */
 int ewal_stage_to_device(ewal_ctx *ctx, const void *h_buf, uint64_t len, void **d_out);

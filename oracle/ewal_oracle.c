@@ -556,3 +556,24 @@ int or_maybe_commit(const uint64_t *match, int n, uint64_t term, uint64_t *commi
   if (t == term) { *committed = mci; return 1; }
   return 0;
 }
+
+/* The same rule over G groups in the GPU API's SoA layout (match[v*G + g],
+ * log terms CSR) -- the CPU baseline of configs[4]; one call, no per-group
+ * FFI cost.  status[g] = 0 or OR_PANIC_BOUNDS. */
+void or_maybe_commit_batch(uint64_t G, const uint64_t *match, const uint8_t *nvoters, const uint64_t *term,
+                           uint64_t *committed, const uint64_t *log_offset, const uint64_t *log_ptr,
+                           const uint64_t *log_terms, uint8_t *changed, uint8_t *status) {
+  for (uint64_t g = 0; g < G; g++) {
+    uint64_t m[16];
+    int n = nvoters[g];
+    changed[g] = 0;
+    status[g] = 0;
+    if (n <= 0 || n > 16) { status[g] = OR_PANIC_BOUNDS; continue; }
+    for (int v = 0; v < n; v++) m[v] = match[(uint64_t)v * G + g];
+    int rc = or_maybe_commit(m, n, term[g], &committed[g], log_terms + log_ptr[g], log_ptr[g + 1] - log_ptr[g],
+                             log_offset[g]);
+    if (rc < 0) status[g] = (uint8_t)(-rc);
+    else changed[g] = (uint8_t)rc;
+  }
+}
+

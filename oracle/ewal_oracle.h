@@ -185,6 +185,9 @@ void or_loadsnap_free(or_loadsnap_result *r);
  * reference's index-out-of-range panic (n_log==0 && offset==0). */
 int or_maybe_commit(const uint64_t *match, int n, uint64_t term, uint64_t *committed,
                     const uint64_t *log_terms, uint64_t n_log, uint64_t offset);
+void or_maybe_commit_batch(uint64_t G, const uint64_t *match, const uint8_t *nvoters, const uint64_t *term,
+                           uint64_t *committed, const uint64_t *log_offset, const uint64_t *log_ptr,
+                           const uint64_t *log_terms, uint8_t *changed, uint8_t *status);
 
 #ifdef __cplusplus
 }

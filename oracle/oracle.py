@@ -270,3 +270,15 @@ def maybe_commit(matches, term, committed, log_terms, offset=0):
     c = C.c_uint64(committed)
     rc = lib.or_maybe_commit(m, len(matches), term, C.byref(c), lt, len(log_terms), offset)
     return rc, c.value
+
+
+lib.or_maybe_commit_batch.restype = None
+lib.or_maybe_commit_batch.argtypes = [C.c_uint64] + [C.c_void_p] * 9
+
+
+def maybe_commit_batch(G, match, nvoters, term, committed, log_offset, log_ptr, log_terms, changed, status):
+    """or_maybe_commit_batch over numpy arrays (committed/changed/status written in place)."""
+    ptr = lambda a: C.c_void_p(a.ctypes.data)   # noqa: E731
+    lib.or_maybe_commit_batch(G, ptr(match), ptr(nvoters), ptr(term), ptr(committed), ptr(log_offset), ptr(log_ptr),
+                              ptr(log_terms), ptr(changed), ptr(status))
+

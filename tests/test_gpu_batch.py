@@ -1,0 +1,164 @@
+"""GPU parity of the batched multi-shard ReadAll (ewal_readall_batch_device,
+SURVEY.md §8(d) C3: thousands of per-raft-group WALs replayed together).
+
+Every shard's batched result must equal the oracle's ReadAll of that shard
+alone (status, failing frame and offset, lastCRC, enti, metadata, HardState,
+ents), whichever path the batch took: the segmented fast path (one stream
+pass for the whole batch) or the one-by-one fallback for batches whose
+shards do not all end on a frame boundary or need the op-list paths."""
+import random
+import struct
+
+import pytest
+
+from oracle import oracle as O
+from etcd_amd import _lib as L
+from etcd_amd import wal as W
+from test_gpu_parity import build_wal
+
+pytestmark = pytest.mark.gpu
+
+
+def check_batch(ctx, shards, ris, expect_fast=None):
+    res = W.readall_batch_bytes(shards, ris, ctx)
+    assert len(res) == len(shards)
+    for s, (buf, ri, g) in enumerate(zip(shards, ris, res)):
+        o = O.readall(bytes(buf), ri)
+        gd = g.as_dict()
+        assert gd["status"] == o["status"], (s, gd["status"], o["status"], gd["fail_record"], o["fail_record"])
+        if o["status"] == O.OK:
+            for k in ("n_records", "last_crc", "enti", "metadata", "state"):
+                assert gd[k] == o[k], (s, k, gd[k], o[k])
+            assert gd["ents"] == o["ents"], s
+        elif o["status"] == O.ERR_INDEX_NOT_FOUND:
+            assert gd["enti"] == o["enti"], s
+        else:
+            assert (gd["fail_record"], gd["fail_offset"]) == (o["fail_record"], o["fail_offset"]), s
+            if o["status"] == O.ERR_UNEXPECTED_TYPE:
+                assert gd["detail"] == o["detail"]
+    if expect_fast is not None:
+        fb = [bool(g.flags & L.FLAG_SHARD_FALLBACK) for g in res]
+        assert not any(fb) if expect_fast else all(fb), fb
+    return res
+
+
+def _variety(rng):
+    """Shards covering ReadAll's outcomes, each framed cleanly (fast path)."""
+    out = []
+    for i in range(24):
+        w = build_wal(rng, rng.randrange(1, 120), rng.choice([50, 2000, 20000]), cuts=rng.randrange(0, 3))
+        kind = i % 6
+        ri = 0
+        if kind == 1:     # payload byte flip -> walpb.ErrCRCMismatch
+            w = bytearray(w)
+            w[-1] ^= 0x40     # the last entry's Data (Entry bytes): its Record CRC breaks
+            w = bytes(w)
+        elif kind == 2:   # ri past the last entry -> ErrIndexNotFound
+            ri = 10 ** 6
+        elif kind == 3:   # a later ri
+            ri = rng.randrange(0, 5)
+        out.append((w, ri))
+    # metadata conflict, crc seam mismatch, unexpected type, gap, empty shard
+    e = O.WalEncoder(0)
+    e.save_crc(0)
+    e.encode(1, b"m1")
+    e.save_entry(0, 1, 0, b"x")
+    e.encode(1, b"m2")
+    out.append((e.getvalue(), 0))
+    a = O.WalEncoder(0)
+    a.save_crc(0)
+    a.encode(1, b"m")
+    a.save_entry(0, 1, 0, b"abc")
+    b = O.WalEncoder(a.crc ^ 1)
+    b.save_crc(0)
+    b.encode(1, b"m")
+    out.append((a.getvalue() + b.getvalue(), 0))
+    e = O.WalEncoder(0)
+    e.save_crc(0)
+    e.encode(1, b"m")
+    e.encode(9, b"payload")
+    out.append((e.getvalue(), 0))
+    e = O.WalEncoder(0)
+    e.save_crc(0)
+    e.encode(1, b"m")
+    e.save_entry(0, 1, 0, b"a")
+    e.save_entry(0, 1, 2, b"b")
+    out.append((e.getvalue(), 0))
+    out.append((b"", 0))
+    out.append((b"", 1))
+    rng.shuffle(out)
+    return out
+
+
+def test_batch_fast_path_outcomes(ctx):
+    rng = random.Random(7)
+    sh = _variety(rng)
+    check_batch(ctx, [w for w, _ in sh], [ri for _, ri in sh], expect_fast=True)
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_batch_random(ctx, seed):
+    rng = random.Random(300 + seed)
+    shards, ris = [], []
+    for _ in range(rng.randrange(1, 40)):
+        shards.append(build_wal(rng, rng.randrange(0, 80), rng.choice([100, 3000]), cuts=rng.randrange(0, 3)))
+        ris.append(rng.choice([0, 0, 0, 3, 50]))
+    check_batch(ctx, shards, ris, expect_fast=True)
+
+
+def test_batch_fallback_torn_and_rewind(ctx):
+    rng = random.Random(11)
+    base = [build_wal(rng, 30, 500) for _ in range(6)]
+    # a torn shard in the middle: its chain runs into the next shard
+    torn = list(base)
+    torn[2] = torn[2][:-5]
+    check_batch(ctx, torn, [0] * 6, expect_fast=False)
+    # a trailing bare length prefix (io.EOF) and a negative length
+    t2 = list(base)
+    t2[1] = t2[1] + struct.pack("<q", 77)
+    t2[4] = t2[4] + struct.pack("<q", -5) + b"zz"
+    check_batch(ctx, t2, [0] * 6, expect_fast=False)
+    # an index rewind (leader overwrite) needs the op-list path
+    e = O.WalEncoder(0)
+    e.save_crc(0)
+    e.encode(1, b"m")
+    for i in (0, 1, 2, 3, 4, 2, 3, 1, 2, 3):
+        e.save_entry(0, i, i, bytes([i]) * i)
+    rw = list(base)
+    rw[3] = e.getvalue()
+    check_batch(ctx, rw, [0, 0, 0, 2, 0, 0], expect_fast=False)
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_batch_random_corruption(ctx, seed):
+    rng = random.Random(900 + seed)
+    shards = [bytearray(build_wal(rng, rng.randrange(5, 60), 2000)) for _ in range(rng.randrange(2, 12))]
+    for _ in range(rng.randrange(1, 3)):
+        w = shards[rng.randrange(len(shards))]
+        if w:
+            w[rng.randrange(len(w))] ^= 1 << rng.randrange(8)
+    res = W.readall_batch_bytes([bytes(x) for x in shards], [0] * len(shards), ctx)
+    for buf, g in zip(shards, res):
+        o = O.readall(bytes(buf), 0)
+        if g.status == L.UNSUPPORTED_ENCODING:   # as in the single-WAL corruption tests
+            assert o["status"] == O.OK or o["fail_record"] >= g.fail_record or o["fail_record"] < 0
+            continue
+        assert g.status == o["status"]
+        if o["status"] not in (O.OK, O.ERR_INDEX_NOT_FOUND):
+            assert g.fail_record == o["fail_record"]
+
+
+def test_batch_synthetic_shards(ctx):
+    """C3-shaped shards (128 B - 4 KiB entries), one corrupt record."""
+    shards, want, n_bad = [], [], 777
+    for s in range(8):
+        buf, n = W.synth_wal(3 << 20, 128, 4096, seed=10 + s, corrupt_record=n_bad if s == 5 else -1)
+        shards.append(bytes(buf))
+        want.append(n)
+    res = check_batch(ctx, shards, [1] * 8, expect_fast=True)
+    assert res[5].status == L.ERR_RECORD_CRC and res[5].fail_record == n_bad
+    assert all(r.status == L.OK and r.n_records == n for i, (r, n) in enumerate(zip(res, want)) if i != 5)
+    # the same batch through the single-WAL path, shard by shard
+    for buf, r in zip(shards, res):
+        g = W.readall_bytes(buf, 1, ctx, with_ents=False)
+        assert (g.status, g.fail_record, g.last_crc, g.enti) == (r.status, r.fail_record, r.last_crc, r.enti)

@@ -137,3 +137,56 @@ def test_compute_fails_loudly_without_gpu():
         pytest.skip("a GPU is present")
     p = C.c_void_p()
     assert L.lib.ewal_ctx_create(0, C.byref(p)) == L.E_NODEVICE
+
+
+def test_snapshot_writer_matches_oracle():
+    """etcd_amd.snap (Snapshotter.save, snap/snapshotter.go:46-60) byte-identical to the oracle's marshal."""
+    from etcd_amd import snap as S
+    rng = random.Random(3)
+    for n in (0, 1, 127, 128, 5000):
+        data = bytes(rng.getrandbits(8) for _ in range(n))
+        nodes = [rng.randrange(1, 1 << 40) for _ in range(rng.randrange(0, 4))]
+        index, term = rng.randrange(1 << 30), rng.randrange(1 << 20)
+        body = S.snapshot_marshal(data, nodes, index, term, (7,))
+        assert body == O.snapshot_marshal(data, nodes, index, term, (7,))
+        f = S.snap_file(body)
+        assert f == O.snappb_marshal(O.crc32_update(0, body), body)
+        assert O.loadsnap(f)["status"] == O.OK
+
+
+def test_commit_batch_oracle_matches_per_group():
+    """The CPU baseline's batched maybeCommit equals the per-group restatement (raft/raft.go:248-258)."""
+    import numpy as np
+    rng = np.random.default_rng(1)
+    G = 2000
+    nv = rng.choice(np.array([0, 1, 2, 3, 5, 7, 16], dtype=np.uint8), size=G)
+    match = rng.integers(0, 30, size=(16, G), dtype=np.uint64)
+    term = rng.integers(1, 4, size=G, dtype=np.uint64)
+    c0 = rng.integers(0, 20, size=G, dtype=np.uint64)
+    off = rng.integers(0, 10, size=G, dtype=np.uint64)
+    lens = rng.integers(0, 20, size=G)
+    ptr = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
+    lt = np.sort(rng.integers(1, 4, size=int(ptr[-1]), dtype=np.uint64))
+    c = c0.copy()
+    ch, st = np.zeros(G, np.uint8), np.zeros(G, np.uint8)
+    O.maybe_commit_batch(G, match.reshape(-1), nv, term, c, off, ptr, lt, ch, st)
+    for g in range(G):
+        rc, want = O.maybe_commit([int(match[v, g]) for v in range(nv[g])], int(term[g]), int(c0[g]),
+                                  [int(x) for x in lt[ptr[g]:ptr[g + 1]]], int(off[g]))
+        if rc < 0:
+            assert st[g] == -rc
+        else:
+            assert (st[g], ch[g], c[g]) == (0, rc, want), g
+
+
+def test_synth_shards_layout():
+    blob, lens, nrec = W.synth_shards([5, 6, 7], 1 << 16, 128, 4096, corrupt={1: 3})
+    assert len(blob) == sum(lens)
+    pos = 0
+    for i, (n, k) in enumerate(zip(lens, nrec)):
+        shard = bytes(blob[pos:pos + n])
+        one, kk = W.synth_wal(1 << 16, 128, 4096, seed=5 + i, corrupt_record=3 if i == 1 else -1)
+        assert shard == bytes(one) and k == kk
+        o = O.readall(shard, 1)
+        assert o["status"] == (O.ERR_RECORD_CRC if i == 1 else O.OK)
+        pos += n
