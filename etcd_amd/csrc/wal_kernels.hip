@@ -1380,6 +1380,18 @@ __device__ __forceinline__ uint32_t lookback_count(unsigned long long *status, u
                        __HIP_MEMORY_SCOPE_AGENT);
   return acc;
 }
+// last shard s in [a, b) with fs[s] <= r (fs ascending, fs[a] <= r)
+__device__ __forceinline__ uint32_t shard_in(const uint32_t *__restrict__ fs, uint32_t a, uint32_t b, uint32_t r) {
+  while (b - a > 1) {
+    const uint32_t m = (a + b) >> 1;
+    if (fs[m] <= r) a = m; else b = m;
+  }
+  return a;
+}
+__device__ __forceinline__ uint32_t shard_of(const uint32_t *__restrict__ fs, uint32_t ns, uint32_t r) {
+  return shard_in(fs, 0, ns, r);
+}
+
 // SEG (ewal_readall_batch_device): the frames are the concatenation of many
 // independent WALs (shards); frame r belongs to the last shard s with
 // fs[s] <= r, every rule restarts at the shard's first frame (the running CRC
@@ -1397,9 +1409,15 @@ __global__ __launch_bounds__(1024) void k_check(const uint32_t *__restrict__ g_s
   __shared__ uint32_t s_sh[17 * 1024];   // S_{2^0} .. S_{2^16}
   __shared__ uint32_t s_red[5];          // block: last entry + 1, last state + 1, first metadata, first failure,
                                          //        last op + 1
+  __shared__ uint32_t s_shr[2];          // SEG: shards of the workgroup's first and last frame
   stage_lds<1024>(s_sh, 17 * 1024, [&](int i) { return g_shift[i]; });
   if (threadIdx.x == 0) {
     s_red[0] = 0; s_red[1] = 0; s_red[2] = 0xffffffffu; s_red[3] = 0xffffffffu; s_red[4] = 0;
+    if (SEG) {
+      const uint32_t f0 = blockIdx.x * blockDim.x;
+      s_shr[0] = shard_of(sg.fs, sg.ns, f0);
+      s_shr[1] = shard_in(sg.fs, s_shr[0], sg.ns, min(f0 + blockDim.x, n) - 1);
+    }
   }
   __syncthreads();
   const uint32_t rt = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1408,15 +1426,10 @@ __global__ __launch_bounds__(1024) void k_check(const uint32_t *__restrict__ g_s
   // every load up front: the frame, its neighbours' CRC / offset, the prefixes
   const RecDesc d = rd[r];
   uint32_t sh = 0, lo = 0;                // the frame's shard and its first frame
-  if (SEG) {
-    uint32_t a = 0, b = sg.ns;            // last s with fs[s] <= r (fs[0] == 0)
-    while (b - a > 1) {
-      const uint32_t m = (a + b) >> 1;
-      if (sg.fs[m] <= r) a = m; else b = m;
-    }
-    sh = a;
-    lo = sg.fs[a];
-    ri = sg.ri[a];
+  if (SEG) {   // usually one shard per workgroup: no search at all
+    sh = s_shr[0] == s_shr[1] ? s_shr[0] : shard_in(sg.fs, s_shr[0], s_shr[1] + 1, r);
+    lo = sg.fs[sh];
+    ri = sg.ri[sh];
   }
   const uint32_t seed = r > lo ? rd[r - 1].crc : 0u;
   const uint64_t noff = r + 1 < n ? rd[r + 1].off : ~0ull;
@@ -1509,7 +1522,12 @@ __global__ __launch_bounds__(1024) void k_check(const uint32_t *__restrict__ g_s
   // so a wave's max is its highest set lane and its min its lowest.
   const unsigned long long me = __ballot(live && d.type == 2), ms = __ballot(live && d.type == 3),
                            mm = __ballot(live && d.type == 1 && d.dlen > 0), mf = __ballot(live && st != 0);
-  if (SEG) {   // per-shard reductions: one atomic per wave and quantity when the wave lies in one shard
+  // SEG: a workgroup inside one shard reduces through s_red like the single
+  // WAL (thread 0 then updates sg.sagg); one that straddles shard
+  // boundaries (rare) reduces per wave, or lane by lane where a boundary
+  // lies inside the wave
+  const bool wg1 = SEG && s_shr[0] == s_shr[1];
+  if (SEG && !wg1) {
     const uint32_t s0 = __shfl(sh, 0);
     ShardAgg *A = sg.sagg + s0;
     if (__ballot(live && sh != s0) == 0) {
@@ -1552,6 +1570,15 @@ __global__ __launch_bounds__(1024) void k_check(const uint32_t *__restrict__ g_s
       if (s_red[2] != 0xffffffffu) atomicMin(&agg->first_meta, (unsigned long long)s_red[2]);
       if (s_red[3] != 0xffffffffu) atomicMin(&agg->first_fail, (unsigned long long)s_red[3]);
       if (s_red[4]) atomicMax(&ds->lastop, s_red[4]);
+      if (wg1) {
+        ShardAgg *A = sg.sagg + s_shr[0];
+        if (s_red[0]) atomicMax(&A->last_entry, (long long)(s_red[0] - 1));
+        if (s_red[1]) atomicMax(&A->last_state, (long long)(s_red[1] - 1));
+        if (s_red[2] != 0xffffffffu) atomicMin(&A->first_meta, (unsigned long long)s_red[2]);
+        if (s_red[3] != 0xffffffffu) atomicMin(&A->first_fail, (unsigned long long)s_red[3]);
+        if (s_red[4]) atomicMax(&A->lastop, s_red[4]);
+        if (cnt) atomicMin(&A->ent_first, (unsigned long long)base);   // the workgroup's first op is op `base`
+      }
     }
   }
   __syncthreads();
@@ -1569,7 +1596,7 @@ __global__ __launch_bounds__(1024) void k_check(const uint32_t *__restrict__ g_s
     e.type = d.etype;
     e.data_nil = d.enil;
     ents[j] = e;
-    if (SEG && bsh == 0) atomicMin(&sg.sagg[sh].ent_first, (unsigned long long)j);   // the shard's first op in the wave
+    if (SEG && !wg1 && bsh == 0) atomicMin(&sg.sagg[sh].ent_first, (unsigned long long)j);   // the shard's first op in the wave
   }
 }
 
@@ -1678,15 +1705,6 @@ __global__ __launch_bounds__(256) void k_result(const uint8_t *__restrict__ buf,
 // concatenation, so the frame chain of the batch runs through every shard
 // when each one ends on a frame boundary -- which k_shard_start confirms
 // (otherwise the host verifies the shards one by one).
-
-__device__ __forceinline__ uint32_t shard_of(const uint32_t *__restrict__ fs, uint32_t ns, uint32_t r) {
-  uint32_t a = 0, b = ns;   // last s with fs[s] <= r
-  while (b - a > 1) {
-    const uint32_t m = (a + b) >> 1;
-    if (fs[m] <= r) a = m; else b = m;
-  }
-  return a;
-}
 
 // fs[s] = first frame at or after the shard's first byte; a non-empty shard
 // must start exactly on a frame.  Also initialises the per-shard reductions.
