@@ -66,6 +66,7 @@ struct ewal_ctx {
   int device = 0;
   int num_cu = 256;
   int ablate = 0;      // EWAL_STREAM_ABLATE (timing experiments only; results are wrong)
+  int frame_wg = 3;    // k_frame resident workgroups per CU (EWAL_FRAME_WG: A/B timing)
   hipStream_t stream = nullptr;
   bool own_stream = false;
   hipEvent_t ev0 = nullptr, ev1 = nullptr, evs0 = nullptr, evs1 = nullptr;
@@ -320,21 +321,40 @@ static int readall_impl(ewal_ctx *c, const uint8_t *d_buf, uint64_t B, uint64_t 
     EW_CHECK(c->exc.ensure(ccap));
     // descriptor capacity of the speculative frame pass: the previous call's
     // frame count with headroom, at least one frame per 4 KiB
-    const uint64_t rdcap = std::min<uint64_t>(ccap, std::max<uint64_t>(c->last_k + c->last_k / 8 + 1024,
-                                                                       B / 4096 + 1024));
-    EW_CHECK(c->rd.ensure(rdcap * sizeof(RecDesc)));
-    EW_CHECK(c->pf.ensure(rdcap * 8));
-    EW_CHECK(c->slow.ensure(rdcap * 4));
-    c->pfcap = rdcap;
+    uint64_t rdcap = std::min<uint64_t>(ccap, std::max<uint64_t>(c->last_k + c->last_k / 8 + 1024,
+                                                                 B / 4096 + 1024));
     rc = run_stream(c, tb, d_buf, B, 1, ccap);
     if (rc) return rc;
-    uint32_t *pf = c->pf.as<uint32_t>();
-    const unsigned fgrid = (unsigned)std::max(1, c->num_cu) * 3;   // persistent: 3 resident workgroups per CU
-    hipLaunchKernelGGL(k_frame, dim3(fgrid), dim3(256), 0, c->stream, d_buf, B, c->cpos.as<uint64_t>(), ccap, rdcap,
-                       c->pwave.as<uint32_t>(), c->v.as<uint32_t>(), tb->slice, tb->shift, c->rd.as<RecDesc>(), pf,
-                       pf + rdcap, c->slow.as<uint32_t>(), ds, c->ablate);
-    EW_CHECK(hipGetLastError());
-    if ((rc = sync_small(c))) return rc;
+    uint32_t *pf = nullptr;
+    bool rescanned = false;
+    for (int pass = 0; pass < 3; ++pass) {
+      EW_CHECK(c->rd.ensure(rdcap * sizeof(RecDesc)));
+      EW_CHECK(c->pf.ensure(rdcap * 8));
+      EW_CHECK(c->slow.ensure(rdcap * 4));
+      c->pfcap = rdcap;
+      pf = c->pf.as<uint32_t>();
+      const unsigned fgrid = (unsigned)std::max(1, c->num_cu) * c->frame_wg;   // persistent: resident WGs per CU
+      hipLaunchKernelGGL(k_frame, dim3(fgrid), dim3(256), 0, c->stream, d_buf, B, c->cpos.as<uint64_t>(), ccap,
+                         rdcap, c->pwave.as<uint32_t>(), c->v.as<uint32_t>(), tb->slice, tb->shift,
+                         c->rd.as<RecDesc>(), pf, pf + rdcap, c->slow.as<uint32_t>(), ds, c->ablate);
+      EW_CHECK(hipGetLastError());
+      if ((rc = sync_small(c))) return rc;
+      // k_frame declined before decoding anything: more candidates than
+      // descriptors (a first call on record-dense WALs) or units with more
+      // than EW_SLOTS candidates (small records) -> grow / k_rescan, run again
+      const uint64_t Kf = c->h_small->total;
+      const bool grow = Kf > rdcap && Kf <= ccap;
+      const bool resc = c->h_small->novf && Kf <= ccap && !rescanned;
+      if (!grow && !resc) break;
+      if (resc) {
+        hipLaunchKernelGGL(k_rescan, dim3(64), dim3(256), 0, c->stream, d_buf, B, c->ovf.as<uint32_t>(), &ds->novf,
+                           c->cbase.as<unsigned long long>(), c->cpos.as<uint64_t>(), c->clen.as<uint64_t>(), ccap);
+        EW_CHECK(hipGetLastError());
+        EW_CHECK(hipMemsetAsync(&ds->novf, 0, 4, c->stream));
+        rescanned = true;
+      }
+      if (grow) rdcap = Kf + Kf / 8 + 1024;
+    }
     K = c->h_small->total;
     c->last_k = K;
     if (K && K <= ccap && K <= rdcap && !c->h_small->novf && c->h_small->pos0 == 0 && !c->h_small->irregular) {
@@ -600,7 +620,7 @@ static int readall_batch_impl(ewal_ctx *c, const uint8_t *d_buf, uint32_t ns, co
       EW_CHECK(c->slow.ensure(rdcap * 4));
       c->pfcap = rdcap;
       pf = c->pf.as<uint32_t>();
-      const unsigned fgrid = (unsigned)std::max(1, c->num_cu) * 3;
+      const unsigned fgrid = (unsigned)std::max(1, c->num_cu) * c->frame_wg;
       hipLaunchKernelGGL(k_frame, dim3(fgrid), dim3(256), 0, c->stream, d_buf, B, c->cpos.as<uint64_t>(), ccap,
                          rdcap, c->pwave.as<uint32_t>(), c->v.as<uint32_t>(), tb->slice, tb->shift,
                          c->rd.as<RecDesc>(), pf, pf + rdcap, c->slow.as<uint32_t>(), ds, c->ablate);
@@ -750,6 +770,7 @@ int ewal_ctx_create(int device, ewal_ctx **out) {
   EW_CHECK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
   c->own_stream = true;
   if (const char *e = std::getenv("EWAL_STREAM_ABLATE")) c->ablate = std::atoi(e);
+  if (const char *e = std::getenv("EWAL_FRAME_WG")) c->frame_wg = std::max(1, std::min(16, std::atoi(e)));
   EW_CHECK(hipEventCreate(&c->ev0));
   EW_CHECK(hipEventCreate(&c->ev1));
   EW_CHECK(hipEventCreate(&c->evs0));
