@@ -111,10 +111,9 @@ def run_shards(a, dist, rank, world, local):
     def step():
         rr = W.readall_batch_device(dbuf, lens, ris)
         last["r"] = rr
-        if dist is not None:
-            fails = [(i, x.fail_record) for i, x in enumerate(rr) if x.status != L.OK]
-            i0, fr = fails[0] if fails else (0, -1)
-            shard.combine(dist, first + i0, fr, sum(x.n_records for x in rr), len(fails) > 0, out=summary)
+        if dist is not None:   # one all-reduce of the batch's verdicts (etcd_amd/shard.py)
+            shard.combine_batch(dist, first, [(x.fail_record if x.status != L.OK else -1, x.n_records,
+                                               x.status != L.OK) for x in rr], out=summary)
 
     elapsed = timed(dist, a.steps, step)
     ms = elapsed / a.steps * 1e3

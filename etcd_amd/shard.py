@@ -40,6 +40,27 @@ def combine(dist, shard: int, fail_record: int, n_records: int, failed: bool, de
     return int(t[0].item()), int(t[1].item()), int(t[2].item())
 
 
+def combine_batch(dist, first_shard: int, verdicts, device="cpu", out=None):
+    """All-reduce the verdicts of a rank's batch of shards (one batched
+    ReadAll, ewal_readall_batch_device): verdicts[i] = (fail_record,
+    n_records, failed) of shard first_shard + i.  Same reduction as
+    `combine` -- MIN of the failing shards' keys, SUM of frames verified, SUM
+    of failing shards -- over the whole batch, in the same one exchange."""
+    key, frames, nfail = NO_FAILURE, 0, 0
+    for i, (fr, n, failed) in enumerate(verdicts):
+        if failed:
+            key = min(key, failure_key(first_shard + i, fr))
+            nfail += 1
+        frames += fr if fr >= 0 else n
+    t = out if out is not None else torch.zeros(3, dtype=torch.int64, device=device)
+    t[0] = key
+    t[1] = frames
+    t[2] = nfail
+    dist.all_reduce(t[0:1], op=dist.ReduceOp.MIN)
+    dist.all_reduce(t[1:3], op=dist.ReduceOp.SUM)
+    return int(t[0].item()), int(t[1].item()), int(t[2].item())
+
+
 def decode_key(key: int):
     """(shard, frame) of a combined key, or None when no shard failed."""
     if key >= NO_FAILURE:

@@ -27,6 +27,9 @@ def _worker(rank, world, port, cases, q):
         for c in cases:
             fr, n, failed = c["shards"][rank]
             out.append(shard.combine(dist, rank, fr, n, failed))
+        for c in cases:   # the same shards as one batch per rank (bench.py --workload shards)
+            if "batch" in c:
+                out.append(shard.combine_batch(dist, c["batch_first"][rank], c["batch"][rank]))
         seams = []
         for s in c_seams(cases):
             first, last = s[rank]
@@ -81,3 +84,16 @@ def test_combine_four_ranks():
         assert shard.decode_key(key) == (2, 3)
         assert frames == 10 + 20 + 3 + 1 and fails == 2
         assert seams == [-1, 2]
+
+
+def test_combine_batch_two_ranks():
+    # rank 0 holds shards 0..2, rank 1 shards 3..5; shard 4 fails at frame 9, shard 1 at frame 30
+    cases = [{"shards": [(-1, 1, False), (-1, 1, False)],
+              "batch_first": [0, 3],
+              "batch": [[(-1, 100, False), (30, 30, True), (-1, 50, False)],
+                        [(-1, 10, False), (9, 9, True), (-1, 0, False)]]}]
+    res = _run(2, cases)
+    for rank, out, seams in res:
+        key, frames, fails = out[1]
+        assert shard.decode_key(key) == (1, 30)
+        assert frames == 100 + 30 + 50 + 10 + 9 and fails == 2
