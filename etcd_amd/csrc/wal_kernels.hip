@@ -83,11 +83,17 @@ __device__ __forceinline__ uint32_t load_word_guarded(const uint8_t *buf, uint64
 // Exact frame-start test at lane-local byte o = 4*j + k.  D holds the lane's
 // 16 dwords plus the next 3.  A candidate has int64 length L in [4, B-p-8]
 // and the canonical Record head 08 <type<0x80> 10 (record.pb.go:175-196).
+// The per-dword pre-test is "byte p+7 == 00 (the top byte of L, 0 for every
+// L <= B < 2^40) and byte p+8 == 08": a necessary condition that, unlike the
+// 08 ?? 10 head alone, skips the Entry head (08 00 10) inside every entry
+// record -- the byte before it ends Record.Data's length varint, never 0 --
+// so record-dense streams run the exact test about half as often (configs[2]
+// k_stream -9 %).
 #define CAND_TEST(J)                                                                 \
   {                                                                                  \
     uint32_t x_ = D[(J) + 2];                                                        \
-    uint32_t y_ = __builtin_amdgcn_alignbyte(D[(J) + 3], D[(J) + 2], 2);             \
-    uint32_t z_ = (x_ ^ 0x08080808u) | (y_ ^ 0x10101010u);                           \
+    uint32_t y_ = __builtin_amdgcn_alignbyte(D[(J) + 2], D[(J) + 1], 3);             \
+    uint32_t z_ = (x_ ^ 0x08080808u) | y_;                                           \
     uint32_t m_ = (z_ - 0x01010101u) & ~z_ & 0x80808080u;                            \
     while (m_) {                                                                     \
       uint32_t k_ = (uint32_t)__builtin_ctz(m_) >> 3;                                \
