@@ -90,7 +90,8 @@ class DeviceBuffer:
 
     def upload(self, data, offset=0):
         b = bytes(data) if not isinstance(data, (bytes, bytearray)) else data
-        src = (C.c_char * len(b)).from_buffer_copy(b) if isinstance(b, bytes) else (C.c_char * len(b)).from_buffer(b)
+        # zero-copy views of the host bytes (the copy only reads them)
+        src = C.c_char_p(b) if isinstance(b, bytes) else (C.c_char * len(b)).from_buffer(b)
         check(lib.ewal_upload(self.ctx.handle, C.c_void_p(self.ptr.value + offset), src, len(b)))
 
     def upload_ptr(self, host_ptr, n, offset=0):

@@ -162,3 +162,20 @@ def test_batch_synthetic_shards(ctx):
     for buf, r in zip(shards, res):
         g = W.readall_bytes(buf, 1, ctx, with_ents=False)
         assert (g.status, g.fail_record, g.last_crc, g.enti) == (r.status, r.fail_record, r.last_crc, r.enti)
+
+
+def test_batch_edges_and_ctx_reuse(ctx):
+    """No shards, only empty shards, one shard, and single ReadAll calls interleaved
+    with batches on the same ctx (workspace reuse)."""
+    assert W.readall_batch_bytes([], [], ctx) == []
+    check_batch(ctx, [b"", b"", b""], [0, 1, 0])
+    rng = random.Random(21)
+    one = build_wal(rng, 40, 3000, cuts=1)
+    r = check_batch(ctx, [one], [0], expect_fast=True)[0]
+    g = W.readall_bytes(one, 0, ctx)
+    assert g.as_dict() == r.as_dict()
+    big = [build_wal(rng, 200, 20000) for _ in range(5)]
+    check_batch(ctx, big, [0] * 5, expect_fast=True)
+    g2 = W.readall_bytes(one, 0, ctx)           # a single ReadAll after a larger batch
+    assert g2.as_dict() == g.as_dict()
+    check_batch(ctx, [one, b"", one], [0, 0, 3], expect_fast=True)
