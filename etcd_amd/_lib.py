@@ -58,6 +58,15 @@ FLAG_SHARD_FALLBACK = 1   # ewal_readall_batch_device verified this shard on its
 CASTAGNOLI, IEEE, KOOPMAN = 0x82F63B78, 0xEDB88320, 0xEB31D82E
 
 
+class MessageDesc(C.Structure):   # emsg_message
+    _fields_ = [("status", C.c_int32), ("reject", C.c_int32), ("type", C.c_uint64), ("to", C.c_uint64),
+                ("from_", C.c_uint64), ("term", C.c_uint64), ("log_term", C.c_uint64), ("index", C.c_uint64),
+                ("commit", C.c_uint64), ("ents_first", C.c_uint64), ("n_ents", C.c_uint64),
+                ("snap_index", C.c_uint64), ("snap_term", C.c_uint64), ("snap_data_off", C.c_int64),
+                ("snap_data_len", C.c_int64), ("snap_n_nodes", C.c_uint64), ("snap_n_removed", C.c_uint64),
+                ("unrec_len", C.c_int64)]
+
+
 class Result(C.Structure):
     _fields_ = [("status", C.c_int32), ("flags", C.c_int32), ("detail", C.c_int64), ("fail_record", C.c_int64),
                 ("fail_offset", C.c_int64), ("n_records", C.c_int64), ("last_crc", C.c_uint32),
@@ -104,6 +113,9 @@ _SIGS = {
     "ewal_last_stream_ms": (C.c_float, [vp]),
     "ewal_readall_batch_device": (C.c_int, [vp, vp, C.c_uint64, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64),
                                             C.POINTER(Result)]),
+    "emsg_decode_batch_device": (C.c_int, [vp, vp, C.c_uint64, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64),
+                                           C.c_uint32, C.POINTER(MessageDesc), C.POINTER(C.c_uint64)]),
+    "emsg_copy_entries": (C.c_int64, [vp, C.c_uint64, C.POINTER(EntryDesc), C.c_int64]),
     "ewal_batch_copy_entries": (C.c_int64, [vp, C.c_uint64, C.POINTER(EntryDesc), C.c_int64]),
     "ewal_copy_records": (C.c_int64, [vp, C.POINTER(RecordDesc), C.c_int64]),
     "ewal_open_at_index": (C.c_int, [C.c_char_p, C.c_uint64, C.POINTER(vp)]),

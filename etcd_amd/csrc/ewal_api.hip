@@ -21,6 +21,7 @@
 #include "crc_math.h"
 #include "wal_kernels.hip"
 #include "aux_kernels.hip"
+#include "msg_kernels.hip"
 
 #define EW_CHECK(x)                                                          \
   do {                                                                       \
@@ -76,6 +77,9 @@ struct ewal_ctx {
       ents, recs, tmp, small, sdesc, snaps, hbuf_dev;
   // batched ReadAll (ewal_readall_batch_device): shard tables, results, ents
   DevBuf bfs, bsoff, bri, bsagg, bres, bef, bents, bshard;
+  // batched raftpb.Message decode (emsg_decode_batch_device)
+  DevBuf moff, mlen, mcnt, mfirst, mout, ments;
+  uint64_t mtotal = 0;
   std::vector<uint64_t> bent_first, bnents;   // per shard: first ent in bents, count
   Small *h_small = nullptr;        // host-mapped pinned mirrors (written by k_export_small / k_result)
   ResultDev *h_res = nullptr;
@@ -1045,6 +1049,60 @@ int esnap_copy_snapshot(ewal_ctx *c, uint32_t i, esnap_snapshot *out) {
   if (!c || !out) return EWAL_E_INVAL;
   EW_CHECK(hipMemcpy(out, c->snaps.as<esnap_snapshot>() + i, sizeof(*out), hipMemcpyDeviceToHost));
   return EWAL_OK;
+}
+
+int emsg_decode_batch_device(ewal_ctx *c, const void *d_buf, uint64_t buf_len, const uint64_t *offs,
+                             const uint64_t *lens, uint32_t n, emsg_message *out, uint64_t *n_entries) {
+  if (!c || (!d_buf && buf_len) || (n && (!offs || !lens || !out))) return EWAL_E_INVAL;
+  for (uint32_t i = 0; i < n; ++i)
+    if (offs[i] + lens[i] > buf_len || offs[i] + lens[i] < offs[i] || lens[i] >= (1ull << 62)) return EWAL_E_INVAL;
+  EW_CHECK(hipSetDevice(c->device));
+  if (n_entries) *n_entries = 0;
+  if (!n) return EWAL_OK;
+  EW_CHECK(c->moff.ensure((size_t)n * 8));
+  EW_CHECK(c->mlen.ensure((size_t)n * 8));
+  EW_CHECK(c->mcnt.ensure((size_t)n * 8));
+  EW_CHECK(c->mfirst.ensure((size_t)n * 8));
+  EW_CHECK(c->mout.ensure((size_t)n * sizeof(emsg_message)));
+  EW_CHECK(hipMemcpyAsync(c->moff.p, offs, (size_t)n * 8, hipMemcpyHostToDevice, c->stream));
+  EW_CHECK(hipMemcpyAsync(c->mlen.p, lens, (size_t)n * 8, hipMemcpyHostToDevice, c->stream));
+  EW_CHECK(hipEventRecord(c->ev0, c->stream));
+  const uint8_t *b = (const uint8_t *)d_buf;
+  unsigned long long *cnt = c->mcnt.as<unsigned long long>(), *first = c->mfirst.as<unsigned long long>();
+  hipLaunchKernelGGL(k_msg<false>, dim3(grid_for(n, 256)), dim3(256), 0, c->stream, b, c->moff.as<uint64_t>(),
+                     c->mlen.as<uint64_t>(), n, cnt, (const unsigned long long *)nullptr, (emsg_message *)nullptr,
+                     (ewal_entry *)nullptr);
+  size_t bytes = 0;
+  EW_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, cnt, first, (int)n, c->stream));
+  EW_CHECK(c->tmp.ensure(bytes));
+  EW_CHECK(hipcub::DeviceScan::ExclusiveSum(c->tmp.p, bytes, cnt, first, (int)n, c->stream));
+  unsigned long long tail[2];
+  EW_CHECK(hipMemcpyAsync(&tail[0], first + (n - 1), 8, hipMemcpyDeviceToHost, c->stream));
+  EW_CHECK(hipMemcpyAsync(&tail[1], cnt + (n - 1), 8, hipMemcpyDeviceToHost, c->stream));
+  EW_CHECK(hipStreamSynchronize(c->stream));
+  const uint64_t total = tail[0] + tail[1];
+  EW_CHECK(c->ments.ensure((size_t)std::max<uint64_t>(total, 1) * sizeof(ewal_entry)));
+  hipLaunchKernelGGL(k_msg<true>, dim3(grid_for(n, 256)), dim3(256), 0, c->stream, b, c->moff.as<uint64_t>(),
+                     c->mlen.as<uint64_t>(), n, cnt, (const unsigned long long *)first, c->mout.as<emsg_message>(),
+                     c->ments.as<ewal_entry>());
+  EW_CHECK(hipGetLastError());
+  EW_CHECK(hipEventRecord(c->ev1, c->stream));
+  EW_CHECK(hipMemcpyAsync(out, c->mout.p, (size_t)n * sizeof(emsg_message), hipMemcpyDeviceToHost, c->stream));
+  EW_CHECK(hipStreamSynchronize(c->stream));
+  c->mtotal = total;
+  if (n_entries) *n_entries = total;
+  return EWAL_OK;
+}
+
+int64_t emsg_copy_entries(ewal_ctx *c, uint64_t first, ewal_entry *out, int64_t cap) {
+  if (!c || (!out && cap) || first > c->mtotal) return EWAL_E_INVAL;
+  const int64_t n = std::min<int64_t>(cap, (int64_t)(c->mtotal - first));
+  if (n > 0) {
+    EW_CHECK(hipMemcpyAsync(out, c->ments.as<ewal_entry>() + first, (size_t)n * sizeof(ewal_entry),
+                            hipMemcpyDeviceToHost, c->stream));
+    EW_CHECK(hipStreamSynchronize(c->stream));
+  }
+  return n;
 }
 
 float ewal_last_device_ms(ewal_ctx *c) {

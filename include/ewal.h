@@ -251,6 +251,30 @@ int ecommit_batch_device(ewal_ctx *ctx, uint64_t G, const uint64_t *match, const
                          const uint64_t *log_ptr, const uint64_t *log_terms, uint8_t *changed,
                          uint8_t *status, double *device_ms);
 
+/* ---- raft ingress: raftpb.Message.Unmarshal, raft/raftpb/raft.pb.go:407-617
+ * (called per POST /raft in etcdserver/etcdhttp/http.go:119-146), batched
+ * over n messages resident in one device buffer at offs[i], lens[i] (host
+ * arrays).  status = EWAL_OK / EWAL_ERR_UNEXPECTED_EOF / EWAL_ERR_WRONG_TYPE /
+ * EWAL_PANIC_BOUNDS / EWAL_NONTERMINATING as Unmarshal returns or panics, or
+ * EWAL_UNSUPPORTED_ENCODING when the message would carry unrecognized
+ * fields / a split bytes field this layout does not return.  The fields hold
+ * what Go leaves in the struct (partial on error).  Entries go to a ctx-owned
+ * array: message i's are [ents_first, ents_first + n_ents), fetched with
+ * emsg_copy_entries (Data offsets are offsets into d_buf). */
+typedef struct emsg_message {
+  int32_t status;
+  int32_t reject;
+  uint64_t type, to, from, term, log_term, index, commit;
+  uint64_t ents_first, n_ents;
+  uint64_t snap_index, snap_term;
+  int64_t snap_data_off, snap_data_len;   /* Snapshot.Data in d_buf; off -1 == nil */
+  uint64_t snap_n_nodes, snap_n_removed;
+  int64_t unrec_len;                       /* len(XXX_unrecognized) */
+} emsg_message;
+int emsg_decode_batch_device(ewal_ctx *ctx, const void *d_buf, uint64_t buf_len, const uint64_t *offs,
+                             const uint64_t *lens, uint32_t n, emsg_message *out, uint64_t *n_entries);
+int64_t emsg_copy_entries(ewal_ctx *ctx, uint64_t first, ewal_entry *out, int64_t cap);
+
 #ifdef __cplusplus
 }
 #endif

@@ -278,6 +278,92 @@ int or_snappb_unmarshal(const uint8_t *d, int64_t l, or_snappb *m) {
   return pb_unmarshal(d, l, fs, 2, &m->unrec_len);
 }
 
+/* raftpb.Message.Unmarshal, raft/raftpb/raft.pb.go:407-617.  Quirks kept:
+ * an Entry's Unmarshal error is discarded (:535, the return value is not
+ * checked) but a panic inside it propagates; Snapshot errors return (:575);
+ * Reject is assigned (v != 0), not OR-ed (:593); repeated Snapshot fields
+ * accumulate into the same struct. */
+static int msg_varint(const uint8_t *d, int64_t *index, int64_t l, uint64_t *v) {
+  for (uint64_t shift = 0;; shift += 7) {
+    if (*index >= l) return OR_ERR_UNEXPECTED_EOF;
+    uint8_t b = d[(*index)++];
+    *v |= shl64((uint64_t)(b & 0x7F), shift);
+    if (b < 0x80) return OR_OK;
+  }
+}
+int or_message_unmarshal(const uint8_t *d, int64_t l, or_message *m) {
+  int64_t index = 0;
+  while (index < l) {
+    uint64_t wire = 0;
+    if (msg_varint(d, &index, l, &wire)) return OR_ERR_UNEXPECTED_EOF;
+    int32_t fieldNum = (int32_t)(uint32_t)(wire >> 3);
+    int wireType = (int)(wire & 7);
+    uint64_t *u = NULL;
+    switch (fieldNum) {
+    case 1: u = &m->type; break;
+    case 2: u = &m->to; break;
+    case 3: u = &m->from; break;
+    case 4: u = &m->term; break;
+    case 5: u = &m->log_term; break;
+    case 6: u = &m->index; break;
+    case 8: u = &m->commit; break;
+    default: break;
+    }
+    if (u) {
+      if (wireType != 0) return OR_ERR_WRONG_TYPE;
+      if (msg_varint(d, &index, l, u)) return OR_ERR_UNEXPECTED_EOF;
+      continue;
+    }
+    if (fieldNum == 7 || fieldNum == 9) {
+      if (wireType != 2) return OR_ERR_WRONG_TYPE;
+      uint64_t ml = 0;
+      if (msg_varint(d, &index, l, &ml)) return OR_ERR_UNEXPECTED_EOF;
+      int64_t postIndex = wadd(index, (int64_t)ml);
+      if (postIndex > l) return OR_ERR_UNEXPECTED_EOF;
+      if (postIndex < index) return OR_PANIC_BOUNDS;   /* data[index:postIndex] */
+      if (fieldNum == 7) {
+        m->ents = (or_entry *)realloc(m->ents, sizeof(or_entry) * (size_t)(m->n_ents + 1));
+        or_entry *e = &m->ents[m->n_ents++];
+        memset(e, 0, sizeof(*e));
+        int st = or_entry_unmarshal(d + index, postIndex - index, e);
+        if (st == OR_PANIC_BOUNDS || st == OR_NONTERMINATING) return st;   /* panics propagate */
+      } else {
+        int st = or_snapshot_unmarshal(d + index, postIndex - index, &m->snap);
+        if (st) return st;
+      }
+      index = postIndex;
+      continue;
+    }
+    if (fieldNum == 10) {
+      if (wireType != 0) return OR_ERR_WRONG_TYPE;
+      uint64_t v = 0;
+      if (msg_varint(d, &index, l, &v)) return OR_ERR_UNEXPECTED_EOF;
+      m->reject = v != 0;
+      continue;
+    }
+    int64_t sizeOfWire = 0;
+    uint64_t w = wire;
+    do { sizeOfWire++; w >>= 7; } while (w != 0);
+    index -= sizeOfWire;
+    int64_t skippy;
+    int st = or_proto_skip(d + index, l - index, &skippy);
+    if (st) return st;
+    int64_t hi = wadd(index, skippy);
+    if (hi > l) return OR_ERR_UNEXPECTED_EOF;
+    if (hi < index) return OR_PANIC_BOUNDS;
+    if (skippy == 0) return OR_NONTERMINATING;
+    m->unrec_len += skippy;
+    index = hi;
+  }
+  return OR_OK;
+}
+void or_message_free(or_message *m) {
+  for (int64_t i = 0; i < m->n_ents; i++) or_entry_free(&m->ents[i]);
+  free(m->ents);
+  or_snapshot_free(&m->snap);
+  memset(m, 0, sizeof(*m));
+}
+
 void or_record_free(or_record *m) { free(m->data); memset(m, 0, sizeof(*m)); }
 void or_entry_free(or_entry *m) { free(m->data); memset(m, 0, sizeof(*m)); }
 void or_snapshot_free(or_snapshot *m) { free(m->data); free(m->nodes); free(m->removed); memset(m, 0, sizeof(*m)); }
@@ -575,5 +661,27 @@ void or_maybe_commit_batch(uint64_t G, const uint64_t *match, const uint8_t *nvo
     if (rc < 0) status[g] = (uint8_t)(-rc);
     else changed[g] = (uint8_t)rc;
   }
+}
+
+/* raftpb.Message.MarshalTo, raft/raftpb/raft.pb.go:1010-1068 */
+int64_t or_message_marshal(uint64_t type, uint64_t to, uint64_t from, uint64_t term, uint64_t log_term,
+                           uint64_t index, const uint8_t *ents, const int64_t *ent_lens, int64_t n_ents,
+                           uint64_t commit, const uint8_t *snap, int64_t snap_len, int reject, uint8_t *out) {
+  int64_t i = 0, o = 0;
+  i = put_byte(out, i, 0x08); i = put_varint(out, i, type);
+  i = put_byte(out, i, 0x10); i = put_varint(out, i, to);
+  i = put_byte(out, i, 0x18); i = put_varint(out, i, from);
+  i = put_byte(out, i, 0x20); i = put_varint(out, i, term);
+  i = put_byte(out, i, 0x28); i = put_varint(out, i, log_term);
+  i = put_byte(out, i, 0x30); i = put_varint(out, i, index);
+  for (int64_t k = 0; k < n_ents; k++) {
+    i = put_byte(out, i, 0x3a); i = put_varint(out, i, (uint64_t)ent_lens[k]);
+    i = put_bytes(out, i, ents + o, ent_lens[k]);
+    o += ent_lens[k];
+  }
+  i = put_byte(out, i, 0x40); i = put_varint(out, i, commit);
+  i = put_byte(out, i, 0x4a); i = put_varint(out, i, (uint64_t)snap_len); i = put_bytes(out, i, snap, snap_len);
+  i = put_byte(out, i, 0x50); i = put_byte(out, i, reject ? 1 : 0);
+  return i;
 }
 

@@ -95,6 +95,15 @@ typedef struct {
   int64_t unrec_len;
 } or_snappb;
 
+/* raftpb.Message, raft/raftpb/raft.pb.go:125-137 */
+typedef struct {
+  uint64_t type, to, from, term, log_term, index, commit;
+  int reject;
+  or_entry *ents; int64_t n_ents;
+  or_snapshot snap;
+  int64_t unrec_len;
+} or_message;
+
 /* Unmarshal: return OR_OK, OR_ERR_UNEXPECTED_EOF, OR_ERR_WRONG_TYPE,
  * OR_PANIC_BOUNDS or OR_NONTERMINATING.  The struct is left as Go leaves
  * it on error (partially filled); *_free releases owned buffers. */
@@ -106,6 +115,13 @@ int or_snappb_unmarshal(const uint8_t *d, int64_t l, or_snappb *m);     /* snap/
 /* proto.Skip, third_party/code.google.com/p/gogoprotobuf/proto/skip_gogo.go:33-116.
  * Returns status; *n receives the skip length on OR_OK. */
 int or_proto_skip(const uint8_t *d, int64_t l, int64_t *n);
+int or_message_unmarshal(const uint8_t *d, int64_t l, or_message *m);   /* raft/raftpb/raft.pb.go:407-617 */
+void or_message_free(or_message *m);
+/* Message.MarshalTo (raft.pb.go:1010-1068); ents = the n marshalled Entry
+ * bodies back to back with their lengths, snap = marshalled Snapshot. */
+int64_t or_message_marshal(uint64_t type, uint64_t to, uint64_t from, uint64_t term, uint64_t log_term,
+                           uint64_t index, const uint8_t *ents, const int64_t *ent_lens, int64_t n_ents,
+                           uint64_t commit, const uint8_t *snap, int64_t snap_len, int reject, uint8_t *out);
 void or_record_free(or_record *m);
 void or_entry_free(or_entry *m);
 void or_snapshot_free(or_snapshot *m);

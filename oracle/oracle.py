@@ -282,3 +282,45 @@ def maybe_commit_batch(G, match, nvoters, term, committed, log_offset, log_ptr, 
     lib.or_maybe_commit_batch(G, ptr(match), ptr(nvoters), ptr(term), ptr(committed), ptr(log_offset), ptr(log_ptr),
                               ptr(log_terms), ptr(changed), ptr(status))
 
+
+# ---- raftpb.Message (raft/raftpb/raft.pb.go:407-617, 1010-1068) ----------
+class Message(C.Structure):
+    _fields_ = [("type", C.c_uint64), ("to", C.c_uint64), ("from_", C.c_uint64), ("term", C.c_uint64),
+                ("log_term", C.c_uint64), ("index", C.c_uint64), ("commit", C.c_uint64), ("reject", C.c_int),
+                ("ents", C.POINTER(Entry)), ("n_ents", C.c_int64), ("snap", Snapshot), ("unrec_len", C.c_int64)]
+
+
+lib.or_message_unmarshal.argtypes = [C.c_char_p, C.c_int64, C.POINTER(Message)]
+lib.or_message_free.argtypes = [C.POINTER(Message)]
+lib.or_message_free.restype = None
+lib.or_message_marshal.restype = C.c_int64
+lib.or_message_marshal.argtypes = [C.c_uint64] * 6 + [C.c_char_p, C.POINTER(C.c_int64), C.c_int64, C.c_uint64,
+                                                      C.c_char_p, C.c_int64, C.c_int, C.c_void_p]
+
+
+def message_marshal(type_=0, to=0, from_=0, term=0, log_term=0, index=0, entries=(), commit=0, snapshot=b"",
+                    reject=False):
+    """entries: marshalled Entry bodies; snapshot: marshalled raftpb.Snapshot."""
+    ents = b"".join(entries)
+    lens = (C.c_int64 * max(len(entries), 1))(*[len(e) for e in entries])
+    args = (type_, to, from_, term, log_term, index, ents, lens, len(entries), commit, snapshot, len(snapshot),
+            int(bool(reject)))
+    n = lib.or_message_marshal(*args, None)
+    out = C.create_string_buffer(max(n, 1))
+    lib.or_message_marshal(*args, out)
+    return out.raw[:n]
+
+
+def message_unmarshal(b):
+    m = Message()
+    st = lib.or_message_unmarshal(b, len(b), C.byref(m))
+    ents = [dict(type=e.type, term=e.term, index=e.index, data=_bytes(e.data, e.data_len), unrec_len=e.unrec_len)
+            for e in m.ents[:m.n_ents]]
+    s = m.snap
+    out = dict(status=st, type=m.type, to=m.to, from_=m.from_, term=m.term, log_term=m.log_term, index=m.index,
+               commit=m.commit, reject=bool(m.reject), ents=ents, unrec_len=m.unrec_len,
+               snap=dict(data=_bytes(s.data, s.data_len), index=s.index, term=s.term, n_nodes=s.n_nodes,
+                         n_removed=s.n_removed, unrec_len=s.unrec_len))
+    lib.or_message_free(C.byref(m))
+    return out
+

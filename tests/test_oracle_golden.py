@@ -190,3 +190,29 @@ def test_skip_group_and_nontermination():
     assert O.record_unmarshal(bytes([0x2A]) + neg(-12))[0] == O.PANIC_BOUNDS
     # skippy > 0 but short: parsing resumes inside the length varint (0xFF 0x01 -> wire type 7)
     assert O.record_unmarshal(bytes([0x2A]) + neg(-2))[0] == O.ERR_WRONG_TYPE
+
+
+def test_message_oracle_round_trip_and_quirks():
+    """raftpb.Message restatement (raft/raftpb/raft.pb.go:407-617, 1010-1068)."""
+    ents = [O.entry_marshal(0, 1, 5, b"hello"), O.entry_marshal(1, 2, 6, None)]
+    snap = O.snapshot_marshal(b"xyz", [1, 2], 7, 3)
+    m = O.message_marshal(3, 1, 2, 5, 4, 6, ents, 9, snap, True)
+    # MarshalTo byte layout: fields 1-6, 7 per entry, 8, 9, 10 (raft.pb.go:1015-1063)
+    assert m.hex() == ("0803100118022005280430063a0d080010011805220568656c6c6f3a08080110021806220040094a0d0a"
+                       "0378797a10011002180720035001")
+    d = O.message_unmarshal(m)
+    assert d["status"] == O.OK and (d["type"], d["to"], d["from_"], d["term"], d["log_term"], d["index"],
+                                    d["commit"], d["reject"]) == (3, 1, 2, 5, 4, 6, 9, True)
+    assert [(e["term"], e["index"], e["data"]) for e in d["ents"]] == [(1, 5, b"hello"), (2, 6, None)]
+    assert (d["snap"]["data"], d["snap"]["index"], d["snap"]["term"], d["snap"]["n_nodes"]) == (b"xyz", 7, 3, 2)
+    # an Entry's Unmarshal error is discarded (:535): the message still decodes
+    d = O.message_unmarshal(O.message_marshal(0, 0, 0, 0, 0, 0, [bytes([0x08, 0x01, 0x10])], 0, b"", False))
+    assert d["status"] == O.OK and len(d["ents"]) == 1 and d["ents"][0]["type"] == 1
+    # a panic inside it propagates (negative Data length -> slice bounds)
+    neg = bytes([0x22]) + bytes([0xff] * 9) + bytes([0x01])
+    assert O.message_unmarshal(bytes([0x3a, len(neg)]) + neg)["status"] == O.PANIC_BOUNDS
+    # Reject is assigned; a negative embedded length panics; truncation -> ErrUnexpectedEOF
+    assert O.message_unmarshal(bytes([0x50, 0x01, 0x50, 0x00]))["reject"] is False
+    assert O.message_unmarshal(bytes([0x4a]) + bytes([0xff] * 9) + bytes([0x01]))["status"] == O.PANIC_BOUNDS
+    assert O.message_unmarshal(m[:-1])["status"] == O.ERR_UNEXPECTED_EOF
+    assert O.message_unmarshal(bytes([0x0a, 0x00]))["status"] == O.ERR_WRONG_TYPE
