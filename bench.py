@@ -39,10 +39,10 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
-    ap.add_argument("--workload", choices=["wal", "c1", "shards", "snap", "commit"], default="wal",
+    ap.add_argument("--workload", choices=["wal", "c1", "shards", "snap", "commit", "msg"], default="wal",
                     help="wal = configs[1] (the headline, default); c1 = configs[0]'s WAL (1M x 256 B entries) on "
                          "the GPU; shards = configs[2] (4096 x 64 MiB per-group WALs over the node, 512 per GPU); "
-                         "snap = configs[3]; commit = configs[4]")
+                         "snap = configs[3]; commit = configs[4]; msg = raftpb.Message ingress decode")
     ap.add_argument("--shards-per-gpu", type=int, default=512)
     ap.add_argument("--shard-mib", type=int, default=64)
     return ap.parse_args()
@@ -321,6 +321,64 @@ def run_commit(a, dist, rank, world, local):
     ctx.close()
 
 
+def run_msg(a, dist, rank, world, local):
+    """batched raftpb.Message decode for the /raft
+    ingress (raft/raftpb/raft.pb.go:407-617): 256 Ki message bodies resident
+    in HBM (1024 distinct bodies tiled: MsgApp with 1-8 entries of 64 B-1 KiB,
+    heartbeats and votes with none), one emsg_decode_batch_device per step
+    (count pass, scan, decode pass, results copied to the host)."""
+    import random
+    from etcd_amd import raftmsg as M
+    rng = random.Random(9 + rank)
+    distinct, nents = [], []
+    for i in range(1024):
+        ne = rng.choice([0, 0, 1, 2, 4, 8])
+        nents.append(ne)
+        ents = [M.entry_marshal(0, 5, 1000 + i * 8 + k, rng.randbytes(rng.randrange(64, 1025))) for k in range(ne)]
+        distinct.append(M.message_marshal(3 if ne else rng.choice([1, 5, 8]), 2, 1, 5, 5, 1000 + i * 8, ents,
+                                          999 + i, b"", False))
+    n = 256 * 1024
+    bodies = [distinct[i % len(distinct)] for i in range(n)]
+    lens = [len(b) for b in bodies]
+    offs, pos = [], 0
+    for x in lens:
+        offs.append(pos)
+        pos += x
+    blob = b"".join(bodies)
+    nb = len(blob)
+    ctx = W.Context(local)
+    dbuf = ctx.alloc(nb + 64)
+    dbuf.upload(blob)
+    co, cl = (C.c_uint64 * n)(*offs), (C.c_uint64 * n)(*lens)
+    out = (L.MessageDesc * n)()
+    tot = C.c_uint64(0)
+
+    def step():
+        rc = L.lib.emsg_decode_batch_device(ctx.handle, dbuf.ptr, nb, co, cl, n, out, C.byref(tot))
+        assert rc == 0, rc
+
+    for _ in range(max(a.warmup, 1)):
+        step()
+    want_ents = sum(nents[i % len(distinct)] for i in range(n))
+    assert all(m.status == 0 for m in out) and tot.value == want_ents, (tot.value, want_ents)
+    elapsed = timed(dist, a.steps, step)
+    ms = elapsed / a.steps * 1e3
+    dms = float(L.lib.ewal_last_device_ms(ctx.handle))
+    if rank == 0:
+        print(json.dumps({
+            "metric": "raftpb.Message decode messages/s (SURVEY 8(f) rank 4); WAL verify GB/s is the headline",
+            "value": round(world * n / (ms / 1e3), 1), "unit": "messages/s", "n_gpus": world, "steps": a.steps,
+            "warmup": a.warmup, "ms_per_step": round(ms, 4), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "u8", "data": "synthetic",
+            "config": {"workload": "%d raftpb.Message bodies (%.1f MB) per GPU, %d entries decoded per step; "
+                                   "results copied to the host each step" % (n, nb / 1e6, tot.value),
+                       "parallelism": "dp%d" % world},
+            "gbps": round(world * nb / (ms / 1e3) / 1e9, 3), "device_ms": round(dms, 4),
+            "cpu_baseline": None}), flush=True)
+    dbuf.free()
+    ctx.close()
+
+
 def main():
     a = parse()
     rank = int(os.environ.get("RANK", "0"))
@@ -343,7 +401,7 @@ def main():
     elif (a.size_gib, a.min_data, a.max_data) != (8.0, 64, 65536):
         label = "configs[1]-shaped"
     if a.workload not in ("wal", "c1"):
-        {"shards": run_shards, "snap": run_snap, "commit": run_commit}[a.workload](a, dist, rank, world, local)
+        {"shards": run_shards, "snap": run_snap, "commit": run_commit, "msg": run_msg}[a.workload](a, dist, rank, world, local)
         if dist is not None:
             dist.destroy_process_group()
         return
