@@ -32,20 +32,22 @@ __device__ int msg_walk(const uint8_t *p, int64_t l, uint64_t base, emsg_message
     if (rd_varint(p, i, l, wire, 64)) { st = 2; break; }
     const uint32_t fn = (uint32_t)(wire >> 3);
     const int wt = (int)(wire & 7);
-    uint64_t *u = nullptr;
-    switch (fn) {
-    case 1: u = &m.type; break;
-    case 2: u = &m.to; break;
-    case 3: u = &m.from; break;
-    case 4: u = &m.term; break;
-    case 5: u = &m.log_term; break;
-    case 6: u = &m.index; break;
-    case 8: u = &m.commit; break;
-    default: break;
-    }
-    if (u) {
+    if ((fn >= 1 && fn <= 6) || fn == 8) {
       if (wt != 0) { st = 7; break; }
-      if (rd_varint(p, i, l, *u, 64)) { st = 2; break; }
+      // m.X |= chunk << shift per byte == m.X |= the varint's value, also
+      // for the bits read before a truncation (Go leaves them in the field)
+      uint64_t v = 0;
+      const int e = rd_varint(p, i, l, v, 64);
+      switch (fn) {   // named fields, no pointer into m (it stays in registers)
+      case 1: m.type |= v; break;
+      case 2: m.to |= v; break;
+      case 3: m.from |= v; break;
+      case 4: m.term |= v; break;
+      case 5: m.log_term |= v; break;
+      case 6: m.index |= v; break;
+      default: m.commit |= v; break;
+      }
+      if (e) { st = 2; break; }
       continue;
     }
     if (fn == 7 || fn == 9) {
