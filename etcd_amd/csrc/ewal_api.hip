@@ -293,8 +293,9 @@ static int read_le64_at(ewal_ctx *c, const uint8_t *d_buf, uint64_t B, uint64_t 
   return 0;
 }
 
-// (*WAL).ReadAll, wal/wal.go:164-216.  Regular case: two host syncs in all
-// (after k_link, and the final result copy).
+// (*WAL).ReadAll, wal/wal.go:164-216.  Regular case: ONE host sync in all
+// (k_check / k_result queued behind k_frame, gated on the device by
+// k_spec_gate); the slow framing paths add their own.
 static int readall_impl(ewal_ctx *c, const uint8_t *d_buf, uint64_t B, uint64_t ri, ewal_result *out) {
   std::memset(out, 0, sizeof(*out));
   out->fail_record = -1;
@@ -317,6 +318,7 @@ static int readall_impl(ewal_ctx *c, const uint8_t *d_buf, uint64_t B, uint64_t 
   int64_t qlen = 0;
   bool regular = false;
   bool decoded = false;    // k_frame's speculative decode holds
+  bool spec_checked = false;   // ... and k_check / k_result already ran behind it
   if (B > 0) {
     uint64_t ccap = std::min<uint64_t>(B / 128 + 65536, 0xfffffff0ull);
     EW_CHECK(c->cpos.ensure(ccap * 8));
@@ -342,7 +344,41 @@ static int readall_impl(ewal_ctx *c, const uint8_t *d_buf, uint64_t B, uint64_t 
                          rdcap, c->pwave.as<uint32_t>(), c->v.as<uint32_t>(), tb->slice, tb->shift,
                          c->rd.as<RecDesc>(), pf, pf + rdcap, c->slow.as<uint32_t>(), ds, c->ablate);
       EW_CHECK(hipGetLastError());
-      if ((rc = sync_small(c))) return rc;
+      if (pass == 0) {
+        // Queue the check behind the frame pass before the host has seen its
+        // verdict: k_spec_gate decides on the device (spec_n = frames, or 0)
+        // and k_check / k_result run only when it held -- ONE host sync for
+        // the whole call in the regular case.
+        hipLaunchKernelGGL(k_spec_gate, dim3(1), dim3(64), 0, c->stream, ds, ccap, rdcap, c->h_small_dev);
+        hipLaunchKernelGGL(k_decode_slow, dim3(64), dim3(256), 0, c->stream, d_buf, B, c->cpos.as<uint64_t>(),
+                           (const uint32_t *)nullptr, c->slow.as<uint32_t>(), ds, c->pwave.as<uint32_t>(),
+                           c->v.as<uint32_t>(), tb->slice, tb->shift, c->rd.as<RecDesc>(), pf, pf + rdcap, 0u);
+        const uint32_t nbs = grid_for(rdcap, 1024);
+        const size_t had = c->lbstat.cap;
+        EW_CHECK(c->lbstat.ensure((size_t)nbs * 8));
+        c->epoch = (c->epoch + 1) & 0xffffffu;
+        if (c->lbstat.cap != had || c->epoch == 0) {
+          EW_CHECK(hipMemsetAsync(c->lbstat.p, 0, c->lbstat.cap, c->stream));
+          if (c->epoch == 0) c->epoch = 1;
+        }
+        EW_CHECK(c->opf.ensure((size_t)nbs * 4));
+        EW_CHECK(c->mlist.ensure((size_t)rdcap * 4));
+        EW_CHECK(c->ents.ensure((size_t)rdcap * sizeof(ewal_entry)));
+        hipLaunchKernelGGL(k_check<false>, dim3(nbs), dim3(1024), 0, c->stream, tb->shift, c->rd.as<RecDesc>(),
+                           (uint32_t)rdcap, (const uint32_t *)pf, (const uint32_t *)(pf + rdcap), ri,
+                           c->lbstat.as<unsigned long long>(), c->epoch, c->opf.as<uint32_t>(),
+                           c->ents.as<ewal_entry>(), c->mlist.as<uint32_t>(), ds, SegArgs{},
+                           (const uint32_t *)&ds->spec_n);
+        hipLaunchKernelGGL(k_result, dim3(1), dim3(256), 0, c->stream, d_buf, c->rd.as<RecDesc>(),
+                           c->mlist.as<uint32_t>(), 0u, ri, ds, c->h_res_dev, (const uint32_t *)&ds->spec_n);
+        EW_CHECK(hipGetLastError());
+        EW_CHECK(hipStreamSynchronize(c->stream));
+        if (c->h_small->errflag) return EWAL_E_TIMEOUT;
+        spec_checked = c->h_small->spec_n != 0;
+        if (spec_checked) break;
+      } else if ((rc = sync_small(c))) {
+        return rc;
+      }
       // k_frame declined before decoding anything: more candidates than
       // descriptors (a first call on record-dense WALs) or units with more
       // than EW_SLOTS candidates (small records) -> grow / k_rescan, run again
@@ -363,7 +399,7 @@ static int readall_impl(ewal_ctx *c, const uint8_t *d_buf, uint64_t B, uint64_t 
     c->last_k = K;
     if (K && K <= ccap && K <= rdcap && !c->h_small->novf && c->h_small->pos0 == 0 && !c->h_small->irregular) {
       decoded = true;
-      if (c->h_small->nslow) {   // frames the canonical parser declined (a launch only when there are any)
+      if (c->h_small->nslow && !spec_checked) {   // frames the canonical parser declined
         hipLaunchKernelGGL(k_decode_slow, dim3(std::min<uint64_t>(grid_for(c->h_small->nslow, 256), 1024)),
                            dim3(256), 0, c->stream, d_buf, B, c->cpos.as<uint64_t>(), (const uint32_t *)nullptr,
                            c->slow.as<uint32_t>(), ds, c->pwave.as<uint32_t>(), c->v.as<uint32_t>(), tb->slice,
@@ -445,27 +481,29 @@ static int readall_impl(ewal_ctx *c, const uint8_t *d_buf, uint64_t B, uint64_t 
     RecDesc *rd = c->rd.as<RecDesc>();
     const uint32_t *pfd = c->pf.as<uint32_t>(), *pfo = pfd + c->pfcap;
     const uint32_t nb = grid_for(n, 1024);
-    // look-back status words of k_check: zeroed when (re)allocated and when
-    // the 24-bit epoch wraps; otherwise the epoch tells old words apart
-    const size_t had = c->lbstat.cap;
-    EW_CHECK(c->lbstat.ensure((size_t)nb * 8));
-    c->epoch = (c->epoch + 1) & 0xffffffu;
-    if (c->lbstat.cap != had || c->epoch == 0) {
-      EW_CHECK(hipMemsetAsync(c->lbstat.p, 0, c->lbstat.cap, c->stream));
-      if (c->epoch == 0) c->epoch = 1;
-    }
     EW_CHECK(c->ops.ensure((size_t)n * 4));
-    EW_CHECK(c->opf.ensure((size_t)nb * 4));   // k_check's per-workgroup op bases
-    EW_CHECK(c->mlist.ensure((size_t)n * 4));
     EW_CHECK(c->kk.ensure((size_t)n * 8));
-    EW_CHECK(c->ents.ensure((size_t)n * sizeof(ewal_entry)));
-    hipLaunchKernelGGL(k_check<false>, dim3(nb), dim3(1024), 0, c->stream, tb->shift, rd, n32, pfd, pfo, ri,
-                       c->lbstat.as<unsigned long long>(), c->epoch, c->opf.as<uint32_t>(), c->ents.as<ewal_entry>(),
-                       c->mlist.as<uint32_t>(), ds, SegArgs{});
-    hipLaunchKernelGGL(k_result, dim3(1), dim3(256), 0, c->stream, d_buf, rd, c->mlist.as<uint32_t>(), n32, ri, ds,
-                       c->h_res_dev);
-    EW_CHECK(hipGetLastError());
-    EW_CHECK(hipStreamSynchronize(c->stream));
+    if (!spec_checked) {
+      // look-back status words of k_check: zeroed when (re)allocated and when
+      // the 24-bit epoch wraps; otherwise the epoch tells old words apart
+      const size_t had = c->lbstat.cap;
+      EW_CHECK(c->lbstat.ensure((size_t)nb * 8));
+      c->epoch = (c->epoch + 1) & 0xffffffu;
+      if (c->lbstat.cap != had || c->epoch == 0) {
+        EW_CHECK(hipMemsetAsync(c->lbstat.p, 0, c->lbstat.cap, c->stream));
+        if (c->epoch == 0) c->epoch = 1;
+      }
+      EW_CHECK(c->opf.ensure((size_t)nb * 4));   // k_check's per-workgroup op bases
+      EW_CHECK(c->mlist.ensure((size_t)n * 4));
+      EW_CHECK(c->ents.ensure((size_t)n * sizeof(ewal_entry)));
+      hipLaunchKernelGGL(k_check<false>, dim3(nb), dim3(1024), 0, c->stream, tb->shift, rd, n32, pfd, pfo, ri,
+                         c->lbstat.as<unsigned long long>(), c->epoch, c->opf.as<uint32_t>(),
+                         c->ents.as<ewal_entry>(), c->mlist.as<uint32_t>(), ds, SegArgs{}, (const uint32_t *)nullptr);
+      hipLaunchKernelGGL(k_result, dim3(1), dim3(256), 0, c->stream, d_buf, rd, c->mlist.as<uint32_t>(), n32, ri, ds,
+                         c->h_res_dev, (const uint32_t *)nullptr);
+      EW_CHECK(hipGetLastError());
+      EW_CHECK(hipStreamSynchronize(c->stream));
+    }
     std::memcpy(&res, c->h_res, sizeof(ResultDev));
     if (res.errflag) return EWAL_E_TIMEOUT;
     if (res.gapslow || res.nonmono)   // the rare paths work on the op list
@@ -476,7 +514,7 @@ static int readall_impl(ewal_ctx *c, const uint8_t *d_buf, uint64_t B, uint64_t 
       hipLaunchKernelGGL(k_gap, dim3(ggrid), dim3(256), 0, c->stream, rd, c->ops.as<uint32_t>(),
                          c->kk.as<uint64_t>(), ds);
       hipLaunchKernelGGL(k_result, dim3(1), dim3(256), 0, c->stream, d_buf, rd, c->mlist.as<uint32_t>(), n32, ri, ds,
-                       c->h_res_dev);
+                         c->h_res_dev, (const uint32_t *)nullptr);
       EW_CHECK(hipGetLastError());
       EW_CHECK(hipStreamSynchronize(c->stream));
       std::memcpy(&res, c->h_res, sizeof(ResultDev));
@@ -694,7 +732,7 @@ static int readall_batch_impl(ewal_ctx *c, const uint8_t *d_buf, uint32_t ns, co
       sg.sagg = c->bsagg.as<ShardAgg>();
       hipLaunchKernelGGL(k_check<true>, dim3(nb), dim3(1024), 0, c->stream, tb->shift, rd, n32, pf, pf + rdcap, 0ull,
                          c->lbstat.as<unsigned long long>(), c->epoch, c->opf.as<uint32_t>(),
-                         c->bents.as<ewal_entry>(), c->mlist.as<uint32_t>(), ds, sg);
+                         c->bents.as<ewal_entry>(), c->mlist.as<uint32_t>(), ds, sg, (const uint32_t *)nullptr);
       hipLaunchKernelGGL(k_meta_batch, dim3(64), dim3(256), 0, c->stream, d_buf, rd, c->mlist.as<uint32_t>(), ds, sg);
       hipLaunchKernelGGL(k_result_batch, dim3(grid_for(ns, 256)), dim3(256), 0, c->stream, rd, sg,
                          c->bres.as<ewal_result>(), c->bef.as<unsigned long long>());

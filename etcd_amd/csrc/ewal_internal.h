@@ -116,7 +116,7 @@ struct Small {
   uint32_t lastop;                // k_check: 1 + the last entry op's frame (0: none)
   uint32_t gapslow;               // k_check: an op's predecessor lies too far back (list-based k_gap)
   uint32_t segbad;                // k_shard_start: a shard does not start on a frame of the chain
-  uint32_t pad_s;
+  uint32_t spec_n;                // k_spec_gate: frames when k_frame's speculation holds, else 0
 };
 
 // Everything the host needs after the frame pass, gathered by k_result.

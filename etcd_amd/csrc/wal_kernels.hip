@@ -1408,7 +1408,16 @@ template <bool SEG>
 __global__ __launch_bounds__(1024) void k_check(const uint32_t *__restrict__ g_shift, RecDesc *__restrict__ rd,
                          uint32_t n, const uint32_t *__restrict__ pfd, const uint32_t *__restrict__ pfo, uint64_t ri,
                          unsigned long long *__restrict__ status, uint32_t epoch, uint32_t *__restrict__ wbase,
-                         ewal_entry *__restrict__ ents, uint32_t *__restrict__ mlist, Small *ds, SegArgs sg) {
+                         ewal_entry *__restrict__ ents, uint32_t *__restrict__ mlist, Small *ds, SegArgs sg,
+                         const uint32_t *n_dev = nullptr) {
+  // n_dev: launched before the host has seen k_frame's verdict (k_spec_gate
+  // left the frame count there, 0 when the speculation failed); the grid is
+  // sized for the descriptor capacity and the blocks past the frames leave
+  if (n_dev) {
+    n = *n_dev;
+    if (blockIdx.x * blockDim.x >= n) return;
+  }
+  const uint32_t last_block = (n - 1) / blockDim.x;
   ReadAllAgg *agg = &ds->agg;
   __shared__ uint32_t s_wo[16];          // ops per wave
   __shared__ uint32_t s_base;            // ops before the workgroup
@@ -1570,7 +1579,7 @@ __global__ __launch_bounds__(1024) void k_check(const uint32_t *__restrict__ g_s
     if (threadIdx.x == 0) {
       s_base = base;
       wbase[blockIdx.x] = base;   // k_opslist (rare paths) rebuilds ops / kk from it
-      if (blockIdx.x == gridDim.x - 1) ds->nsel3 = base + cnt;
+      if (blockIdx.x == last_block) ds->nsel3 = base + cnt;
       if (s_red[0]) atomicMax(&agg->last_entry, (long long)(s_red[0] - 1));
       if (s_red[1]) atomicMax(&agg->last_state, (long long)(s_red[1] - 1));
       if (s_red[2] != 0xffffffffu) atomicMin(&agg->first_meta, (unsigned long long)s_red[2]);
@@ -1656,6 +1665,18 @@ __global__ void k_gap(RecDesc *__restrict__ rd, const uint32_t *__restrict__ ops
   if (__ballot(nm) && (threadIdx.x & 63) == 0) atomicOr(&ds->nonmono, 1u);
 }
 
+// After k_frame: does the speculative frame pass hold (the host's test in
+// readall_impl, made on the device so that k_check and k_result can be
+// queued behind it without a host round trip)?  spec_n = frame count or 0;
+// then Small -> host-mapped memory like k_export_small.
+__global__ void k_spec_gate(Small *ds, uint64_t ccap, uint64_t rdcap, Small *h) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  const unsigned long long K = ds->total;
+  const bool ok = K && K <= ccap && K <= rdcap && !ds->novf && ds->pos0 == 0 && !ds->irregular;
+  ds->spec_n = ok ? (uint32_t)K : 0u;
+  *h = *ds;
+}
+
 // Small -> host-mapped pinned memory: a one-thread kernel is far cheaper
 // than a device-to-host copy of a few hundred bytes.
 __global__ void k_export_small(const Small *ds, Small *h) {
@@ -1670,7 +1691,11 @@ __global__ void k_export_small(const Small *ds, Small *h) {
 // gathers the result.
 __global__ __launch_bounds__(256) void k_result(const uint8_t *__restrict__ buf, RecDesc *__restrict__ rd,
                                                 const uint32_t *__restrict__ mlist, uint32_t n, uint64_t ri, Small *ds,
-                                                ResultDev *o) {
+                                                ResultDev *o, const uint32_t *n_dev = nullptr) {
+  if (n_dev) {   // speculative launch (see k_check): nothing to gather when it failed
+    n = *n_dev;
+    if (n == 0) return;
+  }
   const uint32_t nm = ds->nmeta;
   const unsigned long long fm = ds->agg.first_meta;
   if (fm != ~0ull) {
