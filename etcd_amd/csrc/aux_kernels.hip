@@ -68,6 +68,29 @@ __global__ __launch_bounds__(256) void k_snap(const uint8_t *__restrict__ buf, c
 
 // q-th largest of n <= 16 voters by rank counting (ties handled as Go's sort
 // would place them: the value at sorted-descending position q-1).
+// q-th largest of the n <= N match indexes of group g (any correct sort of
+// raft.go:252's mis gives the same order statistic): rank-select over N
+// register slots, so a wave of 5/7-voter groups compares 8 x 8, not 16 x 16.
+template <int N>
+__device__ __forceinline__ uint64_t quorum_select(const uint64_t *__restrict__ match, uint64_t G, uint64_t g, int n) {
+  uint64_t m[N];
+#pragma unroll
+  for (int v = 0; v < N; ++v) m[v] = v < n ? match[(uint64_t)v * G + g] : 0ull;
+  const int q = n / 2 + 1;
+  uint64_t mci = 0;
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    int gt = 0, ge = 0;
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+      gt += (j < n && m[j] > m[i]);
+      ge += (j < n && m[j] >= m[i]);
+    }
+    if (i < n && gt < q && q <= ge) mci = m[i];
+  }
+  return mci;
+}
+
 __global__ void k_commit(uint64_t G, const uint64_t *__restrict__ match, const uint8_t *__restrict__ nvoters,
                          const uint64_t *__restrict__ term, uint64_t *__restrict__ committed,
                          const uint64_t *__restrict__ log_offset, const uint64_t *__restrict__ log_ptr,
@@ -80,21 +103,7 @@ __global__ void k_commit(uint64_t G, const uint64_t *__restrict__ match, const u
   if (n <= 0 || n > 16) {
     st = EWAL_PANIC_BOUNDS;   // mis[q-1] on an empty slice (n == 0); n > 16 unsupported
   } else {
-    uint64_t m[16];
-#pragma unroll
-    for (int v = 0; v < 16; ++v) m[v] = v < n ? match[(uint64_t)v * G + g] : 0ull;
-    const int q = n / 2 + 1;
-    uint64_t mci = 0;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      int gt = 0, ge = 0;
-#pragma unroll
-      for (int j = 0; j < 16; ++j) {
-        gt += (j < n && m[j] > m[i]);
-        ge += (j < n && m[j] >= m[i]);
-      }
-      if (i < n && gt < q && q <= ge) mci = m[i];
-    }
+    const uint64_t mci = n <= 8 ? quorum_select<8>(match, G, g, n) : quorum_select<16>(match, G, g, n);
     uint64_t c = committed[g];
     if (mci > c) {
       const uint64_t off = log_offset[g];

@@ -361,7 +361,7 @@ def test_snapshotter_load_dir(ctx, tmp_path):
 def test_commit_batch(ctx):
     rng = random.Random(6)
     G = 5000
-    nv = [rng.choice([1, 3, 4, 5, 7, 16]) for _ in range(G)]
+    nv = [rng.choice([1, 2, 3, 4, 5, 7, 8, 9, 12, 16]) for _ in range(G)]
     match = [[0] * G for _ in range(16)]
     terms, committed, offs, ptr, logs = [], [], [], [0], []
     for g in range(G):
