@@ -267,6 +267,7 @@ def run_commit(a, dist, rank, world, local):
     d_st = torch.zeros(G, dtype=torch.uint8, device=dev)
     ctx = W.Context(local)
     ctx.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+    summary = torch.zeros(3, dtype=torch.int64, device=dev) if dist is not None else None
     dms = C.c_double(0)
     kms = []
 
@@ -279,6 +280,8 @@ def run_commit(a, dist, rank, world, local):
                                         C.c_void_p(d_st.data_ptr()), C.byref(dms))
         assert rc == 0, rc
         kms.append(dms.value)
+        if dist is not None:   # the node's commit-index summary (etcd_amd/shard.py), device scalars
+            shard.combine_commit(dist, d_ch.sum(dtype=torch.int64), d_c.min(), d_c.max(), out=summary)
 
     for _ in range(max(a.warmup, 1)):
         step()

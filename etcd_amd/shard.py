@@ -61,6 +61,20 @@ def combine_batch(dist, first_shard: int, verdicts, device="cpu", out=None):
     return int(t[0].item()), int(t[1].item()), int(t[2].item())
 
 
+def combine_commit(dist, changed, commit_min, commit_max, out=None, device="cpu"):
+    """The commit-index summary of a rank's raft-group range after a batched
+    maybeCommit (configs[4]): SUM of groups whose commit advanced, MIN and MAX
+    commit index over the node -- three words, two all-reduces.  Tensors may
+    be device scalars (no host sync before the exchange)."""
+    t = out if out is not None else torch.zeros(3, dtype=torch.int64, device=device)
+    t[0] = changed
+    t[1] = -commit_min    # MAX of the negation == MIN, so one MAX all-reduce carries both
+    t[2] = commit_max
+    dist.all_reduce(t[0:1], op=dist.ReduceOp.SUM)
+    dist.all_reduce(t[1:3], op=dist.ReduceOp.MAX)
+    return t
+
+
 def decode_key(key: int):
     """(shard, frame) of a combined key, or None when no shard failed."""
     if key >= NO_FAILURE:

@@ -27,6 +27,11 @@ def _worker(rank, world, port, cases, q):
         for c in cases:
             fr, n, failed = c["shards"][rank]
             out.append(shard.combine(dist, rank, fr, n, failed))
+        for c in cases:   # commit-index summaries (bench.py --workload commit)
+            if "commit" in c:
+                ch, lo, hi = c["commit"][rank]
+                out.append(tuple(int(x) for x in shard.combine_commit(dist, torch.tensor(ch), torch.tensor(lo),
+                                                                       torch.tensor(hi)).tolist()))
         for c in cases:   # the same shards as one batch per rank (bench.py --workload shards)
             if "batch" in c:
                 out.append(shard.combine_batch(dist, c["batch_first"][rank], c["batch"][rank]))
@@ -97,3 +102,11 @@ def test_combine_batch_two_ranks():
         key, frames, fails = out[1]
         assert shard.decode_key(key) == (1, 30)
         assert frames == 100 + 30 + 50 + 10 + 9 and fails == 2
+
+
+def test_combine_commit_two_ranks():
+    cases = [{"shards": [(-1, 1, False), (-1, 1, False)], "commit": [(5, 100, 900), (7, 40, 1200)]}]
+    res = _run(2, cases)
+    for rank, out, seams in res:
+        ch, negmin, hi = out[1]
+        assert (ch, -negmin, hi) == (12, 40, 1200)
