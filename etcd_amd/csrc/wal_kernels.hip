@@ -1313,9 +1313,13 @@ __global__ __launch_bounds__(256) void k_frame(const uint8_t *__restrict__ buf, 
   stage_lds<256>(s_svp, 1024, [&](int i) { return g_shift[EW_VLOG * 1024 + i]; });
   __syncthreads();
   uint32_t irr = 0;
+  // the candidate offsets of the NEXT iteration are loaded before this one's
+  // frame head, so their latency hides behind it (one memory round trip per
+  // frame instead of two)
+  uint64_t p = g0 < K ? pos[g0] : 0, pn = g0 + 1 < K ? pos[g0 + 1] : 0;
   for (uint64_t r = g0; r < K; r += stride) {
-    const uint64_t p = pos[r];
-    const uint64_t pn = r + 1 < K ? pos[r + 1] : 0;
+    const uint64_t rn = r + stride;
+    const uint64_t p2 = rn < K ? pos[rn] : 0, pn2 = rn + 1 < K ? pos[rn + 1] : 0;
     const int64_t L = decode_fast(buf, B, p, (uint32_t)r, r + 1 == K, pwave, v, s_t4, s_svp, s_win + threadIdx.x, rd,
                                   pfd, pfo, slow, ds, dbg);
     const uint64_t s = p + 8 + (uint64_t)L;
@@ -1325,6 +1329,8 @@ __global__ __launch_bounds__(256) void k_frame(const uint8_t *__restrict__ buf, 
       ds->q = s;
       ds->qlen = (s <= B && B - s >= 8) ? (int64_t)ld_le64_b(buf, B, s) : 0;
     }
+    p = p2;
+    pn = pn2;
   }
   if (__ballot(irr) && (threadIdx.x & 63) == 0) atomicOr(&ds->irregular, 1u);
 }
