@@ -70,7 +70,7 @@ class MessageDesc(C.Structure):   # emsg_message
 class Result(C.Structure):
     _fields_ = [("status", C.c_int32), ("flags", C.c_int32), ("detail", C.c_int64), ("fail_record", C.c_int64),
                 ("fail_offset", C.c_int64), ("n_records", C.c_int64), ("last_crc", C.c_uint32),
-                ("reserved0", C.c_uint32), ("enti", C.c_uint64), ("metadata_off", C.c_int64),
+                ("n_unrec", C.c_uint32), ("enti", C.c_uint64), ("metadata_off", C.c_int64),
                 ("metadata_len", C.c_int64), ("has_state", C.c_int32), ("n_slow", C.c_int32),
                 ("state_term", C.c_uint64), ("state_vote", C.c_uint64), ("state_commit", C.c_uint64),
                 ("n_ents", C.c_int64), ("n_candidates", C.c_int64), ("n_runs", C.c_int64), ("device_ms", C.c_double),
@@ -80,6 +80,10 @@ class Result(C.Structure):
 class EntryDesc(C.Structure):
     _fields_ = [("term", C.c_uint64), ("index", C.c_uint64), ("data_off", C.c_uint64), ("data_len", C.c_uint64),
                 ("type", C.c_int32), ("data_nil", C.c_int32)]
+
+
+class UnrecDesc(C.Structure):    # ewal_unrec
+    _fields_ = [("ent", C.c_int64), ("off", C.c_uint64), ("len", C.c_uint64)]
 
 
 class RecordDesc(C.Structure):
@@ -118,6 +122,8 @@ _SIGS = {
     "emsg_copy_entries": (C.c_int64, [vp, C.c_uint64, C.POINTER(EntryDesc), C.c_int64]),
     "ewal_batch_copy_entries": (C.c_int64, [vp, C.c_uint64, C.POINTER(EntryDesc), C.c_int64]),
     "ewal_copy_records": (C.c_int64, [vp, C.POINTER(RecordDesc), C.c_int64]),
+    "ewal_copy_unrec": (C.c_int64, [vp, C.POINTER(UnrecDesc), C.c_int64]),
+    "ewal_copy_unrec_bytes": (C.c_int64, [vp, vp, C.c_int64]),
     "ewal_open_at_index": (C.c_int, [C.c_char_p, C.c_uint64, C.POINTER(vp)]),
     "ewal_wal_readall": (C.c_int, [vp, vp, C.POINTER(Result)]),
     "ewal_wal_bytes": (u8p, [vp, C.POINTER(C.c_uint64)]),

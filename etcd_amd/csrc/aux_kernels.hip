@@ -35,7 +35,10 @@ __global__ __launch_bounds__(256) void k_snap(const uint8_t *__restrict__ buf, c
   d.computed = 0;
   if (st == 0) {
     // crc32.Update(0, crcTable, Data) = S_n(~0 ^ P(s)) ^ P(e) ^ ~0
-    if (d.dlen == 0) {
+    if (a2.split) {   // Data = the concatenation of its segments (snap.pb.go append)
+      const uint32_t lin = bytes_field_lin(buf + d.off, (int64_t)d.len, 2, d.off, buf, pwave, v, s_t4, s_svp, g_shift);
+      d.computed = gshift_n(g_shift, d.dlen, 0xffffffffu) ^ lin ^ 0xffffffffu;
+    } else if (d.dlen == 0) {
       d.computed = 0;
     } else {
       const uint32_t Ps = prefix_at(d.doff, pwave, v, buf, s_t4, s_svp);
@@ -44,6 +47,8 @@ __global__ __launch_bounds__(256) void k_snap(const uint8_t *__restrict__ buf, c
     }
     if (d.computed != d.stored) {
       st = EWAL_ERR_SNAP_CRC;
+    } else if (a2.split) {
+      st = EWAL_UNSUPPORTED_ENCODING;   // raftpb.Snapshot over the concatenation: not decoded here
     } else {
       PbField s1, s2, s3, s4, s5;
       pbf_init(s1); pbf_init(s2); pbf_init(s3); pbf_init(s4); pbf_init(s5);
@@ -52,7 +57,9 @@ __global__ __launch_bounds__(256) void k_snap(const uint8_t *__restrict__ buf, c
       int st2 = d.dlen ? pb_walk<PB_BYTES, PB_REP64, PB_VAR64, PB_VAR64, PB_REP64>(
                              buf + d.doff, (int64_t)d.dlen, s1, s2, s3, s4, s5, ur, o->nodes, o->removed, 64)
                        : 0;
-      if (st2 == 0 && ur) st2 = EWAL_UNSUPPORTED_ENCODING;  // Snapshot.XXX_unrecognized is returned
+      // Snapshot.XXX_unrecognized is returned; Data in several segments / more
+      // Nodes or RemovedNodes than esnap_snapshot holds: not decoded here
+      if (st2 == 0 && (ur || s1.split || s2.split || s5.split)) st2 = EWAL_UNSUPPORTED_ENCODING;
       st = st2;
       o->index = s3.v;
       o->term = s4.v;
@@ -91,6 +98,23 @@ __device__ __forceinline__ uint64_t quorum_select(const uint64_t *__restrict__ m
   return mci;
 }
 
+// Any voter count (nvoters is a uint8): rank-select straight from memory
+// (more than 16 voters is rare; the register forms above cover 5 / 7).
+__device__ __noinline__ uint64_t quorum_select_any(const uint64_t *__restrict__ match, uint64_t G, uint64_t g, int n) {
+  const int q = n / 2 + 1;
+  for (int i = 0; i < n; ++i) {
+    const uint64_t mi = match[(uint64_t)i * G + g];
+    int gt = 0, ge = 0;
+    for (int j = 0; j < n; ++j) {
+      const uint64_t mj = match[(uint64_t)j * G + g];
+      gt += mj > mi;
+      ge += mj >= mi;
+    }
+    if (gt < q && q <= ge) return mi;
+  }
+  return 0;
+}
+
 __global__ void k_commit(uint64_t G, const uint64_t *__restrict__ match, const uint8_t *__restrict__ nvoters,
                          const uint64_t *__restrict__ term, uint64_t *__restrict__ committed,
                          const uint64_t *__restrict__ log_offset, const uint64_t *__restrict__ log_ptr,
@@ -100,10 +124,11 @@ __global__ void k_commit(uint64_t G, const uint64_t *__restrict__ match, const u
   if (g >= G) return;
   const int n = nvoters[g];
   uint8_t chg = 0, st = 0;
-  if (n <= 0 || n > 16) {
-    st = EWAL_PANIC_BOUNDS;   // mis[q-1] on an empty slice (n == 0); n > 16 unsupported
+  if (n <= 0) {
+    st = EWAL_PANIC_BOUNDS;   // mis[q-1] on an empty slice (raft/raft.go:255)
   } else {
-    const uint64_t mci = n <= 8 ? quorum_select<8>(match, G, g, n) : quorum_select<16>(match, G, g, n);
+    const uint64_t mci = n <= 8 ? quorum_select<8>(match, G, g, n)
+                         : n <= 16 ? quorum_select<16>(match, G, g, n) : quorum_select_any(match, G, g, n);
     uint64_t c = committed[g];
     if (mci > c) {
       const uint64_t off = log_offset[g];

@@ -39,9 +39,23 @@ struct DevTables {
   uint32_t *shift = nullptr;  // [48][4][256]
 };
 
+// Grow-only device buffer owned by a ctx (freed by its destructor when the
+// ctx is deleted; ewal_ctx_destroy makes the ctx's device current first).
 struct DevBuf {
   void *p = nullptr;
   size_t cap = 0;
+  DevBuf() = default;
+  DevBuf(const DevBuf &) = delete;
+  DevBuf &operator=(const DevBuf &) = delete;
+  ~DevBuf() { release(); }
+  // take o's allocation (ours is released first)
+  void adopt(DevBuf &o) {
+    release();
+    p = o.p;
+    cap = o.cap;
+    o.p = nullptr;
+    o.cap = 0;
+  }
   // grow-only device buffer
   hipError_t ensure(size_t n) {
     if (n <= cap) return hipSuccess;
@@ -74,7 +88,9 @@ struct ewal_ctx {
   std::map<uint32_t, DevTables> tables;
   std::map<uint32_t, std::unique_ptr<ewal::CrcTables>> host_tables;
   DevBuf encw, encs, lbstat, gagg, slow, mlist, pf, v, pwave, ux, tagg, tpx, wcnt, slots, cbase, ovf, cpos, clen, nxt, exc, E, rs, jl, vis, entry, on, rec_cand, rd, opf, ops, kk, kkrev, suf,
-      ents, recs, tmp, small, sdesc, snaps, hbuf_dev;
+      ents, recs, tmp, small, sdesc, snaps, hbuf_dev, xpos, walk, fpos, ulist, uitems, uarena;
+  std::vector<ewal_unrec> unrec;   // XXX_unrecognized of the last ReadAll's result (side list)
+  uint64_t unrec_bytes = 0;
   // batched ReadAll (ewal_readall_batch_device): shard tables, results, ents
   DevBuf bfs, bsoff, bri, bsagg, bres, bef, bents, bshard;
   // batched raftpb.Message decode (emsg_decode_batch_device)
@@ -225,22 +241,28 @@ static int sync_small(ewal_ctx *c) {
   return 0;
 }
 
-// decoder.decode at frame start q when q is not a frame of the chain
+// decoder.decode at frame start q when q is not a candidate of the chain
 // (wal/decoder.go:28-39 + io.ReadFull's EOF/ErrUnexpectedEOF rule); L is the
-// int64 at q (valid when q + 8 <= B).
+// int64 at q (valid when q + 8 <= B).  EWAL_FRAME_FITS: a whole frame lies
+// at q that the candidate filter did not admit -- k_walk decodes it.
+#define EWAL_FRAME_FITS (-100)
 static int classify_terminal(uint64_t B, uint64_t q, int64_t L) {
   if (q == B) return EWAL_OK;
   if (B - q < 8) return EWAL_ERR_UNEXPECTED_EOF;
   const uint64_t rem = B - q - 8;
   if (L < 0) return EWAL_PANIC_NEG_LENGTH;
   if ((uint64_t)L > rem) return rem == 0 ? EWAL_OK : EWAL_ERR_UNEXPECTED_EOF;
-  return EWAL_UNSUPPORTED_ENCODING;   // a frame that fits but is not canonical
+  return EWAL_FRAME_FITS;
 }
 
-// Framing when the candidates do not form one chain from byte 0: runs of
-// consecutive candidates, pointer jumping over runs, membership (k_runs ..
-// k_member); returns the chain length n (c->rec_cand) and its terminal q.
-static int frame_irregular(ewal_ctx *c, uint64_t K, ewal_result *out, uint64_t *n_out, uint64_t *q_out) {
+// Pointer jumping over runs of consecutive candidates (the candidate links
+// from k_link's nxt / exc): run ends E, jump levels J, marks cleared.
+struct JumpState {
+  uint32_t R = 0;
+  int top = 0;
+  bool ready = false;
+};
+static int jump_prepare(ewal_ctx *c, uint64_t K, JumpState *js) {
   Small *ds = c->small.as<Small>();
   const uint32_t K32 = (uint32_t)K;
   EW_CHECK(c->E.ensure((size_t)K * 4));
@@ -248,7 +270,6 @@ static int frame_irregular(ewal_ctx *c, uint64_t K, ewal_result *out, uint64_t *
   if (rc) return rc;
   if ((rc = sync_small(c))) return rc;
   const uint32_t R = c->h_small->nsel;
-  out->n_runs = R;
   int top = 0;
   while ((1ull << top) < R) ++top;
   EW_CHECK(c->jl.ensure((size_t)R * 4 * (top + 1)));
@@ -261,28 +282,65 @@ static int frame_irregular(ewal_ctx *c, uint64_t K, ewal_result *out, uint64_t *
     hipLaunchKernelGGL(k_jump, dim3(grid_for(R, 256)), dim3(256), 0, c->stream, J + (size_t)(k - 1) * R,
                        J + (size_t)k * R, R);
   EW_CHECK(hipMemsetAsync(c->vis.p, 0, R, c->stream));
-  EW_CHECK(hipMemsetAsync(c->vis.p, 1, 1, c->stream));
-  for (int k = top; k >= 0; --k)
+  EW_CHECK(hipMemsetAsync(c->entry.p, 0xff, (size_t)R * 4, c->stream));
+  EW_CHECK(hipGetLastError());
+  js->R = R;
+  js->top = top;
+  js->ready = true;
+  return 0;
+}
+
+// Marks the chain segment starting at candidate `cand` (segments are marked
+// in position order); returns its terminal candidate and the offset after it.
+static int jump_mark(ewal_ctx *c, const JumpState &js, uint32_t cand, uint32_t *last_cand, uint64_t *q_out) {
+  Small *ds = c->small.as<Small>();
+  const uint32_t R = js.R;
+  uint32_t *J = c->jl.as<uint32_t>();
+  hipLaunchKernelGGL(k_jstart, dim3(1), dim3(64), 0, c->stream, c->E.as<uint32_t>(), R, cand, c->vis.as<uint8_t>(),
+                     c->entry.as<uint32_t>(), &ds->ci);
+  for (int k = js.top; k >= 0; --k)
     hipLaunchKernelGGL(k_mark, dim3(grid_for(R, 256)), dim3(256), 0, c->stream, J + (size_t)k * R,
                        c->vis.as<uint8_t>(), R);
-  EW_CHECK(hipMemsetAsync(c->entry.p, 0xff, (size_t)R * 4, c->stream));
   hipLaunchKernelGGL(k_entry, dim3(grid_for(R, 256)), dim3(256), 0, c->stream, c->E.as<uint32_t>(),
                      c->nxt.as<uint32_t>(), J, c->vis.as<uint8_t>(), R, c->entry.as<uint32_t>(), &ds->ci);
-  EW_CHECK(c->on.ensure(K));
-  EW_CHECK(c->rec_cand.ensure((size_t)K * 4));
-  hipLaunchKernelGGL(k_member, dim3(grid_for(K, 256)), dim3(256), 0, c->stream, c->E.as<uint32_t>(), R,
-                     c->vis.as<uint8_t>(), c->entry.as<uint32_t>(), K32, c->on.as<uint8_t>());
-  rc = select_flagged(c, c->on.as<uint8_t>(), K32, c->rec_cand.as<uint32_t>(), &ds->nsel2);
+  EW_CHECK(hipGetLastError());
+  int rc = sync_small(c);
   if (rc) return rc;
-  if ((rc = sync_small(c))) return rc;
   const uint32_t lc = c->h_small->ci.last_cand;
   uint64_t pl[2];
   EW_CHECK(hipMemcpyAsync(&pl[0], c->cpos.as<uint64_t>() + lc, 8, hipMemcpyDeviceToHost, c->stream));
   EW_CHECK(hipMemcpyAsync(&pl[1], c->clen.as<uint64_t>() + lc, 8, hipMemcpyDeviceToHost, c->stream));
   EW_CHECK(hipStreamSynchronize(c->stream));
-  *n_out = c->h_small->nsel2;
+  *last_cand = lc;
   *q_out = pl[0] + 8 + pl[1];
   return 0;
+}
+
+// The marked candidates -> rec_cand (ascending); returns their count.
+static int jump_finish(ewal_ctx *c, uint64_t K, const JumpState &js, uint64_t *n_out) {
+  Small *ds = c->small.as<Small>();
+  const uint32_t K32 = (uint32_t)K;
+  EW_CHECK(c->on.ensure(K));
+  EW_CHECK(c->rec_cand.ensure((size_t)K * 4));
+  hipLaunchKernelGGL(k_member, dim3(grid_for(K, 256)), dim3(256), 0, c->stream, c->E.as<uint32_t>(), js.R,
+                     c->vis.as<uint8_t>(), c->entry.as<uint32_t>(), K32, c->on.as<uint8_t>());
+  int rc = select_flagged(c, c->on.as<uint8_t>(), K32, c->rec_cand.as<uint32_t>(), &ds->nsel2);
+  if (rc) return rc;
+  if ((rc = sync_small(c))) return rc;
+  *n_out = c->h_small->nsel2;
+  return 0;
+}
+
+// Framing when the candidates do not form one chain from byte 0: the chain
+// from candidate 0 by pointer jumping; returns its length n (c->rec_cand),
+// its last candidate and its terminal q.
+static int frame_irregular(ewal_ctx *c, uint64_t K, ewal_result *out, JumpState *js, uint64_t *n_out,
+                           uint32_t *last_cand, uint64_t *q_out) {
+  int rc = jump_prepare(c, K, js);
+  if (rc) return rc;
+  out->n_runs = js->R;
+  if ((rc = jump_mark(c, *js, 0, last_cand, q_out))) return rc;
+  return jump_finish(c, K, *js, n_out);
 }
 
 static int read_le64_at(ewal_ctx *c, const uint8_t *d_buf, uint64_t B, uint64_t q, int64_t *L) {
@@ -290,6 +348,131 @@ static int read_le64_at(ewal_ctx *c, const uint8_t *d_buf, uint64_t B, uint64_t 
   if (q + 8 > B) return 0;
   EW_CHECK(hipMemcpyAsync(L, d_buf + q, 8, hipMemcpyDeviceToHost, c->stream));
   EW_CHECK(hipStreamSynchronize(c->stream));
+  return 0;
+}
+
+// The chain's terminal q holds a frame the candidate filter did not admit
+// (classify_terminal == EWAL_FRAME_FITS): k_walk decodes frames from q on
+// until the chain meets a candidate again (marked from there by pointer
+// jumping; the walk continues at that segment's terminal), ends, or a frame
+// fails.  The walked frames are appended to `xs` (ascending); *tst is the
+// final terminal class (EWAL_OK when a walked frame fails: k_check reports
+// that frame), *q_out its offset.  `regular`: every candidate is on the
+// chain already (no segment can follow).  On return *n_cands is the number
+// of chain candidates (rec_cand when js->ready, else candidates 0..n-1).
+static int walk_chain(ewal_ctx *c, DevTables *tb, const uint8_t *d_buf, uint64_t B, uint64_t K, bool regular,
+                      JumpState *js, uint32_t pc, uint64_t *n_cands, uint64_t *q_out, int *tst,
+                      std::vector<uint64_t> &xs) {
+  const uint32_t xcap = 1u << 16;
+  EW_CHECK(c->xpos.ensure((size_t)xcap * 8));
+  EW_CHECK(c->walk.ensure(sizeof(WalkOut)));
+  uint64_t q = *q_out;
+  bool has_seed = false;
+  uint32_t seed = 0;
+  bool marked = false;   // a segment after the first was marked: rec_cand needs rebuilding
+  for (;;) {
+    hipLaunchKernelGGL(k_walk, dim3(1), dim3(64), 0, c->stream, d_buf, B, q, c->cpos.as<uint64_t>(), K, pc,
+                       (int)has_seed, seed, c->pwave.as<uint32_t>(), c->v.as<uint32_t>(), tb->slice, tb->shift,
+                       c->xpos.as<uint64_t>(), xcap, c->walk.as<WalkOut>());
+    EW_CHECK(hipGetLastError());
+    WalkOut w;
+    EW_CHECK(hipMemcpyAsync(&w, c->walk.p, sizeof(w), hipMemcpyDeviceToHost, c->stream));
+    EW_CHECK(hipStreamSynchronize(c->stream));
+    if (w.n) {
+      const size_t at = xs.size();
+      xs.resize(at + w.n);
+      EW_CHECK(hipMemcpy(xs.data() + at, c->xpos.p, (size_t)w.n * 8, hipMemcpyDeviceToHost));
+    }
+    if (w.stopped) {   // a walked frame fails: ReadAll ends there
+      *tst = EWAL_OK;
+      *q_out = w.x;
+      break;
+    }
+    if (w.term >= 0) {
+      *tst = w.term;
+      *q_out = w.x;
+      break;
+    }
+    if (w.resume == ~0ull) {   // the list filled: continue from x
+      q = w.x;
+      has_seed = true;
+      seed = w.seed;
+      continue;
+    }
+    // the chain meets candidate w.resume: mark the segment from there
+    if (regular) return EWAL_E_INVAL;   // impossible: every candidate lies before q
+    if (!js->ready) {
+      int rc = jump_prepare(c, K, js);
+      if (rc) return rc;
+    }
+    uint32_t lc = 0;
+    int rc = jump_mark(c, *js, (uint32_t)w.resume, &lc, &q);
+    if (rc) return rc;
+    marked = true;
+    int64_t qlen = 0;
+    if ((rc = read_le64_at(c, d_buf, B, q, &qlen))) return rc;
+    const int t = classify_terminal(B, q, qlen);
+    if (t != EWAL_FRAME_FITS) {
+      *tst = t;
+      *q_out = q;
+      break;
+    }
+    pc = lc;
+    has_seed = false;
+  }
+  if (marked) return jump_finish(c, K, *js, n_cands);
+  return 0;
+}
+
+// XXX_unrecognized of the returned ents / HardState (wal/wal.go:164-216
+// returns them inside the structs; raft.pb.go:270 appends each unknown
+// field): the entry ops k_check listed that survive in ents (op j is ents[j]
+// when the ops' indexes rise by one; after index rewinds, ents[k_j] iff every
+// later op has a larger k) and the last HardState.  Their bytes are gathered
+// on the device into the side buffer (rare: etcd's encoder never writes
+// unknown fields).
+static int gather_unrec(ewal_ctx *c, const uint8_t *d_buf, const ResultDev &res, const ReadAllAgg &agg,
+                        uint64_t nents) {
+  std::vector<UnrecItem> items;
+  if (agg.last_state >= 0 && res.sd.pad1) items.push_back(UnrecItem{(uint32_t)agg.last_state, 0, -1, 0, 0});
+  if (res.nunrec) {
+    std::vector<uint2> ul(res.nunrec);
+    EW_CHECK(hipMemcpy(ul.data(), c->ulist.p, (size_t)res.nunrec * sizeof(uint2), hipMemcpyDeviceToHost));
+    for (const uint2 &u : ul) {
+      int64_t slot = u.y;
+      if (res.nonmono) {   // kk = each op's k, kkrev = suffix minimum of kk (the rewind pass above)
+        uint64_t k = 0, later = ~0ull;
+        EW_CHECK(hipMemcpy(&k, c->kk.as<uint64_t>() + u.y, 8, hipMemcpyDeviceToHost));
+        if (u.y + 1 < res.nops)
+          EW_CHECK(hipMemcpy(&later, c->kkrev.as<uint64_t>() + u.y + 1, 8, hipMemcpyDeviceToHost));
+        if (!(k < later && k < nents)) continue;   // overwritten by a later op
+        slot = (int64_t)k;
+      }
+      items.push_back(UnrecItem{u.x, 0, slot, 0, 0});
+    }
+  }
+  std::sort(items.begin(), items.end(), [](const UnrecItem &a, const UnrecItem &b) { return a.ent < b.ent; });
+  const uint32_t m = (uint32_t)items.size();
+  if (!m) return 0;
+  EW_CHECK(c->uitems.ensure((size_t)m * sizeof(UnrecItem)));
+  EW_CHECK(hipMemcpyAsync(c->uitems.p, items.data(), (size_t)m * sizeof(UnrecItem), hipMemcpyHostToDevice, c->stream));
+  hipLaunchKernelGGL(k_unrec<0>, dim3(grid_for(m, 64)), dim3(64), 0, c->stream, d_buf, c->rd.as<RecDesc>(),
+                     c->uitems.as<UnrecItem>(), m, (uint8_t *)nullptr);
+  EW_CHECK(hipMemcpyAsync(items.data(), c->uitems.p, (size_t)m * sizeof(UnrecItem), hipMemcpyDeviceToHost, c->stream));
+  EW_CHECK(hipStreamSynchronize(c->stream));
+  uint64_t tot = 0;
+  for (UnrecItem &it : items) {
+    it.off = tot;
+    tot += it.len;
+  }
+  EW_CHECK(c->uarena.ensure(tot + 16));
+  EW_CHECK(hipMemcpyAsync(c->uitems.p, items.data(), (size_t)m * sizeof(UnrecItem), hipMemcpyHostToDevice, c->stream));
+  hipLaunchKernelGGL(k_unrec<1>, dim3(grid_for(m, 64)), dim3(64), 0, c->stream, d_buf, c->rd.as<RecDesc>(),
+                     c->uitems.as<UnrecItem>(), m, c->uarena.as<uint8_t>());
+  EW_CHECK(hipGetLastError());
+  EW_CHECK(hipStreamSynchronize(c->stream));
+  for (const UnrecItem &it : items) c->unrec.push_back(ewal_unrec{it.ent, it.off, it.len});
+  c->unrec_bytes = tot;
   return 0;
 }
 
@@ -304,6 +487,8 @@ static int readall_impl(ewal_ctx *c, const uint8_t *d_buf, uint64_t B, uint64_t 
   c->last_ok = false;
   c->last_n = 0;
   c->last_nents = 0;
+  c->unrec.clear();
+  c->unrec_bytes = 0;
   if (((uintptr_t)d_buf & 15) != 0 && B) return EWAL_E_INVAL;
   DevTables *tb;
   int rc = get_tables(c, 0x82F63B78u, &tb);
@@ -364,10 +549,13 @@ static int readall_impl(ewal_ctx *c, const uint8_t *d_buf, uint64_t B, uint64_t 
         EW_CHECK(c->opf.ensure((size_t)nbs * 4));
         EW_CHECK(c->mlist.ensure((size_t)rdcap * 4));
         EW_CHECK(c->ents.ensure((size_t)rdcap * sizeof(ewal_entry)));
+        EW_CHECK(c->ulist.ensure((size_t)rdcap * sizeof(uint2)));
+        SegArgs useg{};
+        useg.ulist = c->ulist.as<uint2>();
         hipLaunchKernelGGL(k_check<false>, dim3(nbs), dim3(1024), 0, c->stream, tb->shift, c->rd.as<RecDesc>(),
                            (uint32_t)rdcap, (const uint32_t *)pf, (const uint32_t *)(pf + rdcap), ri,
                            c->lbstat.as<unsigned long long>(), c->epoch, c->opf.as<uint32_t>(),
-                           c->ents.as<ewal_entry>(), c->mlist.as<uint32_t>(), ds, SegArgs{},
+                           c->ents.as<ewal_entry>(), c->mlist.as<uint32_t>(), ds, useg,
                            (const uint32_t *)&ds->spec_n);
         hipLaunchKernelGGL(k_result, dim3(1), dim3(256), 0, c->stream, d_buf, c->rd.as<RecDesc>(),
                            c->mlist.as<uint32_t>(), 0u, ri, ds, c->h_res_dev, (const uint32_t *)&ds->spec_n);
@@ -433,6 +621,8 @@ static int readall_impl(ewal_ctx *c, const uint8_t *d_buf, uint64_t B, uint64_t 
     }
   }
   out->n_candidates = (int64_t)K;
+  JumpState js;
+  uint32_t last_cand = EW_NIL;   // the chain's last candidate
   if (K && c->h_small->pos0 == 0) {
     if (!c->h_small->irregular) {
       regular = true;
@@ -440,8 +630,9 @@ static int readall_impl(ewal_ctx *c, const uint8_t *d_buf, uint64_t B, uint64_t 
       q = c->h_small->q;
       qlen = c->h_small->qlen;
       out->n_runs = 1;
+      last_cand = (uint32_t)(K - 1);
     } else {
-      rc = frame_irregular(c, K, out, &n, &q);
+      rc = frame_irregular(c, K, out, &js, &n, &last_cand, &q);
       if (rc) return rc;
       rc = read_le64_at(c, d_buf, B, q, &qlen);
       if (rc) return rc;
@@ -450,7 +641,36 @@ static int readall_impl(ewal_ctx *c, const uint8_t *d_buf, uint64_t B, uint64_t 
     rc = read_le64_at(c, d_buf, B, 0, &qlen);   // frame 0 is not a candidate: the chain is empty
     if (rc) return rc;
   }
-  const int tst = classify_terminal(B, q, qlen);
+  int tst = classify_terminal(B, q, qlen);
+  // walked frames (not candidates) on the chain: decoded and checked with the
+  // chain's candidates from one frame-position list (fpos)
+  std::vector<uint64_t> xs;
+  const uint64_t *fpos = nullptr;
+  if (tst == EWAL_FRAME_FITS) {
+    if (!K) {   // no candidate list at all: k_walk's search sees an empty one
+      EW_CHECK(c->cpos.ensure(8));
+    }
+    rc = walk_chain(c, tb, d_buf, B, K, regular, &js, n ? last_cand : EW_NIL, &n, &q, &tst, xs);
+    if (rc) return rc;
+    const uint64_t nx = xs.size();
+    if (nx) {
+      const uint64_t nt = n + nx;
+      if (nt >= 0xffffffffull) return EWAL_E_NOMEM;
+      EW_CHECK(c->fpos.ensure((size_t)nt * 8));
+      EW_CHECK(c->xpos.ensure((size_t)nx * 8));
+      EW_CHECK(hipMemcpyAsync(c->xpos.p, xs.data(), (size_t)nx * 8, hipMemcpyHostToDevice, c->stream));
+      const uint32_t *rcl = (regular || !js.ready) ? (const uint32_t *)nullptr : c->rec_cand.as<uint32_t>();
+      hipLaunchKernelGGL(k_fpos, dim3(grid_for(nt, 256)), dim3(256), 0, c->stream, c->cpos.as<uint64_t>(), rcl,
+                         (uint32_t)n, c->xpos.as<uint64_t>(), (uint32_t)nx, c->fpos.as<uint64_t>());
+      // the frame list changed: decode and check it again from fresh reductions
+      hipLaunchKernelGGL(k_reset_check, dim3(1), dim3(64), 0, c->stream, ds);
+      EW_CHECK(hipGetLastError());
+      fpos = c->fpos.as<uint64_t>();
+      n = nt;
+      decoded = false;
+      spec_checked = false;
+    }
+  }
 
   ResultDev res;
   std::memset(&res, 0, sizeof(res));
@@ -468,13 +688,14 @@ static int readall_impl(ewal_ctx *c, const uint8_t *d_buf, uint64_t B, uint64_t 
         c->pfcap = n;
       }
       uint32_t *pf = c->pf.as<uint32_t>();
-      const uint32_t *rc_list = regular ? (const uint32_t *)nullptr : c->rec_cand.as<uint32_t>();
+      const uint32_t *rc_list = (regular || fpos) ? (const uint32_t *)nullptr : c->rec_cand.as<uint32_t>();
+      const uint64_t *plist = fpos ? fpos : c->cpos.as<uint64_t>();
       EW_CHECK(hipMemsetAsync(&ds->nslow, 0, 4, c->stream));
       hipLaunchKernelGGL(k_decode, dim3(grid_for(n, 256)), dim3(256), 0, c->stream, d_buf, B,
-                         c->cpos.as<uint64_t>(), rc_list, n32, c->pwave.as<uint32_t>(), c->v.as<uint32_t>(),
+                         plist, rc_list, n32, c->pwave.as<uint32_t>(), c->v.as<uint32_t>(),
                          tb->slice, tb->shift, c->rd.as<RecDesc>(), pf, pf + c->pfcap, c->slow.as<uint32_t>(), ds);
       hipLaunchKernelGGL(k_decode_slow, dim3(std::min<uint64_t>(grid_for(n, 256), 64)), dim3(256), 0, c->stream,
-                         d_buf, B, c->cpos.as<uint64_t>(), rc_list, c->slow.as<uint32_t>(), ds,
+                         d_buf, B, plist, rc_list, c->slow.as<uint32_t>(), ds,
                          c->pwave.as<uint32_t>(), c->v.as<uint32_t>(), tb->slice, tb->shift, c->rd.as<RecDesc>(), pf,
                          pf + c->pfcap, n32);
     }
@@ -496,9 +717,12 @@ static int readall_impl(ewal_ctx *c, const uint8_t *d_buf, uint64_t B, uint64_t 
       EW_CHECK(c->opf.ensure((size_t)nb * 4));   // k_check's per-workgroup op bases
       EW_CHECK(c->mlist.ensure((size_t)n * 4));
       EW_CHECK(c->ents.ensure((size_t)n * sizeof(ewal_entry)));
+      EW_CHECK(c->ulist.ensure((size_t)n * sizeof(uint2)));
+      SegArgs useg{};
+      useg.ulist = c->ulist.as<uint2>();
       hipLaunchKernelGGL(k_check<false>, dim3(nb), dim3(1024), 0, c->stream, tb->shift, rd, n32, pfd, pfo, ri,
                          c->lbstat.as<unsigned long long>(), c->epoch, c->opf.as<uint32_t>(),
-                         c->ents.as<ewal_entry>(), c->mlist.as<uint32_t>(), ds, SegArgs{}, (const uint32_t *)nullptr);
+                         c->ents.as<ewal_entry>(), c->mlist.as<uint32_t>(), ds, useg, (const uint32_t *)nullptr);
       hipLaunchKernelGGL(k_result, dim3(1), dim3(256), 0, c->stream, d_buf, rd, c->mlist.as<uint32_t>(), n32, ri, ds,
                          c->h_res_dev, (const uint32_t *)nullptr);
       EW_CHECK(hipGetLastError());
@@ -578,6 +802,11 @@ static int readall_impl(ewal_ctx *c, const uint8_t *d_buf, uint64_t B, uint64_t 
           EW_CHECK(hipGetLastError());
         }
         c->last_nents = nents;
+        if (res.nunrec || (hagg.last_state >= 0 && res.sd.pad1)) {
+          rc = gather_unrec(c, d_buf, res, hagg, nents);
+          if (rc) return rc;
+          out->n_unrec = (uint32_t)c->unrec.size();
+        }
       }
       c->last_ok = true;
     }
@@ -609,8 +838,7 @@ static hipError_t grow_keep(DevBuf &b, size_t need, size_t keep, hipStream_t st)
       return e;
     }
   }
-  b.release();
-  b = nb;
+  b.adopt(nb);
   return hipSuccess;
 }
 
@@ -724,7 +952,9 @@ static int readall_batch_impl(ewal_ctx *c, const uint8_t *d_buf, uint32_t ns, co
       EW_CHECK(c->opf.ensure((size_t)nb * 4));
       EW_CHECK(c->mlist.ensure((size_t)K * 4));
       EW_CHECK(grow_keep(c->bents, (size_t)K * sizeof(ewal_entry), 0, c->stream));
+      EW_CHECK(c->ulist.ensure((size_t)K * sizeof(uint2)));
       SegArgs sg;
+      sg.ulist = c->ulist.as<uint2>();
       sg.fs = c->bfs.as<uint32_t>();
       sg.ns = ns;
       sg.ri = c->bri.as<uint64_t>();
@@ -741,10 +971,10 @@ static int readall_batch_impl(ewal_ctx *c, const uint8_t *d_buf, uint32_t ns, co
       EW_CHECK(hipMemcpyAsync(c->bent_first.data(), c->bef.p, (size_t)ns * 8, hipMemcpyDeviceToHost, c->stream));
       EW_CHECK(hipEventRecord(c->ev1, c->stream));
       if ((rc = sync_small(c))) return rc;
-      fast = !c->h_small->segbad && !c->h_small->gapslow && !c->h_small->nonmono;
+      fast = !c->h_small->segbad && !c->h_small->gapslow && !c->h_small->nonmono && !c->h_small->nunrec;
       if (!fast && std::getenv("EWAL_DEBUG"))
-        std::fprintf(stderr, "ewal batch: one by one (segbad %u gapslow %u nonmono %u)\n", c->h_small->segbad,
-                     c->h_small->gapslow, c->h_small->nonmono);
+        std::fprintf(stderr, "ewal batch: one by one (segbad %u gapslow %u nonmono %u nunrec %u)\n",
+                     c->h_small->segbad, c->h_small->gapslow, c->h_small->nonmono, c->h_small->nunrec);
       if (fast) {
         EW_CHECK(hipEventElapsedTime(&dev_ms, c->ev0, c->ev1));
         EW_CHECK(hipEventElapsedTime(&str_ms, c->evs0, c->evs1));
@@ -774,6 +1004,13 @@ static int readall_batch_impl(ewal_ctx *c, const uint8_t *d_buf, uint32_t ns, co
     rc = readall_impl(c, p, lens[i], ris[i], &out[i]);
     if (rc < 0) return rc;
     out[i].flags |= EWAL_FLAG_SHARD_FALLBACK;
+    if (out[i].status == EWAL_OK && out[i].n_unrec) {
+      // the batch keeps no per-shard side list: such a shard (unknown fields
+      // in its returned ents / HardState) is replayed alone for them
+      out[i].status = EWAL_UNSUPPORTED_ENCODING;
+      out[i].detail = 1;
+      out[i].n_unrec = 0;
+    }
     const uint64_t ne = out[i].status == EWAL_OK ? (uint64_t)out[i].n_ents : 0;
     if (ne) {
       EW_CHECK(grow_keep(c->bents, (size_t)(have + ne) * sizeof(ewal_entry), (size_t)have * sizeof(ewal_entry),
@@ -830,10 +1067,6 @@ void ewal_ctx_destroy(ewal_ctx *c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
   (void)hipStreamSynchronize(c->stream);
-  DevBuf *bufs[] = {&c->encw, &c->encs, &c->lbstat, &c->gagg, &c->slow, &c->mlist, &c->pf, &c->v, &c->pwave, &c->ux, &c->tagg, &c->tpx, &c->wcnt, &c->slots, &c->cbase, &c->ovf, &c->cpos, &c->clen, &c->nxt, &c->exc, &c->E, &c->rs, &c->jl,
-                    &c->vis, &c->entry, &c->on, &c->rec_cand, &c->rd, &c->opf, &c->ops, &c->kk, &c->kkrev,
-                    &c->suf, &c->ents, &c->recs, &c->tmp, &c->small, &c->sdesc, &c->snaps, &c->hbuf_dev};
-  for (DevBuf *b : bufs) b->release();
   for (auto &kv : c->tables) {
     (void)hipFree(kv.second.slice);
     (void)hipFree(kv.second.shift);
@@ -938,6 +1171,25 @@ int64_t ewal_copy_entries(ewal_ctx *c, ewal_entry *out, int64_t cap) {
   if (n > 0) {
     EW_CHECK(hipMemcpyAsync(out, c->ents.p, (size_t)n * sizeof(ewal_entry), hipMemcpyDeviceToHost, c->stream));
     EW_CHECK(hipStreamSynchronize(c->stream));
+  }
+  return n;
+}
+
+int64_t ewal_copy_unrec(ewal_ctx *c, ewal_unrec *out, int64_t cap) {
+  if (!c || (!out && cap)) return EWAL_E_INVAL;
+  if (!c->last_ok) return 0;
+  const int64_t n = std::min<int64_t>(cap, (int64_t)c->unrec.size());
+  if (n > 0) std::memcpy(out, c->unrec.data(), (size_t)n * sizeof(ewal_unrec));
+  return n;
+}
+
+int64_t ewal_copy_unrec_bytes(ewal_ctx *c, uint8_t *out, int64_t cap) {
+  if (!c || (!out && cap)) return EWAL_E_INVAL;
+  if (!c->last_ok) return 0;
+  const int64_t n = std::min<int64_t>(cap, (int64_t)c->unrec_bytes);
+  if (n > 0) {
+    EW_CHECK(hipSetDevice(c->device));
+    EW_CHECK(hipMemcpy(out, c->uarena.p, (size_t)n, hipMemcpyDeviceToHost));
   }
   return n;
 }

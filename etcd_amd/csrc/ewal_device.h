@@ -191,9 +191,12 @@ __device__ __noinline__ int pb_skip(const uint8_t *p, int64_t l, int64_t &out) {
 // XXX_unrecognized, sets unrec), PB_VAR64/PB_VAR32 (|= accumulate), PB_BYTES
 // (append; nil when empty), PB_REP64 (append to a repeated list in rep[]).
 // Returns 0, 2 (io.ErrUnexpectedEOF), 7 (proto.ErrWrongType), 33 (bounds
-// panic), 37 (never terminates) or 48 (EWAL_UNSUPPORTED_ENCODING: a bytes
-// field whose repeats concatenate two non-empty segments, a repeated list
-// longer than rep's capacity, or group nesting deeper than the device stack).
+// panic), 37 (never terminates) or 48 (EWAL_UNSUPPORTED_ENCODING: group
+// nesting deeper than the device stack).  The walk always runs to Go's own
+// result: a bytes field whose repeats concatenate non-empty segments (Go's
+// `m.Data = append(m.Data, ...)`) or a repeated list longer than rep's
+// capacity only sets the field's `split` flag (boff = the first segment,
+// blen = the total length), for the caller to decide.
 #define PB_NONE 0
 #define PB_VAR64 1
 #define PB_VAR32 2
@@ -203,8 +206,9 @@ struct PbField {
   uint64_t v;      // varint value (OR-accumulated) / repeated count
   int64_t boff;    // bytes field offset (-1: nil)
   int64_t blen;
+  uint32_t split;  // bytes: more than one non-empty segment; repeated: past rep's capacity
 };
-__device__ __forceinline__ void pbf_init(PbField &f) { f.v = 0; f.boff = -1; f.blen = 0; }
+__device__ __forceinline__ void pbf_init(PbField &f) { f.v = 0; f.boff = -1; f.blen = 0; f.split = 0; }
 
 template <int K, class P>
 __device__ __forceinline__ int pb_field(const P &p, int64_t &i, int64_t l, int wt, PbField &f, uint64_t *rep,
@@ -217,9 +221,13 @@ __device__ __forceinline__ int pb_field(const P &p, int64_t &i, int64_t l, int w
     if (post > l) return 2;
     if (post < i) return 33;
     if (post > i) {
-      if (f.blen > 0) return 48;
-      f.boff = i;
-      f.blen = post - i;
+      if (f.blen > 0) {
+        f.split = 1;
+        f.blen += post - i;
+      } else {
+        f.boff = i;
+        f.blen = post - i;
+      }
     }
     i = post;
     return 0;
@@ -227,8 +235,8 @@ __device__ __forceinline__ int pb_field(const P &p, int64_t &i, int64_t l, int w
     if (wt != 0) return 7;
     uint64_t v = 0;
     if (rd_varint(p, i, l, v, 64)) return 2;
-    if (f.v >= repcap) return 48;
-    if (rep) rep[f.v] = v;
+    if (f.v >= repcap) f.split = 1;
+    else if (rep) rep[f.v] = v;
     f.v++;
     return 0;
   } else {
@@ -237,9 +245,14 @@ __device__ __forceinline__ int pb_field(const P &p, int64_t &i, int64_t l, int w
   }
 }
 
-template <int K1, int K2, int K3, int K4, int K5, class P>
+// unk(i, hi): every unknown field [i, hi) the walk appends to XXX_unrecognized
+struct PbNoUnk {
+  __device__ void operator()(int64_t, int64_t) const {}
+};
+template <int K1, int K2, int K3, int K4, int K5, class P, class U = PbNoUnk>
 __device__ inline int pb_walk(const P &p, int64_t l, PbField &f1, PbField &f2, PbField &f3, PbField &f4,
-                              PbField &f5, int &unrec, uint64_t *rep2, uint64_t *rep5, uint32_t repcap) {
+                              PbField &f5, int &unrec, uint64_t *rep2, uint64_t *rep5, uint32_t repcap,
+                              U unk = U()) {
   int64_t i = 0;
   unrec = 0;
   while (i < l) {
@@ -271,6 +284,7 @@ __device__ inline int pb_walk(const P &p, int64_t l, PbField &f1, PbField &f2, P
     if (hi < i) return 33;
     if (skippy == 0) return 37;
     unrec = 1;
+    unk(i, hi);
     i = hi;
   }
   return 0;

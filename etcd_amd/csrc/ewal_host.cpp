@@ -397,12 +397,17 @@ int ewal_writer_sync(ewal_writer *w) {
   return ::fsync(w->fd) == 0 ? EWAL_OK : EWAL_E_IO;
 }
 int ewal_writer_cut(ewal_writer *w) {
+  // (*WAL).Cut, wal/wal.go:219-238: the next file is opened first; when that
+  // fails the WAL keeps writing to the current one.  Then the current file
+  // is synced (its error ignored, as w.Sync() is there) and closed, and the
+  // new one takes its place.
   const uint64_t nseq = w->seq + 1, nidx = w->enti + 1;
-  int rc = ewal_writer_sync(w);
-  if (rc) return rc;
+  const std::string np = w->dir + "/" + wal_name(nseq, nidx);
+  const int nfd = ::open(np.c_str(), O_WRONLY | O_APPEND | O_CREAT, 0600);
+  if (nfd < 0) return EWAL_E_IO;
+  (void)ewal_writer_sync(w);   // w.Sync()'s error is not checked in Cut either
   ::close(w->fd);
-  w->fd = -1;
-  if (writer_open(w, nseq, nidx) != EWAL_OK) return EWAL_E_IO;
+  w->fd = nfd;
   w->seq = nseq;
   const uint32_t prev = w->enc.crc;   // encoder re-created with prevCrc
   w->enc.crc = prev;
@@ -586,6 +591,18 @@ int esnap_load_dir(ewal_ctx *ctx, const char *dirpath, uint32_t poly, esnap_snap
         if (out_name) *out_name = strdup(name.c_str());
         return EWAL_OK;
       }
+    }
+    // loadSnap's deferred renameBroken runs only on the errors Go returns
+    // (read error, snappb / raftpb Unmarshal errors, ErrCRCMismatch).  A Go
+    // panic (bounds, non-termination) propagates out of Load instead, and
+    // EWAL_UNSUPPORTED_ENCODING is a limit of this engine (a valid file Go
+    // would load): both stop here with the file left in place, so the caller
+    // can decode it on the host.
+    const bool go_error = st == EWAL_E_IO || st == EWAL_ERR_SNAP_CRC || st == EWAL_ERR_UNEXPECTED_EOF ||
+                          st == EWAL_ERR_WRONG_TYPE;
+    if (!go_error) {
+      if (out_name) *out_name = strdup(name.c_str());
+      return st;
     }
     err = st;
     std::string broken = path + ".broken";   // renameBroken

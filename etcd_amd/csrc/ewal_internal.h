@@ -52,7 +52,9 @@ struct RecDesc {
   uint64_t f0, f1, f2;     // Entry: Term, Index; HardState: Term, Vote, Commit
   uint64_t edoff, edlen;   // Entry.Data
   int32_t etype;           // Entry.Type
-  uint8_t dnil, enil, pad0, pad1;
+  uint8_t dnil, enil;
+  uint8_t pad0;            // Record.Data in several segments (their concatenation)
+  uint8_t pad1;            // the Entry / HardState carries XXX_unrecognized
 };
 
 struct ChainInfo {
@@ -80,6 +82,7 @@ struct ShardAgg {
 };
 
 struct SegArgs {
+  uint2 *ulist;            // (frame, op index) of entry ops with XXX_unrecognized (both modes)
   const uint32_t *fs;      // first frame of every shard [ns + 1], fs[ns] = n
   uint32_t ns;
   const uint64_t *ri;      // w.ri of every shard [ns]
@@ -117,6 +120,17 @@ struct Small {
   uint32_t gapslow;               // k_check: an op's predecessor lies too far back (list-based k_gap)
   uint32_t segbad;                // k_shard_start: a shard does not start on a frame of the chain
   uint32_t spec_n;                // k_spec_gate: frames when k_frame's speculation holds, else 0
+  uint32_t nunrec;                // k_check: entry ops carrying XXX_unrecognized (listed in ulist)
+  uint32_t pad2;
+};
+
+// A returned Entry (ent = its index in ents) or the HardState (ent = -1)
+// whose XXX_unrecognized bytes k_unrec gathers into the side buffer.
+struct UnrecItem {
+  uint32_t r;              // its frame
+  uint32_t pad;
+  int64_t ent;
+  uint64_t off, len;       // in the side buffer
 };
 
 // Everything the host needs after the frame pass, gathered by k_result.
@@ -126,5 +140,5 @@ struct ResultDev {
   uint32_t nops, nonmono;
   uint64_t klast;
   uint32_t nslow, gapslow;
-  uint32_t errflag, pad;
+  uint32_t errflag, nunrec;
 };

@@ -64,7 +64,7 @@ __device__ int msg_walk(const uint8_t *p, int64_t l, uint64_t base, emsg_message
         const int es = pb_walk<PB_VAR32, PB_VAR64, PB_VAR64, PB_BYTES, PB_NONE>(p + i, post - i, a1, a2, a3, a4, a5,
                                                                                unrec, nullptr, nullptr, 0);
         if (es == 33 || es == 37) { st = es; break; }   // panics propagate, errors do not
-        if (es == 48 || unrec) unsup = 1;
+        if (es == 48 || unrec || a4.split) unsup = 1;
         if (FILL) {
           ewal_entry e;
           e.type = (int32_t)(uint32_t)a1.v;
@@ -81,7 +81,7 @@ __device__ int msg_walk(const uint8_t *p, int64_t l, uint64_t base, emsg_message
         const int ss = pb_walk<PB_BYTES, PB_REP64, PB_VAR64, PB_VAR64, PB_REP64>(p + i, post - i, s1, s2, s3, s4, s5,
                                                                                 unrec, nullptr, nullptr, 0xffffffffu);
         if (had == 0 && s1.blen > 0) m.snap_data_off = (int64_t)(base + (uint64_t)i + (uint64_t)s1.boff);
-        if (unrec) unsup = 1;
+        if (unrec || s1.split) unsup = 1;
         if (ss) { st = ss; break; }
       }
       i = post;

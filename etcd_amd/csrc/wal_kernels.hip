@@ -888,16 +888,32 @@ __global__ void k_mark(const uint32_t *__restrict__ J, uint8_t *vis, uint32_t R)
   }
 }
 
+// Chain entries of the marked runs.  A chain segment's first run has its
+// entry set by k_jstart; every later run is entered at its predecessor's
+// link.  last_cand = the largest terminal candidate of the marked runs: the
+// chain segments are marked in position order, so that is the terminal of
+// the segment marked last (k_jstart resets it).
 __global__ void k_entry(const uint32_t *__restrict__ E, const uint32_t *__restrict__ nxt,
                         const uint32_t *__restrict__ rs, const uint8_t *__restrict__ vis, uint32_t R,
                         uint32_t *__restrict__ entry, ChainInfo *ci) {
   uint32_t a = blockIdx.x * blockDim.x + threadIdx.x;
   if (a >= R) return;
-  if (a == 0) entry[0] = 0;
   if (!vis[a]) return;
   uint32_t r = rs[a];
   if (r != EW_NIL) entry[r] = nxt[E[a]];
-  else ci->last_cand = E[a];
+  else atomicMax(&ci->last_cand, E[a]);
+}
+
+// A chain segment starts at candidate `cand`: mark its run, entered there.
+__global__ void k_jstart(const uint32_t *__restrict__ E, uint32_t R, uint32_t cand, uint8_t *__restrict__ vis,
+                         uint32_t *__restrict__ entry, ChainInfo *ci) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  const uint32_t a = lower_bound_u32(E, R, cand);
+  if (a < R) {
+    vis[a] = 1;
+    entry[a] = cand;
+  }
+  ci->last_cand = 0;
 }
 
 __global__ void k_member(const uint32_t *__restrict__ E, uint32_t R, const uint8_t *__restrict__ vis,
@@ -1024,6 +1040,41 @@ __device__ __forceinline__ uint32_t prefix_at(uint64_t x, const uint32_t *__rest
   return prefix_finish(in, t4, svp);
 }
 
+// lin of the concatenation of every non-empty segment of bytes field fnum
+// of a message pb_walk accepted (Go's `m.Data = append(m.Data, ...)` over
+// repeats), the message read at stream offset base:
+//   lin(A || B) = S_|B|(lin A) ^ lin B,  lin[s, e) = S_{e-s}(P(s)) ^ P(e).
+// Every other field is stepped over as proto.Skip would (its extent is the
+// one the walker consumed).  Rare: split fields only.
+template <class P>
+__device__ uint32_t bytes_field_lin(const P &p, int64_t l, uint32_t fnum, uint64_t base, const uint8_t *__restrict__ buf,
+                                    const uint32_t *__restrict__ pwave, const uint32_t *__restrict__ v,
+                                    const uint32_t *t4, const uint32_t *svp, const uint32_t *__restrict__ g_shift) {
+  int64_t i = 0;
+  uint32_t lin = 0;
+  while (i < l) {
+    const int64_t at = i;
+    uint64_t wire = 0;
+    if (rd_varint(p, i, l, wire, 64)) break;
+    if ((uint32_t)(wire >> 3) == fnum && (wire & 7) == 2) {
+      uint64_t bl = 0;
+      if (rd_varint(p, i, l, bl, 64)) break;
+      const int64_t post = (int64_t)((uint64_t)i + bl);
+      if (post > i) {
+        const uint64_t s0 = base + (uint64_t)i, e0 = base + (uint64_t)post;
+        lin = gshift_n(g_shift, e0 - s0, lin ^ prefix_at(s0, pwave, v, buf, t4, svp)) ^
+              prefix_at(e0, pwave, v, buf, t4, svp);
+      }
+      i = post;
+      continue;
+    }
+    int64_t skippy = 0;
+    if (pb_skip(gptr(p) + at, l - at, skippy) || skippy <= 0) break;
+    i = at + skippy;
+  }
+  return lin;
+}
+
 // General decode of frame r (any encoding the reference accepts): the
 // gogoprotobuf walkers over an LDS copy of the frame head, and P at its frame
 // start and data start:
@@ -1034,7 +1085,8 @@ __device__ __forceinline__ uint32_t prefix_at(uint64_t x, const uint32_t *__rest
 __device__ __forceinline__ void decode_general(const uint8_t *__restrict__ buf, uint64_t B, uint64_t p, int64_t L,
                                                uint32_t r, uint32_t n, const uint32_t *__restrict__ pwave,
                                                const uint32_t *__restrict__ v, const uint32_t *s_t4,
-                                               const uint32_t *s_svp, uint4 (&win)[5], RecDesc *__restrict__ rd,
+                                               const uint32_t *s_svp, const uint32_t *__restrict__ g_shift,
+                                               uint4 (&win)[5], RecDesc *__restrict__ rd,
                                                uint32_t *__restrict__ pfd, uint32_t *__restrict__ pfo) {
   const uint64_t p16 = p & ~15ull;
 #pragma unroll
@@ -1056,7 +1108,7 @@ __device__ __forceinline__ void decode_general(const uint8_t *__restrict__ buf, 
   d.off = p;
   d.type = 0; d.crc = 0; d.chained = 0; d.st = 0; d.sub_st = 0;
   d.doff = p + 8; d.dlen = 0; d.dnil = 1;
-  d.f0 = d.f1 = d.f2 = 0; d.edoff = 0; d.edlen = 0; d.enil = 1; d.etype = 0;
+  d.f0 = d.f1 = d.f2 = 0; d.edoff = 0; d.edlen = 0; d.enil = 1; d.etype = 0; d.pad1 = 0;
   PbField a1, a2, a3, a4, a5;
   pbf_init(a1); pbf_init(a2); pbf_init(a3); pbf_init(a4); pbf_init(a5);
   int unrec;
@@ -1066,6 +1118,20 @@ __device__ __forceinline__ void decode_general(const uint8_t *__restrict__ buf, 
   d.crc = (uint32_t)a2.v;
   if (a3.blen > 0) { d.doff = p + 8 + a3.boff; d.dlen = a3.blen; d.dnil = 0; }
   d.st = st;
+  const bool split = st == 0 && a3.split;   // Data in several segments: their concatenation
+  d.pad0 = split ? 1 : 0;
+  if (split) {
+    // the CRC over the concatenation: k_check's Update(seed, D) =
+    // S_n(seed ^ ~0 ^ P(s)) ^ P(e) ^ ~0 with P(s) := 0, P(e) := lin(D)
+    pfo[r] = prefix_at(p, pwave, v, buf, s_t4, s_svp);
+    pfd[r] = 0;
+    d.chained = bytes_field_lin(R + 8, L, 3, p + 8, buf, pwave, v, s_t4, s_svp, g_shift);
+    // metadata / Entry / HardState over the concatenation are not decoded
+    // here: reported (EWAL_UNSUPPORTED_ENCODING) when the CRC holds
+    d.sub_st = 48;
+    rd[r] = d;
+    return;
+  }
   if (st == 0) {
     const WinReader dp = R + (int64_t)(d.doff - p);
     if (d.type == 2) {           // entryType: mustUnmarshalEntry
@@ -1075,7 +1141,7 @@ __device__ __forceinline__ void decode_general(const uint8_t *__restrict__ buf, 
       if (!d.dnil)
         s2 = pb_walk<PB_VAR32, PB_VAR64, PB_VAR64, PB_BYTES, PB_NONE>(dp, (int64_t)d.dlen, e1, e2, e3, e4, e5, ur,
                                                                        nullptr, nullptr, 0);
-      if (s2 == 0 && ur) s2 = 48;   // Entry.XXX_unrecognized is returned by ReadAll
+      d.pad1 = (s2 == 0 && ur) ? 1 : 0;   // Entry.XXX_unrecognized: returned through the side list
       d.sub_st = s2;
       d.etype = (int32_t)(uint32_t)e1.v;
       d.f0 = e2.v;                  // Term
@@ -1088,7 +1154,7 @@ __device__ __forceinline__ void decode_general(const uint8_t *__restrict__ buf, 
       if (!d.dnil)
         s2 = pb_walk<PB_VAR64, PB_VAR64, PB_VAR64, PB_NONE, PB_NONE>(dp, (int64_t)d.dlen, h1, h2, h3, h4, h5, ur,
                                                                       nullptr, nullptr, 0);
-      if (s2 == 0 && ur) s2 = 48;   // HardState.XXX_unrecognized is returned
+      d.pad1 = (s2 == 0 && ur) ? 1 : 0;   // HardState.XXX_unrecognized: returned through the side list
       d.sub_st = s2;
       d.f0 = h1.v; d.f1 = h2.v; d.f2 = h3.v;
     }
@@ -1129,9 +1195,173 @@ __global__ __launch_bounds__(256) void k_decode_slow(const uint8_t *__restrict__
   for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < ns; j += gridDim.x * blockDim.x) {
     const uint32_t r = slow[j];
     const uint64_t p = pos[rec_cand ? rec_cand[r] : r];
-    decode_general(buf, B, p, (int64_t)ld_le64_b(buf, B, p), r, n, pwave, v, s_t4, s_svp, s_win[threadIdx.x], rd,
-                   pfd, pfo);
+    decode_general(buf, B, p, (int64_t)ld_le64_b(buf, B, p), r, n, pwave, v, s_t4, s_svp, g_shift, s_win[threadIdx.x],
+                   rd, pfd, pfo);
   }
+}
+
+// ---- frames that are not candidates ---------------------------------------
+// The candidate filter only admits the canonical Record head (08 <type<0x80>
+// 10), so a frame that fits in the stream but is not a candidate -- a
+// corrupted tag / type byte, a type >= 0x80, a non-canonical encoding --
+// ends the candidate chain.  decoder.decode still reads it (wal/decoder.go:
+// 28-47): k_walk follows the true frame chain from there, one frame at a
+// time, with the exact walkers (Record.Unmarshal, record.pb.go:43-136; the
+// CRC from the stream prefixes; Entry / HardState Unmarshal), until it meets
+// a candidate again (the candidate chain resumes there), the stream's end /
+// a frame that does not fit (the terminal), or a frame that fails (ReadAll
+// stops there: nothing after it can change the result).  The frames it
+// passes are listed in xpos and decoded with the chain's other frames.
+
+// Would ReadAll continue after the frame at x (length L, fits), given the
+// previous frame's stored CRC as the running CRC (k_check's local rule)?
+// *crc = this frame's stored CRC.  Rules ReadAll applies across frames
+// (metadata equality, the ents index gap) are left to k_check / k_result:
+// continuing past such a frame costs only walk steps.
+__device__ bool walk_passes(const uint8_t *__restrict__ buf, uint64_t x, int64_t L, uint32_t seed,
+                            const uint32_t *__restrict__ pwave, const uint32_t *__restrict__ v,
+                            const uint32_t *__restrict__ g_slice, const uint32_t *__restrict__ g_shift, uint32_t *crc) {
+  const uint8_t *rb = buf + x + 8;
+  PbField a1, a2, a3, a4, a5;
+  pbf_init(a1); pbf_init(a2); pbf_init(a3); pbf_init(a4); pbf_init(a5);
+  int unrec = 0;
+  const int st = pb_walk<PB_VAR64, PB_VAR32, PB_BYTES, PB_NONE, PB_NONE>(rb, L, a1, a2, a3, a4, a5, unrec, nullptr,
+                                                                         nullptr, 0);
+  *crc = (uint32_t)a2.v;
+  if (st) return false;
+  const int64_t type = (int64_t)a1.v;
+  if (type == 4) return !(seed != 0 && *crc != seed);   // wal/wal.go:184-192
+  uint32_t computed = seed;
+  const uint32_t *svp = g_shift + EW_VLOG * 1024;
+  if (a3.split) {   // Data = the concatenation of its segments
+    const uint32_t lin = bytes_field_lin(rb, L, 3, x + 8, buf, pwave, v, g_slice, svp, g_shift);
+    computed = gshift_n(g_shift, (uint64_t)a3.blen, seed ^ 0xffffffffu) ^ lin ^ 0xffffffffu;
+  } else if (a3.blen > 0) {
+    const uint64_t s = x + 8 + (uint64_t)a3.boff, e = s + (uint64_t)a3.blen;
+    const uint32_t Ps = prefix_at(s, pwave, v, buf, g_slice, svp), Pe = prefix_at(e, pwave, v, buf, g_slice, svp);
+    computed = gshift_n(g_shift, (uint64_t)a3.blen, seed ^ 0xffffffffu ^ Ps) ^ Pe ^ 0xffffffffu;
+  }
+  if (computed != *crc) return false;                   // walpb.ErrCRCMismatch
+  if (a3.split) return false;                           // k_check reports it (not decoded here)
+  if (type == 1) return true;
+  if (type != 2 && type != 3) return false;             // unexpected block type
+  if (a3.blen <= 0) return true;                        // Unmarshal(nil): the zero message
+  const uint8_t *dp = rb + a3.boff;
+  PbField e1, e2, e3, e4, e5;
+  pbf_init(e1); pbf_init(e2); pbf_init(e3); pbf_init(e4); pbf_init(e5);
+  int s2, ur = 0;
+  if (type == 2)
+    s2 = pb_walk<PB_VAR32, PB_VAR64, PB_VAR64, PB_BYTES, PB_NONE>(dp, a3.blen, e1, e2, e3, e4, e5, ur, nullptr,
+                                                                  nullptr, 0);
+  else
+    s2 = pb_walk<PB_VAR64, PB_VAR64, PB_VAR64, PB_NONE, PB_NONE>(dp, a3.blen, e1, e2, e3, e4, e5, ur, nullptr,
+                                                                 nullptr, 0);
+  return s2 == 0;   // XXX_unrecognized does not stop ReadAll
+}
+
+struct WalkOut {
+  uint64_t x;         // where the walk ended
+  uint64_t resume;    // the candidate at x (the candidate chain resumes there), ~0: none
+  int32_t term;       // x is the terminal: EWAL_OK (clean end) or its class; -1: not a terminal
+  int32_t stopped;    // the last listed frame fails: ReadAll stops there
+  uint32_t n;         // frames listed in xpos
+  uint32_t seed;      // the last listed frame's stored CRC
+};
+
+// One thread walks the frame chain from q.  The running CRC starts at the
+// stored CRC of the frame before q: candidate pc's (EW_NIL: none, 0), or
+// seed0 when has_seed (a walk continued after its list filled).
+__global__ void k_walk(const uint8_t *__restrict__ buf, uint64_t B, uint64_t q, const uint64_t *__restrict__ cpos,
+                       uint64_t K, uint32_t pc, int has_seed, uint32_t seed0, const uint32_t *__restrict__ pwave,
+                       const uint32_t *__restrict__ v, const uint32_t *__restrict__ g_slice,
+                       const uint32_t *__restrict__ g_shift, uint64_t *__restrict__ xpos, uint32_t xcap, WalkOut *o) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  uint32_t seed = seed0;
+  if (!has_seed) {
+    seed = 0;
+    if (pc != EW_NIL) {
+      const uint64_t p = cpos[pc];
+      PbField a1, a2, a3, a4, a5;
+      pbf_init(a1); pbf_init(a2); pbf_init(a3); pbf_init(a4); pbf_init(a5);
+      int unrec = 0;
+      (void)pb_walk<PB_VAR64, PB_VAR32, PB_BYTES, PB_NONE, PB_NONE>(buf + p + 8, (int64_t)ld_le64_b(buf, B, p), a1, a2,
+                                                                    a3, a4, a5, unrec, nullptr, nullptr, 0);
+      seed = (uint32_t)a2.v;
+    }
+  }
+  WalkOut r;
+  r.resume = ~0ull;
+  r.term = -1;
+  r.stopped = 0;
+  uint64_t x = q;
+  uint32_t n = 0;
+  for (;;) {
+    if (x == B) { r.term = EWAL_OK; break; }
+    if (B - x < 8) { r.term = EWAL_ERR_UNEXPECTED_EOF; break; }
+    const int64_t L = (int64_t)ld_le64_b(buf, B, x);
+    const uint64_t rem = B - x - 8;
+    if (L < 0) { r.term = EWAL_PANIC_NEG_LENGTH; break; }
+    if ((uint64_t)L > rem) { r.term = rem == 0 ? EWAL_OK : EWAL_ERR_UNEXPECTED_EOF; break; }
+    uint64_t lo = 0, hi = K;   // a candidate: the chain of candidates resumes here
+    while (lo < hi) {
+      const uint64_t mid = lo + ((hi - lo) >> 1);
+      if (cpos[mid] < x) lo = mid + 1; else hi = mid;
+    }
+    if (lo < K && cpos[lo] == x) { r.resume = lo; break; }
+    if (n == xcap) break;      // list full: the host continues from x
+    xpos[n++] = x;
+    uint32_t crc;
+    const bool pass = walk_passes(buf, x, L, seed, pwave, v, g_slice, g_shift, &crc);
+    seed = crc;
+    x += 8 + (uint64_t)L;
+    if (!pass) { r.stopped = 1; break; }
+  }
+  r.x = x;
+  r.n = n;
+  r.seed = seed;
+  *o = r;
+}
+
+// The chain's frame positions when walked frames join the candidate chain:
+// the nc chain candidates (cand list rc, or candidates 0..nc-1 when rc is
+// null) merged with the nx walked frames (both ascending) -> fpos.
+__global__ void k_fpos(const uint64_t *__restrict__ cpos, const uint32_t *__restrict__ rc, uint32_t nc,
+                       const uint64_t *__restrict__ xpos, uint32_t nx, uint64_t *__restrict__ fpos) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t < nc) {
+    const uint64_t p = cpos[rc ? rc[t] : t];
+    uint32_t lo = 0, hi = nx;
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (xpos[mid] < p) lo = mid + 1; else hi = mid;
+    }
+    fpos[t + lo] = p;
+  } else if (t < nc + nx) {
+    const uint32_t e = t - nc;
+    const uint64_t p = xpos[e];
+    uint32_t lo = 0, hi = nc;
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (cpos[rc ? rc[mid] : mid] < p) lo = mid + 1; else hi = mid;
+    }
+    fpos[e + lo] = p;
+  }
+}
+
+// Fresh ReadAll reductions before a frame list is decoded and checked again.
+__global__ void k_reset_check(Small *ds) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  ds->agg.first_fail = ~0ull;
+  ds->agg.last_entry = -1;
+  ds->agg.last_state = -1;
+  ds->agg.first_meta = ~0ull;
+  ds->nmeta = 0;
+  ds->nslow = 0;
+  ds->nsel3 = 0;
+  ds->lastop = 0;
+  ds->gapslow = 0;
+  ds->nonmono = 0;
+  ds->nunrec = 0;
 }
 
 // ---- canonical fast path ---------------------------------------------------
@@ -1217,7 +1447,7 @@ __device__ __forceinline__ int64_t decode_fast(const uint8_t *__restrict__ buf, 
   d.crc = (uint32_t)cr;
   d.chained = 0; d.st = 0; d.sub_st = 0;
   d.doff = p + 8; d.dlen = 0; d.dnil = 1;
-  d.f0 = d.f1 = d.f2 = 0; d.edoff = 0; d.edlen = 0; d.enil = 1; d.etype = 0;
+  d.f0 = d.f1 = d.f2 = 0; d.edoff = 0; d.edlen = 0; d.enil = 1; d.etype = 0; d.pad0 = 0; d.pad1 = 0;
   const int ho = o;                   // window offset of the data start
   if (hasd && dl > 0) { d.doff = p + (uint64_t)(o - base); d.dlen = dl; d.dnil = 0; }
   if (ok && !d.dnil && (d.type == 2 || d.type == 3)) {
@@ -1470,7 +1700,7 @@ __global__ __launch_bounds__(1024) void k_check(const uint32_t *__restrict__ g_s
         const uint64_t e = d.doff + d.dlen;
         // P(data end) = P(next frame start) in the canonical layout (pfo[r+1]),
         // else k_decode left it in d.chained.  U(seed, D) = S_n(seed ^ ~0 ^ P(s)) ^ P(e) ^ ~0
-        const uint32_t Pe = noff == e ? pn : d.chained;
+        const uint32_t Pe = (noff == e && !d.pad0) ? pn : d.chained;
         uint32_t x = seed ^ 0xffffffffu ^ ps;
         uint64_t m = d.dlen;
         for (int lvl = 0; m; ++lvl, m >>= 1) {
@@ -1491,6 +1721,8 @@ __global__ __launch_bounds__(1024) void k_check(const uint32_t *__restrict__ g_s
         else if (d.sub_st) st = EWAL_PANIC_STATE;
       } else if (d.type != 1) {
         st = EWAL_ERR_UNEXPECTED_TYPE;
+      } else if (d.sub_st == 48) {          // metadata Data in several segments
+        st = EWAL_UNSUPPORTED_ENCODING;
       }
     }
   }
@@ -1618,6 +1850,7 @@ __global__ __launch_bounds__(1024) void k_check(const uint32_t *__restrict__ g_s
     e.data_nil = d.enil;
     ents[j] = e;
     if (SEG && !wg1 && bsh == 0) atomicMin(&sg.sagg[sh].ent_first, (unsigned long long)j);   // the shard's first op in the wave
+    if (d.pad1) sg.ulist[atomicAdd(&ds->nunrec, 1u)] = make_uint2(r, j);   // rare: Entry.XXX_unrecognized
   }
 }
 
@@ -1729,6 +1962,7 @@ __global__ __launch_bounds__(256) void k_result(const uint8_t *__restrict__ buf,
   o->nslow = ds->nslow;
   o->gapslow = ds->gapslow;
   o->errflag = ds->errflag;
+  o->nunrec = ds->nunrec;
   if (g.first_fail < n) o->fail = rd[g.first_fail];
   if (g.last_entry >= 0) o->lastent = rd[g.last_entry];
   if (n) o->last = rd[n - 1];
@@ -1867,6 +2101,36 @@ __global__ void k_ents(const RecDesc *__restrict__ rd, const uint32_t *__restric
     e.data_nil = d.enil;
     ents[k] = e;
   }
+}
+
+// XXX_unrecognized of listed Entry / HardState frames (rare): PASS 0 sizes
+// (the unknown fields the walker steps over, in order), PASS 1 copies them to
+// arena + off -- Go's `m.XXX_unrecognized = append(m.XXX_unrecognized,
+// data[iNdEx:iNdEx+skippy]...)` (raft/raftpb/raft.pb.go:270, :697).
+template <int PASS>
+__global__ void k_unrec(const uint8_t *__restrict__ buf, const RecDesc *__restrict__ rd, UnrecItem *__restrict__ it,
+                        uint32_t m, uint8_t *__restrict__ arena) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= m) return;
+  const RecDesc d = rd[it[i].r];
+  const uint8_t *dp = buf + d.doff;
+  uint64_t tot = 0;
+  uint8_t *dst = PASS ? arena + it[i].off : nullptr;
+  auto unk = [&](int64_t a, int64_t b) {
+    if (PASS)
+      for (int64_t k = a; k < b; ++k) dst[tot + (uint64_t)(k - a)] = dp[k];
+    tot += (uint64_t)(b - a);
+  };
+  PbField f1, f2, f3, f4, f5;
+  pbf_init(f1); pbf_init(f2); pbf_init(f3); pbf_init(f4); pbf_init(f5);
+  int ur = 0;
+  if (d.type == 2)
+    (void)pb_walk<PB_VAR32, PB_VAR64, PB_VAR64, PB_BYTES, PB_NONE>(dp, (int64_t)d.dlen, f1, f2, f3, f4, f5, ur, nullptr,
+                                                                   nullptr, 0, unk);
+  else
+    (void)pb_walk<PB_VAR64, PB_VAR64, PB_VAR64, PB_NONE, PB_NONE>(dp, (int64_t)d.dlen, f1, f2, f3, f4, f5, ur, nullptr,
+                                                                  nullptr, 0, unk);
+  if (!PASS) it[i].len = tot;
 }
 
 __global__ void k_records_out(const RecDesc *__restrict__ rd, uint32_t n, ewal_record *__restrict__ out) {

@@ -38,6 +38,7 @@ class HardState:
     Term: int = 0
     Vote: int = 0
     Commit: int = 0
+    XXX_unrecognized: Optional[bytes] = None
 
 
 @dataclass
@@ -47,6 +48,7 @@ class Entry:
     Term: int = 0
     Index: int = 0
     Data: Optional[bytes] = None
+    XXX_unrecognized: Optional[bytes] = None
 
 
 class Context:
@@ -142,8 +144,10 @@ class ReadAllResult:
         return dict(status=self.status, detail=self.detail, fail_record=self.fail_record,
                     fail_offset=self.fail_offset, n_records=self.n_records, last_crc=self.last_crc, enti=self.enti,
                     metadata=self.metadata, state=dict(term=self.state.Term, vote=self.state.Vote,
-                                                       commit=self.state.Commit),
-                    ents=[dict(type=e.Type, term=e.Term, index=e.Index, data=e.Data) for e in self.ents])
+                                                       commit=self.state.Commit,
+                                                       unrec=self.state.XXX_unrecognized),
+                    ents=[dict(type=e.Type, term=e.Term, index=e.Index, data=e.Data, unrec=e.XXX_unrecognized)
+                          for e in self.ents])
 
 
 def _collect(ctx, r, buf_view, with_ents=True, shard=None):
@@ -163,9 +167,28 @@ def _collect(ctx, r, buf_view, with_ents=True, shard=None):
         for e in arr[:n]:
             data = None if e.data_nil else bytes(buf_view[e.data_off:e.data_off + e.data_len])
             ents.append(Entry(e.type, e.term, e.index, data))
+    if ok and r.n_unrec and shard is None:
+        for ent, b in unrecognized(ctx, r.n_unrec):
+            if ent < 0:
+                st.XXX_unrecognized = b
+            elif ent < len(ents):
+                ents[ent].XXX_unrecognized = b
     return ReadAllResult(r.status, r.detail, r.fail_record, r.fail_offset, r.n_records, r.last_crc if ok else 0,
                          r.enti, md, st, ents, r.n_candidates, r.n_runs, r.device_ms, r.stream_ms, r.n_slow,
                          r.flags)
+
+
+def unrecognized(ctx, n):
+    """The last ReadAll's XXX_unrecognized side list: [(ent index or -1 for
+    the HardState, bytes)] (ewal_copy_unrec / ewal_copy_unrec_bytes)."""
+    arr = (L.UnrecDesc * max(n, 1))()
+    k = lib.ewal_copy_unrec(ctx.handle, arr, n)
+    check(0 if k >= 0 else int(k))
+    tot = max([a.off + a.len for a in arr[:k]] + [0])
+    raw = (C.c_char * max(tot, 1))()
+    got = lib.ewal_copy_unrec_bytes(ctx.handle, raw, tot)
+    check(0 if got >= 0 else int(got))
+    return [(a.ent, raw.raw[a.off:a.off + a.len]) for a in arr[:k]]
 
 
 def readall_bytes(buf: bytes, ri: int = 0, ctx: Context = None, with_ents=True) -> ReadAllResult:

@@ -71,7 +71,7 @@ typedef struct ewal_result {
   int64_t fail_offset;     /* byte offset of that frame in the stream, -1 */
   int64_t n_records;       /* frames decoded before the end / failure */
   uint32_t last_crc;       /* decoder.lastCRC() -> seeds the encoder, wal/wal.go:213 */
-  uint32_t reserved0;
+  uint32_t n_unrec;        /* ents / HardState carrying XXX_unrecognized: ewal_copy_unrec */
   uint64_t enti;           /* w.enti: Index of the last entry record */
   int64_t metadata_off;    /* metadata []byte as (offset,len) into the stream; -1 == nil */
   int64_t metadata_len;
@@ -95,6 +95,15 @@ typedef struct ewal_entry {
   int32_t type;
   int32_t data_nil;
 } ewal_entry;
+
+/* XXX_unrecognized of a returned Entry / the HardState (raft.pb.go:100-106,
+ * 143-148: the unknown fields Unmarshal appended, raft.pb.go:270), bytes at
+ * [off, off+len) of the side buffer (ewal_copy_unrec_bytes).  Entries and a
+ * HardState not listed have a nil XXX_unrecognized. */
+typedef struct ewal_unrec {
+  int64_t ent;             /* index into ents, or -1: the HardState */
+  uint64_t off, len;
+} ewal_unrec;
 
 /* One decoded frame (walpb.Record + chain state), wal/walpb/record.pb.go:30-35 */
 typedef struct ewal_record {
@@ -155,6 +164,10 @@ int ewal_readall_host(ewal_ctx *ctx, const void *h_buf, uint64_t len, uint64_t r
  * Return the number copied (<= cap) or a negative error. */
 int64_t ewal_copy_entries(ewal_ctx *ctx, ewal_entry *out, int64_t cap);
 int64_t ewal_copy_records(ewal_ctx *ctx, ewal_record *out, int64_t cap);
+/* After a successful readall with n_unrec > 0: the side list (sorted by ent)
+ * and its bytes. */
+int64_t ewal_copy_unrec(ewal_ctx *ctx, ewal_unrec *out, int64_t cap);
+int64_t ewal_copy_unrec_bytes(ewal_ctx *ctx, uint8_t *out, int64_t cap);
 
 /* ---- directory-level API: wal.OpenAtIndex + ReadAll + writer ----------- */
 typedef struct ewal_wal ewal_wal;
@@ -242,10 +255,11 @@ int esnap_load_dir(ewal_ctx *ctx, const char *dirpath, uint32_t poly, esnap_snap
 
 /* ---- raft quorum commit: raft.maybeCommit, raft/raft.go:248-258 ---------- */
 /* Batched over G independent raft groups (SoA).  match[v*G + g] for voter
- * v < nvoters[g] (<= 16); log terms for group g are log_terms[log_ptr[g] ..
+ * v < nvoters[g] (1..255); log terms for group g are log_terms[log_ptr[g] ..
  * log_ptr[g+1]) at raft indices log_offset[g] + k.  committed[] is updated in
- * place; changed[g] = maybeCommit's return; status[g] = 0 or EWAL_PANIC_BOUNDS.
- * All pointers are DEVICE pointers. */
+ * place; changed[g] = maybeCommit's return; status[g] = 0, or
+ * EWAL_PANIC_BOUNDS where Go panics (no voters: mis[q-1] on an empty slice;
+ * raftLog.at past the log).  All pointers are DEVICE pointers. */
 int ecommit_batch_device(ewal_ctx *ctx, uint64_t G, const uint64_t *match, const uint8_t *nvoters,
                          const uint64_t *term, uint64_t *committed, const uint64_t *log_offset,
                          const uint64_t *log_ptr, const uint64_t *log_terms, uint8_t *changed,

@@ -188,7 +188,10 @@ typedef struct {
   int64_t *plen;      /* bytes length / repeated count */
 } fspec;
 
-static int pb_unmarshal(const uint8_t *d, int64_t l, fspec *fs, int nf, int64_t *unrec_len) {
+/* unknown fields: Skip, then `m.XXX_unrecognized = append(m.XXX_unrecognized,
+ * data[index:index+skippy]...)` (e.g. raft.pb.go:270); unrec may be NULL for
+ * messages whose XXX_unrecognized the path never returns. */
+static int pb_unmarshal(const uint8_t *d, int64_t l, fspec *fs, int nf, int64_t *unrec_len, uint8_t **unrec) {
   int64_t index = 0;
   while (index < l) {
     uint64_t wire = 0;
@@ -248,7 +251,8 @@ static int pb_unmarshal(const uint8_t *d, int64_t l, fspec *fs, int nf, int64_t 
     if (hi > l) return OR_ERR_UNEXPECTED_EOF;
     if (hi < index) return OR_PANIC_BOUNDS;      /* data[index:index+skippy] */
     if (skippy == 0) return OR_NONTERMINATING;   /* index never advances */
-    *unrec_len += skippy;
+    if (unrec) bytes_append(unrec, unrec_len, d + index, skippy);
+    else *unrec_len += skippy;
     index = hi;
   }
   return OR_OK;
@@ -256,26 +260,26 @@ static int pb_unmarshal(const uint8_t *d, int64_t l, fspec *fs, int nf, int64_t 
 
 int or_record_unmarshal(const uint8_t *d, int64_t l, or_record *m) {
   fspec fs[3] = {{1, F_I64, &m->type, 0}, {2, F_U32, &m->crc, 0}, {3, F_BYTES, &m->data, &m->data_len}};
-  return pb_unmarshal(d, l, fs, 3, &m->unrec_len);
+  return pb_unmarshal(d, l, fs, 3, &m->unrec_len, NULL);
 }
 int or_entry_unmarshal(const uint8_t *d, int64_t l, or_entry *m) {
   fspec fs[4] = {{1, F_I32, &m->type, 0}, {2, F_U64, &m->term, 0}, {3, F_U64, &m->index, 0},
                  {4, F_BYTES, &m->data, &m->data_len}};
-  return pb_unmarshal(d, l, fs, 4, &m->unrec_len);
+  return pb_unmarshal(d, l, fs, 4, &m->unrec_len, &m->unrec);
 }
 int or_hardstate_unmarshal(const uint8_t *d, int64_t l, or_hardstate *m) {
   fspec fs[3] = {{1, F_U64, &m->term, 0}, {2, F_U64, &m->vote, 0}, {3, F_U64, &m->commit, 0}};
-  return pb_unmarshal(d, l, fs, 3, &m->unrec_len);
+  return pb_unmarshal(d, l, fs, 3, &m->unrec_len, &m->unrec);
 }
 int or_snapshot_unmarshal(const uint8_t *d, int64_t l, or_snapshot *m) {
   fspec fs[5] = {{1, F_BYTES, &m->data, &m->data_len}, {2, F_U64REP, &m->nodes, &m->n_nodes},
                  {3, F_U64, &m->index, 0}, {4, F_U64, &m->term, 0},
                  {5, F_U64REP, &m->removed, &m->n_removed}};
-  return pb_unmarshal(d, l, fs, 5, &m->unrec_len);
+  return pb_unmarshal(d, l, fs, 5, &m->unrec_len, NULL);
 }
 int or_snappb_unmarshal(const uint8_t *d, int64_t l, or_snappb *m) {
   fspec fs[2] = {{1, F_U32, &m->crc, 0}, {2, F_BYTES, &m->data, &m->data_len}};
-  return pb_unmarshal(d, l, fs, 2, &m->unrec_len);
+  return pb_unmarshal(d, l, fs, 2, &m->unrec_len, NULL);
 }
 
 /* raftpb.Message.Unmarshal, raft/raftpb/raft.pb.go:407-617.  Quirks kept:
@@ -365,7 +369,8 @@ void or_message_free(or_message *m) {
 }
 
 void or_record_free(or_record *m) { free(m->data); memset(m, 0, sizeof(*m)); }
-void or_entry_free(or_entry *m) { free(m->data); memset(m, 0, sizeof(*m)); }
+void or_entry_free(or_entry *m) { free(m->data); free(m->unrec); memset(m, 0, sizeof(*m)); }
+void or_hardstate_free(or_hardstate *m) { free(m->unrec); memset(m, 0, sizeof(*m)); }
 void or_snapshot_free(or_snapshot *m) { free(m->data); free(m->nodes); free(m->removed); memset(m, 0, sizeof(*m)); }
 void or_snappb_free(or_snappb *m) { free(m->data); memset(m, 0, sizeof(*m)); }
 
@@ -500,7 +505,8 @@ int or_readall(const uint8_t *buf, int64_t len, uint64_t ri, or_readall_result *
     case 3: { /* stateType */
       or_hardstate s; memset(&s, 0, sizeof(s));
       int s2 = or_hardstate_unmarshal(rec.data, rec.data_len, &s);
-      if (s2) { st = panic_class(s2, OR_PANIC_STATE); goto fail; }
+      if (s2) { or_hardstate_free(&s); st = panic_class(s2, OR_PANIC_STATE); goto fail; }
+      or_hardstate_free(&state);   /* state = mustUnmarshalState(rec.Data): the last one wins */
       state = s; has_state = 1;
       break;
     }
@@ -542,6 +548,7 @@ fail2:
   out->enti = enti;
   or_record_free(&rec);
   free(metadata);
+  or_hardstate_free(&state);
   for (int64_t j = 0; j < n_ents; j++) or_entry_free(&ents[j]);
   free(ents);
   return st;
@@ -549,6 +556,7 @@ fail2:
 
 void or_readall_free(or_readall_result *r) {
   free(r->metadata);
+  or_hardstate_free(&r->state);
   for (int64_t j = 0; j < r->n_ents; j++) or_entry_free(&r->ents[j]);
   free(r->ents);
   memset(r, 0, sizeof(*r));
@@ -650,11 +658,12 @@ void or_maybe_commit_batch(uint64_t G, const uint64_t *match, const uint8_t *nvo
                            uint64_t *committed, const uint64_t *log_offset, const uint64_t *log_ptr,
                            const uint64_t *log_terms, uint8_t *changed, uint8_t *status) {
   for (uint64_t g = 0; g < G; g++) {
-    uint64_t m[16];
+    uint64_t m[256];
     int n = nvoters[g];
     changed[g] = 0;
     status[g] = 0;
-    if (n <= 0 || n > 16) { status[g] = OR_PANIC_BOUNDS; continue; }
+    /* no voters: mis[q-1] on an empty slice panics (raft/raft.go:255) */
+    if (n <= 0) { status[g] = OR_PANIC_BOUNDS; continue; }
     for (int v = 0; v < n; v++) m[v] = match[(uint64_t)v * G + g];
     int rc = or_maybe_commit(m, n, term[g], &committed[g], log_terms + log_ptr[g], log_ptr[g + 1] - log_ptr[g],
                              log_offset[g]);

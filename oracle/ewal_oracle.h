@@ -74,11 +74,13 @@ typedef struct {
   uint8_t *data;      /* NULL == nil */
   int64_t data_len;
   int64_t unrec_len;
+  uint8_t *unrec;     /* XXX_unrecognized (NULL == nil) */
 } or_entry;
 
 typedef struct {
   uint64_t term, vote, commit;
   int64_t unrec_len;
+  uint8_t *unrec;     /* XXX_unrecognized (NULL == nil) */
 } or_hardstate;
 
 typedef struct {
@@ -124,6 +126,7 @@ int64_t or_message_marshal(uint64_t type, uint64_t to, uint64_t from, uint64_t t
                            uint64_t commit, const uint8_t *snap, int64_t snap_len, int reject, uint8_t *out);
 void or_record_free(or_record *m);
 void or_entry_free(or_entry *m);
+void or_hardstate_free(or_hardstate *m);
 void or_snapshot_free(or_snapshot *m);
 void or_snappb_free(or_snappb *m);
 

@@ -40,11 +40,12 @@ class Record(C.Structure):
 
 class Entry(C.Structure):
     _fields_ = [("type", C.c_int32), ("term", C.c_uint64), ("index", C.c_uint64), ("data", u8p),
-                ("data_len", C.c_int64), ("unrec_len", C.c_int64)]
+                ("data_len", C.c_int64), ("unrec_len", C.c_int64), ("unrec", u8p)]
 
 
 class HardState(C.Structure):
-    _fields_ = [("term", C.c_uint64), ("vote", C.c_uint64), ("commit", C.c_uint64), ("unrec_len", C.c_int64)]
+    _fields_ = [("term", C.c_uint64), ("vote", C.c_uint64), ("commit", C.c_uint64), ("unrec_len", C.c_int64),
+                ("unrec", u8p)]
 
 
 class Snapshot(C.Structure):
@@ -84,6 +85,8 @@ lib.or_encoder_free.argtypes = [C.POINTER(Encoder)]
 lib.or_decoder_init.argtypes = [C.POINTER(Decoder), C.c_char_p, C.c_int64]
 lib.or_decode.argtypes = [C.POINTER(Decoder), C.POINTER(Record)]
 lib.or_record_free.argtypes = [C.POINTER(Record)]
+lib.or_entry_free.argtypes = [C.POINTER(Entry)]
+lib.or_hardstate_free.argtypes = [C.POINTER(HardState)]
 for _n, _t in (("record", Record), ("entry", Entry), ("hardstate", HardState), ("snapshot", Snapshot)):
     getattr(lib, "or_%s_unmarshal" % _n).argtypes = [C.c_char_p, C.c_int64, C.POINTER(_t)]
 lib.or_proto_skip.argtypes = [C.c_char_p, C.c_int64, C.POINTER(C.c_int64)]
@@ -162,13 +165,18 @@ def record_unmarshal(b):
 def entry_unmarshal(b):
     e = Entry()
     st = lib.or_entry_unmarshal(b, len(b), C.byref(e))
-    return st, dict(type=e.type, term=e.term, index=e.index, data=_bytes(e.data, e.data_len), unrec_len=e.unrec_len)
+    out = dict(type=e.type, term=e.term, index=e.index, data=_bytes(e.data, e.data_len), unrec_len=e.unrec_len,
+               unrec=_bytes(e.unrec, e.unrec_len))
+    lib.or_entry_free(C.byref(e))
+    return st, out
 
 
 def hardstate_unmarshal(b):
     h = HardState()
     st = lib.or_hardstate_unmarshal(b, len(b), C.byref(h))
-    return st, dict(term=h.term, vote=h.vote, commit=h.commit)
+    out = dict(term=h.term, vote=h.vote, commit=h.commit, unrec=_bytes(h.unrec, h.unrec_len))
+    lib.or_hardstate_free(C.byref(h))
+    return st, out
 
 
 def proto_skip(b):
@@ -199,10 +207,12 @@ def readall(buf, ri=0):
     out = dict(status=r.status, detail=r.detail, fail_record=r.fail_record, fail_offset=r.fail_offset,
                n_records=r.n_records, last_crc=r.last_crc, enti=r.enti,
                metadata=_bytes(r.metadata, r.metadata_len),
-               state=dict(term=r.state.term, vote=r.state.vote, commit=r.state.commit) if r.has_state else
-               dict(term=0, vote=0, commit=0),
+               state=dict(term=r.state.term, vote=r.state.vote, commit=r.state.commit,
+                          unrec=_bytes(r.state.unrec, r.state.unrec_len)) if r.has_state else
+               dict(term=0, vote=0, commit=0, unrec=None),
                ents=[dict(type=r.ents[i].type, term=r.ents[i].term, index=r.ents[i].index,
-                          data=_bytes(r.ents[i].data, r.ents[i].data_len)) for i in range(r.n_ents)])
+                          data=_bytes(r.ents[i].data, r.ents[i].data_len),
+                          unrec=_bytes(r.ents[i].unrec, r.ents[i].unrec_len)) for i in range(r.n_ents)])
     lib.or_readall_free(C.byref(r))
     return out
 

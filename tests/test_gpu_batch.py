@@ -140,12 +140,11 @@ def test_batch_random_corruption(ctx, seed):
     res = W.readall_batch_bytes([bytes(x) for x in shards], [0] * len(shards), ctx)
     for buf, g in zip(shards, res):
         o = O.readall(bytes(buf), 0)
-        if g.status == L.UNSUPPORTED_ENCODING:   # as in the single-WAL corruption tests
-            assert o["status"] == O.OK or o["fail_record"] >= g.fail_record or o["fail_record"] < 0
-            continue
         assert g.status == o["status"]
         if o["status"] not in (O.OK, O.ERR_INDEX_NOT_FOUND):
-            assert g.fail_record == o["fail_record"]
+            assert (g.fail_record, g.fail_offset) == (o["fail_record"], o["fail_offset"])
+        if o["status"] == O.OK:
+            assert (g.n_records, g.last_crc, g.enti) == (o["n_records"], o["last_crc"], o["enti"])
 
 
 def test_batch_synthetic_shards(ctx):

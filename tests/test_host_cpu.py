@@ -83,7 +83,7 @@ def test_synth_wal_is_valid_and_corruption_lands():
     r = O.readall(bytes(buf), 1)
     assert r["status"] == O.OK and r["n_records"] == n
     assert [e["index"] for e in r["ents"]] == list(range(1, n - 2))
-    assert r["metadata"] == b"\x08\x01" and r["state"] == dict(term=1, vote=1, commit=0)
+    assert r["metadata"] == b"\x08\x01" and r["state"] == dict(term=1, vote=1, commit=0, unrec=None)
     bad, n2 = W.synth_wal(1 << 20, 64, 4096, seed=5, corrupt_record=17)
     r2 = O.readall(bytes(bad), 1)
     assert n2 == n and r2["status"] == O.ERR_RECORD_CRC and r2["fail_record"] == 17
@@ -105,7 +105,7 @@ def test_writer_dir_matches_oracle(tmp_path):
     whole = b"".join(open(os.path.join(d, x), "rb").read() for x in names)
     r = O.readall(whole, 0)
     assert r["status"] == O.OK and [e["index"] for e in r["ents"]] == list(range(6))
-    assert r["state"] == dict(term=1, vote=1, commit=5)
+    assert r["state"] == dict(term=1, vote=1, commit=5, unrec=None)
     with pytest.raises(FileExistsError):
         W.Create(d, None)
 

@@ -75,7 +75,7 @@ def test_recover():
     r = O.readall(_recover_wal(), 0)
     assert r["status"] == O.OK
     assert r["metadata"] == g["metadata"].encode()
-    assert r["state"] == g["want_state"]
+    assert r["state"] == dict(g["want_state"], unrec=None)
     assert [(x["index"], x["term"], x["data"]) for x in r["ents"]] == \
         [(x["index"], x["term"], bytes.fromhex(x["data_hex"]) if x["data_hex"] else None) for x in g["ents"]]
 
