@@ -4,9 +4,11 @@ Product layout:
   csrc/        HIP kernels (gfx950) + host C++ behind the C ABI in include/ewal.h
   libewal.so   built in-tree by build.sh
   wal.py       mirror of the reference `wal` package (OpenAtIndex/ReadAll/Create/...)
-  snap.py      mirror of `snap.Snapshotter` (Load / batch verify)
+  snap.py      mirror of `snap.Snapshotter` (Load / snapNames / batch verify)
   raft.py      batched `raft.maybeCommit`
   crc.py       `pkg/crc` digest (chained CRC-32C) over host or device buffers
+  raftmsg.py   batched `raftpb.Message` decode (the /raft ingress)
+  shard.py     per-rank shard assignment + the RCCL summary all-reduce
 """
 from . import _lib  # noqa: F401  (fails loudly if libewal.so is missing)
 from .wal import Context, OpenAtIndex, Create, Encoder, readall_bytes, synth_wal  # noqa: F401

@@ -129,6 +129,11 @@ _SIGS = {
     "ewal_wal_bytes": (u8p, [vp, C.POINTER(C.c_uint64)]),
     "ewal_wal_seq": (C.c_uint64, [vp]),
     "ewal_wal_close": (None, [vp]),
+    "ewal_parse_wal_name": (C.c_int, [C.c_char_p, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
+    "ewal_search_index": (C.c_int64, [C.POINTER(C.c_char_p), C.c_uint64, C.c_uint64]),
+    "ewal_is_valid_seq": (C.c_int, [C.POINTER(C.c_char_p), C.c_uint64]),
+    "ewal_wal_name": (None, [C.c_uint64, C.c_uint64, C.c_char_p]),
+    "esnap_names": (C.c_int64, [C.c_char_p, C.c_char_p, C.c_uint64, C.POINTER(C.c_uint64)]),
     "ewal_create": (C.c_int, [C.c_char_p, C.c_char_p, C.c_uint64, C.c_int, C.POINTER(vp)]),
     "ewal_writer_save_entry": (C.c_int, [vp, C.c_int32, C.c_uint64, C.c_uint64, C.c_char_p, C.c_uint64]),
     "ewal_writer_save_state": (C.c_int, [vp, C.c_uint64, C.c_uint64, C.c_uint64]),

@@ -252,6 +252,39 @@ uint32_t ewal_crc32_combine(uint32_t poly, uint32_t crc_a, uint32_t crc_b, uint6
   return tables(poly).combine(crc_a, crc_b, len_b);
 }
 
+// ---- wal file names, wal/util.go:20-88 ---------------------------------------
+int ewal_parse_wal_name(const char *name, uint64_t *seq, uint64_t *index) {
+  uint64_t a = 0, b = 0;
+  if (!name || !parse_wal_name(name, &a, &b)) return 0;
+  if (seq) *seq = a;
+  if (index) *index = b;
+  return 1;
+}
+
+int64_t ewal_search_index(const char *const *names, uint64_t n, uint64_t index) {
+  for (uint64_t k = n; k-- > 0;) {
+    uint64_t s, i;
+    if (!parse_wal_name(names[k], &s, &i)) return EWAL_E_INVAL;   // Go: panic("parse correct name error")
+    if (index >= i) return (int64_t)k;
+  }
+  return -1;
+}
+
+int ewal_is_valid_seq(const char *const *names, uint64_t n) {
+  uint64_t last = 0;
+  for (uint64_t k = 0; k < n; ++k) {
+    uint64_t s, i;
+    if (!parse_wal_name(names[k], &s, &i)) return EWAL_E_INVAL;
+    if (last != 0 && last != s - 1) return 0;
+    last = s;
+  }
+  return 1;
+}
+
+void ewal_wal_name(uint64_t seq, uint64_t index, char *out) {
+  std::snprintf(out, 38, "%016llx-%016llx.wal", (unsigned long long)seq, (unsigned long long)index);
+}
+
 // ---- wal.OpenAtIndex, wal/wal.go:108-159 ------------------------------------
 int ewal_open_at_index(const char *dirpath, uint64_t index, ewal_wal **out) {
   *out = nullptr;
@@ -263,22 +296,11 @@ int ewal_open_at_index(const char *dirpath, uint64_t index, ewal_wal **out) {
   }
   if (names.empty()) return EWAL_ERR_FILE_NOT_FOUND;
   std::sort(names.begin(), names.end());
-  // searchIndex: last name whose start index <= index
-  long ni = -1;
-  for (long k = (long)names.size() - 1; k >= 0; --k) {
-    uint64_t s, i;
-    parse_wal_name(names[(size_t)k], &s, &i);
-    if (index >= i) { ni = k; break; }
-  }
+  std::vector<const char *> np;
+  for (auto &n : names) np.push_back(n.c_str());
+  const int64_t ni = ewal_search_index(np.data(), np.size(), index);
   if (ni < 0) return EWAL_ERR_FILE_NOT_FOUND;
-  // isValidSeq(names[nameIndex:])
-  uint64_t last = 0;
-  for (size_t k = (size_t)ni; k < names.size(); ++k) {
-    uint64_t s, i;
-    parse_wal_name(names[k], &s, &i);
-    if (last != 0 && last != s - 1) return EWAL_ERR_FILE_NOT_FOUND;
-    last = s;
-  }
+  if (ewal_is_valid_seq(np.data() + ni, np.size() - (size_t)ni) != 1) return EWAL_ERR_FILE_NOT_FOUND;
   auto *w = new ewal_wal();
   w->dir = dirpath;
   w->ri = index;
@@ -560,14 +582,36 @@ int64_t ewal_synth_wal(uint64_t seed, uint64_t target, uint32_t min_data, uint32
 }
 
 // ---- Snapshotter.Load, snap/snapshotter.go:62-74, 76-111, 115-150 ----------
-int esnap_load_dir(ewal_ctx *ctx, const char *dirpath, uint32_t poly, esnap_snapshot *out, char **out_name) {
-  if (out_name) *out_name = nullptr;
-  std::vector<std::string> all, snaps;
+// snapNames: the directory's *.snap names, newest (largest) first
+static int snap_names(const char *dirpath, std::vector<std::string> *snaps) {
+  std::vector<std::string> all;
   if (!read_dir(dirpath, &all)) return EWAL_E_IO;
   for (auto &n : all)   // checkSuffix
-    if (n.size() >= 5 && n.compare(n.size() - 5, 5, ".snap") == 0) snaps.push_back(n);
-  if (snaps.empty()) return EWAL_ERR_NO_SNAPSHOT;
-  std::sort(snaps.rbegin(), snaps.rend());   // sort.Reverse(sort.StringSlice)
+    if (n.size() >= 5 && n.compare(n.size() - 5, 5, ".snap") == 0) snaps->push_back(n);
+  if (snaps->empty()) return EWAL_ERR_NO_SNAPSHOT;
+  std::sort(snaps->rbegin(), snaps->rend());   // sort.Reverse(sort.StringSlice)
+  return EWAL_OK;
+}
+
+int64_t esnap_names(const char *dirpath, char *out, uint64_t cap, uint64_t *len) {
+  std::vector<std::string> snaps;
+  const int st = snap_names(dirpath, &snaps);
+  if (st != EWAL_OK) return st == EWAL_ERR_NO_SNAPSHOT ? 0 : st;
+  std::string joined;
+  for (auto &n : snaps) {
+    joined += n;
+    joined.push_back('\0');
+  }
+  if (len) *len = joined.size();
+  if (out && cap) std::memcpy(out, joined.data(), std::min<uint64_t>(cap, joined.size()));
+  return (int64_t)snaps.size();
+}
+
+int esnap_load_dir(ewal_ctx *ctx, const char *dirpath, uint32_t poly, esnap_snapshot *out, char **out_name) {
+  if (out_name) *out_name = nullptr;
+  std::vector<std::string> snaps;
+  const int sn = snap_names(dirpath, &snaps);
+  if (sn != EWAL_OK) return sn;
   int err = EWAL_ERR_NO_SNAPSHOT;
   for (auto &name : snaps) {
     const std::string path = std::string(dirpath) + "/" + name;

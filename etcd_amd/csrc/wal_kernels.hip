@@ -115,19 +115,25 @@ __device__ __forceinline__ uint32_t load_word_guarded(const uint8_t *buf, uint64
 // only for such lanes).  E = D ^ 08080808, so x ^ 08.. = E[J+2] and
 // y ^ 10.. = alignbyte(E[J+3], E[J+2], 2) ^ 18..; one bitop3 each for z and
 // for the accumulated zero-byte test.
+// The pattern is CAND_TEST's pre-test, "length MSB 00 + tag 08" at p+7 / p+8:
+// byte k of z = (stream byte b ^ 08) | (byte b-1), zero iff the pair
+// matches.  Per dword pair: 2 alignbyte + 2 bitop3 (z) + ONE 64-bit add for
+// both borrow tests + 2 bitop3 (accumulate) = 3.5 VALU per dword.
 __device__ __forceinline__ uint32_t cand_filter(const uint32_t (&D)[19]) {
-  // per dword: 1 xor, 1 alignbyte, 3 bitop3/add (5 VALU)
-  //   z   = e0 | (y ^ 18..)            bitop3 0xF6 (a | (b ^ c))
+  //   z   = (x ^ 08..) | y             bitop3 0xDE ((a ^ c) | b)
   //   acc = ((z - 01..) & ~z) | acc    bitop3 0xBA ((a & ~b) | c)
-  uint32_t acc = 0;
+  uint32_t acc0 = 0, acc1 = 0;
 #pragma unroll
-  for (int J = 0; J < 16; ++J) {
-    const uint32_t e = D[J + 2] ^ 0x08080808u;                            // x ^ 08..
-    const uint32_t y = __builtin_amdgcn_alignbyte(D[J + 3], D[J + 2], 2);   // raw: no xor to carry
-    const uint32_t z = __builtin_amdgcn_bitop3_b32(e, y, 0x10101010u, 0xF6);
-    acc = __builtin_amdgcn_bitop3_b32(z + 0xFEFEFEFFu, z, acc, 0xBA);
+  for (int J = 0; J < 16; J += 2) {
+    const uint32_t y0 = __builtin_amdgcn_alignbyte(D[J + 2], D[J + 1], 3);
+    const uint32_t y1 = __builtin_amdgcn_alignbyte(D[J + 3], D[J + 2], 3);
+    const uint32_t z0 = __builtin_amdgcn_bitop3_b32(D[J + 2], y0, 0x08080808u, 0xDE);
+    const uint32_t z1 = __builtin_amdgcn_bitop3_b32(D[J + 3], y1, 0x08080808u, 0xDE);
+    const uint64_t s = (((uint64_t)z1 << 32) | z0) + 0xFEFEFEFEFEFEFEFFull;
+    acc0 = __builtin_amdgcn_bitop3_b32((uint32_t)s, z0, acc0, 0xBA);
+    acc1 = __builtin_amdgcn_bitop3_b32((uint32_t)(s >> 32), z1, acc1, 0xBA);
   }
-  return acc & 0x80808080u;
+  return (acc0 | acc1) & 0x80808080u;
 }
 
 __device__ __forceinline__ uint32_t count_cands(const uint32_t (&D)[19], uint64_t off, uint64_t B) {

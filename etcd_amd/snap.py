@@ -8,7 +8,7 @@
 * `verify_packed` -- loadSnap's CRC check for many files at once
   (esnap_verify_packed; snap/snapshotter.go:76-111).
 * `load_dir` -- Snapshotter.Load (newest first, tried failures renamed
-  .broken; snap/snapshotter.go:62-74).
+  .broken; snap/snapshotter.go:62-74); `snap_names` -- snapNames.
 """
 import ctypes as C
 
@@ -59,3 +59,17 @@ def load_dir(ctx, dirpath, poly=L.CASTAGNOLI):
     name = C.c_char_p()
     check(lib.esnap_load_dir(ctx.handle, dirpath.encode(), poly, C.byref(s), C.byref(name)))
     return name.value.decode(), s
+
+
+def snap_names(dirpath):
+    """Snapshotter.snapNames: *.snap names newest first; raises EwalError
+    (ErrNoSnapshot) when there are none (snap/snapshotter.go:115-131)."""
+    need = C.c_uint64(0)
+    n = lib.esnap_names(dirpath.encode(), None, 0, C.byref(need))
+    if n < 0:
+        check(int(n))
+    if n == 0:
+        check(L.ERR_NO_SNAPSHOT)
+    buf = C.create_string_buffer(max(1, need.value))
+    lib.esnap_names(dirpath.encode(), buf, need.value, C.byref(need))
+    return buf.raw[:need.value].decode().split("\0")[:n]

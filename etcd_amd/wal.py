@@ -288,6 +288,41 @@ class WAL:
             pass
 
 
+def parseWalName(name: str):
+    """(seq, index) of "%016x-%016x.wal", or raises ValueError (wal/util.go:77-84)."""
+    s, i = C.c_uint64(), C.c_uint64()
+    if not lib.ewal_parse_wal_name(name.encode(), C.byref(s), C.byref(i)):
+        raise ValueError("bad wal name: %s" % name)
+    return s.value, i.value
+
+
+def _names(names):
+    return (C.c_char_p * max(1, len(names)))(*[n.encode() for n in names])
+
+
+def searchIndex(names, index):
+    """(last i with parseWalName(names[i]).index <= index, found) (wal/util.go:20-32)."""
+    k = lib.ewal_search_index(_names(names), len(names), index)
+    if k < -1:
+        check(int(k))
+    return int(k), k >= 0
+
+
+def isValidSeq(names):
+    """The seqs of sorted names increase by one (the check skipped while the
+    last seq is 0), wal/util.go:36-49."""
+    r = lib.ewal_is_valid_seq(_names(names), len(names))
+    if r < 0:
+        check(r)
+    return r == 1
+
+
+def walName(seq, index):
+    out = C.create_string_buffer(38)
+    lib.ewal_wal_name(seq, index, out)
+    return out.value.decode()
+
+
 def OpenAtIndex(dirpath: str, index: int, ctx: Context = None) -> WAL:
     h = C.c_void_p()
     st = lib.ewal_open_at_index(dirpath.encode(), index, C.byref(h))

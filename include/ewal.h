@@ -174,6 +174,13 @@ typedef struct ewal_wal ewal_wal;
 /* wal.OpenAtIndex(dirpath, index), wal/wal.go:108-159 (file selection:
  * wal/util.go:20-88).  Reads names[nameIndex:] into one buffer. */
 int ewal_open_at_index(const char *dirpath, uint64_t index, ewal_wal **out);
+/* The file-name helpers OpenAtIndex uses (host-only), wal/util.go:20-88:
+ * parseWalName (1 = parsed), searchIndex over sorted names (the index, -1
+ * when none), isValidSeq (1 / 0), walName (out: 38 bytes). */
+int ewal_parse_wal_name(const char *name, uint64_t *seq, uint64_t *index);
+int64_t ewal_search_index(const char *const *names, uint64_t n, uint64_t index);
+int ewal_is_valid_seq(const char *const *names, uint64_t n);
+void ewal_wal_name(uint64_t seq, uint64_t index, char *out);
 int ewal_wal_readall(ewal_wal *w, ewal_ctx *ctx, ewal_result *out);
 const uint8_t *ewal_wal_bytes(ewal_wal *w, uint64_t *len);
 uint64_t ewal_wal_seq(ewal_wal *w);
@@ -241,7 +248,10 @@ int esnap_verify_packed(ewal_ctx *ctx, const void *d_buf, uint64_t buf_len, cons
                         uint32_t *stored_crc, uint32_t *computed_crc);
 /* Snapshotter.Load(): newest-first over dir's *.snap, first success wins,
  * tried failures renamed *.broken.  On success *out_name (malloc'd, caller
- * frees with free()) names the snapshot file loaded; snapshot fields out. */
+ * frees with free()) names the snapshot file loaded; snapshot fields out.
+ * Only the errors Go's loadSnap returns rename a file .broken; a Go panic
+ * class or EWAL_UNSUPPORTED_ENCODING (a valid file this layout cannot
+ * return in full) stops Load with *out_name naming that file, not renamed. */
 typedef struct esnap_snapshot {
   uint64_t index, term;
   uint64_t data_off, data_len;   /* raftpb.Snapshot.Data within the file */
@@ -252,6 +262,10 @@ typedef struct esnap_snapshot {
  * meaningful when status[i] == EWAL_OK). */
 int esnap_copy_snapshot(ewal_ctx *ctx, uint32_t i, esnap_snapshot *out);
 int esnap_load_dir(ewal_ctx *ctx, const char *dirpath, uint32_t poly, esnap_snapshot *out, char **out_name);
+/* Snapshotter.snapNames (snap/snapshotter.go:115-131): the *.snap names,
+ * newest first, NUL-separated into out (cap bytes; *len = bytes needed).
+ * Returns the count (0: ErrNoSnapshot) or a negative error. */
+int64_t esnap_names(const char *dirpath, char *out, uint64_t cap, uint64_t *len);
 
 /* ---- raft quorum commit: raft.maybeCommit, raft/raft.go:248-258 ---------- */
 /* Batched over G independent raft groups (SoA).  match[v*G + g] for voter
