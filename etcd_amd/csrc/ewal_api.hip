@@ -22,6 +22,7 @@
 #include "wal_kernels.hip"
 #include "aux_kernels.hip"
 #include "msg_kernels.hip"
+#include "fused_kernels.hip"
 
 #define EW_CHECK(x)                                                          \
   do {                                                                       \
@@ -88,7 +89,7 @@ struct ewal_ctx {
   std::map<uint32_t, DevTables> tables;
   std::map<uint32_t, std::unique_ptr<ewal::CrcTables>> host_tables;
   DevBuf encw, encs, lbstat, gagg, slow, mlist, pf, v, pwave, ux, tagg, tpx, wcnt, slots, cbase, ovf, cpos, clen, nxt, exc, E, rs, jl, vis, entry, on, rec_cand, rd, opf, ops, kk, kkrev, suf,
-      ents, recs, tmp, small, sdesc, snaps, hbuf_dev, xpos, walk, fpos, ulist, uitems, uarena;
+      ents, recs, tmp, small, sdesc, snaps, hbuf_dev, xpos, walk, fpos, ulist, uitems, uarena, fstat, ftrec;
   std::vector<ewal_unrec> unrec;   // XXX_unrecognized of the last ReadAll's result (side list)
   uint64_t unrec_bytes = 0;
   // batched ReadAll (ewal_readall_batch_device): shard tables, results, ents
@@ -105,6 +106,11 @@ struct ewal_ctx {
   uint64_t last_n = 0, last_nents = 0;
   uint64_t last_k = 0;     // candidates of the previous call (sizes k_frame's descriptors)
   uint32_t epoch = 0;      // k_check look-back epoch (24 bits)
+  uint32_t fepoch = 0;     // k_fc look-back epoch (24 bits)
+  int fused = 1;           // the fused frame + check pass first (EWAL_FUSED=0: the general path only)
+  bool rd_valid = false;   // c->rd holds the last call's per-frame descriptors
+  const uint8_t *last_buf = nullptr;   // the last ReadAll's stream (materialise_records)
+  uint64_t last_B = 0, last_ri = 0;
   uint64_t pfcap = 0;      // pf = [P at data starts | P at frame starts], pfcap each
   bool last_ok = false;
 };
@@ -424,6 +430,71 @@ static int walk_chain(ewal_ctx *c, DevTables *tb, const uint8_t *d_buf, uint64_t
   return 0;
 }
 
+// The fused frame + check pass (k_fc + k_result_fc, fused_kernels.hip) over
+// the stream pass's candidates: ONE host sync.  *done when the regular case
+// held (ResultDev in c->h_res, ents in c->ents); otherwise the reductions are
+// reset and the caller runs the general path over the same stream pass.
+// ents / mlist are sized for every candidate being an op (*ecap), grown when
+// the candidate count exceeds them (k_fc declines before doing any work).
+static int fused_pass(ewal_ctx *c, DevTables *tb, const uint8_t *d_buf, uint64_t B, uint64_t ri, uint64_t ccap,
+                      uint64_t ecap, bool *done) {
+  Small *ds = c->small.as<Small>();
+  *done = false;
+  const uint64_t ntiles = ccap / FC_THREADS + 2;
+  const size_t had = c->fstat.cap;
+  EW_CHECK(c->fstat.ensure((size_t)ntiles * 8));
+  EW_CHECK(c->ftrec.ensure((size_t)ntiles * sizeof(TileRec)));
+  for (int pass = 0; pass < 2; ++pass) {
+    EW_CHECK(c->ents.ensure((size_t)ecap * sizeof(ewal_entry)));
+    EW_CHECK(c->mlist.ensure((size_t)ecap * 4));
+    c->fepoch = (c->fepoch + 1) & 0xffffffu;
+    if (c->fstat.cap != had || c->fepoch == 0 || pass) {
+      EW_CHECK(hipMemsetAsync(c->fstat.p, 0, c->fstat.cap, c->stream));
+      if (c->fepoch == 0) c->fepoch = 1;
+    }
+    FcArgs a;
+    a.buf = d_buf;
+    a.B = B;
+    a.cpos = c->cpos.as<uint64_t>();
+    a.ccap = ccap;
+    a.ecap = ecap;
+    a.pwave = c->pwave.as<uint32_t>();
+    a.v = c->v.as<uint32_t>();
+    a.g_slice = tb->slice;
+    a.g_shift = tb->shift;
+    a.ri = ri;
+    a.status = c->fstat.as<unsigned long long>();
+    a.trec = c->ftrec.as<TileRec>();
+    a.epoch = c->fepoch;
+    a.ents = c->ents.as<ewal_entry>();
+    a.mlist = c->mlist.as<uint32_t>();
+    a.ds = ds;
+    hipLaunchKernelGGL(k_fc<false>, dim3((unsigned)std::max(1, c->num_cu) * FC_WGS), dim3(FC_THREADS), 0, c->stream,
+                       a, SegArgs{});
+    hipLaunchKernelGGL(k_fc_seam<false>, dim3(grid_for(ntiles, 256)), dim3(256), 0, c->stream, d_buf, B, a.cpos,
+                       tb->shift, a.trec, a.ents, ri, ccap, ecap, ds, SegArgs{});
+    hipLaunchKernelGGL(k_result_fc, dim3(1), dim3(256), 0, c->stream, d_buf, B, a.cpos, ccap, ecap, ri, a.mlist, ds,
+                       c->h_res_dev, c->h_small_dev);
+    EW_CHECK(hipGetLastError());
+    EW_CHECK(hipStreamSynchronize(c->stream));
+    if (c->h_small->errflag) return EWAL_E_TIMEOUT;
+    if (c->h_small->spec_n) {
+      *done = true;
+      return 0;
+    }
+    hipLaunchKernelGGL(k_reset_check, dim3(1), dim3(64), 0, c->stream, ds);
+    EW_CHECK(hipGetLastError());
+    const uint64_t K = c->h_small->total;
+    // k_fc declined for capacity only: room for every candidate, once more
+    if (c->h_small->fc.rare == 4u && K > ecap && K <= ccap && !c->h_small->novf) {
+      ecap = K + K / 8 + 1024;
+      continue;
+    }
+    break;
+  }
+  return 0;
+}
+
 // XXX_unrecognized of the returned ents / HardState (wal/wal.go:164-216
 // returns them inside the structs; raft.pb.go:270 appends each unknown
 // field): the entry ops k_check listed that survive in ents (op j is ents[j]
@@ -489,6 +560,10 @@ static int readall_impl(ewal_ctx *c, const uint8_t *d_buf, uint64_t B, uint64_t 
   c->last_nents = 0;
   c->unrec.clear();
   c->unrec_bytes = 0;
+  c->rd_valid = false;
+  c->last_buf = d_buf;
+  c->last_B = B;
+  c->last_ri = ri;
   if (((uintptr_t)d_buf & 15) != 0 && B) return EWAL_E_INVAL;
   DevTables *tb;
   int rc = get_tables(c, 0x82F63B78u, &tb);
@@ -516,9 +591,14 @@ static int readall_impl(ewal_ctx *c, const uint8_t *d_buf, uint64_t B, uint64_t 
                                                                  B / 4096 + 1024));
     rc = run_stream(c, tb, d_buf, B, 1, ccap);
     if (rc) return rc;
+    bool fused_done = false;
+    if (c->fused) {
+      rc = fused_pass(c, tb, d_buf, B, ri, ccap, rdcap, &fused_done);
+      if (rc) return rc;
+    }
     uint32_t *pf = nullptr;
     bool rescanned = false;
-    for (int pass = 0; pass < 3; ++pass) {
+    for (int pass = 0; pass < 3 && !fused_done; ++pass) {
       EW_CHECK(c->rd.ensure(rdcap * sizeof(RecDesc)));
       EW_CHECK(c->pf.ensure(rdcap * 8));
       EW_CHECK(c->slow.ensure(rdcap * 4));
@@ -585,8 +665,13 @@ static int readall_impl(ewal_ctx *c, const uint8_t *d_buf, uint64_t B, uint64_t 
     }
     K = c->h_small->total;
     c->last_k = K;
-    if (K && K <= ccap && K <= rdcap && !c->h_small->novf && c->h_small->pos0 == 0 && !c->h_small->irregular) {
+    if (fused_done) {   // frames decoded and checked by k_fc; the result is in h_res
       decoded = true;
+      spec_checked = true;
+    } else if (K && K <= ccap && K <= rdcap && !c->h_small->novf && c->h_small->pos0 == 0 &&
+               !c->h_small->irregular) {
+      decoded = true;
+      c->rd_valid = true;
       if (c->h_small->nslow && !spec_checked) {   // frames the canonical parser declined
         hipLaunchKernelGGL(k_decode_slow, dim3(std::min<uint64_t>(grid_for(c->h_small->nslow, 256), 1024)),
                            dim3(256), 0, c->stream, d_buf, B, c->cpos.as<uint64_t>(), (const uint32_t *)nullptr,
@@ -691,6 +776,7 @@ static int readall_impl(ewal_ctx *c, const uint8_t *d_buf, uint64_t B, uint64_t 
       const uint32_t *rc_list = (regular || fpos) ? (const uint32_t *)nullptr : c->rec_cand.as<uint32_t>();
       const uint64_t *plist = fpos ? fpos : c->cpos.as<uint64_t>();
       EW_CHECK(hipMemsetAsync(&ds->nslow, 0, 4, c->stream));
+      c->rd_valid = true;
       hipLaunchKernelGGL(k_decode, dim3(grid_for(n, 256)), dim3(256), 0, c->stream, d_buf, B,
                          plist, rc_list, n32, c->pwave.as<uint32_t>(), c->v.as<uint32_t>(),
                          tb->slice, tb->shift, c->rd.as<RecDesc>(), pf, pf + c->pfcap, c->slow.as<uint32_t>(), ds);
@@ -842,6 +928,102 @@ static hipError_t grow_keep(DevBuf &b, size_t need, size_t keep, hipStream_t st)
   return hipSuccess;
 }
 
+// The batch on the fused pass (k_shard_start_fc, k_fc<true>, per-shard
+// metadata rule and results): ONE host sync.  *done when every shard took
+// the regular case (out[] and the ents / ent_first tables filled); otherwise
+// the reductions are reset and the caller runs the general batch path.
+static int fused_batch(ewal_ctx *c, DevTables *tb, const uint8_t *d_buf, uint64_t B, uint32_t ns,
+                       const std::vector<uint64_t> &soff, const uint64_t *ris, uint64_t ccap, uint64_t ecap,
+                       ewal_result *out, bool *done) {
+  Small *ds = c->small.as<Small>();
+  *done = false;
+  const uint64_t ntiles = ccap / FC_THREADS + 2;
+  const size_t had = c->fstat.cap;
+  EW_CHECK(c->fstat.ensure((size_t)ntiles * 8));
+  EW_CHECK(c->ftrec.ensure((size_t)ntiles * sizeof(TileRec)));
+  EW_CHECK(c->bsoff.ensure((size_t)(ns + 1) * 8));
+  EW_CHECK(c->bri.ensure((size_t)ns * 8));
+  EW_CHECK(c->bfs.ensure((size_t)(ns + 1) * 4));
+  EW_CHECK(c->bsagg.ensure((size_t)ns * sizeof(ShardAgg)));
+  EW_CHECK(c->bres.ensure((size_t)ns * sizeof(ewal_result)));
+  EW_CHECK(c->bef.ensure((size_t)ns * 8));
+  EW_CHECK(hipMemcpyAsync(c->bsoff.p, soff.data(), (size_t)(ns + 1) * 8, hipMemcpyHostToDevice, c->stream));
+  EW_CHECK(hipMemcpyAsync(c->bri.p, ris, (size_t)ns * 8, hipMemcpyHostToDevice, c->stream));
+  SegArgs sg;
+  sg.ulist = nullptr;
+  sg.fs = c->bfs.as<uint32_t>();
+  sg.ns = ns;
+  sg.ri = c->bri.as<uint64_t>();
+  sg.soff = c->bsoff.as<uint64_t>();
+  sg.sagg = c->bsagg.as<ShardAgg>();
+  for (int pass = 0; pass < 2; ++pass) {
+    EW_CHECK(grow_keep(c->bents, (size_t)ecap * sizeof(ewal_entry), 0, c->stream));
+    EW_CHECK(c->mlist.ensure((size_t)ecap * 4));
+    c->fepoch = (c->fepoch + 1) & 0xffffffu;
+    if (c->fstat.cap != had || c->fepoch == 0 || pass) {
+      EW_CHECK(hipMemsetAsync(c->fstat.p, 0, c->fstat.cap, c->stream));
+      if (c->fepoch == 0) c->fepoch = 1;
+    }
+    FcArgs a;
+    a.buf = d_buf;
+    a.B = B;
+    a.cpos = c->cpos.as<uint64_t>();
+    a.ccap = ccap;
+    a.ecap = ecap;
+    a.pwave = c->pwave.as<uint32_t>();
+    a.v = c->v.as<uint32_t>();
+    a.g_slice = tb->slice;
+    a.g_shift = tb->shift;
+    a.ri = 0;
+    a.status = c->fstat.as<unsigned long long>();
+    a.trec = c->ftrec.as<TileRec>();
+    a.epoch = c->fepoch;
+    a.ents = c->bents.as<ewal_entry>();
+    a.mlist = c->mlist.as<uint32_t>();
+    a.ds = ds;
+    hipLaunchKernelGGL(k_shard_start_fc, dim3(grid_for(ns + 1, 256)), dim3(256), 0, c->stream, a.cpos, ccap,
+                       c->bsoff.as<uint64_t>(), ns, c->bfs.as<uint32_t>(), sg.sagg, ds);
+    hipLaunchKernelGGL(k_fc<true>, dim3((unsigned)std::max(1, c->num_cu) * FC_WGS), dim3(FC_THREADS), 0, c->stream, a,
+                       sg);
+    hipLaunchKernelGGL(k_fc_seam<true>, dim3(grid_for(ntiles, 256)), dim3(256), 0, c->stream, d_buf, B, a.cpos,
+                       tb->shift, a.trec, a.ents, 0ull, ccap, ecap, ds, sg);
+    hipLaunchKernelGGL(k_meta_batch_fc, dim3(64), dim3(256), 0, c->stream, d_buf, B, a.cpos, ccap, ecap, a.mlist, ds,
+                       sg);
+    hipLaunchKernelGGL(k_result_batch_fc, dim3(grid_for((uint64_t)ns * 8, 256)), dim3(256), 0, c->stream, d_buf, B, a.cpos, ccap,
+                       ecap, ds, sg, c->bres.as<ewal_result>(), c->bef.as<unsigned long long>());
+    hipLaunchKernelGGL(k_batch_gate_fc, dim3(1), dim3(64), 0, c->stream, ds, ccap, ecap, B, c->h_small_dev);
+    EW_CHECK(hipGetLastError());
+    EW_CHECK(hipMemcpyAsync(out, c->bres.p, (size_t)ns * sizeof(ewal_result), hipMemcpyDeviceToHost, c->stream));
+    EW_CHECK(hipMemcpyAsync(c->bent_first.data(), c->bef.p, (size_t)ns * 8, hipMemcpyDeviceToHost, c->stream));
+    EW_CHECK(hipEventRecord(c->ev1, c->stream));
+    EW_CHECK(hipStreamSynchronize(c->stream));
+    if (c->h_small->errflag) return EWAL_E_TIMEOUT;
+    const uint64_t K = c->h_small->total;
+    c->last_k = K;
+    if (c->h_small->spec_n) {
+      float dev_ms = 0, str_ms = 0;
+      EW_CHECK(hipEventElapsedTime(&dev_ms, c->ev0, c->ev1));
+      EW_CHECK(hipEventElapsedTime(&str_ms, c->evs0, c->evs1));
+      for (uint32_t i = 0; i < ns; ++i) {
+        out[i].device_ms = dev_ms;
+        out[i].stream_ms = str_ms;
+        c->bnents[i] = (uint64_t)out[i].n_ents;
+        if (!out[i].n_ents) c->bent_first[i] = 0;
+      }
+      *done = true;
+      return 0;
+    }
+    hipLaunchKernelGGL(k_reset_check, dim3(1), dim3(64), 0, c->stream, ds);
+    EW_CHECK(hipGetLastError());
+    if (c->h_small->fc.rare == 4u && K > ecap && K <= ccap && !c->h_small->novf) {
+      ecap = K + K / 8 + 1024;
+      continue;
+    }
+    break;
+  }
+  return 0;
+}
+
 // Batched ReadAll over many independent WALs (per-raft-group shards, SURVEY
 // §8(d) C3) laid end to end in one device buffer: ONE stream pass, ONE frame
 // pass and ONE segmented check (k_check<true>) for the whole batch, two host
@@ -882,6 +1064,12 @@ static int readall_batch_impl(ewal_ctx *c, const uint8_t *d_buf, uint32_t ns, co
                                                                  B / 1024 + 1024));
     rc = run_stream(c, tb, d_buf, B, 1, ccap);
     if (rc) return rc;
+    if (c->fused) {
+      bool done = false;
+      rc = fused_batch(c, tb, d_buf, B, ns, soff, ris, ccap, rdcap, out, &done);
+      if (rc) return rc;
+      if (done) return 0;
+    }
     uint32_t *pf = nullptr;
     bool rescanned = false;
     for (int pass = 0; pass < 3; ++pass) {
@@ -1027,6 +1215,50 @@ static int readall_batch_impl(ewal_ctx *c, const uint8_t *d_buf, uint32_t ns, co
   return 0;
 }
 
+// The per-frame descriptors of the last ReadAll when the fused pass decided
+// it (it keeps none in HBM): the general path's frame pass and check over the
+// same stream pass (still in the ctx), for ewal_copy_records.
+static int materialise_records(ewal_ctx *c) {
+  const uint64_t n = c->last_n;
+  DevTables *tb;
+  int rc = get_tables(c, 0x82F63B78u, &tb);
+  if (rc) return rc;
+  Small *ds = c->small.as<Small>();
+  const uint64_t ccap = std::min<uint64_t>(c->last_B / 128 + 65536, 0xfffffff0ull);
+  EW_CHECK(c->rd.ensure((size_t)n * sizeof(RecDesc)));
+  EW_CHECK(c->pf.ensure((size_t)n * 8));
+  EW_CHECK(c->slow.ensure((size_t)n * 4));
+  c->pfcap = n;
+  uint32_t *pf = c->pf.as<uint32_t>();
+  hipLaunchKernelGGL(k_reset_check, dim3(1), dim3(64), 0, c->stream, ds);
+  const unsigned fgrid = (unsigned)std::max(1, c->num_cu) * c->frame_wg;
+  hipLaunchKernelGGL(k_frame, dim3(fgrid), dim3(256), 0, c->stream, c->last_buf, c->last_B, c->cpos.as<uint64_t>(),
+                     ccap, n, c->pwave.as<uint32_t>(), c->v.as<uint32_t>(), tb->slice, tb->shift, c->rd.as<RecDesc>(),
+                     pf, pf + n, c->slow.as<uint32_t>(), ds, 0);
+  const uint32_t nb = grid_for(n, 1024);
+  const size_t had = c->lbstat.cap;
+  EW_CHECK(c->lbstat.ensure((size_t)nb * 8));
+  c->epoch = (c->epoch + 1) & 0xffffffu;
+  if (c->lbstat.cap != had || c->epoch == 0) {
+    EW_CHECK(hipMemsetAsync(c->lbstat.p, 0, c->lbstat.cap, c->stream));
+    if (c->epoch == 0) c->epoch = 1;
+  }
+  EW_CHECK(c->opf.ensure((size_t)nb * 4));
+  EW_CHECK(c->mlist.ensure((size_t)n * 4));
+  EW_CHECK(c->ents.ensure((size_t)n * sizeof(ewal_entry)));
+  EW_CHECK(c->ulist.ensure((size_t)n * sizeof(uint2)));
+  SegArgs useg{};
+  useg.ulist = c->ulist.as<uint2>();
+  hipLaunchKernelGGL(k_check<false>, dim3(nb), dim3(1024), 0, c->stream, tb->shift, c->rd.as<RecDesc>(), (uint32_t)n,
+                     (const uint32_t *)pf, (const uint32_t *)(pf + n), c->last_ri, c->lbstat.as<unsigned long long>(),
+                     c->epoch, c->opf.as<uint32_t>(), c->ents.as<ewal_entry>(), c->mlist.as<uint32_t>(), ds, useg,
+                     (const uint32_t *)nullptr);
+  EW_CHECK(hipGetLastError());
+  EW_CHECK(hipStreamSynchronize(c->stream));
+  c->rd_valid = true;
+  return 0;
+}
+
 extern "C" {
 
 int ewal_device_count(void) {
@@ -1050,6 +1282,7 @@ int ewal_ctx_create(int device, ewal_ctx **out) {
   c->own_stream = true;
   if (const char *e = std::getenv("EWAL_STREAM_ABLATE")) c->ablate = std::atoi(e);
   if (const char *e = std::getenv("EWAL_FRAME_WG")) c->frame_wg = std::max(1, std::min(16, std::atoi(e)));
+  if (const char *e = std::getenv("EWAL_FUSED")) c->fused = std::atoi(e) != 0;
   EW_CHECK(hipEventCreate(&c->ev0));
   EW_CHECK(hipEventCreate(&c->ev1));
   EW_CHECK(hipEventCreate(&c->evs0));
@@ -1197,6 +1430,11 @@ int64_t ewal_copy_unrec_bytes(ewal_ctx *c, uint8_t *out, int64_t cap) {
 int64_t ewal_copy_records(ewal_ctx *c, ewal_record *out, int64_t cap) {
   if (!c || (!out && cap)) return EWAL_E_INVAL;
   int64_t n = std::min<int64_t>(cap, (int64_t)c->last_n);
+  if (n > 0 && !c->rd_valid) {   // the fused pass kept no descriptors: decode them now
+    EW_CHECK(hipSetDevice(c->device));
+    int rc = materialise_records(c);
+    if (rc) return rc;
+  }
   if (n > 0) {
     EW_CHECK(c->recs.ensure((size_t)n * sizeof(ewal_record)));
     hipLaunchKernelGGL(k_records_out, dim3(grid_for(n, 256)), dim3(256), 0, c->stream, c->rd.as<RecDesc>(),

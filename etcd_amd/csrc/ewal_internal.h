@@ -98,6 +98,18 @@ struct SnapDesc {
   int32_t st, pad;
 };
 
+// The fused frame + check pass's reductions (k_fc).  Zero means none, so
+// k_stream's zeroing of Small initialises them.
+struct FcAgg {
+  unsigned long long fail_inv;    // ~((frame << 8) | status) of the first failing frame (max)
+  unsigned long long meta_inv;    // ~frame of the first non-empty metadata frame (max)
+  uint32_t last_entry1;           // 1 + the last entry frame (max)
+  uint32_t last_state1;           // 1 + the last state frame (max)
+  uint32_t rare;                  // a frame k_fc leaves to the general path (bit 0: declined
+                                  // encoding, 1: index rewind, 2: ents capacity)
+  uint32_t last_chained;          // the running CRC after the last frame
+};
+
 // Per-call device scratch (zeroed / initialised each call).
 struct Small {
   uint32_t ticket;
@@ -122,6 +134,7 @@ struct Small {
   uint32_t spec_n;                // k_spec_gate: frames when k_frame's speculation holds, else 0
   uint32_t nunrec;                // k_check: entry ops carrying XXX_unrecognized (listed in ulist)
   uint32_t pad2;
+  FcAgg fc;
 };
 
 // A returned Entry (ent = its index in ents) or the HardState (ent = -1)

@@ -1,0 +1,742 @@
+// fused_kernels.hip -- the regular-path frame pass fused with the chained CRC
+// check.  ONE kernel (k_fc) decodes every frame, checks its CRC against its
+// predecessor's stored CRC, applies ReadAll's per-frame rules and places the
+// entry ops in ents, so the per-frame descriptors (RecDesc: 96 B written by
+// k_frame and read back by k_check, plus the 8 B of prefixes) never touch
+// HBM, and two launches (k_spec_gate, k_decode_slow) disappear.
+//
+// Reference: (*WAL).ReadAll wal/wal.go:164-216, decoder.decode
+// wal/decoder.go:28-47, walpb.Record.Unmarshal wal/walpb/record.pb.go:43-136,
+// raftpb.Entry / HardState.Unmarshal raft/raftpb/raft.pb.go:170-277, 618-704.
+//
+// k_fc decides the regular case: the candidates form one chain from byte 0,
+// every frame is in the canonical encoding etcd's encoder writes, and entry
+// indexes never rewind.  Anything else sets Small.irregular / Small.fc.rare
+// and the host runs the general path (k_frame, k_decode_slow, k_check, the
+// op-list passes) over the same stream pass -- nothing is guessed.
+//
+// Frames are processed in tiles of FC_THREADS consecutive frames, one frame
+// per thread, by a persistent grid of FC_WGS workgroups per CU: tile t =
+// blockIdx.x + i * gridDim.x.  Within a tile the predecessor's stored CRC and
+// the successor's prefix come from the neighbouring lane (wave shuffles, LDS
+// across waves); the tile's first frame re-reads its predecessor's head, its
+// last frame computes its own data-end prefix.  Entry ops are numbered by a
+// decoupled look-back over the tiles' op counts (relaxed atomics on one word
+// per tile, like k_check's); the index-gap rule for a tile's FIRST op, whose
+// predecessor op lives in an earlier tile, is applied by k_fc_seam once every
+// op is in ents (ents[j - 1].Index is op j's predecessor).
+#include "ewal_device.h"
+#include "ewal_internal.h"
+
+#define FC_THREADS 256
+#define FC_WAVES (FC_THREADS / 64)
+#define FC_WGS 3          // resident workgroups per CU (LDS ~49 KiB each)
+
+// Per tile, for k_fc_seam: its op count and base, the frame of its first op,
+// and whether that op's predecessor lies before the tile (the seam to check).
+struct TileRec {
+  uint32_t count, base;
+  uint32_t first_frame, last_frame;   // of its first / last op
+  uint32_t seam;       // 1: the first op's predecessor op (if any) lies before the tile
+  uint32_t lastcrc;    // the stored CRC of the tile's last frame (the next tile's first seed)
+  uint32_t pfo0;       // P at the tile's first frame start (the previous tile's last P(data end))
+  // the CRC checks k_fc leaves to k_fc_seam: [0] the tile's first frame
+  // (seed: the frame before the tile), [1] its last frame (P(data end): the
+  // next tile's first frame start); same frame when the tile has one frame
+  uint32_t dfirst, dlast;
+  uint32_t crc[2], pfd[2], seed1, pe0;
+  int32_t type[2];
+  uint64_t dlen[2];
+};
+
+// decoder.decode's check + ReadAll's crc-record rule for one frame (k_check's
+// per-frame verdict): *chained = the running CRC after it.
+__device__ __forceinline__ int fc_check_one(const uint32_t *g_shift, int32_t type, uint32_t crc, uint32_t seed,
+                                            uint32_t pfd, uint32_t pe, uint64_t dlen, uint32_t *chained) {
+  if (type == 4) {
+    *chained = crc;
+    return (seed != 0 && crc != seed) ? EWAL_ERR_WAL_CRC : 0;
+  }
+  uint32_t computed = seed;
+  if (dlen) computed = gshift_n(g_shift, dlen, seed ^ 0xffffffffu ^ pfd) ^ pe ^ 0xffffffffu;
+  *chained = computed;
+  if (computed != crc) return EWAL_ERR_RECORD_CRC;
+  return (type != 1 && type != 2 && type != 3) ? EWAL_ERR_UNEXPECTED_TYPE : 0;
+}
+
+// k_fc ran over every frame (its tile records, ents and mlist are filled):
+// what the kernels after it need before they read them.
+__device__ __forceinline__ bool fc_ran(const Small *ds, uint64_t ccap, uint64_t ecap) {
+  const uint64_t K = ds->total;
+  return K && K <= ccap && K <= ecap && K < 0xffffff00ull && !ds->novf && !ds->errflag;
+}
+// ... and decided the regular case (the results are the reference's).
+__device__ __forceinline__ bool fc_valid(const Small *ds, uint64_t ccap, uint64_t ecap) {
+  return fc_ran(ds, ccap, ecap) && ds->pos0 == 0 && !ds->irregular && !ds->fc.rare;
+}
+
+// S_{2^m} as nibble tables: N[m][k][d] = S_{2^m}(d << 4k), 8 x 16 entries per
+// operator (512 B; m = 0..16 in 8.5 KiB of LDS instead of 68 KiB of byte
+// tables), 8 lookups per application.
+#define FC_NIB_LEVELS 17
+__device__ __forceinline__ uint32_t nib_src(const uint32_t *g_shift, int i) {
+  const int m = i >> 7, k = (i >> 4) & 7, d = i & 15;
+  return g_shift[m * 1024 + (k >> 1) * 256 + (d << (4 * (k & 1)))];
+}
+__device__ __forceinline__ uint32_t nib_apply(const uint32_t *t, uint32_t x) {
+  uint32_t r = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) r ^= t[k * 16 + ((x >> (4 * k)) & 15)];
+  return r;
+}
+
+struct FcArgs {
+  const uint8_t *buf;
+  uint64_t B;
+  const uint64_t *cpos;
+  uint64_t ccap;        // capacity of the candidate list
+  uint64_t ecap;        // capacity of ents / mlist
+  const uint32_t *pwave, *v, *g_slice, *g_shift;
+  uint64_t ri;          // w.ri (single WAL)
+  unsigned long long *status;   // per tile look-back word (lookback_count)
+  TileRec *trec;
+  uint32_t epoch;
+  ewal_entry *ents;
+  uint32_t *mlist;
+  Small *ds;
+};
+
+// walpb.Record's stored Crc from a canonical frame head at p (08 type 10
+// crc): the tile's first frame takes its seed from it.  *ok clears when the
+// head is not canonical (that frame's own tile reports it rare anyway).
+__device__ __forceinline__ uint32_t fc_head_crc(const uint8_t *__restrict__ buf, uint64_t B, uint64_t p, bool *ok) {
+  uint8_t h[24];
+#pragma unroll
+  for (int i = 0; i < 24; ++i) h[i] = (p + 8 + i < B) ? buf[p + 8 + i] : 0;
+  int o = 0;
+  bool good = h[o++] == 0x08;
+  while (o < 12 && (h[o] & 0x80)) ++o;   // type varint
+  ++o;
+  good = good && o < 12 && h[o++] == 0x10;
+  uint64_t c = 0;
+  for (uint32_t sh = 0; o < 24; sh += 7) {
+    const uint8_t b = h[o++];
+    if (sh < 32) c |= (uint64_t)(b & 0x7f) << sh;
+    if (b < 0x80) break;
+  }
+  *ok = good;
+  return (uint32_t)c;
+}
+
+// Every field a later pass needs of one canonical frame, re-read from global
+// memory (the passes after k_fc touch a handful of frames): Record type /
+// crc / Data, Entry / HardState fields.  The first 96 bytes come in with six
+// vector loads into this thread's LDS slot w (96 B), the walkers read the
+// rest (if any) from global memory.
+__device__ RecDesc fc_frame_fields(const uint8_t *__restrict__ buf, uint64_t B, uint64_t p, uint4 *w) {
+  RecDesc d;
+  d.off = p;
+  d.type = 0; d.crc = 0; d.chained = 0; d.st = 0; d.sub_st = 0;
+  d.doff = p + 8; d.dlen = 0; d.dnil = 1;
+  d.f0 = d.f1 = d.f2 = 0; d.edoff = 0; d.edlen = 0; d.enil = 1; d.etype = 0; d.pad0 = 0; d.pad1 = 0;
+  const int64_t L = (int64_t)ld_le64_b(buf, B, p);
+  if (p + 8 > B || L < 0 || (uint64_t)L > B - p - 8) {   // not a frame (only a void pass asks)
+    d.st = EWAL_ERR_UNEXPECTED_EOF;
+    return d;
+  }
+  const uint64_t p16 = p & ~15ull;
+#pragma unroll
+  for (int k = 0; k < 6; ++k) {
+    const uint64_t o = p16 + 16 * k;
+    uint4 x;
+    if (o + 16 <= B) {
+      x = *(const uint4 *)(buf + o);
+    } else {
+      uint32_t y[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) y[j] = load_word_guarded(buf, B, o + 4 * j);
+      x = make_uint4(y[0], y[1], y[2], y[3]);
+    }
+    w[k] = x;
+  }
+  const WinReader R0{(const uint8_t *)w + (p - p16), (int64_t)(96 - (p - p16)), buf + p};
+  const WinReader rb = R0 + 8;
+  PbField a1, a2, a3, a4, a5;
+  pbf_init(a1); pbf_init(a2); pbf_init(a3); pbf_init(a4); pbf_init(a5);
+  int unrec = 0;
+  d.st = pb_walk<PB_VAR64, PB_VAR32, PB_BYTES, PB_NONE, PB_NONE>(rb, L, a1, a2, a3, a4, a5, unrec, nullptr, nullptr, 0);
+  d.type = (int64_t)a1.v;
+  d.crc = (uint32_t)a2.v;
+  if (a3.blen > 0) { d.doff = p + 8 + (uint64_t)a3.boff; d.dlen = (uint64_t)a3.blen; d.dnil = 0; }
+  if (d.st == 0 && d.dlen && (d.type == 2 || d.type == 3)) {
+    const WinReader dp = R0 + (int64_t)(d.doff - p);
+    PbField e1, e2, e3, e4, e5;
+    pbf_init(e1); pbf_init(e2); pbf_init(e3); pbf_init(e4); pbf_init(e5);
+    int ur = 0;
+    if (d.type == 2) {
+      d.sub_st = pb_walk<PB_VAR32, PB_VAR64, PB_VAR64, PB_BYTES, PB_NONE>(dp, (int64_t)d.dlen, e1, e2, e3, e4, e5, ur,
+                                                                          nullptr, nullptr, 0);
+      d.etype = (int32_t)(uint32_t)e1.v;
+      d.f0 = e2.v;
+      d.f1 = e3.v;
+      if (e4.blen > 0) { d.edoff = d.doff + (uint64_t)e4.boff; d.edlen = (uint64_t)e4.blen; d.enil = 0; }
+    } else {
+      d.sub_st = pb_walk<PB_VAR64, PB_VAR64, PB_VAR64, PB_NONE, PB_NONE>(dp, (int64_t)d.dlen, e1, e2, e3, e4, e5, ur,
+                                                                         nullptr, nullptr, 0);
+      d.f0 = e1.v; d.f1 = e2.v; d.f2 = e3.v;
+    }
+  }
+  return d;
+}
+
+template <bool SEG>
+__global__ __launch_bounds__(FC_THREADS, FC_WGS) void k_fc(FcArgs a, SegArgs sg) {
+  __shared__ uint32_t s_t4[16 * 256];          // slicing-by-16
+  __shared__ uint32_t s_svp[1024];             // S_256 (prefix Horner step)
+  __shared__ uint32_t s_nib[FC_NIB_LEVELS * 128];   // S_{2^0} .. S_{2^16}, nibble tables (the seed shift)
+  __shared__ uint32_t s_win[20 * FC_THREADS];  // frame heads, transposed (bank = thread & 31)
+  __shared__ uint32_t s_wcrc[FC_WAVES], s_wpfo[FC_WAVES], s_wo[FC_WAVES];
+  __shared__ uint64_t s_wlast[FC_WAVES];       // per wave: its last op's index ...
+  __shared__ uint32_t s_wlastf[FC_WAVES];      // ... and frame (EW_NIL: no op)
+  __shared__ uint32_t s_wfirstf[FC_WAVES];     // per wave: its first op's frame (EW_NIL: no op)
+  __shared__ uint32_t s_base, s_seam, s_ff, s_shr[2];
+  __shared__ uint32_t s_red[4];                // last entry + 1, last state + 1, ~first meta, last op + 1
+  __shared__ unsigned long long s_fail;        // min (frame << 8 | status)
+  Small *ds = a.ds;
+  const uint64_t K = ds->total;
+  if (K == 0 || K > a.ccap || ds->novf || K >= 0xffffff00ull) return;   // the host takes the general path
+  if (K > a.ecap) {                           // no room for every op: the host grows ents, once
+    if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(&ds->fc.rare, 4u);
+    return;
+  }
+  stage_lds<FC_THREADS>(s_t4, 16 * 256, [&](int i) { return a.g_slice[i]; });
+  stage_lds<FC_THREADS>(s_svp, 1024, [&](int i) { return a.g_shift[EW_VLOG * 1024 + i]; });
+  stage_lds<FC_THREADS>(s_nib, FC_NIB_LEVELS * 128, [&](int i) { return nib_src(a.g_shift, i); });
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const uint32_t K32 = (uint32_t)K;
+  const uint32_t ntiles = (K32 + FC_THREADS - 1) / FC_THREADS;
+  uint32_t rare = 0, irr = 0;
+  // this thread's candidate offsets, one tile ahead (their latency hides
+  // behind the previous tile's barriers and look-back)
+  auto cand = [&](uint32_t tt, uint64_t &pp, uint64_t &pq) {
+    const uint32_t rr = min(tt * FC_THREADS + (uint32_t)tid, K32 - 1);
+    pp = a.cpos[rr];
+    pq = rr + 1 < K32 ? a.cpos[rr + 1] : ~0ull;
+  };
+  uint64_t p_nx = 0, pn_nx = 0;
+  if (blockIdx.x < ntiles) cand(blockIdx.x, p_nx, pn_nx);
+  for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    const uint32_t r0 = t * FC_THREADS;
+    const uint32_t rt = r0 + (uint32_t)tid;
+    const bool live = rt < K32;
+    const uint32_t r = live ? rt : K32 - 1;    // the whole tile reaches every barrier; writes masked
+    __syncthreads();                           // the previous tile's LDS reads are done
+    if (tid == 0) {
+      s_red[0] = 0; s_red[1] = 0; s_red[2] = 0; s_red[3] = 0;
+      s_fail = ~0ull;
+      if (SEG) {
+        s_shr[0] = shard_of(sg.fs, sg.ns, r0);
+        s_shr[1] = shard_in(sg.fs, s_shr[0], sg.ns, min(r0 + FC_THREADS, K32) - 1);
+      }
+      if (t == 0) ds->pos0 = a.cpos[0];
+    }
+    const uint64_t p = p_nx, pn = pn_nx;
+    if (t + gridDim.x < ntiles) cand(t + gridDim.x, p_nx, pn_nx);
+    RecDesc d;
+    int64_t L = 0;
+    uint32_t Pfo = 0, Pfd = 0;
+    const bool ok = decode_canon<FC_THREADS>(a.buf, a.B, p, a.pwave, a.v, s_t4, s_svp, s_win + tid, d, L, Pfo, Pfd);
+    const uint64_t s = p + 8 + (uint64_t)L;
+    if (live && !ok) rare |= 1u;
+    if (!ok) {   // not decoded (the pass is void): no field of it may address memory
+      d.type = 0;
+      d.dlen = 0;
+      d.doff = p + 8;
+    }
+    if (live && r + 1 < K32 && pn != s) irr = 1;
+    if (live && r + 1 == K32) {   // the chain's terminal
+      ds->q = s;
+      ds->qlen = (s <= a.B && a.B - s >= 8) ? (int64_t)ld_le64_b(a.buf, a.B, s) : 0;
+    }
+    // neighbours: the predecessor's stored CRC, the successor's P at its frame start
+    uint32_t cprev = (uint32_t)__shfl_up((int)d.crc, 1);
+    uint32_t pnext = (uint32_t)__shfl_down((int)Pfo, 1);
+    if (lane == 63) s_wcrc[wv] = d.crc;
+    if (lane == 0) s_wpfo[wv] = Pfo;
+    __syncthreads();
+    if (lane == 0 && wv) cprev = s_wcrc[wv - 1];
+    if (lane == 63 && wv + 1 < FC_WAVES) pnext = s_wpfo[wv + 1];
+    uint32_t sh = 0, lo = 0;                   // SEG: the frame's shard and its first frame
+    uint64_t ri = a.ri;
+    if (SEG) {
+      sh = s_shr[0] == s_shr[1] ? s_shr[0] : shard_in(sg.fs, s_shr[0], s_shr[1] + 1, r);
+      lo = sg.fs[sh];
+      ri = sg.ri[sh];
+    }
+    // decoder.decode's check + ReadAll's crc-record rule (as k_check).  The
+    // tile's first frame takes its seed from the frame before the tile, its
+    // last frame P(data end) from the frame after it: k_fc_seam makes those
+    // checks with the neighbouring tiles' records (their verdict is
+    // provisionally 0 here; the frame's other reports carry larger keys, so a
+    // CRC failure still wins)
+    const bool dfirst = tid == 0 && r > lo;
+    const bool dlast = tid == FC_THREADS - 1 && r + 1 < K32;
+    const uint32_t seed = r > lo ? cprev : 0u;
+    int st = 0;
+    uint32_t chained = seed;
+    uint32_t Pe = 0;
+    if (d.type == 4) {
+      if (seed != 0 && d.crc != seed) st = EWAL_ERR_WAL_CRC;
+      chained = d.crc;
+    } else {
+      uint32_t computed = seed;
+      if (d.dlen) {
+        const uint64_t e = d.doff + d.dlen;
+        // P(data end) = the successor's P at its frame start (canonical
+        // layout), else computed here (the chain's last frame)
+        Pe = pnext;
+        if (!(e == pn && r + 1 < K32)) Pe = prefix_at(e, a.pwave, a.v, a.buf, s_t4, s_svp);
+        if (dlast) Pe = 0;   // the next tile's (k_fc_seam)
+        uint32_t x = seed ^ 0xffffffffu ^ Pfd;
+        uint64_t m = d.dlen;
+        for (int lvl = 0; m; ++lvl, m >>= 1)
+          if (m & 1) x = lvl < FC_NIB_LEVELS ? nib_apply(s_nib + lvl * 128, x) : gshift_pow2(a.g_shift, lvl, x);
+        computed = x ^ Pe ^ 0xffffffffu;
+      }
+      chained = computed;
+      if (computed != d.crc) st = EWAL_ERR_RECORD_CRC;
+      else if (d.type != 1 && d.type != 2 && d.type != 3) st = EWAL_ERR_UNEXPECTED_TYPE;
+    }
+    if (live && (tid == 0 || tid == FC_THREADS - 1 || r + 1 == K32)) {
+      TileRec *tr = a.trec + t;
+      const int32_t ty = (int32_t)(d.type < 0 || d.type > 1000 ? 1000 : d.type);
+      if (tid == 0) {
+        tr->pfo0 = Pfo;
+        tr->dfirst = dfirst;
+        tr->crc[0] = d.crc;
+        tr->pfd[0] = Pfd;
+        tr->pe0 = Pe;
+        tr->type[0] = ty;
+        tr->dlen[0] = d.dlen;
+      }
+      if (tid == FC_THREADS - 1 || r + 1 == K32) {   // the tile's last frame
+        tr->lastcrc = d.crc;
+        tr->dlast = dlast;
+        tr->crc[1] = d.crc;
+        tr->pfd[1] = Pfd;
+        tr->seed1 = seed;
+        tr->type[1] = ty;
+        tr->dlen[1] = d.dlen;
+      }
+    }
+    if (dfirst || dlast) st = 0;
+    else if (live && r + 1 == K32) ds->fc.last_chained = chained;
+    // entry ops (wal/wal.go:170-176): the op's predecessor in the wave, else
+    // in an earlier wave of the tile; the tile's first op is k_fc_seam's
+    const uint32_t rw0 = r0 + (uint32_t)(tid & ~63);
+    const bool op = live && d.type == 2 && d.f1 >= ri;
+    const unsigned long long mo = __ballot(op);
+    const unsigned long long below = mo & ((1ull << lane) - 1ull);
+    unsigned long long bsh = below;
+    if (SEG && lo > rw0) bsh = (lo - rw0 >= 64) ? 0ull : below & ~((1ull << (lo - rw0)) - 1ull);
+    const int pl = bsh ? 63 - __clzll((long long)bsh) : lane;
+    const uint64_t fprev = __shfl(d.f1, pl);
+    const int wl = mo ? 63 - __clzll((long long)mo) : 0;
+    const uint64_t wli = __shfl(d.f1, wl);
+    if (lane == 0) {
+      s_wo[wv] = (uint32_t)__popcll(mo);
+      s_wlastf[wv] = mo ? rw0 + (uint32_t)wl : EW_NIL;
+      s_wfirstf[wv] = mo ? rw0 + (uint32_t)(__ffsll((long long)mo) - 1) : EW_NIL;
+      s_wlast[wv] = wli;
+    }
+    // reductions (one LDS atomic per wave and quantity)
+    const unsigned long long mf = __ballot(live && st != 0), me = __ballot(live && d.type == 2),
+                             ms = __ballot(live && d.type == 3), mm = __ballot(live && d.type == 1 && d.dlen > 0);
+    const int ffl = mf ? __ffsll((long long)mf) - 1 : 0;
+    const uint32_t fst = (uint32_t)__shfl(st, ffl);
+    if (live && d.type == 1 && st == 0) {     // ReadAll's metadata rule runs after the pass
+      const uint32_t mi = atomicAdd(&ds->nmeta, 1u);
+      if (mi < a.ecap) a.mlist[mi] = r; else rare |= 4u;
+    }
+    const bool wg1 = !SEG || s_shr[0] == s_shr[1];
+    if (lane == 0 && wg1) {
+      if (mf) atomicMin(&s_fail, ((unsigned long long)(rw0 + (uint32_t)ffl) << 8) | fst);
+      if (me) atomicMax(&s_red[0], rw0 + (uint32_t)(63 - __clzll((long long)me)) + 1u);
+      if (ms) atomicMax(&s_red[1], rw0 + (uint32_t)(63 - __clzll((long long)ms)) + 1u);
+      if (mm) atomicMax(&s_red[2], ~(rw0 + (uint32_t)(__ffsll((long long)mm) - 1)));
+      if (mo) atomicMax(&s_red[3], rw0 + (uint32_t)wl + 1u);
+    }
+    if (SEG && !wg1 && live) {   // a shard boundary inside the tile (rare): lane by lane
+      ShardAgg *A = sg.sagg + sh;
+      if (st != 0) atomicMin(&A->first_fail, ((unsigned long long)r << 8) | (uint32_t)st);
+      if (d.type == 2) atomicMax(&A->last_entry, (long long)r);
+      if (d.type == 3) atomicMax(&A->last_state, (long long)r);
+      if (d.type == 1 && d.dlen > 0) atomicMin(&A->first_meta, (unsigned long long)r);
+      if (op) atomicMax(&A->lastop, r + 1u);
+    }
+    __syncthreads();
+    if (wv == 0) {   // the tile's op base (decoupled look-back over op counts)
+      uint32_t cnt = 0, ff = EW_NIL, lf = EW_NIL;
+#pragma unroll
+      for (int w = 0; w < FC_WAVES; ++w) {
+        cnt += s_wo[w];
+        if (ff == EW_NIL) ff = s_wfirstf[w];
+        if (s_wlastf[w] != EW_NIL) lf = s_wlastf[w];
+      }
+      const uint32_t base = lookback_count(a.status, t, cnt, a.epoch, &ds->errflag);
+      if (lane == 0) {
+        // the tile's first op has its predecessor op (if any) before the tile:
+        // k_fc_seam applies the gap rule to it once ents holds every op
+        uint32_t seam = 0;
+        if (cnt) {
+          if (SEG) seam = sg.fs[shard_of(sg.fs, sg.ns, ff)] < r0;
+          else seam = base > 0;
+        }
+        s_base = base;
+        s_seam = seam;
+        s_ff = ff;
+        TileRec *tr = a.trec + t;
+        tr->count = cnt;
+        tr->base = base;
+        tr->first_frame = ff;
+        tr->last_frame = lf;
+        tr->seam = seam;
+        if (t == ntiles - 1) ds->nsel3 = base + cnt;
+        if (!SEG) {
+          if (s_fail != ~0ull) atomicMax(&ds->fc.fail_inv, ~s_fail);
+          if (s_red[0]) atomicMax(&ds->fc.last_entry1, s_red[0]);
+          if (s_red[1]) atomicMax(&ds->fc.last_state1, s_red[1]);
+          if (s_red[2]) atomicMax(&ds->fc.meta_inv, ~(unsigned long long)(uint32_t)~s_red[2]);
+          if (s_red[3]) atomicMax(&ds->lastop, s_red[3]);
+        } else if (s_shr[0] == s_shr[1]) {
+          ShardAgg *A = sg.sagg + s_shr[0];
+          if (s_fail != ~0ull) atomicMin(&A->first_fail, s_fail);
+          if (s_red[0]) atomicMax(&A->last_entry, (long long)(s_red[0] - 1));
+          if (s_red[1]) atomicMax(&A->last_state, (long long)(s_red[1] - 1));
+          if (s_red[2]) atomicMin(&A->first_meta, (unsigned long long)(uint32_t)~s_red[2]);
+          if (s_red[3]) atomicMax(&A->lastop, s_red[3]);
+        }
+      }
+    }
+    __syncthreads();
+    if (op) {
+      uint32_t j = s_base + (uint32_t)__popcll(below);
+#pragma unroll
+      for (int w = 0; w < FC_WAVES; ++w) j += (w < wv) ? s_wo[w] : 0u;
+      uint64_t kp = fprev;
+      uint32_t pf = bsh ? 0u : EW_NIL;         // the predecessor op: in the wave, or an earlier wave
+      for (int w = wv - 1; w >= 0 && pf == EW_NIL; --w)
+        if (s_wlastf[w] != EW_NIL) { pf = s_wlastf[w]; kp = s_wlast[w]; }
+      const bool has = pf != EW_NIL && (bsh || pf >= lo);   // SEG: in this shard
+      const uint64_t k = d.f1 - ri;
+      // no predecessor in the tile: this is the tile's first op (or a shard's
+      // first op inside it); decided here unless k_fc_seam owns it
+      const bool seam_op = !has && s_seam && r == s_ff;
+      if (!seam_op) {
+        bool gap;
+        if (has) {
+          const uint64_t kq = kp - ri;
+          if (k <= kq) rare |= 2u;             // an index rewind: the general path's survivor pass
+          gap = k > kq && k - kq > 1;
+        } else {
+          gap = k > 0;
+          if (SEG) sg.sagg[sh].ent_first = j;  // the shard's first op
+        }
+        if (gap) {
+          const int gs = st ? st : EWAL_PANIC_INDEX_GAP;
+          if (SEG) atomicMin(&sg.sagg[sh].first_fail, ((unsigned long long)r << 8) | (uint32_t)gs);
+          else atomicMax(&ds->fc.fail_inv, ~(((unsigned long long)r << 8) | (uint32_t)gs));
+        }
+      }
+      ewal_entry e;
+      e.term = d.f0;
+      e.index = d.f1;
+      e.data_off = SEG ? d.edoff - sg.soff[sh] : d.edoff;
+      e.data_len = d.edlen;
+      e.type = d.etype;
+      e.data_nil = d.enil;
+      a.ents[j] = e;
+    }
+  }
+  // flags of every lane, then one atomic per wave
+  uint32_t rr = rare;
+  for (int o = 32; o; o >>= 1) rr |= (uint32_t)__shfl_xor((int)rr, o);
+  if (lane == 0 && rr) atomicOr(&ds->fc.rare, rr);
+  if (__ballot(irr) && lane == 0) atomicOr(&ds->irregular, 1u);
+}
+
+// The index-gap rule (wal/wal.go:173) for each tile's first op whose
+// predecessor op lies in an earlier tile: ents[j - 1] is op j's predecessor
+// (ops are numbered in frame order) -- in the same shard when an op of the
+// shard precedes the tile.  One thread per tile.
+template <bool SEG>
+__global__ void k_fc_seam(const uint8_t *__restrict__ buf, uint64_t B, const uint64_t *__restrict__ cpos,
+                          const uint32_t *__restrict__ g_shift, const TileRec *__restrict__ trec,
+                          const ewal_entry *__restrict__ ents, uint64_t ri_one, uint64_t ccap, uint64_t ecap, Small *ds,
+                          SegArgs sg) {
+  if (!fc_ran(ds, ccap, ecap)) return;
+  const uint64_t K = ds->total;
+  const uint32_t ntiles = (uint32_t)((K + FC_THREADS - 1) / FC_THREADS);
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= ntiles) return;
+  const TileRec tr = trec[t];
+  const uint32_t r0 = t * FC_THREADS;
+  const uint32_t rl = min(r0 + FC_THREADS, (uint32_t)K) - 1;   // the tile's last frame
+  for (int w = 0; w < 2; ++w) {   // the edge frames' CRC checks k_fc left
+    const bool first = w == 0;
+    if (first ? !tr.dfirst : (!tr.dlast || (tr.dfirst && rl == r0))) continue;
+    const uint32_t r = first ? r0 : rl;
+    const uint32_t seed = first ? trec[t - 1].lastcrc : tr.seed1;
+    const bool next = !first || (tr.dlast && rl == r0);   // P(data end) from the next tile
+    const uint32_t pe = next ? trec[t + 1].pfo0 : tr.pe0;
+    uint32_t chained;
+    const int st = fc_check_one(g_shift, tr.type[w], tr.crc[w], seed, tr.pfd[w], pe, tr.dlen[w], &chained);
+    if (st) {
+      if (SEG) atomicMin(&sg.sagg[shard_of(sg.fs, sg.ns, r)].first_fail, ((unsigned long long)r << 8) | (uint32_t)st);
+      else atomicMax(&ds->fc.fail_inv, ~(((unsigned long long)r << 8) | (uint32_t)st));
+    }
+    if (!SEG && r + 1 == K) ds->fc.last_chained = chained;
+  }
+  if (!tr.seam) return;
+  const uint32_t j = tr.base, f = tr.first_frame;
+  if (j >= ecap || f >= K) return;
+  uint64_t ri = ri_one;
+  uint32_t sh = 0;
+  bool has = j > 0;
+  if (SEG) {
+    sh = shard_of(sg.fs, sg.ns, f);
+    ri = sg.ri[sh];
+    const uint32_t lo = sg.fs[sh];
+    has = false;
+    for (int64_t u = (int64_t)t - 1; u >= 0 && (uint64_t)(u + 1) * FC_THREADS > lo; --u) {
+      const TileRec q = trec[u];
+      if (!q.count) continue;
+      has = q.last_frame >= lo;   // the nearest earlier tile with ops holds op j - 1
+      break;
+    }
+  }
+  const uint64_t k = ents[j].index - ri;
+  bool gap;
+  if (has) {
+    const uint64_t kq = ents[j - 1].index - ri;
+    if (k <= kq) atomicOr(&ds->fc.rare, 2u);
+    gap = k > kq && k - kq > 1;
+  } else {
+    gap = k > 0;
+    if (SEG) sg.sagg[sh].ent_first = j;
+  }
+  if (gap) {
+    if (SEG) atomicMin(&sg.sagg[sh].first_fail, ((unsigned long long)f << 8) | EWAL_PANIC_INDEX_GAP);
+    else atomicMax(&ds->fc.fail_inv, ~(((unsigned long long)f << 8) | EWAL_PANIC_INDEX_GAP));
+  }
+}
+
+// After k_fc (one workgroup): does the regular case hold?  Then ReadAll's
+// metadata rule (wal/wal.go:178-183) over the listed metadata frames and the
+// ResultDev gather k_result makes on the general path (the few frames it
+// needs re-read in parallel); spec_n = frames, or 0 (the host takes the
+// general path); Small -> host-mapped memory.
+__global__ __launch_bounds__(256) void k_result_fc(const uint8_t *__restrict__ buf, uint64_t B,
+                                                   const uint64_t *__restrict__ cpos, uint64_t ccap, uint64_t ecap,
+                                                   uint64_t ri, const uint32_t *__restrict__ mlist, Small *ds,
+                                                   ResultDev *o, Small *h) {
+  __shared__ uint4 s_w[256][6];
+  __shared__ RecDesc s_d[6];
+  const uint64_t K = ds->total;
+  if (!fc_valid(ds, ccap, ecap)) {
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      ds->spec_n = 0;
+      *h = *ds;
+    }
+    return;
+  }
+  const uint32_t tid = threadIdx.x;
+  const uint64_t fm = ds->fc.meta_inv ? ~ds->fc.meta_inv : ~0ull;
+  if (fm != ~0ull && ds->nmeta > 1) {
+    const RecDesc m = fc_frame_fields(buf, B, cpos[fm], s_w[tid]);
+    for (uint32_t i = tid; i < ds->nmeta; i += blockDim.x) {
+      const uint32_t r = mlist[i];
+      if (r <= fm) continue;
+      const RecDesc d = fc_frame_fields(buf, B, cpos[r], s_w[tid]);
+      bool eq = d.dlen == m.dlen;
+      for (uint64_t k = 0; eq && k < d.dlen; ++k) eq = buf[d.doff + k] == buf[m.doff + k];
+      if (!eq) atomicMax(&ds->fc.fail_inv, ~(((unsigned long long)r << 8) | EWAL_ERR_METADATA_CONFLICT));
+    }
+  }
+  __threadfence();
+  __syncthreads();
+  // the frames the result needs: first failure, last entry, last state,
+  // first metadata, last op -- one thread each
+  const unsigned long long key = ds->fc.fail_inv ? ~ds->fc.fail_inv : ~0ull;
+  const long long le = (long long)ds->fc.last_entry1 - 1, ls = (long long)ds->fc.last_state1 - 1;
+  const long long lo = (long long)ds->lastop - 1;
+  const long long want[5] = {key != ~0ull ? (long long)(key >> 8) : -1, le, ls, fm != ~0ull ? (long long)fm : -1, lo};
+  if (tid < 5 && want[tid] >= 0) s_d[tid] = fc_frame_fields(buf, B, cpos[want[tid]], s_w[tid]);
+  __syncthreads();
+  if (tid != 0) return;
+  ResultDev res;
+  memset(&res, 0, sizeof(res));
+  res.agg.first_fail = key != ~0ull ? (key >> 8) : ~0ull;
+  res.agg.last_entry = le;
+  res.agg.last_state = ls;
+  res.agg.first_meta = fm;
+  if (key != ~0ull) {
+    res.fail = s_d[0];
+    res.fail.st = (int32_t)(key & 0xff);
+  }
+  if (le >= 0) res.lastent = s_d[1];
+  if (ls >= 0) res.sd = s_d[2];
+  if (fm != ~0ull) res.md = s_d[3];
+  res.last.chained = ds->fc.last_chained;
+  res.nops = ds->nsel3;
+  res.klast = lo >= 0 ? s_d[4].f1 - ri : 0;
+  res.errflag = ds->errflag;
+  *o = res;
+  ds->spec_n = (uint32_t)K;
+  *h = *ds;
+}
+
+// ---- batched ReadAll (ewal_readall_batch_device) on the fused pass --------
+// fs[s] = first frame at or after the shard's first byte (frame r is
+// candidate r on the regular path); the per-shard reductions initialised.
+__global__ void k_shard_start_fc(const uint64_t *__restrict__ cpos, uint64_t ccap, const uint64_t *__restrict__ soff,
+                                 uint32_t ns, uint32_t *__restrict__ fs, ShardAgg *__restrict__ sagg, Small *ds) {
+  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s > ns) return;
+  const uint64_t K = ds->total;
+  const uint32_t n = (uint32_t)(K <= ccap && K < 0xffffff00ull ? K : 0);
+  if (s == ns) {
+    fs[ns] = n;
+    return;
+  }
+  const uint64_t o = soff[s];
+  uint32_t a = 0, b = n;
+  while (a < b) {
+    const uint32_t m = (a + b) >> 1;
+    if (cpos[m] < o) a = m + 1; else b = m;
+  }
+  fs[s] = a;
+  if (soff[s + 1] > o && (a >= n || cpos[a] != o)) atomicOr(&ds->segbad, 1u);
+  ShardAgg g;
+  g.first_fail = ~0ull;
+  g.last_entry = -1;
+  g.last_state = -1;
+  g.first_meta = ~0ull;
+  g.ent_first = ~0ull;
+  g.lastop = 0;
+  g.pad = 0;
+  sagg[s] = g;
+}
+
+// Per shard: ReadAll's metadata rule (wal/wal.go:178-183) over the metadata
+// frames k_fc<true> listed.
+__global__ void k_meta_batch_fc(const uint8_t *__restrict__ buf, uint64_t B, const uint64_t *__restrict__ cpos,
+                                uint64_t ccap, uint64_t ecap, const uint32_t *__restrict__ mlist, const Small *ds,
+                                SegArgs sg) {
+  __shared__ uint4 s_w[256][6];
+  if (!fc_valid(ds, ccap, ecap)) return;
+  const uint32_t nm = ds->nmeta;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nm; i += gridDim.x * blockDim.x) {
+    const uint32_t r = mlist[i];
+    const uint32_t s = shard_of(sg.fs, sg.ns, r);
+    const unsigned long long fm = sg.sagg[s].first_meta;
+    if (fm == ~0ull || r <= fm) continue;
+    const RecDesc d = fc_frame_fields(buf, B, cpos[r], s_w[threadIdx.x]);
+    const RecDesc m = fc_frame_fields(buf, B, cpos[fm], s_w[threadIdx.x]);
+    bool eq = d.dlen == m.dlen;
+    for (uint64_t k = 0; eq && k < d.dlen; ++k) eq = buf[d.doff + k] == buf[m.doff + k];
+    if (!eq) atomicMin(&sg.sagg[s].first_fail, ((unsigned long long)r << 8) | EWAL_ERR_METADATA_CONFLICT);
+  }
+}
+
+// Per shard: its ReadAll result (k_result_batch's assembly with first_fail =
+// frame << 8 | status), the frames it needs re-read from the stream -- eight
+// lanes per shard, one frame each (first failure, last entry, last frame,
+// first metadata, last state, last op), lane 0 assembles.
+__global__ __launch_bounds__(256) void k_result_batch_fc(const uint8_t *__restrict__ buf, uint64_t B,
+                                                         const uint64_t *__restrict__ cpos, uint64_t ccap,
+                                                         uint64_t ecap, const Small *ds, SegArgs sg,
+                                                         ewal_result *__restrict__ out,
+                                                         unsigned long long *__restrict__ ent_first) {
+  __shared__ uint4 s_w[256][6];
+  __shared__ RecDesc s_d[256];
+  const uint32_t s = (blockIdx.x * blockDim.x + threadIdx.x) >> 3, k = threadIdx.x & 7;
+  if (!fc_valid(ds, ccap, ecap)) return;   // (a void pass: the host discards out[])
+  const bool in = s < sg.ns;
+  ShardAgg A;
+  uint32_t f0 = 0, f1 = 0;
+  if (in) {
+    A = sg.sagg[s];
+    f0 = sg.fs[s];
+    f1 = sg.fs[s + 1];
+    long long fr = -1;
+    switch (k) {
+    case 0: fr = A.first_fail != ~0ull ? (long long)(A.first_fail >> 8) : -1; break;
+    case 1: fr = A.last_entry; break;
+    case 2: fr = f1 > f0 ? (long long)f1 - 1 : -1; break;
+    case 3: fr = A.first_meta != ~0ull ? (long long)A.first_meta : -1; break;
+    case 4: fr = A.last_state; break;
+    case 5: fr = A.lastop ? (long long)A.lastop - 1 : -1; break;
+    default: break;
+    }
+    if (fr >= 0) s_d[threadIdx.x] = fc_frame_fields(buf, B, cpos[fr], s_w[threadIdx.x]);
+  }
+  __syncthreads();
+  if (!in || k != 0) return;
+  const RecDesc *D = s_d + threadIdx.x;   // D[k]: lane k's frame
+  const uint64_t so = sg.soff[s], ri = sg.ri[s];
+  ewal_result o;
+  memset(&o, 0, sizeof(o));
+  o.fail_record = -1;
+  o.fail_offset = -1;
+  o.metadata_off = -1;
+  o.n_records = (int64_t)(f1 - f0);
+  o.n_candidates = (int64_t)(f1 - f0);
+  o.n_runs = 1;
+  unsigned long long ef = 0;
+  if (A.first_fail != ~0ull) {
+    const uint32_t fr = (uint32_t)(A.first_fail >> 8);
+    o.status = (int32_t)(A.first_fail & 0xff);
+    o.fail_record = (int64_t)(fr - f0);
+    o.fail_offset = (int64_t)(D[0].off - so);
+    o.n_records = o.fail_record;
+    if (o.status == EWAL_ERR_UNEXPECTED_TYPE) o.detail = D[0].type;
+    if (o.status == EWAL_PANIC_INDEX_GAP) o.detail = (int64_t)D[0].f1;
+  } else {
+    const uint64_t enti = A.last_entry >= 0 ? D[1].f1 : 0;
+    o.enti = enti;
+    if (enti < ri) {
+      o.status = EWAL_ERR_INDEX_NOT_FOUND;
+    } else if (f1 > f0) {
+      // the running CRC after the shard's last frame: the stored CRC of a
+      // verified frame (crcType re-seeds to it; every other frame's check
+      // passed, so computed == stored)
+      o.last_crc = D[2].crc;
+      if (A.first_meta != ~0ull) {
+        o.metadata_off = (int64_t)(D[3].doff - so);
+        o.metadata_len = (int64_t)D[3].dlen;
+      }
+      if (A.last_state >= 0) {
+        o.has_state = 1;
+        o.state_term = D[4].f0;
+        o.state_vote = D[4].f1;
+        o.state_commit = D[4].f2;
+      }
+      o.n_ents = A.lastop ? (int64_t)(D[5].f1 - ri + 1) : 0;
+      ef = o.n_ents ? A.ent_first : 0;
+    }
+  }
+  out[s] = o;
+  ent_first[s] = ef;
+}
+
+// The batch's verdict on the fused pass (one thread): the regular case for
+// every shard -> spec_n = frames, else 0; Small -> host-mapped memory.
+__global__ void k_batch_gate_fc(Small *ds, uint64_t ccap, uint64_t ecap, uint64_t B, Small *h) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  const uint64_t K = ds->total;
+  const bool ok = fc_valid(ds, ccap, ecap) && !ds->segbad && ds->q == B;
+  ds->spec_n = ok ? (uint32_t)K : 0u;
+  *h = *ds;
+}

@@ -1368,28 +1368,41 @@ __global__ void k_reset_check(Small *ds) {
   ds->gapslow = 0;
   ds->nonmono = 0;
   ds->nunrec = 0;
+  ds->irregular = 0;
+  ds->segbad = 0;
+  ds->spec_n = 0;
+  ds->fc.fail_inv = 0;
+  ds->fc.meta_inv = 0;
+  ds->fc.last_entry1 = 0;
+  ds->fc.last_state1 = 0;
+  ds->fc.rare = 0;
+  ds->fc.last_chained = 0;
 }
 
 // ---- canonical fast path ---------------------------------------------------
 // The frame head (80 bytes from the 16-B boundary below the frame start) in
 // LDS, TRANSPOSED: dword k of thread t at w[k * 256] (w = s_win + t), so the
 // bank of every read is t & 31 whatever offset each lane reads.
+// (WS: the window's dword stride, the workgroup size)
+template <int WS = 256>
 __device__ __forceinline__ uint32_t win4(const uint32_t *w, int o) {
   const int k = o >> 2;
-  return __builtin_amdgcn_alignbyte(w[(k + 1) * 256], w[k * 256], (uint32_t)(o & 3));
+  return __builtin_amdgcn_alignbyte(w[(k + 1) * WS], w[k * WS], (uint32_t)(o & 3));
 }
+template <int WS = 256>
 __device__ __forceinline__ uint64_t win8(const uint32_t *w, int o) {
   const int k = o >> 2;
-  const uint32_t a = w[k * 256], b = w[(k + 1) * 256], c = w[(k + 2) * 256];
+  const uint32_t a = w[k * WS], b = w[(k + 1) * WS], c = w[(k + 2) * WS];
   const uint32_t sh = (uint32_t)(o & 3);
   return ((uint64_t)__builtin_amdgcn_alignbyte(c, b, sh) << 32) | __builtin_amdgcn_alignbyte(b, a, sh);
 }
 // tag byte + varint of at most 7 bytes at window offset o: returns the offset
 // after the field, clears ok on a different tag, a longer varint or a field
 // outside the window (the general walker then takes the frame).
+template <int WS = 256>
 __device__ __forceinline__ int pb_field_fast(const uint32_t *w, int o, uint32_t tag, uint64_t &v, bool &ok) {
   const int oc = o <= 71 ? o : 71;
-  const uint64_t x = win8(w, oc);
+  const uint64_t x = win8<WS>(w, oc);
   const uint64_t t = ~(x >> 8) & 0x0080808080808080ull;   // terminators among the 7 bytes after the tag
   const int nb = t ? (__builtin_ctzll(t) >> 3) + 1 : 8;
   uint64_t y = (x >> 8) & (nb >= 8 ? 0x00ffffffffffffffull : ((1ull << (8 * nb)) - 1));
@@ -1401,21 +1414,21 @@ __device__ __forceinline__ int pb_field_fast(const uint32_t *w, int o, uint32_t 
   return o + 1 + nb;
 }
 
-// Canonical fast decode of frame r at p (int64 length L read from the
-// window, so no earlier pass has to fetch it): canonical encodings -- Record
-// {08 type 10 crc [1a len Data]}, Entry {08 type 10 term 18 index [22 len
-// Data]}, HardState {08 term 10 vote 18 commit}, every varint at most 7
-// bytes, the last field ending exactly at the message end -- are parsed with
-// word operations; any other frame goes to the slow list (k_decode_slow: the
-// general walkers, exact gogoprotobuf semantics).  Then P at the frame start
-// and at the data start.  The frame head and prefix_at's operands are loaded
-// together, one memory round trip.  Returns L.
-__device__ __forceinline__ int64_t decode_fast(const uint8_t *__restrict__ buf, uint64_t B, uint64_t p, uint32_t r,
-                                               bool last, const uint32_t *__restrict__ pwave,
-                                               const uint32_t *__restrict__ v, const uint32_t *s_t4,
-                                               const uint32_t *s_svp, uint32_t *w, RecDesc *__restrict__ rd,
-                                               uint32_t *__restrict__ pfd, uint32_t *__restrict__ pfo,
-                                               uint32_t *__restrict__ slow, Small *ds, int dbg = 0) {
+// Canonical decode of the frame at p (int64 length L read from the window,
+// so no earlier pass has to fetch it): canonical encodings -- Record {08 type
+// 10 crc [1a len Data]}, Entry {08 type 10 term 18 index [22 len Data]},
+// HardState {08 term 10 vote 18 commit}, every varint at most 7 bytes, the
+// last field ending exactly at the message end -- are parsed with word
+// operations; returns false for any other frame (the general walkers take
+// it: exact gogoprotobuf semantics).  Then P at the frame start (Pfo) and at
+// the data start (Pfd, when type != 4 and Data is not empty).  The frame
+// head and prefix_at's operands are loaded together, one memory round trip.
+// w: this thread's LDS window column (stride WS dwords).
+template <int WS>
+__device__ __forceinline__ bool decode_canon(const uint8_t *__restrict__ buf, uint64_t B, uint64_t p,
+                                             const uint32_t *__restrict__ pwave, const uint32_t *__restrict__ v,
+                                             const uint32_t *s_t4, const uint32_t *s_svp, uint32_t *w, RecDesc &d,
+                                             int64_t &L, uint32_t &Pfo, uint32_t &Pfd) {
   const uint64_t p16 = p & ~15ull;
   uint4 hq[5];
 #pragma unroll
@@ -1431,23 +1444,22 @@ __device__ __forceinline__ int64_t decode_fast(const uint8_t *__restrict__ buf, 
     }
   }
   PrefixIn pin;
-  prefix_load((dbg & 256) ? (p & ~255ull) : (dbg & 512) ? (p & ~4095ull) + (p & 255) : p, pwave, v, buf, pin);
+  prefix_load(p, pwave, v, buf, pin);
 #pragma unroll
   for (int k = 0; k < 5; ++k) {
-    w[(4 * k) * 256] = hq[k].x; w[(4 * k + 1) * 256] = hq[k].y;
-    w[(4 * k + 2) * 256] = hq[k].z; w[(4 * k + 3) * 256] = hq[k].w;
+    w[(4 * k) * WS] = hq[k].x; w[(4 * k + 1) * WS] = hq[k].y;
+    w[(4 * k + 2) * WS] = hq[k].z; w[(4 * k + 3) * WS] = hq[k].w;
   }
   const int base = (int)(p - p16);
-  const int64_t L = (int64_t)win8(w, base);
+  L = (int64_t)win8<WS>(w, base);
   const int64_t end = 8 + L;          // message end, relative to p
   bool ok = L >= 0 && L < (1ll << 40);
   uint64_t ty = 0, cr = 0, dl = 0;
-  int o = pb_field_fast(w, base + 8, 0x08, ty, ok);
-  o = pb_field_fast(w, o, 0x10, cr, ok);
+  int o = pb_field_fast<WS>(w, base + 8, 0x08, ty, ok);
+  o = pb_field_fast<WS>(w, o, 0x10, cr, ok);
   const bool hasd = ok && (int64_t)(o - base) < end;
-  if (hasd) o = pb_field_fast(w, o, 0x1a, dl, ok);
+  if (hasd) o = pb_field_fast<WS>(w, o, 0x1a, dl, ok);
   ok = ok && (hasd ? (end - (int64_t)(o - base) == (int64_t)dl) : ((int64_t)(o - base) == end));
-  RecDesc d;
   d.off = p;
   d.type = (int64_t)ty;
   d.crc = (uint32_t)cr;
@@ -1459,13 +1471,13 @@ __device__ __forceinline__ int64_t decode_fast(const uint8_t *__restrict__ buf, 
   if (ok && !d.dnil && (d.type == 2 || d.type == 3)) {
     const int64_t eend = (int64_t)(ho - base) + (int64_t)dl;
     uint64_t f0 = 0, f1 = 0, f2 = 0;
-    int e = pb_field_fast(w, ho, 0x08, f0, ok);
-    e = pb_field_fast(w, e, 0x10, f1, ok);
-    e = pb_field_fast(w, e, 0x18, f2, ok);
+    int e = pb_field_fast<WS>(w, ho, 0x08, f0, ok);
+    e = pb_field_fast<WS>(w, e, 0x10, f1, ok);
+    e = pb_field_fast<WS>(w, e, 0x18, f2, ok);
     if (d.type == 2) {                // Entry: Type, Term, Index [, Data]
       const bool hase = ok && (int64_t)(e - base) < eend;
       uint64_t el = 0;
-      if (hase) e = pb_field_fast(w, e, 0x22, el, ok);
+      if (hase) e = pb_field_fast<WS>(w, e, 0x22, el, ok);
       ok = ok && (hase ? (eend - (int64_t)(e - base) == (int64_t)el) : ((int64_t)(e - base) == eend));
       d.etype = (int32_t)(uint32_t)f0;
       d.f0 = f1;
@@ -1476,21 +1488,39 @@ __device__ __forceinline__ int64_t decode_fast(const uint8_t *__restrict__ buf, 
       d.f0 = f0; d.f1 = f1; d.f2 = f2;
     }
   }
-  if (!ok) {
-    slow[atomicAdd(&ds->nslow, 1u)] = r;
-    return L;
-  }
-  const uint32_t Pfo = prefix_finish16(pin, s_t4, s_svp);
-  if (dbg & 1024) { if (Pfo == 0x12345678u) rd[r] = d; return L; }
-  pfo[r] = Pfo;
+  if (!ok) return false;
+  Pfo = prefix_finish16(pin, s_t4, s_svp);
   if (d.type != 4 && d.dlen > 0) {    // P(data start): the header bytes after P(frame start)
     uint32_t c = Pfo;
     const int nh = ho - base;
     int j = 0;
-    for (; j + 4 <= nh; j += 4) c = step4_flat(s_t4, c ^ win4(w, base + j));
-    uint32_t t = win4(w, base + j);
+    for (; j + 4 <= nh; j += 4) c = step4_flat(s_t4, c ^ win4<WS>(w, base + j));
+    uint32_t t = win4<WS>(w, base + j);
     for (; j < nh; ++j, t >>= 8) c = s_t4[(c ^ t) & 0xff] ^ (c >> 8);
-    pfd[r] = c;
+    Pfd = c;
+  }
+  return true;
+}
+
+// decode_canon for frame r of the general path: the descriptor and prefixes
+// to HBM (rd, pfo, pfd; P(data end) in d.chained for the chain's last frame),
+// or the frame to the slow list.  Returns L.
+__device__ __forceinline__ int64_t decode_fast(const uint8_t *__restrict__ buf, uint64_t B, uint64_t p, uint32_t r,
+                                               bool last, const uint32_t *__restrict__ pwave,
+                                               const uint32_t *__restrict__ v, const uint32_t *s_t4,
+                                               const uint32_t *s_svp, uint32_t *w, RecDesc *__restrict__ rd,
+                                               uint32_t *__restrict__ pfd, uint32_t *__restrict__ pfo,
+                                               uint32_t *__restrict__ slow, Small *ds) {
+  RecDesc d;
+  int64_t L = 0;
+  uint32_t Pfo = 0, Pfd = 0;
+  if (!decode_canon<256>(buf, B, p, pwave, v, s_t4, s_svp, w, d, L, Pfo, Pfd)) {
+    slow[atomicAdd(&ds->nslow, 1u)] = r;
+    return L;
+  }
+  pfo[r] = Pfo;
+  if (d.type != 4 && d.dlen > 0) {
+    pfd[r] = Pfd;
     if (last) d.chained = prefix_at(d.doff + d.dlen, pwave, v, buf, s_t4, s_svp);   // P(data end)
   }
   rd[r] = d;
@@ -1557,7 +1587,7 @@ __global__ __launch_bounds__(256) void k_frame(const uint8_t *__restrict__ buf, 
     const uint64_t rn = r + stride;
     const uint64_t p2 = rn < K ? pos[rn] : 0, pn2 = rn + 1 < K ? pos[rn + 1] : 0;
     const int64_t L = decode_fast(buf, B, p, (uint32_t)r, r + 1 == K, pwave, v, s_t4, s_svp, s_win + threadIdx.x, rd,
-                                  pfd, pfo, slow, ds, dbg);
+                                  pfd, pfo, slow, ds);
     const uint64_t s = p + 8 + (uint64_t)L;
     if (r + 1 < K) {
       irr |= pn != s;
