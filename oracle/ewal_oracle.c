@@ -694,3 +694,35 @@ int64_t or_message_marshal(uint64_t type, uint64_t to, uint64_t from, uint64_t t
   return i;
 }
 
+
+/* ---- checker helpers (test infrastructure, not restatements) ----------- */
+/* A digest of ReadAll's ents for large parity cases: CRC-32C over every
+ * entry's (type, term, index, nil flag, len, Data) in order. */
+static uint32_t ents_digest_step(uint32_t h, int32_t type, uint64_t term, uint64_t index, int nil,
+                                 const uint8_t *data, uint64_t n) {
+  uint8_t hd[8 + 8 + 4 + 4 + 8];
+  memcpy(hd, &term, 8);
+  memcpy(hd + 8, &index, 8);
+  memcpy(hd + 16, &type, 4);
+  int32_t z = nil;
+  memcpy(hd + 20, &z, 4);
+  memcpy(hd + 24, &n, 8);
+  h = or_crc32_update(h, OR_CASTAGNOLI, hd, sizeof(hd));
+  return n ? or_crc32_update(h, OR_CASTAGNOLI, data, n) : h;
+}
+
+uint32_t or_ents_digest(const or_readall_result *r) {
+  uint32_t h = 0;
+  for (int64_t i = 0; i < r->n_ents; i++) {
+    const or_entry *e = &r->ents[i];
+    h = ents_digest_step(h, e->type, e->term, e->index, e->data == NULL, e->data, (uint64_t)e->data_len);
+  }
+  return h;
+}
+
+uint32_t or_ent_views_digest(const uint8_t *buf, const or_ent_view *v, int64_t n) {
+  uint32_t h = 0;
+  for (int64_t i = 0; i < n; i++)
+    h = ents_digest_step(h, v[i].type, v[i].term, v[i].index, v[i].data_nil != 0, buf + v[i].data_off, v[i].data_len);
+  return h;
+}

@@ -208,6 +208,14 @@ void or_maybe_commit_batch(uint64_t G, const uint64_t *match, const uint8_t *nvo
                            uint64_t *committed, const uint64_t *log_offset, const uint64_t *log_ptr,
                            const uint64_t *log_terms, uint8_t *changed, uint8_t *status);
 
+/* ---- checker helpers (test infrastructure, not restatements) ----------- */
+/* Digest of ReadAll's ents: CRC-32C over (type, term, index, nil, len, Data)
+ * of every entry in order; the same digest over the engine's ewal_entry
+ * descriptors (Data at buf + data_off). */
+typedef struct { uint64_t term, index, data_off, data_len; int32_t type, data_nil; } or_ent_view;
+uint32_t or_ents_digest(const or_readall_result *r);
+uint32_t or_ent_views_digest(const uint8_t *buf, const or_ent_view *v, int64_t n);
+
 #ifdef __cplusplus
 }
 #endif

@@ -105,6 +105,10 @@ lib.or_loadsnap.argtypes = [C.c_char_p, C.c_int64, C.c_uint32, C.POINTER(LoadSna
 lib.or_loadsnap_free.argtypes = [C.POINTER(LoadSnapResult)]
 lib.or_maybe_commit.argtypes = [C.POINTER(C.c_uint64), C.c_int, C.c_uint64, C.POINTER(C.c_uint64),
                                 C.POINTER(C.c_uint64), C.c_uint64, C.c_uint64]
+lib.or_ents_digest.restype = C.c_uint32
+lib.or_ents_digest.argtypes = [C.POINTER(ReadAllResult)]
+lib.or_ent_views_digest.restype = C.c_uint32
+lib.or_ent_views_digest.argtypes = [C.c_char_p, C.c_void_p, C.c_int64]
 lib.or_chain_crcs.restype = C.c_int64
 lib.or_chain_crcs.argtypes = [C.c_char_p, C.c_int64, C.POINTER(C.c_uint32), C.c_int64, C.POINTER(C.c_int64)]
 
@@ -215,6 +219,25 @@ def readall(buf, ri=0):
                           unrec=_bytes(r.ents[i].unrec, r.ents[i].unrec_len)) for i in range(r.n_ents)])
     lib.or_readall_free(C.byref(r))
     return out
+
+
+def readall_digest(buf, ri=0):
+    """readall() for large inputs: the ents as (count, digest) instead of a
+    list (or_ents_digest; test-side helper, not a restatement)."""
+    r = ReadAllResult()
+    lib.or_readall(buf, len(buf), ri, C.byref(r))
+    out = dict(status=r.status, detail=r.detail, fail_record=r.fail_record, fail_offset=r.fail_offset,
+               n_records=r.n_records, last_crc=r.last_crc, enti=r.enti,
+               metadata=_bytes(r.metadata, r.metadata_len),
+               state=(r.state.term, r.state.vote, r.state.commit) if r.has_state else (0, 0, 0),
+               n_ents=r.n_ents, ents_digest=lib.or_ents_digest(C.byref(r)))
+    lib.or_readall_free(C.byref(r))
+    return out
+
+
+def ent_views_digest(buf, views, n):
+    """The same digest over n ewal_entry descriptors (ctypes array) into buf."""
+    return lib.or_ent_views_digest(buf, C.cast(views, C.c_void_p), n)
 
 
 def chain_crcs(buf, cap=None):

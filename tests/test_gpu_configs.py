@@ -1,0 +1,157 @@
+"""GPU parity at BASELINE.json's config sizes.
+
+* configs[0]: a WAL of 1M x 256 B entries (wal.Save's layout: crc, metadata,
+  HardState, entries; ~286 MB) -- the whole ReadAll result against the
+  oracle's: status, frames, lastCRC, enti, metadata, HardState, the ents (a
+  digest over every entry's fields and Data) and all 1M chained CRCs.
+* configs[2]: 512 per-raft-group WAL shards x 64 MiB in ONE batched ReadAll
+  (32 GiB, ~29 M frames: more than 2^24 frames, the segmented check spans
+  many 1 GiB tile groups): every clean shard OK with its exact frame count,
+  the corrupt shard's walpb.ErrCRCMismatch at its exact frame, no shard on
+  the one-by-one fallback; the oracle's full result on a sample of shards.
+* configs[3]: snapshot files of 1-256 MiB (log-uniform) in one
+  esnap_verify_packed call against or_loadsnap, corrupt files included.
+
+References: wal/wal.go:164-216, wal/decoder.go:28-47, snap/snapshotter.go:76-111.
+"""
+import ctypes as C
+import math
+import random
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+from etcd_amd import _lib as L
+from etcd_amd import wal as W
+from etcd_amd import snap as S
+
+pytestmark = pytest.mark.gpu
+
+
+def _device_ents_digest(ctx, buf, n, shard=None):
+    arr = (L.EntryDesc * max(n, 1))()
+    k = L.lib.ewal_copy_entries(ctx.handle, arr, n) if shard is None else \
+        L.lib.ewal_batch_copy_entries(ctx.handle, shard, arr, n)
+    assert k == n
+    return O.ent_views_digest(buf, arr, n)
+
+
+def _assert_result(ctx, g, o, buf, shard=None):
+    assert (g.status, g.fail_record, g.fail_offset) == (o["status"], o["fail_record"], o["fail_offset"])
+    if o["status"] != O.OK:
+        return
+    assert (g.n_records, g.last_crc, g.enti) == (o["n_records"], o["last_crc"], o["enti"])
+    assert g.metadata == o["metadata"]
+    assert (g.state.Term, g.state.Vote, g.state.Commit) == o["state"]
+    assert g.n_ents == o["n_ents"]
+    assert _device_ents_digest(ctx, buf, g.n_ents, shard) == o["ents_digest"]
+
+
+def _readall(ctx, dbuf, nb, ri, host):
+    r = L.Result()
+    rc = L.lib.ewal_readall_device(ctx.handle, dbuf.ptr, nb, ri, C.byref(r))
+    assert rc >= 0, rc
+    res = W._collect(ctx, r, host, with_ents=False)
+    res.n_ents = r.n_ents
+    return res
+
+
+def test_configs0_1m_x_256b(ctx):
+    buf, n = W.synth_wal(285_000_000, 256, 256, seed=1)
+    b = bytes(buf)
+    d = ctx.alloc(len(b) + 64)
+    try:
+        d.upload(b)
+        g = _readall(ctx, d, len(b), 1, memoryview(b))
+        o = O.readall_digest(b, 1)
+        assert o["status"] == O.OK and o["n_ents"] > 990_000
+        _assert_result(ctx, g, o, b)
+        # every chained CRC and frame offset
+        crcs, offs = O.chain_crcs(b, cap=n + 16)
+        recs = (L.RecordDesc * n)()
+        assert L.lib.ewal_copy_records(ctx.handle, recs, n) == n
+        ra = np.frombuffer(recs, dtype=np.dtype([("offset", "<u8"), ("data_off", "<u8"), ("data_len", "<u8"),
+                                                 ("type", "<i8"), ("crc", "<u4"), ("chained_crc", "<u4")]))
+        assert np.array_equal(ra["chained_crc"], np.array(crcs, dtype=np.uint32))
+        assert np.array_equal(ra["offset"], np.array(offs, dtype=np.uint64))
+        # one corrupt record in the middle
+        k = n // 2
+        p = int(ra["data_off"][k]) + int(ra["data_len"][k]) // 2
+        bad = bytearray(b)
+        bad[p] ^= 0x01
+        d.upload(bytes(bad[p:p + 1]), p)
+        g = _readall(ctx, d, len(b), 1, memoryview(bad))
+        o = O.readall_digest(bytes(bad), 1)
+        assert o["status"] == O.ERR_RECORD_CRC and o["fail_record"] == k
+        _assert_result(ctx, g, o, bytes(bad))
+    finally:
+        d.free()
+
+
+def test_configs2_512_shards_x_64mib(ctx):
+    nsh, bad_shard, bad_rec = 512, 2749 % 512, 1000
+    blob, lens, nrec = W.synth_shards(list(range(nsh)), 64 << 20, 128, 4096, corrupt={bad_shard: bad_rec})
+    assert sum(nrec) > (1 << 24)
+    d = ctx.alloc(len(blob) + 64)
+    try:
+        d.upload_ptr(C.addressof((C.c_char * len(blob)).from_buffer(blob)), len(blob))
+        out = (L.Result * nsh)()
+        rc = L.lib.ewal_readall_batch_device(ctx.handle, d.ptr, nsh, (C.c_uint64 * nsh)(*lens),
+                                             (C.c_uint64 * nsh)(*([1] * nsh)), out)
+        assert rc == 0, rc
+        for s in range(nsh):
+            r = out[s]
+            assert not (r.flags & L.FLAG_SHARD_FALLBACK), s
+            if s == bad_shard:
+                assert (r.status, r.fail_record) == (L.ERR_RECORD_CRC, bad_rec), (s, r.status, r.fail_record)
+            else:
+                assert (r.status, r.n_records) == (L.OK, nrec[s]), (s, r.status, r.n_records, nrec[s])
+        offs = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+        rng = random.Random(2)
+        sample = sorted({0, 1, bad_shard, nsh - 1} | set(rng.sample(range(nsh), 4)))
+        for s in sample:
+            sb = bytes(blob[offs[s]:offs[s + 1]])
+            o = O.readall_digest(sb, 1)
+            g = W._collect(ctx, out[s], memoryview(sb), with_ents=False, shard=s)
+            g.n_ents = out[s].n_ents
+            _assert_result(ctx, g, o, sb, shard=s)
+    finally:
+        d.free()
+
+
+def test_configs3_snapshots_1_to_256mib(ctx):
+    rng, crng = random.Random(4), random.Random(5)
+    pool = np.random.default_rng(4).integers(0, 256, size=(256 << 20) + 4096, dtype=np.uint8).tobytes()
+    sizes = [int(math.exp(rng.uniform(math.log(1 << 20), math.log(64 << 20)))) for _ in range(14)] + [(256 << 20) - 64]
+    files, bad = [], []
+    for i, n in enumerate(sizes):
+        st = rng.randrange(0, len(pool) - n)
+        f = bytearray(S.snap_file(S.snapshot_marshal(pool[st:st + n], (1, 2, 3), i + 1, 1)))
+        if i in (3, 9) or crng.random() < 0.05:
+            f[crng.randrange(len(f) // 4, len(f))] ^= 0x10
+            bad.append(i)
+        files.append(bytes(f))
+    offs, pos = [], 0
+    for f in files:
+        offs.append(pos)
+        pos += len(f) + 16            # files need not be packed back to back
+    packed = bytearray(pos)
+    for o_, f in zip(offs, files):
+        packed[o_:o_ + len(f)] = f
+    d = ctx.alloc(len(packed) + 64)
+    try:
+        d.upload_ptr(C.addressof((C.c_char * len(packed)).from_buffer(packed)), len(packed))
+        st, sc, cc = S.verify_packed(d, len(packed), offs, [len(f) for f in files])
+        for i, f in enumerate(files):
+            o = O.loadsnap(f)
+            assert st[i] == o["status"], (i, st[i], o["status"])
+            assert (sc[i], cc[i]) == (o["stored_crc"], o["computed_crc"]), i
+            if o["status"] == O.OK:
+                s = L.SnapshotDesc()
+                assert L.lib.esnap_copy_snapshot(ctx.handle, i, C.byref(s)) == 0
+                assert (s.index, s.term, list(s.nodes[:s.n_nodes])) == (i + 1, 1, [1, 2, 3])
+                assert packed[s.data_off:s.data_off + s.data_len] == o["snap"]["data"]
+        assert [i for i in range(len(files)) if st[i] != L.OK] == bad
+    finally:
+        d.free()
