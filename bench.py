@@ -39,10 +39,15 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
-    ap.add_argument("--workload", choices=["wal", "c1", "shards", "snap", "commit", "msg"], default="wal",
+    ap.add_argument("--snap-files", type=int, default=10000)
+    ap.add_argument("--pool-gib", type=float, default=24.0)
+    ap.add_argument("--batch-gib", type=float, default=8.0)
+    ap.add_argument("--workload", choices=["wal", "c1", "shards", "snap", "snapstream", "commit", "msg"],
+                    default="wal",
                     help="wal = configs[1] (the headline, default); c1 = configs[0]'s WAL (1M x 256 B entries) on "
                          "the GPU; shards = configs[2] (4096 x 64 MiB per-group WALs over the node, 512 per GPU); "
-                         "snap = configs[3]; commit = configs[4]; msg = raftpb.Message ingress decode")
+                         "snap = configs[3] (a resident batch); snapstream = configs[3]'s 10k-file set streamed "
+                         "from pinned host memory; commit = configs[4]; msg = raftpb.Message ingress decode")
     ap.add_argument("--shards-per-gpu", type=int, default=512)
     ap.add_argument("--shard-mib", type=int, default=64)
     return ap.parse_args()
@@ -59,6 +64,40 @@ def load_traffic():
 
 
 METRIC = "WAL verify GB/s (and records/s) per GPU + 8-GPU node, % of HBM roofline"
+
+
+def cpu_threads():
+    """The host cores the CPU baselines may use: the process's CPU set,
+    capped at the box's 16-CPU share (nproc shows the whole machine)."""
+    return max(1, min(16, len(os.sched_getaffinity(0))))
+
+
+def host_info():
+    """Recorded with every cpu_baseline (BASELINE.md:29)."""
+    import shutil
+    model = ""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    go = shutil.which("go")
+    return {"cpu_model": model, "nproc": os.cpu_count(), "cpus_allowed": len(os.sched_getaffinity(0)),
+            "gomaxprocs": "n/a (no Go toolchain on this host; the C restatement is timed instead)" if not go else
+                          "n/a (go at %s not used: the reference is not built here)" % go}
+
+
+def timed_cpu(seconds, fn):
+    """Run fn until `seconds` have passed (at least once): (passes, elapsed)."""
+    it, t0 = 0, time.perf_counter()
+    while True:
+        fn()
+        it += 1
+        if time.perf_counter() - t0 >= seconds:
+            return it, time.perf_counter() - t0
 
 
 def timed(dist, steps, fn):
@@ -124,6 +163,28 @@ def run_shards(a, dist, rank, world, local):
     ms = elapsed / a.steps * 1e3
     r0 = last["r"][0]
     frames = sum(nrec)
+    cpu = None
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        from oracle import oracle as O   # baseline only
+        nth = cpu_threads()
+        offs = [0]
+        for x in lens[:-1]:
+            offs.append(offs[-1] + x)
+        addr = C.addressof((C.c_char * nb).from_buffer(blob))
+        k = max(nth, min(nsh, 4 * nth))          # a bounded sample: k shards per pass
+        so, sl = offs[:k], lens[:k]
+        sb = sum(sl)
+        it, cs = timed_cpu(a.cpu_seconds, lambda: O.fast_readall_batch(addr, so, sl, 1, nth, faithful=True))
+        it2, cs2 = timed_cpu(a.cpu_seconds / 2, lambda: O.fast_readall_batch(addr, so, sl, 1, nth))
+        st, fr = O.fast_readall_batch(addr, so, sl, 1, nth)
+        assert all(x in (O.OK, O.ERR_RECORD_CRC) for x in st), st
+        cpu = dict(host_info(), **{
+            "value": round(sb * it / cs / 1e9, 4), "unit": "GB/s", "cores": nth, "kind": "port",
+            "sample": "oracle/ or_readall (the faithful C restatement of wal.ReadAll) on all %d cores, one shard per "
+                      "worker, over the first %d shards (%.2f GiB), %d passes, %.1f s" % (nth, k, sb / (1 << 30), it, cs),
+            "optimised": {"value": round(sb * it2 / cs2 / 1e9, 4), "unit": "GB/s", "cores": nth,
+                          "sample": "oracle/ewal_cpu_fast.c orf_readall (3-stream SSE4.2 CRC-32C, no per-record "
+                                    "allocation) one shard per worker, same shards, %d passes, %.1f s" % (it2, cs2)}})
     if rank == 0:
         out = {
             "metric": METRIC, "value": round(world * nb / (ms / 1e3) / 1e9, 3), "unit": "GB/s", "n_gpus": world,
@@ -139,9 +200,11 @@ def run_shards(a, dist, rank, world, local):
                          "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": round(nb / (r0.stream_ms / 1e3) / 1e9 / HBM_PEAK_GBPS, 4), "traffic": None,
                          "kernel": "k_stream", "kernel_ms": round(r0.stream_ms, 4),
-                         "algorithmic_bytes_per_launch": nb},
+                         "algorithmic_bytes_per_launch": nb,
+                         "pipeline_achieved": round(nb / (r0.device_ms / 1e3) / 1e9, 2),
+                         "pipeline_frac": round(nb / (r0.device_ms / 1e3) / 1e9 / HBM_PEAK_GBPS, 4)},
             "pipeline_device_ms": round(r0.device_ms, 4),
-            "cpu_baseline": None,
+            "cpu_baseline": cpu,
             "gen_seconds": round(gen_s, 2),
         }
         print(json.dumps(out), flush=True)
@@ -209,17 +272,24 @@ def run_snap(a, dist, rank, world, local):
             pick.append(i)
             acc += lens[i]
         views = [blob[offs[i]:offs[i] + lens[i]] for i in pick]
-        it, t2 = 0, time.perf_counter()
-        while True:
+
+        def one_pass():
             for v in views:
                 O.loadsnap(v)
-            it += 1
-            if time.perf_counter() - t2 >= a.cpu_seconds:
-                break
-        cs = time.perf_counter() - t2
-        cpu = {"value": round(acc * it / cs / 1e9, 4), "unit": "GB/s", "cores": 1, "kind": "port",
-               "sample": "oracle/ or_loadsnap (snappb + raftpb.Snapshot Unmarshal, crc32.Update, 1 thread) over "
-                         "%d of the files (%.2f GiB), %d passes, %.1f s" % (len(pick), acc / (1 << 30), it, cs)}
+        it, cs = timed_cpu(a.cpu_seconds, one_pass)
+        nth = cpu_threads()
+        addr = C.cast(C.c_char_p(blob), C.c_void_p).value   # blob's own bytes (no copy)
+        it2, cs2 = timed_cpu(a.cpu_seconds / 2, lambda: O.fast_snap_verify_batch(addr, offs, lens, nth))
+        st2, _ = O.fast_snap_verify_batch(addr, offs, lens, nth)
+        assert [i for i, x in enumerate(st2) if x != O.OK] == bad
+        cpu = dict(host_info(), **{
+            "value": round(acc * it / cs / 1e9, 4), "unit": "GB/s", "cores": 1, "kind": "port",
+            "sample": "oracle/ or_loadsnap (snappb + raftpb.Snapshot Unmarshal, crc32.Update, 1 thread) over "
+                      "%d of the files (%.2f GiB), %d passes, %.1f s" % (len(pick), acc / (1 << 30), it, cs),
+            "optimised": {"value": round(nb * it2 / cs2 / 1e9, 4), "unit": "GB/s", "cores": nth,
+                          "sample": "oracle/ewal_cpu_fast.c orf_snap_verify_batch (envelope + 3-stream SSE4.2 "
+                                    "CRC-32C) one file per worker over all %d files, %d passes, %.1f s"
+                                    % (len(lens), it2, cs2)}})
     if rank == 0:
         print(json.dumps({
             "metric": METRIC, "value": round(world * nb / (ms / 1e3) / 1e9, 3), "unit": "GB/s", "n_gpus": world,
@@ -234,10 +304,145 @@ def run_snap(a, dist, rank, world, local):
             "roofline": {"bound": "hbm", "achieved": round(nb / (kms / 1e3) / 1e9, 2), "peak": HBM_PEAK_GBPS,
                          "unit": "GB/s", "frac": round(nb / (kms / 1e3) / 1e9 / HBM_PEAK_GBPS, 4), "traffic": None,
                          "kernel": "k_stream<false>", "kernel_ms": round(kms, 4),
-                         "algorithmic_bytes_per_launch": nb},
+                         "algorithmic_bytes_per_launch": nb,
+                         "pipeline_achieved": round(nb / (dev_ms / 1e3) / 1e9, 2),
+                         "pipeline_frac": round(nb / (dev_ms / 1e3) / 1e9 / HBM_PEAK_GBPS, 4)},
             "pipeline_device_ms": round(dev_ms, 4), "e2e_gbps_incl_h2d": e2e,
             "cpu_baseline": cpu, "gen_seconds": round(gen_s, 2)}), flush=True)
     dbuf.free()
+    ctx.close()
+
+
+def run_snapstream(a, dist, rank, world, local):
+    """configs[3] at its full size on one GPU: the 10k-file snapshot set
+    (~450 GiB, sizes log-uniform 1-256 MiB) streamed from pinned host
+    memory through two HBM batch buffers: the H2D copies of batch b+1 (a
+    copy stream) overlap the verification of batch b (esnap_verify_packed,
+    snap/snapshotter.go:76-111).  The files are drawn (seed 6) from a pool
+    of distinct procedurally generated files held in pinned memory (the
+    host holds ~270 GiB at most, not 450 GiB), ~1 % of them corrupt; every
+    file of the stream is copied and verified.  value = streamed GB/s
+    (host-resident pinned -> verdict); the line also carries the resident
+    (kernel-only) rate over the same batches."""
+    import math
+    import random
+    import numpy as np
+    from etcd_amd import snap as S
+    nfiles = a.snap_files
+    rng, crng, prng = random.Random(4 + 7919 * rank), random.Random(5 + 7919 * rank), random.Random(6 + 7919 * rank)
+    t = time.time()
+    src = np.random.default_rng(4 + rank).integers(0, 256, size=(256 << 20) + 4096, dtype=np.uint8).tobytes()
+    sizes, total = [], 0
+    budget = int(a.pool_gib * (1 << 30))
+    while total < budget:
+        n = int(math.exp(rng.uniform(math.log(1 << 20), math.log(256 << 20))))
+        sizes.append(n + 64)    # + the snappb / raftpb.Snapshot envelope (upper bound)
+        total += n + 64
+    pool = torch.empty(total + 16 * len(sizes) + 4096, dtype=torch.uint8).pin_memory()
+    pv = pool.numpy()
+    poffs, plens, pbad = [], [], []
+    pos = 0
+    for i, n in enumerate(sizes):
+        st = rng.randrange(0, len(src) - n)
+        f = bytearray(S.snap_file(S.snapshot_marshal(src[st:st + n - 64], (1, 2, 3), i + 1, 1)))
+        if crng.random() < 0.01 or (i == len(sizes) - 1 and not pbad):
+            f[len(f) // 2] ^= 0x10
+            pbad.append(i)
+        pv[pos:pos + len(f)] = np.frombuffer(f, dtype=np.uint8)
+        poffs.append(pos)
+        plens.append(len(f))
+        pos += (len(f) + 15) & ~15
+    del src
+    stream = [prng.randrange(len(sizes)) for _ in range(nfiles)]
+    gen_s = time.time() - t
+    sbytes = sum(plens[i] for i in stream)
+    # batches of consecutive stream files up to --batch-gib each (16-B aligned offsets)
+    cap = int(a.batch_gib * (1 << 30))
+    batches, cur, cpos = [], [], 0
+    for fi in stream:
+        ln = (plens[fi] + 15) & ~15
+        if cur and cpos + ln > cap:
+            batches.append(cur)
+            cur, cpos = [], 0
+        cur.append(fi)
+        cpos += ln
+    batches.append(cur)
+    dev = torch.device("cuda", local)
+    bufs = [torch.empty(cap + 64, dtype=torch.uint8, device=dev) for _ in range(2)]
+    ctx = W.Context(local)
+    cs = torch.cuda.Stream(dev)
+    copied = [torch.cuda.Event() for _ in range(2)]
+
+    def enqueue(b):
+        d = bufs[b % 2]
+        offs, lens, o = [], [], 0
+        with torch.cuda.stream(cs):
+            for fi in batches[b]:
+                d[o:o + plens[fi]].copy_(pool[poffs[fi]:poffs[fi] + plens[fi]], non_blocking=True)
+                offs.append(o)
+                lens.append(plens[fi])
+                o += (plens[fi] + 15) & ~15
+            copied[b % 2].record(cs)
+        return offs, lens, o
+
+    stt_all, kms, dms = [], [], []
+
+    def run_all():
+        stt_all.clear(), kms.clear(), dms.clear()
+        nxt = enqueue(0)
+        for b in range(len(batches)):
+            offs, lens, used = nxt
+            if b + 1 < len(batches):
+                copied[b % 2].synchronize()        # batch b landed; (b+1)'s buffer is free
+                nxt = enqueue(b + 1)
+            else:
+                copied[b % 2].synchronize()
+            n = len(offs)
+            st = (C.c_int32 * n)()
+            rc = L.lib.esnap_verify_packed(ctx.handle, C.c_void_p(bufs[b % 2].data_ptr()), used,
+                                           (C.c_uint64 * n)(*offs), (C.c_uint64 * n)(*lens), n, L.CASTAGNOLI, st,
+                                           None, None)
+            assert rc == 0, rc
+            stt_all.extend(st)
+            kms.append(float(L.lib.ewal_last_stream_ms(ctx.handle)))
+            dms.append(float(L.lib.ewal_last_device_ms(ctx.handle)))
+
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    run_all()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    badset = set(pbad)
+    want = [L.ERR_SNAP_CRC if fi in badset else L.OK for fi in stream]
+    assert stt_all == want, "verdict mismatch"
+    nbad = sum(1 for x in want if x != L.OK)
+    used_total = sum(sum((plens[fi] + 15) & ~15 for fi in bt) for bt in batches)
+    if rank == 0:
+        print(json.dumps({
+            "metric": METRIC, "value": round(world * sbytes / el / 1e9, 3), "unit": "GB/s", "n_gpus": world,
+            "steps": 1, "warmup": 0, "ms_per_step": round(el * 1e3, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
+            "config": {"workload": "configs[3] streamed: %d snapshot files (%.1f GiB) per GPU, sizes log-uniform "
+                                   "1-256 MiB, drawn from a pinned pool of %d distinct files (%.1f GiB), %d corrupt "
+                                   "in the stream; %d HBM batches of <= %.0f GiB, copies of batch b+1 overlapping "
+                                   "the verification of batch b" % (nfiles, sbytes / (1 << 30), len(sizes),
+                                                                    pos / (1 << 30), nbad, len(batches), a.batch_gib),
+                       "files_per_gpu": nfiles, "snapshot_bytes_per_gpu": sbytes,
+                       "parallelism": "dp%d (independent files)" % world},
+            "files_per_s": round(world * nfiles / el, 1),
+            "streamed_gbps_pinned": round(sbytes / el / 1e9, 3),
+            "resident_gbps": round(used_total / (sum(dms) / 1e3) / 1e9, 2),
+            "roofline": {"bound": "hbm", "achieved": round(used_total / (sum(kms) / 1e3) / 1e9, 2),
+                         "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                         "frac": round(used_total / (sum(kms) / 1e3) / 1e9 / HBM_PEAK_GBPS, 4), "traffic": None,
+                         "kernel": "k_stream<false>", "kernel_ms": round(sum(kms) / len(kms), 4),
+                         "algorithmic_bytes_per_launch": round(used_total / len(batches)),
+                         "pipeline_achieved": round(used_total / (sum(dms) / 1e3) / 1e9, 2),
+                         "pipeline_frac": round(used_total / (sum(dms) / 1e3) / 1e9 / HBM_PEAK_GBPS, 4),
+                         "note": "streamed value is PCIe-bound (host -> HBM); the roofline is the resident kernel"},
+            "cpu_baseline": None, "gen_seconds": round(gen_s, 2)}), flush=True)
     ctx.close()
 
 
@@ -309,9 +514,19 @@ def run_commit(a, dist, rank, world, local):
             if time.perf_counter() - t2 >= a.cpu_seconds:
                 break
         cs = time.perf_counter() - t2
-        cpu = {"value": round(G * it / cs, 1), "unit": "groups/s", "cores": 1, "kind": "port",
-               "sample": "oracle/ or_maybe_commit_batch (insertion sort + q-th largest + term check per group, 1 "
-                         "thread) over all %d groups, %d passes, %.1f s" % (G, it, cs)}
+        nth = cpu_threads()
+
+        def all_cores():
+            c[:] = committed0
+            O.fast_maybe_commit_batch(G, match.reshape(-1), nv, term, c, log_offset, log_ptr, log_terms, chc, stc, nth)
+        it2, cs2 = timed_cpu(a.cpu_seconds / 2, all_cores)
+        cpu = dict(host_info(), **{
+            "value": round(G * it / cs, 1), "unit": "groups/s", "cores": 1, "kind": "port",
+            "sample": "oracle/ or_maybe_commit_batch (insertion sort + q-th largest + term check per group, 1 "
+                      "thread) over all %d groups, %d passes, %.1f s" % (G, it, cs),
+            "optimised": {"value": round(G * it2 / cs2, 1), "unit": "groups/s", "cores": nth,
+                          "sample": "the same per-group code on all %d cores over group ranges "
+                                    "(orf_maybe_commit_batch), %d passes, %.1f s" % (nth, it2, cs2)}})
     if rank == 0:
         print(json.dumps({
             "metric": "maybeCommit groups/s (configs[4]); WAL verify GB/s is the headline metric",
@@ -409,7 +624,8 @@ def main():
     elif (a.size_gib, a.min_data, a.max_data) != (8.0, 64, 65536):
         label = "configs[1]-shaped"
     if a.workload not in ("wal", "c1"):
-        {"shards": run_shards, "snap": run_snap, "commit": run_commit, "msg": run_msg}[a.workload](a, dist, rank, world, local)
+        {"shards": run_shards, "snap": run_snap, "snapstream": run_snapstream, "commit": run_commit,
+         "msg": run_msg}[a.workload](a, dist, rank, world, local)
         if dist is not None:
             dist.destroy_process_group()
         return
@@ -467,6 +683,7 @@ def main():
     recs_per_s = world * n / (ms_per_step / 1e3)
 
     stream_avg = sum(stream_ms) / len(stream_ms)
+    dev_avg = sum(dev_ms) / len(dev_ms)
     achieved = nb / (stream_avg / 1e3) / 1e9
 
     # ---- end-to-end variant (host -> device included), one pass -------------
@@ -495,10 +712,25 @@ def main():
                 break
         cpu_s = time.perf_counter() - t2
         assert o["status"] == O.OK
-        cpu = {"value": round(len(sample) * iters / cpu_s / 1e9, 4), "unit": "GB/s", "cores": 1, "kind": "port",
-               "sample": "oracle/ or_readall (C restatement of wal.ReadAll: per-record alloc+copy, SSE4.2 "
-                         "CRC-32C, 1 thread) over the first %.2f GiB (%d frames) of the same WAL, %d passes, "
-                         "%.1f s" % (len(sample) / (1 << 30), o["n_records"], iters, cpu_s)}
+        # the optimised CPU ReadAll on all cores, over the whole WAL (its corrupt frame included)
+        nth = cpu_threads()
+        addr = C.addressof((C.c_char * nb).from_buffer(buf))
+        fst = O.fast_readall_status(addr, nb, 1, nth)
+        assert fst[0] == O.ERR_RECORD_CRC and fst[2] == k, fst
+        it2, cs2 = timed_cpu(a.cpu_seconds / 2, lambda: O.fast_readall_status(addr, nb, 1, nth))
+        it3, cs3 = timed_cpu(a.cpu_seconds / 4, lambda: O.fast_readall_status(addr, nb, 1, 1))
+        cpu = dict(host_info(), **{
+            "value": round(len(sample) * iters / cpu_s / 1e9, 4), "unit": "GB/s", "cores": 1, "kind": "port",
+            "sample": "oracle/ or_readall (C restatement of wal.ReadAll: per-record alloc+copy, SSE4.2 "
+                      "CRC-32C, 1 thread) over the first %.2f GiB (%d frames) of the same WAL, %d passes, "
+                      "%.1f s" % (len(sample) / (1 << 30), o["n_records"], iters, cpu_s),
+            "optimised": {"value": round(nb * it2 / cs2 / 1e9, 4), "unit": "GB/s", "cores": nth,
+                          "one_core_gbps": round(nb * it3 / cs3 / 1e9, 4),
+                          "sample": "oracle/ewal_cpu_fast.c orf_readall over the whole %.2f GiB WAL (stops at the "
+                                    "corrupt frame %d like the reference): serial framing walk, every frame's CRC "
+                                    "with the local-verify rule on %d cores (3-stream SSE4.2 CRC-32C), ReadAll's "
+                                    "dispatch over the frame table; %d passes, %.1f s" %
+                                    (nb / (1 << 30), k, nth, it2, cs2)}})
 
     if rank == 0:
         out = {
@@ -514,9 +746,14 @@ def main():
             "records_per_s": round(recs_per_s, 1),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": load_traffic() if label == "configs[1]" else None,
+                         "traffic_source": "profiles/k_stream_pmc.json: the committed rocprofv3 PMC pass of this "
+                                           "config (FETCH_SIZE x2 + WRITE_SIZE per launch), not measured in this run",
                          "kernel": "k_stream", "kernel_ms": round(stream_avg, 4),
-                         "algorithmic_bytes_per_launch": nb},
-            "pipeline_device_ms": round(sum(dev_ms) / len(dev_ms), 4),
+                         "algorithmic_bytes_per_launch": nb,
+                         "pipeline_achieved": round(nb / (dev_avg / 1e3) / 1e9, 2),
+                         "pipeline_frac": round(nb / (dev_avg / 1e3) / 1e9 / HBM_PEAK_GBPS, 4),
+                         "step_frac": round(gbps / world / HBM_PEAK_GBPS, 4)},
+            "pipeline_device_ms": round(dev_avg, 4),
             "first_call_ms": round(first_ms, 3),
             "e2e_gbps_incl_h2d": e2e,
             "cpu_baseline": cpu,

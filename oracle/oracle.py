@@ -109,6 +109,16 @@ lib.or_ents_digest.restype = C.c_uint32
 lib.or_ents_digest.argtypes = [C.POINTER(ReadAllResult)]
 lib.or_ent_views_digest.restype = C.c_uint32
 lib.or_ent_views_digest.argtypes = [C.c_char_p, C.c_void_p, C.c_int64]
+lib.orf_crc32c_update.restype = C.c_uint32
+lib.orf_crc32c_update.argtypes = [C.c_uint32, C.c_char_p, C.c_uint64]
+lib.orf_readall.argtypes = [C.c_void_p, C.c_int64, C.c_uint64, C.c_int, C.c_void_p]
+lib.orf_result_free.argtypes = [C.c_void_p]
+lib.orf_readall_batch.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.c_uint64, C.c_int, C.c_void_p,
+                                  C.c_void_p]
+lib.orf_readall_batch_faithful.argtypes = lib.orf_readall_batch.argtypes
+lib.orf_snap_verify_batch.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.c_int, C.c_void_p,
+                                      C.c_void_p]
+lib.orf_maybe_commit_batch.argtypes = [C.c_uint64] + [C.c_void_p] * 9 + [C.c_int]
 lib.or_chain_crcs.restype = C.c_int64
 lib.or_chain_crcs.argtypes = [C.c_char_p, C.c_int64, C.POINTER(C.c_uint32), C.c_int64, C.POINTER(C.c_int64)]
 
@@ -238,6 +248,82 @@ def readall_digest(buf, ri=0):
 def ent_views_digest(buf, views, n):
     """The same digest over n ewal_entry descriptors (ctypes array) into buf."""
     return lib.or_ent_views_digest(buf, C.cast(views, C.c_void_p), n)
+
+
+# ---- the optimised CPU baseline (ewal_cpu_fast.c; bench.py's cpu_baseline) ----
+IRREGULAR = 100
+
+
+class FastEnt(C.Structure):
+    _fields_ = [("term", C.c_uint64), ("index", C.c_uint64), ("data_off", C.c_uint64), ("data_len", C.c_uint64),
+                ("type", C.c_int32), ("data_nil", C.c_int32)]
+
+
+class FastResult(C.Structure):
+    _fields_ = [("status", C.c_int), ("detail", C.c_int64), ("fail_record", C.c_int64), ("fail_offset", C.c_int64),
+                ("n_records", C.c_int64), ("last_crc", C.c_uint32), ("enti", C.c_uint64),
+                ("metadata_off", C.c_int64), ("metadata_len", C.c_int64), ("has_state", C.c_int),
+                ("state_term", C.c_uint64), ("state_vote", C.c_uint64), ("state_commit", C.c_uint64),
+                ("ents", C.POINTER(FastEnt)), ("n_ents", C.c_int64)]
+
+
+def fast_crc32c(crc, data):
+    return lib.orf_crc32c_update(crc, data, len(data))
+
+
+def fast_readall(buf, ri=0, nthreads=1):
+    """orf_readall: readall_digest()'s dict, or None when the input is
+    outside the fast path (ORF_IRREGULAR)."""
+    r = FastResult()
+    keep = C.create_string_buffer(bytes(buf), len(buf))
+    st = lib.orf_readall(C.addressof(keep), len(buf), ri, nthreads, C.byref(r))
+    if st == IRREGULAR:
+        return None
+    md = buf[r.metadata_off:r.metadata_off + r.metadata_len] if r.metadata_off >= 0 else None
+    out = dict(status=r.status, detail=r.detail, fail_record=r.fail_record, fail_offset=r.fail_offset,
+               n_records=r.n_records, last_crc=r.last_crc, enti=r.enti, metadata=md,
+               state=(r.state_term, r.state_vote, r.state_commit) if r.has_state else (0, 0, 0),
+               n_ents=r.n_ents, ents_digest=lib.or_ent_views_digest(keep, C.cast(r.ents, C.c_void_p), r.n_ents))
+    lib.orf_result_free(C.byref(r))
+    return out
+
+
+def fast_readall_status(buf_addr, n, ri=0, nthreads=1):
+    """orf_readall over n bytes at buf_addr: (status, n_records, fail_record)
+    only (the bench's timed call)."""
+    r = FastResult()
+    st = lib.orf_readall(C.c_void_p(buf_addr), n, ri, nthreads, C.byref(r))
+    out = (st, r.n_records, r.fail_record)
+    lib.orf_result_free(C.byref(r))
+    return out
+
+
+def _u64arr(x):
+    return (C.c_uint64 * max(len(x), 1))(*x)
+
+
+def fast_readall_batch(buf_addr, offs, lens, ri, nthreads, faithful=False):
+    """orf_readall_batch (faithful: or_readall per shard) over shards at
+    buf_addr (an address), one shard per worker: (status, frames)."""
+    n = len(offs)
+    st, fr = (C.c_int32 * max(n, 1))(), (C.c_int64 * max(n, 1))()
+    fn = lib.orf_readall_batch_faithful if faithful else lib.orf_readall_batch
+    fn(C.c_void_p(buf_addr), _u64arr(offs), _u64arr(lens), n, ri, nthreads, st, fr)
+    return list(st[:n]), list(fr[:n])
+
+
+def fast_snap_verify_batch(buf_addr, offs, lens, nthreads):
+    n = len(offs)
+    st, cc = (C.c_int32 * max(n, 1))(), (C.c_uint32 * max(n, 1))()
+    lib.orf_snap_verify_batch(C.c_void_p(buf_addr), _u64arr(offs), _u64arr(lens), n, nthreads, st, cc)
+    return list(st[:n]), list(cc[:n])
+
+
+def fast_maybe_commit_batch(G, match, nvoters, term, committed, log_offset, log_ptr, log_terms, changed, status,
+                            nthreads):
+    P = lambda a: a.ctypes.data_as(C.c_void_p)   # noqa: E731  (numpy arrays)
+    lib.orf_maybe_commit_batch(G, P(match), P(nvoters), P(term), P(committed), P(log_offset), P(log_ptr),
+                               P(log_terms), P(changed), P(status), nthreads)
 
 
 def chain_crcs(buf, cap=None):
