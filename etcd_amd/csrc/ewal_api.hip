@@ -145,9 +145,20 @@ static int select_flagged(ewal_ctx *c, const uint8_t *flags, uint32_t n, uint32_
   return 0;
 }
 
+// The general framing path's per-candidate arrays (lengths, links, link
+// exceptions): allocated only when that path runs, so the regular path's
+// first call does not pay for them.
+static int ensure_cand_aux(ewal_ctx *c, uint64_t ccap) {
+  EW_CHECK(c->clen.ensure(ccap * 8));
+  EW_CHECK(c->nxt.ensure(ccap * 4));
+  EW_CHECK(c->exc.ensure(ccap));
+  return 0;
+}
+
 // The overflow path of the candidate compaction (the list outgrew ccap):
 // slots -> dense list again (k_compact), then the overflow units (k_rescan).
 static int compact_cands(ewal_ctx *c, const uint8_t *d_buf, uint64_t B, uint32_t nunits, uint64_t ccap) {
+  if (int rc = ensure_cand_aux(c, ccap)) return rc;
   Small *ds = c->small.as<Small>();
   EW_CHECK(hipMemsetAsync(&ds->novf, 0, 4, c->stream));
   hipLaunchKernelGGL(k_compact, dim3(grid_for(nunits, 256)), dim3(256), 0, c->stream, d_buf, nunits,
@@ -159,12 +170,18 @@ static int compact_cands(ewal_ctx *c, const uint8_t *d_buf, uint64_t B, uint32_t
   return 0;
 }
 
+// Capacity of the dense candidate list for a B-byte stream: a frame is at
+// least 12 bytes, but candidates denser than one per 128 B only come from
+// tiny records; those calls grow the list (compact_cands) and run again.
+static inline uint64_t cand_cap(uint64_t B) { return std::min<uint64_t>(B / 128 + 65536, 0xfffffff0ull); }
+
 // Run the HBM pass (k_stream) and the unit scan over d_buf[0..B): fills
 // c->v, c->pwave; with find_cand also the dense, position-sorted candidate
 // list cpos[] (k_uapply's epilogue; units with more than EW_SLOTS candidates
 // are counted in Small.novf and filled in by k_rescan later), its size in
 // Small.total.  Asynchronous: nothing waits for the device here.
-static int run_stream(ewal_ctx *c, DevTables *tb, const uint8_t *d_buf, uint64_t B, int find_cand, uint64_t ccap) {
+// The stream pass's and unit scan's workspace for a B-byte stream.
+static int stream_ensure(ewal_ctx *c, uint64_t B, int find_cand) {
   const uint64_t nunits64 = B / EW_WAVE_BYTES + 1;
   if (nunits64 >= 0xffff0000ull) return EWAL_E_INVAL;
   const uint32_t nunits = (uint32_t)nunits64;
@@ -181,6 +198,15 @@ static int run_stream(ewal_ctx *c, DevTables *tb, const uint8_t *d_buf, uint64_t
   EW_CHECK(c->tagg.ensure((size_t)nstiles * 16));
   EW_CHECK(c->tpx.ensure((size_t)nstiles * 16));
   EW_CHECK(c->gagg.ensure((size_t)((nstiles + 1023) / 1024) * 16));
+  return 0;
+}
+
+static int run_stream(ewal_ctx *c, DevTables *tb, const uint8_t *d_buf, uint64_t B, int find_cand, uint64_t ccap) {
+  const uint64_t nunits64 = B / EW_WAVE_BYTES + 1;
+  if (nunits64 >= 0xffff0000ull) return EWAL_E_INVAL;
+  const uint32_t nunits = (uint32_t)nunits64;
+  const uint32_t nstiles = (nunits + EW_TILE_UNITS - 1) / EW_TILE_UNITS;
+  if (int rc = stream_ensure(c, B, find_cand)) return rc;
   Small *ds = c->small.as<Small>();   // zeroed by k_stream (workgroup 0), the first kernel of every call
   StreamArgs a;
   a.buf = d_buf;
@@ -580,11 +606,8 @@ static int readall_impl(ewal_ctx *c, const uint8_t *d_buf, uint64_t B, uint64_t 
   bool decoded = false;    // k_frame's speculative decode holds
   bool spec_checked = false;   // ... and k_check / k_result already ran behind it
   if (B > 0) {
-    uint64_t ccap = std::min<uint64_t>(B / 128 + 65536, 0xfffffff0ull);
+    uint64_t ccap = cand_cap(B);
     EW_CHECK(c->cpos.ensure(ccap * 8));
-    EW_CHECK(c->clen.ensure(ccap * 8));
-    EW_CHECK(c->nxt.ensure(ccap * 4));
-    EW_CHECK(c->exc.ensure(ccap));
     // descriptor capacity of the speculative frame pass: the previous call's
     // frame count with headroom, at least one frame per 4 KiB
     uint64_t rdcap = std::min<uint64_t>(ccap, std::max<uint64_t>(c->last_k + c->last_k / 8 + 1024,
@@ -655,6 +678,7 @@ static int readall_impl(ewal_ctx *c, const uint8_t *d_buf, uint64_t B, uint64_t 
       const bool resc = c->h_small->novf && Kf <= ccap && !rescanned;
       if (!grow && !resc) break;
       if (resc) {
+        if ((rc = ensure_cand_aux(c, ccap))) return rc;
         hipLaunchKernelGGL(k_rescan, dim3(64), dim3(256), 0, c->stream, d_buf, B, c->ovf.as<uint32_t>(), &ds->novf,
                            c->cbase.as<unsigned long long>(), c->cpos.as<uint64_t>(), c->clen.as<uint64_t>(), ccap);
         EW_CHECK(hipGetLastError());
@@ -683,6 +707,7 @@ static int readall_impl(ewal_ctx *c, const uint8_t *d_buf, uint64_t B, uint64_t 
       // the speculation failed: frame by candidate links (k_link), growing
       // the candidate list first if it overflowed
       const unsigned lgrid = (unsigned)std::max(1, c->num_cu) * 8;
+      if ((rc = ensure_cand_aux(c, ccap))) return rc;
       if (K <= ccap && c->h_small->novf) {   // candidates of the overflow units
         hipLaunchKernelGGL(k_rescan, dim3(64), dim3(256), 0, c->stream, d_buf, B, c->ovf.as<uint32_t>(), &ds->novf,
                            c->cbase.as<unsigned long long>(), c->cpos.as<uint64_t>(), c->clen.as<uint64_t>(), ccap);
@@ -692,9 +717,6 @@ static int readall_impl(ewal_ctx *c, const uint8_t *d_buf, uint64_t B, uint64_t 
         if (K >= 0xfffffff0ull) return EWAL_E_NOMEM;
         ccap = K + 1024;
         EW_CHECK(c->cpos.ensure(ccap * 8));
-        EW_CHECK(c->clen.ensure(ccap * 8));
-        EW_CHECK(c->nxt.ensure(ccap * 4));
-        EW_CHECK(c->exc.ensure(ccap));
         rc = compact_cands(c, d_buf, B, (uint32_t)(B / EW_WAVE_BYTES + 1), ccap);
         if (rc) return rc;
       }
@@ -1055,11 +1077,8 @@ static int readall_batch_impl(ewal_ctx *c, const uint8_t *d_buf, uint32_t ns, co
   float dev_ms = 0, str_ms = 0;
   if (fast) {
     EW_CHECK(hipEventRecord(c->ev0, c->stream));
-    const uint64_t ccap = std::min<uint64_t>(B / 128 + 65536, 0xfffffff0ull);
+    const uint64_t ccap = cand_cap(B);
     EW_CHECK(c->cpos.ensure(ccap * 8));
-    EW_CHECK(c->clen.ensure(ccap * 8));
-    EW_CHECK(c->nxt.ensure(ccap * 4));
-    EW_CHECK(c->exc.ensure(ccap));
     uint64_t rdcap = std::min<uint64_t>(ccap, std::max<uint64_t>(c->last_k + c->last_k / 8 + 1024,
                                                                  B / 1024 + 1024));
     rc = run_stream(c, tb, d_buf, B, 1, ccap);
@@ -1092,6 +1111,7 @@ static int readall_batch_impl(ewal_ctx *c, const uint8_t *d_buf, uint32_t ns, co
       const bool resc = c->h_small->novf && Kf <= ccap && !rescanned;
       if (!grow && !resc) break;
       if (resc) {
+        if ((rc = ensure_cand_aux(c, ccap))) return rc;
         hipLaunchKernelGGL(k_rescan, dim3(64), dim3(256), 0, c->stream, d_buf, B, c->ovf.as<uint32_t>(), &ds->novf,
                            c->cbase.as<unsigned long long>(), c->cpos.as<uint64_t>(), c->clen.as<uint64_t>(), ccap);
         EW_CHECK(hipGetLastError());
@@ -1326,6 +1346,37 @@ int ewal_ctx_set_stream(ewal_ctx *c, void *s) {
     c->own_stream = true;
   }
   return EWAL_OK;
+}
+
+int ewal_ctx_reserve(ewal_ctx *c, uint64_t wal_bytes) {
+  if (!c) return EWAL_E_INVAL;
+  EW_CHECK(hipSetDevice(c->device));
+  DevTables *tb;
+  int rc = get_tables(c, 0x82F63B78u, &tb);
+  if (rc) return rc;
+  const uint64_t B = wal_bytes;
+  if ((rc = stream_ensure(c, B, 1))) return rc;
+  const uint64_t ccap = cand_cap(B);
+  EW_CHECK(c->cpos.ensure(ccap * 8));
+  // the fused pass: look-back words, tile records, ents / mlist for the
+  // first call's descriptor capacity (readall_impl's rdcap)
+  const uint64_t ntiles = ccap / FC_THREADS + 2;
+  const size_t had = c->fstat.cap;
+  EW_CHECK(c->fstat.ensure((size_t)ntiles * 8));
+  EW_CHECK(c->ftrec.ensure((size_t)ntiles * sizeof(TileRec)));
+  if (c->fstat.cap != had) EW_CHECK(hipMemsetAsync(c->fstat.p, 0, c->fstat.cap, c->stream));
+  const uint64_t ecap = std::min<uint64_t>(ccap, B / 4096 + 1024);
+  EW_CHECK(c->ents.ensure((size_t)ecap * sizeof(ewal_entry)));
+  EW_CHECK(c->mlist.ensure((size_t)ecap * 4));
+  // load the device code: a ReadAll over a one-frame WAL (a crcType record)
+  static const uint8_t tiny[16] = {4, 0, 0, 0, 0, 0, 0, 0, 0x08, 0x04, 0x10, 0x00};
+  EW_CHECK(c->hbuf_dev.ensure(64));
+  EW_CHECK(hipMemcpyAsync(c->hbuf_dev.p, tiny, sizeof(tiny), hipMemcpyHostToDevice, c->stream));
+  ewal_result r;
+  rc = readall_impl(c, c->hbuf_dev.as<uint8_t>(), 12, 0, &r);
+  c->last_k = 0;
+  EW_CHECK(hipStreamSynchronize(c->stream));
+  return rc < 0 ? rc : EWAL_OK;
 }
 
 int ewal_readall_device(ewal_ctx *c, const void *d_buf, uint64_t len, uint64_t ri, ewal_result *out) {

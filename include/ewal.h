@@ -120,6 +120,13 @@ int ewal_ctx_create(int device, ewal_ctx **out);
 void ewal_ctx_destroy(ewal_ctx *ctx);
 /* Run on a caller-owned hipStream_t (NULL = the ctx's own stream). */
 int ewal_ctx_set_stream(ewal_ctx *ctx, void *hip_stream);
+/* Pre-size ctx's workspace for a ReadAll over up to wal_bytes and load the
+ * device code, so that the first ReadAll (the one-shot restart,
+ * etcdserver/server.go:153-156) allocates nothing.  A server calls it while
+ * it reads the WAL files from disk: OpenAtIndex's directory listing gives
+ * their total size first.  Optional: without it the first call sizes the
+ * workspace itself. */
+int ewal_ctx_reserve(ewal_ctx *ctx, uint64_t wal_bytes);
 const char *ewal_status_string(int status);
 /* Device time (ms) of the last pipeline call on this ctx (HIP events). */
 float ewal_last_device_ms(ewal_ctx *ctx);
