@@ -82,6 +82,14 @@ class EntryDesc(C.Structure):
                 ("type", C.c_int32), ("data_nil", C.c_int32)]
 
 
+class SaveRec(C.Structure):      # ewal_save_rec
+    _fields_ = [("kind", C.c_int32), ("etype", C.c_int32), ("a", C.c_uint64), ("b", C.c_uint64), ("c", C.c_uint64),
+                ("data_off", C.c_uint64), ("data_len", C.c_uint64), ("data_nil", C.c_int32), ("pad", C.c_int32)]
+
+
+SAVE_ENTRY, SAVE_STATE, SAVE_CUT = 2, 3, 4
+
+
 class UnrecDesc(C.Structure):    # ewal_unrec
     _fields_ = [("ent", C.c_int64), ("off", C.c_uint64), ("len", C.c_uint64)]
 
@@ -152,6 +160,8 @@ _SIGS = {
                                    C.POINTER(C.c_int64)]),
     "ewal_encode_entries_device": (C.c_int, [vp, vp, C.c_uint64, vp, C.c_uint64, C.c_uint32, vp, C.c_uint64,
                                              C.POINTER(C.c_uint64), C.POINTER(C.c_uint32)]),
+    "ewal_save_device": (C.c_int, [vp, vp, C.c_uint64, vp, C.c_uint64, C.c_uint32, vp, C.c_uint64,
+                                   C.POINTER(C.c_uint64), C.POINTER(C.c_uint32), vp]),
     "ewal_crc32_update_device": (C.c_int, [vp, C.c_uint32, C.c_uint32, vp, C.c_uint64, C.POINTER(C.c_uint32)]),
     "ewal_crc32_update_host": (C.c_uint32, [C.c_uint32, C.c_uint32, C.c_char_p, C.c_uint64]),
     "ewal_crc32_combine": (C.c_uint32, [C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint64]),

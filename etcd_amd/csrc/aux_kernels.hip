@@ -301,3 +301,164 @@ __global__ __launch_bounds__(256) void k_enc_frame(const uint8_t *__restrict__ e
     wave_copy(dst + o, es + xoff[i], L, es, es_len);
   }
 }
+
+// ===========================================================================
+// Batched WAL writes: Save (SaveState + SaveEntry, wal/wal.go:248-279) and Cut
+// (wal/wal.go:219-238: a crcType record carrying the running CRC, then the
+// metadata record) as ONE chained call.  Every save record contributes one
+// contiguous chunk to the data-only stream (Entry / HardState marshal, the
+// Cut's metadata bytes; a crcType record adds nothing: Data is nil), so ONE
+// stream pass gives every chained CRC as in k_enc_*:
+//   crc after the chunk ending at x = ~(P'(x) ^ (x < 4 ? R0 >> 8x : 0)),
+// P' over the stream whose first min(4, E) bytes are XORed with R0 = ~prev
+// (a reflected register started at R0 over k < 4 bytes equals one started at
+// 0 over the XORed bytes, then XORed with R0 >> 8k).
+// ===========================================================================
+__device__ __forceinline__ uint32_t hardstate_head(uint8_t *h, uint64_t term, uint64_t vote, uint64_t commit) {
+  uint32_t o = 0;
+  h[o++] = 0x08; o += put_varint_dev(h + o, term);
+  h[o++] = 0x10; o += put_varint_dev(h + o, vote);
+  h[o++] = 0x18; o += put_varint_dev(h + o, commit);
+  return o;
+}
+
+// chunk size of save record i (0: no chunk -- an empty HardState writes
+// nothing, raft.IsEmptyHardState, wal/wal.go:266-268)
+__global__ void k_save_sizes(const ewal_save_rec *__restrict__ recs, uint64_t n, uint64_t data_len,
+                             uint64_t *__restrict__ esz, uint32_t *__restrict__ errflag) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const ewal_save_rec r = recs[i];
+  uint64_t z = 0;
+  const bool hasd = (r.kind == EWAL_SAVE_ENTRY || r.kind == EWAL_SAVE_CUT) && !(r.kind == EWAL_SAVE_CUT && r.data_nil);
+  if (hasd && (r.data_len > data_len || r.data_off > data_len - r.data_len)) atomicOr(errflag, 1u);
+  if (r.kind == EWAL_SAVE_ENTRY) {
+    z = 4 + sov64((uint64_t)(int64_t)r.etype) + sov64(r.a) + sov64(r.b) + sov64(r.data_len) + r.data_len;
+  } else if (r.kind == EWAL_SAVE_STATE) {
+    if (r.a | r.b | r.c) z = 3 + sov64(r.a) + sov64(r.b) + sov64(r.c);
+  } else if (r.kind == EWAL_SAVE_CUT) {
+    z = r.data_nil ? 0 : r.data_len;
+  } else {
+    atomicOr(errflag, 1u);
+  }
+  esz[i] = z;
+}
+
+// chunk i at xoff[i]; one wave per record (grid-stride)
+__global__ __launch_bounds__(256) void k_save_body(const uint8_t *__restrict__ data, uint64_t data_len,
+                                                   const ewal_save_rec *__restrict__ recs, uint64_t n,
+                                                   const uint64_t *__restrict__ xoff, uint8_t *__restrict__ es) {
+  const int lane = threadIdx.x & 63;
+  const uint64_t nw = (uint64_t)gridDim.x * (blockDim.x >> 6);
+  for (uint64_t i = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); i < n; i += nw) {
+    const ewal_save_rec r = recs[i];
+    uint8_t h[48];
+    uint32_t hl = 0;
+    uint64_t dl = 0;
+    if (r.kind == EWAL_SAVE_ENTRY) {
+      ewal_entry e;
+      e.type = r.etype; e.term = r.a; e.index = r.b; e.data_len = r.data_len;
+      hl = entry_head(h, e);
+      dl = r.data_len;
+    } else if (r.kind == EWAL_SAVE_STATE) {
+      if (r.a | r.b | r.c) hl = hardstate_head(h, r.a, r.b, r.c);
+    } else if (r.kind == EWAL_SAVE_CUT && !r.data_nil) {
+      dl = r.data_len;
+    }
+    uint8_t *o = es + xoff[i];
+    if ((uint32_t)lane < hl) {
+      uint8_t b = 0;
+#pragma unroll
+      for (int k = 0; k < 48; ++k) b = (k == lane) ? h[k] : b;
+      o[lane] = b;
+    }
+    if (dl) wave_copy(o + hl, data + r.data_off, dl, data, data_len);
+  }
+}
+
+// XOR the stream's first min(4, E) bytes with r (and back)
+__global__ void k_save_xor4(uint8_t *es, uint64_t E, uint32_t r) {
+  if (threadIdx.x < 4 && threadIdx.x < E) es[threadIdx.x] ^= (uint8_t)(r >> (8 * threadIdx.x));
+}
+
+__device__ __forceinline__ uint32_t save_crc_at(uint64_t x, uint32_t R0, uint64_t E, const uint32_t *pwave,
+                                                const uint32_t *v, const uint8_t *es, const uint32_t *t4,
+                                                const uint32_t *svp) {
+  const uint32_t p = (E && x) ? prefix_at(x, pwave, v, es, t4, svp) : 0u;
+  return ~(p ^ (x < 4 ? (R0 >> (8 * x)) : 0u));
+}
+
+// crc[i] = the running CRC after record i's chunk (its Record.Crc), pcrc[i]
+// = before it (a Cut's crcType record); fsz[i] = bytes of record i's frames
+__global__ __launch_bounds__(256) void k_save_crc(const uint8_t *__restrict__ es, uint64_t E,
+                                                  const ewal_save_rec *__restrict__ recs,
+                                                  const uint64_t *__restrict__ xoff, const uint64_t *__restrict__ esz,
+                                                  uint64_t n, uint32_t R0, const uint32_t *__restrict__ pwave,
+                                                  const uint32_t *__restrict__ v, const uint32_t *__restrict__ g_slice,
+                                                  const uint32_t *__restrict__ g_shift, uint32_t *__restrict__ crc,
+                                                  uint32_t *__restrict__ pcrc, uint64_t *__restrict__ fsz) {
+  __shared__ uint32_t s_t4[1024];
+  __shared__ uint32_t s_svp[1024];
+  stage_lds<256>(s_t4, 1024, [&](int i) { return g_slice[i]; });
+  stage_lds<256>(s_svp, 1024, [&](int i) { return g_shift[EW_VLOG * 1024 + i]; });
+  __syncthreads();
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const ewal_save_rec r = recs[i];
+  const uint64_t L = esz[i];
+  const uint32_t c = save_crc_at(xoff[i] + L, R0, E, pwave, v, es, s_t4, s_svp);
+  crc[i] = c;
+  uint64_t f = 0;
+  if (r.kind == EWAL_SAVE_ENTRY || (r.kind == EWAL_SAVE_STATE && L)) {
+    f = 8 + 1 + 1 + 1 + sov64(c) + 1 + sov64(L) + L;              // 08 t 10 v(c) 1a v(L) chunk
+  } else if (r.kind == EWAL_SAVE_CUT) {
+    const uint32_t c0 = save_crc_at(xoff[i], R0, E, pwave, v, es, s_t4, s_svp);
+    pcrc[i] = c0;
+    f = 8 + 1 + 1 + 1 + sov64(c0);                                 // crcType: 08 04 10 v(c0), Data nil
+    f += 8 + 1 + 1 + 1 + sov64(c) + (r.data_nil ? 0 : 1 + sov64(L) + L);   // metadataType
+  }
+  fsz[i] = f;
+}
+
+// one frame (int64 len || 08 t 10 v(c) [1a v(L) chunk]) at dst; one wave
+__device__ __forceinline__ void save_frame(uint8_t *dst, int32_t t, uint32_t c, bool hasd, const uint8_t *chunk,
+                                           uint64_t L, const uint8_t *es, uint64_t es_len) {
+  const int lane = threadIdx.x & 63;
+  uint8_t h[32];
+  uint32_t o = 8;
+  h[o++] = 0x08; h[o++] = (uint8_t)t;
+  h[o++] = 0x10; o += put_varint_dev(h + o, c);
+  if (hasd) { h[o++] = 0x1a; o += put_varint_dev(h + o, L); }
+  const uint64_t rec = (uint64_t)(o - 8) + (hasd ? L : 0);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) h[k] = (uint8_t)(rec >> (8 * k));
+  if ((uint32_t)lane < o) {
+    uint8_t b = 0;
+#pragma unroll
+    for (int k = 0; k < 32; ++k) b = (k == lane) ? h[k] : b;
+    dst[lane] = b;
+  }
+  if (hasd && L) wave_copy(dst + o, chunk, L, es, es_len);
+}
+
+__global__ __launch_bounds__(256) void k_save_frame(const uint8_t *__restrict__ es, uint64_t es_len,
+                                                    const ewal_save_rec *__restrict__ recs,
+                                                    const uint64_t *__restrict__ xoff, const uint64_t *__restrict__ esz,
+                                                    const uint32_t *__restrict__ crc, const uint32_t *__restrict__ pcrc,
+                                                    const uint64_t *__restrict__ foff, uint64_t n,
+                                                    uint8_t *__restrict__ out) {
+  const uint64_t nw = (uint64_t)gridDim.x * (blockDim.x >> 6);
+  for (uint64_t i = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); i < n; i += nw) {
+    const ewal_save_rec r = recs[i];
+    const uint64_t L = esz[i];
+    uint8_t *dst = out + foff[i];
+    if (r.kind == EWAL_SAVE_ENTRY || (r.kind == EWAL_SAVE_STATE && L)) {
+      save_frame(dst, r.kind == EWAL_SAVE_ENTRY ? 2 : 3, crc[i], true, es + xoff[i], L, es, es_len);
+    } else if (r.kind == EWAL_SAVE_CUT) {
+      const uint32_t c0 = pcrc[i];
+      save_frame(dst, 4, c0, false, nullptr, 0, es, es_len);
+      dst += 8 + 1 + 1 + 1 + sov64(c0);
+      save_frame(dst, 1, crc[i], !r.data_nil, es + xoff[i], L, es, es_len);
+    }
+  }
+}

@@ -76,12 +76,43 @@ struct DevBuf {
   }
 };
 
+// Grow-only pinned host buffer mapped into the device address space: small
+// per-call tables the kernels read and write in place (no DMA copies to queue
+// behind a caller's bulk transfers).
+struct HostBuf {
+  void *h = nullptr, *d = nullptr;
+  size_t cap = 0;
+  HostBuf() = default;
+  HostBuf(const HostBuf &) = delete;
+  HostBuf &operator=(const HostBuf &) = delete;
+  ~HostBuf() { release(); }
+  hipError_t ensure(size_t n) {
+    if (n <= cap) return hipSuccess;
+    release();
+    const size_t want = std::max<size_t>(n, 4096);
+    hipError_t e = hipHostMalloc(&h, want, hipHostMallocMapped);
+    if (e != hipSuccess) { h = nullptr; return e; }
+    e = hipHostGetDevicePointer(&d, h, 0);
+    if (e != hipSuccess) { release(); return e; }
+    cap = want;
+    return hipSuccess;
+  }
+  template <typename T> T *host() { return static_cast<T *>(h); }
+  template <typename T> T *dev() { return static_cast<T *>(d); }
+  void release() {
+    if (h) (void)hipHostFree(h);
+    h = d = nullptr;
+    cap = 0;
+  }
+};
+
 }  // namespace
 
 struct ewal_ctx {
   int device = 0;
   int num_cu = 256;
   int ablate = 0;      // EWAL_STREAM_ABLATE (timing experiments only; results are wrong)
+  uint32_t fc_ablate = 0;   // EWAL_FC_ABLATE (k_fc timing experiments only; results are wrong)
   int frame_wg = 3;    // k_frame resident workgroups per CU (EWAL_FRAME_WG: A/B timing)
   hipStream_t stream = nullptr;
   bool own_stream = false;
@@ -90,6 +121,7 @@ struct ewal_ctx {
   std::map<uint32_t, std::unique_ptr<ewal::CrcTables>> host_tables;
   DevBuf encw, encs, lbstat, gagg, slow, mlist, pf, v, pwave, ux, tagg, tpx, wcnt, slots, cbase, ovf, cpos, clen, nxt, exc, E, rs, jl, vis, entry, on, rec_cand, rd, opf, ops, kk, kkrev, suf,
       ents, recs, tmp, small, sdesc, snaps, hbuf_dev, xpos, walk, fpos, ulist, uitems, uarena, fstat, ftrec;
+  HostBuf hsdesc;                  // esnap_verify_packed's per-file table (host-mapped)
   std::vector<ewal_unrec> unrec;   // XXX_unrecognized of the last ReadAll's result (side list)
   uint64_t unrec_bytes = 0;
   // batched ReadAll (ewal_readall_batch_device): shard tables, results, ents
@@ -495,6 +527,7 @@ static int fused_pass(ewal_ctx *c, DevTables *tb, const uint8_t *d_buf, uint64_t
     a.ents = c->ents.as<ewal_entry>();
     a.mlist = c->mlist.as<uint32_t>();
     a.ds = ds;
+    a.ablate = c->fc_ablate;
     hipLaunchKernelGGL(k_fc<false>, dim3((unsigned)std::max(1, c->num_cu) * FC_WGS), dim3(FC_THREADS), 0, c->stream,
                        a, SegArgs{});
     hipLaunchKernelGGL(k_fc_seam<false>, dim3(grid_for(ntiles, 256)), dim3(256), 0, c->stream, d_buf, B, a.cpos,
@@ -1003,6 +1036,7 @@ static int fused_batch(ewal_ctx *c, DevTables *tb, const uint8_t *d_buf, uint64_
     a.ents = c->bents.as<ewal_entry>();
     a.mlist = c->mlist.as<uint32_t>();
     a.ds = ds;
+    a.ablate = c->fc_ablate;
     hipLaunchKernelGGL(k_shard_start_fc, dim3(grid_for(ns + 1, 256)), dim3(256), 0, c->stream, a.cpos, ccap,
                        c->bsoff.as<uint64_t>(), ns, c->bfs.as<uint32_t>(), sg.sagg, ds);
     hipLaunchKernelGGL(k_fc<true>, dim3((unsigned)std::max(1, c->num_cu) * FC_WGS), dim3(FC_THREADS), 0, c->stream, a,
@@ -1301,6 +1335,7 @@ int ewal_ctx_create(int device, ewal_ctx **out) {
   EW_CHECK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
   c->own_stream = true;
   if (const char *e = std::getenv("EWAL_STREAM_ABLATE")) c->ablate = std::atoi(e);
+  if (const char *e = std::getenv("EWAL_FC_ABLATE")) c->fc_ablate = (uint32_t)std::atoi(e);
   if (const char *e = std::getenv("EWAL_FRAME_WG")) c->frame_wg = std::max(1, std::min(16, std::atoi(e)));
   if (const char *e = std::getenv("EWAL_FUSED")) c->fused = std::atoi(e) != 0;
   EW_CHECK(hipEventCreate(&c->ev0));
@@ -1559,6 +1594,73 @@ int ewal_encode_entries_device(ewal_ctx *c, const void *d_data, uint64_t data_le
   return EWAL_OK;
 }
 
+int ewal_save_device(ewal_ctx *c, const void *d_data, uint64_t data_len_total, const ewal_save_rec *d_recs, uint64_t n,
+                     uint32_t prev_crc, void *d_out, uint64_t cap, uint64_t *out_len, uint32_t *last_crc,
+                     uint64_t *h_rec_off) {
+  if (!c || !out_len || !last_crc || (n && (!d_recs || !d_out)) || (data_len_total && !d_data)) return EWAL_E_INVAL;
+  *out_len = 0;
+  *last_crc = prev_crc;
+  if (n == 0) return EWAL_OK;
+  if (n >= 0x7fffffffull) return EWAL_E_INVAL;
+  EW_CHECK(hipSetDevice(c->device));
+  DevTables *tb;
+  int rc = get_tables(c, 0x82F63B78u, &tb);
+  if (rc) return rc;
+  EW_CHECK(c->small.ensure(sizeof(Small)));
+  Small *ds = c->small.as<Small>();
+  EW_CHECK(hipMemsetAsync(&ds->errflag, 0, 4, c->stream));
+  // per-record scratch: esz, xoff, fsz, foff (u64) + crc, pcrc (u32)
+  EW_CHECK(c->encw.ensure((size_t)n * 40 + 64));
+  uint64_t *esz = c->encw.as<uint64_t>(), *xoff = esz + n, *fsz = xoff + n, *foff = fsz + n;
+  uint32_t *crc = (uint32_t *)(foff + n), *pcrc = crc + n;
+  hipLaunchKernelGGL(k_save_sizes, dim3(grid_for(n, 256)), dim3(256), 0, c->stream, d_recs, n, data_len_total, esz,
+                     &ds->errflag);
+  size_t tbytes = 0;
+  EW_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, tbytes, esz, xoff, (int)n, c->stream));
+  EW_CHECK(c->tmp.ensure(tbytes));
+  EW_CHECK(hipcub::DeviceScan::ExclusiveSum(c->tmp.p, tbytes, esz, xoff, (int)n, c->stream));
+  uint64_t tail[2];
+  uint32_t bad = 0;
+  EW_CHECK(hipMemcpyAsync(&tail[0], xoff + n - 1, 8, hipMemcpyDeviceToHost, c->stream));
+  EW_CHECK(hipMemcpyAsync(&tail[1], esz + n - 1, 8, hipMemcpyDeviceToHost, c->stream));
+  EW_CHECK(hipMemcpyAsync(&bad, &ds->errflag, 4, hipMemcpyDeviceToHost, c->stream));
+  EW_CHECK(hipStreamSynchronize(c->stream));
+  if (bad) return EWAL_E_INVAL;
+  const uint64_t E = tail[0] + tail[1];                 // bytes of the data-only stream
+  EW_CHECK(c->encs.ensure(E + 64));
+  uint8_t *es = c->encs.as<uint8_t>();
+  const unsigned wgrid = (unsigned)std::min<uint64_t>(grid_for(n, 4), (uint64_t)c->num_cu * 8);
+  const uint32_t R0 = ~prev_crc;
+  hipLaunchKernelGGL(k_save_body, dim3(wgrid), dim3(256), 0, c->stream, (const uint8_t *)d_data, data_len_total,
+                     d_recs, n, xoff, es);
+  if (E) {
+    hipLaunchKernelGGL(k_save_xor4, dim3(1), dim3(64), 0, c->stream, es, E, R0);
+    rc = run_stream(c, tb, es, E, 0, 0);
+    if (rc) return rc;
+  }
+  hipLaunchKernelGGL(k_save_crc, dim3(grid_for(n, 256)), dim3(256), 0, c->stream, es, E, d_recs, xoff, esz, n, R0,
+                     c->pwave.as<uint32_t>(), c->v.as<uint32_t>(), tb->slice, tb->shift, crc, pcrc, fsz);
+  if (E) hipLaunchKernelGGL(k_save_xor4, dim3(1), dim3(64), 0, c->stream, es, E, R0);   // the bytes back
+  EW_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, tbytes, fsz, foff, (int)n, c->stream));
+  EW_CHECK(c->tmp.ensure(tbytes));
+  EW_CHECK(hipcub::DeviceScan::ExclusiveSum(c->tmp.p, tbytes, fsz, foff, (int)n, c->stream));
+  uint32_t lc = 0;
+  EW_CHECK(hipMemcpyAsync(&tail[0], foff + n - 1, 8, hipMemcpyDeviceToHost, c->stream));
+  EW_CHECK(hipMemcpyAsync(&tail[1], fsz + n - 1, 8, hipMemcpyDeviceToHost, c->stream));
+  EW_CHECK(hipMemcpyAsync(&lc, crc + n - 1, 4, hipMemcpyDeviceToHost, c->stream));
+  if (h_rec_off) EW_CHECK(hipMemcpyAsync(h_rec_off, foff, (size_t)n * 8, hipMemcpyDeviceToHost, c->stream));
+  EW_CHECK(hipStreamSynchronize(c->stream));
+  const uint64_t total = tail[0] + tail[1];
+  if (total > cap) return EWAL_E_NOMEM;
+  hipLaunchKernelGGL(k_save_frame, dim3(wgrid), dim3(256), 0, c->stream, es, E, d_recs, xoff, esz, crc, pcrc, foff, n,
+                     (uint8_t *)d_out);
+  EW_CHECK(hipGetLastError());
+  EW_CHECK(hipStreamSynchronize(c->stream));
+  *out_len = total;
+  *last_crc = lc;
+  return EWAL_OK;
+}
+
 int ewal_crc32_update_device(ewal_ctx *c, uint32_t crc, uint32_t poly, const void *d_buf, uint64_t n, uint32_t *out) {
   if (!c || !out || (!d_buf && n)) return EWAL_E_INVAL;
   if (n == 0) { *out = crc; return EWAL_OK; }
@@ -1599,20 +1701,21 @@ int esnap_verify_packed(ewal_ctx *c, const void *d_buf, uint64_t buf_len, const 
     rc = run_stream(c, tb, (const uint8_t *)d_buf, buf_len, 0, 0);
     if (rc) return rc;
   }
-  std::vector<SnapDesc> h(n);
+  // the per-file table lives in host-mapped pinned memory: k_snap reads the
+  // extents and writes the verdicts in place
+  EW_CHECK(c->hsdesc.ensure((size_t)std::max<uint32_t>(n, 1) * sizeof(SnapDesc)));
+  SnapDesc *h = c->hsdesc.host<SnapDesc>();
   for (uint32_t i = 0; i < n; ++i) {
     std::memset(&h[i], 0, sizeof(SnapDesc));
     h[i].off = offs[i];
     h[i].len = lens[i];
   }
   if (n) {
-    EW_CHECK(c->sdesc.ensure((size_t)n * sizeof(SnapDesc)));
-    EW_CHECK(hipMemcpyAsync(c->sdesc.p, h.data(), (size_t)n * sizeof(SnapDesc), hipMemcpyHostToDevice, c->stream));
     EW_CHECK(c->snaps.ensure((size_t)n * sizeof(esnap_snapshot)));
     hipLaunchKernelGGL(k_snap, dim3(grid_for(n, 256)), dim3(256), 0, c->stream, (const uint8_t *)d_buf,
-                       c->pwave.as<uint32_t>(), c->v.as<uint32_t>(), tb->slice, tb->shift, c->sdesc.as<SnapDesc>(),
+                       c->pwave.as<uint32_t>(), c->v.as<uint32_t>(), tb->slice, tb->shift, c->hsdesc.dev<SnapDesc>(),
                        c->snaps.as<esnap_snapshot>(), n);
-    EW_CHECK(hipMemcpyAsync(h.data(), c->sdesc.p, (size_t)n * sizeof(SnapDesc), hipMemcpyDeviceToHost, c->stream));
+    EW_CHECK(hipGetLastError());
   }
   EW_CHECK(hipEventRecord(c->ev1, c->stream));
   EW_CHECK(hipStreamSynchronize(c->stream));

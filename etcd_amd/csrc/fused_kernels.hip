@@ -104,6 +104,8 @@ struct FcArgs {
   ewal_entry *ents;
   uint32_t *mlist;
   Small *ds;
+  uint32_t ablate;      // EWAL_FC_ABLATE timing experiments only (results are wrong): 1 shift, 2 prefixes,
+                        // 4 look-back, 8 ents stores
 };
 
 // walpb.Record's stored Crc from a canonical frame head at p (08 type 10
@@ -245,7 +247,8 @@ __global__ __launch_bounds__(FC_THREADS, FC_WGS) void k_fc(FcArgs a, SegArgs sg)
     RecDesc d;
     int64_t L = 0;
     uint32_t Pfo = 0, Pfd = 0;
-    const bool ok = decode_canon<FC_THREADS>(a.buf, a.B, p, a.pwave, a.v, s_t4, s_svp, s_win + tid, d, L, Pfo, Pfd);
+    const bool ok = decode_canon<FC_THREADS>(a.buf, a.B, p, a.pwave, a.v, s_t4, s_svp, s_win + tid, d, L, Pfo, Pfd,
+                                             (a.ablate & 2) != 0);
     const uint64_t s = p + 8 + (uint64_t)L;
     if (live && !ok) rare |= 1u;
     if (!ok) {   // not decoded (the pass is void): no field of it may address memory
@@ -299,8 +302,9 @@ __global__ __launch_bounds__(FC_THREADS, FC_WGS) void k_fc(FcArgs a, SegArgs sg)
         if (dlast) Pe = 0;   // the next tile's (k_fc_seam)
         uint32_t x = seed ^ 0xffffffffu ^ Pfd;
         uint64_t m = d.dlen;
-        for (int lvl = 0; m; ++lvl, m >>= 1)
-          if (m & 1) x = lvl < FC_NIB_LEVELS ? nib_apply(s_nib + lvl * 128, x) : gshift_pow2(a.g_shift, lvl, x);
+        if (!(a.ablate & 1))
+          for (int lvl = 0; m; ++lvl, m >>= 1)
+            if (m & 1) x = lvl < FC_NIB_LEVELS ? nib_apply(s_nib + lvl * 128, x) : gshift_pow2(a.g_shift, lvl, x);
         computed = x ^ Pe ^ 0xffffffffu;
       }
       chained = computed;
@@ -383,7 +387,7 @@ __global__ __launch_bounds__(FC_THREADS, FC_WGS) void k_fc(FcArgs a, SegArgs sg)
         if (ff == EW_NIL) ff = s_wfirstf[w];
         if (s_wlastf[w] != EW_NIL) lf = s_wlastf[w];
       }
-      const uint32_t base = lookback_count(a.status, t, cnt, a.epoch, &ds->errflag);
+      const uint32_t base = (a.ablate & 4) ? t * 64u : lookback_count(a.status, t, cnt, a.epoch, &ds->errflag);
       if (lane == 0) {
         // the tile's first op has its predecessor op (if any) before the tile:
         // k_fc_seam applies the gap rule to it once ents holds every op
@@ -455,7 +459,7 @@ __global__ __launch_bounds__(FC_THREADS, FC_WGS) void k_fc(FcArgs a, SegArgs sg)
       e.data_len = d.edlen;
       e.type = d.etype;
       e.data_nil = d.enil;
-      a.ents[j] = e;
+      if (!(a.ablate & 8)) a.ents[j] = e;
     }
   }
   // flags of every lane, then one atomic per wave

@@ -1428,7 +1428,7 @@ template <int WS>
 __device__ __forceinline__ bool decode_canon(const uint8_t *__restrict__ buf, uint64_t B, uint64_t p,
                                              const uint32_t *__restrict__ pwave, const uint32_t *__restrict__ v,
                                              const uint32_t *s_t4, const uint32_t *s_svp, uint32_t *w, RecDesc &d,
-                                             int64_t &L, uint32_t &Pfo, uint32_t &Pfd) {
+                                             int64_t &L, uint32_t &Pfo, uint32_t &Pfd, bool noprefix = false) {
   const uint64_t p16 = p & ~15ull;
   uint4 hq[5];
 #pragma unroll
@@ -1489,7 +1489,7 @@ __device__ __forceinline__ bool decode_canon(const uint8_t *__restrict__ buf, ui
     }
   }
   if (!ok) return false;
-  Pfo = prefix_finish16(pin, s_t4, s_svp);
+  Pfo = noprefix ? pin.pw : prefix_finish16(pin, s_t4, s_svp);
   if (d.type != 4 && d.dlen > 0) {    // P(data start): the header bytes after P(frame start)
     uint32_t c = Pfo;
     const int nh = ho - base;

@@ -432,6 +432,48 @@ def encode_entries_device(ctx: Context, entries, prev_crc: int = 0):
             b.free()
 
 
+def save_device(ctx: Context, ops, prev_crc: int = 0):
+    """A sequence of (*WAL).SaveState / SaveEntry / Cut calls encoded on the
+    GPU in one chained call (ewal_save_device; wal/wal.go:219-279).  ops:
+    ("entry", Entry) | ("state", HardState) | ("cut", metadata bytes or None).
+    Returns (frame bytes, the running CRC after the last op, the offset of
+    each op's first frame)."""
+    n = len(ops)
+    arr = (L.SaveRec * max(1, n))()
+    parts, off = [], 0
+    for i, (kind, x) in enumerate(ops):
+        r = arr[i]
+        if kind == "entry":
+            d = x.Data or b""
+            r.kind, r.etype, r.a, r.b = L.SAVE_ENTRY, x.Type, x.Term, x.Index
+        elif kind == "state":
+            d = b""
+            r.kind, r.a, r.b, r.c = L.SAVE_STATE, x.Term, x.Vote, x.Commit
+        elif kind == "cut":
+            d = x or b""
+            r.kind, r.data_nil = L.SAVE_CUT, int(x is None)
+        else:
+            raise ValueError(kind)
+        r.data_off, r.data_len = off, len(d)
+        parts.append(d)
+        off += len(d)
+    payload = b"".join(parts)
+    cap = len(payload) + 120 * n + 64
+    dd, dr, do = ctx.alloc(len(payload) + 64), ctx.alloc(C.sizeof(arr)), ctx.alloc(cap)
+    try:
+        if payload:
+            dd.upload(payload)
+        dr.upload(bytes(arr))
+        out_len, crc = C.c_uint64(), C.c_uint32()
+        offs = (C.c_uint64 * max(1, n))()
+        check(lib.ewal_save_device(ctx.handle, dd.ptr, len(payload), dr.ptr, n, prev_crc, do.ptr, cap,
+                                   C.byref(out_len), C.byref(crc), offs))
+        return (do.download(out_len.value) if out_len.value else b""), crc.value, list(offs[:n])
+    finally:
+        for b in (dd, dr, do):
+            b.free()
+
+
 def synth_wal(target_bytes, min_data=64, max_data=65536, seed=2, corrupt_record=-1):
     """Synthetic WAL (bench/test input); returns (bytearray, n_records)."""
     cap = target_bytes + max_data * 2 + (1 << 20)

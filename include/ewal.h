@@ -236,6 +236,35 @@ int ewal_encode_entries_device(ewal_ctx *ctx, const void *d_data, uint64_t data_
                                uint64_t n, uint32_t prev_crc, void *d_out, uint64_t cap, uint64_t *out_len,
                                uint32_t *last_crc);
 
+/* Batched WAL writes on the GPU: a sequence of (*WAL).SaveState / SaveEntry /
+ * Cut calls (wal/wal.go:219-279) encoded as ONE chained call.  Each record:
+ *   EWAL_SAVE_ENTRY  SaveEntry(&Entry{Type: etype, Term: a, Index: b, Data})
+ *   EWAL_SAVE_STATE  SaveState(&HardState{Term: a, Vote: b, Commit: c});
+ *                    an empty HardState writes nothing (wal/wal.go:266-268)
+ *   EWAL_SAVE_CUT    Cut's records: crcType{Crc: running CRC}, then
+ *                    metadataType{Data: w.md} (wal/wal.go:232-237); Data is
+ *                    the (data_off, data_len) bytes, or nil when data_nil
+ * Data lives in d_data; d_recs on the device.  The frames go to d_out (cap
+ * bytes): *out_len bytes, *last_crc the running CRC after the last record
+ * (prev_crc when nothing was written).  h_rec_off (nullable, host, n
+ * entries): the offset of each record's first frame in d_out -- a Cut's is
+ * where the next file (walName(seq+1, enti+1)) starts.  Byte-identical to
+ * the reference encoder (wal/encoder.go:25-37) over the same calls. */
+#define EWAL_SAVE_ENTRY 2
+#define EWAL_SAVE_STATE 3
+#define EWAL_SAVE_CUT 4
+typedef struct ewal_save_rec {
+  int32_t kind;
+  int32_t etype;
+  uint64_t a, b, c;
+  uint64_t data_off, data_len;
+  int32_t data_nil;
+  int32_t pad;
+} ewal_save_rec;
+int ewal_save_device(ewal_ctx *ctx, const void *d_data, uint64_t data_len_total, const ewal_save_rec *d_recs,
+                     uint64_t n, uint32_t prev_crc, void *d_out, uint64_t cap, uint64_t *out_len, uint32_t *last_crc,
+                     uint64_t *h_rec_off);
+
 /* ---- CRC primitives (pkg/crc, pkg/crc/crc.go:23-41) ---------------------- */
 /* crc32.Update(crc, MakeTable(poly), p) on a DEVICE buffer. */
 int ewal_crc32_update_device(ewal_ctx *ctx, uint32_t crc, uint32_t poly, const void *d_buf, uint64_t n,
