@@ -1,0 +1,142 @@
+/* readall_shim.c -- the cgo shim of INTEGRATION.md ("readAllGPU"), in C.
+ *
+ * What a Go maintainer's `wal.OpenAtIndex(dir, index).ReadAll()` drop-in does
+ * through the C ABI, step for step: create a context, reserve its workspace
+ * for the WAL's size while the files are read (ewal_ctx_reserve), select and
+ * read the files (ewal_open_at_index: wal/wal.go:108-159), ReadAll on the GPU
+ * (ewal_wal_readall: wal/wal.go:164-216), then map the status to the
+ * reference's sentinel / panic (the Go switch) and materialise the return
+ * values the way the shim does: raftpb.Entry structs whose Data are
+ * zero-copy views into the gathered WAL bytes, the metadata view, the
+ * HardState, w.enti and the encoder seed (lastCRC).
+ *
+ * Usage: readall_shim DIR INDEX      prints one JSON line: the sentinel, the
+ * result, a digest of ents (CRC-32C over each entry's (term, index, type,
+ * nil, len, Data), the oracle's or_ents_digest format) and the time of each
+ * step.  Exit 0 whenever the call completed (whatever the sentinel).
+ */
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+
+#include "ewal.h"
+
+/* raftpb.Entry as the shim materialises it (Go: {Type, Term, Index, Data []byte}) */
+typedef struct {
+  int32_t type;
+  uint64_t term, index;
+  const uint8_t *data;   /* NULL == nil; a view into the WAL bytes */
+  uint64_t len;
+} go_entry;
+
+static double now_ms(void) {
+  struct timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return ts.tv_sec * 1e3 + ts.tv_nsec / 1e6;
+}
+
+/* the Go switch of readAllGPU: status -> the reference's value */
+static const char *go_sentinel(int rc) {
+  switch (rc) {
+  case EWAL_OK: return "nil";
+  case EWAL_ERR_UNEXPECTED_EOF: return "io.ErrUnexpectedEOF";
+  case EWAL_ERR_RECORD_CRC: return "walpb.ErrCRCMismatch";
+  case EWAL_ERR_WAL_CRC: return "wal.ErrCRCMismatch";
+  case EWAL_ERR_METADATA_CONFLICT: return "wal.ErrMetadataConflict";
+  case EWAL_ERR_INDEX_NOT_FOUND: return "wal.ErrIndexNotFound";
+  case EWAL_ERR_WRONG_TYPE: return "proto.ErrWrongType";
+  case EWAL_ERR_UNEXPECTED_TYPE: return "unexpected block type";
+  case EWAL_ERR_FILE_NOT_FOUND: return "wal.ErrFileNotFound";
+  case EWAL_UNSUPPORTED_ENCODING: return "fallback: Go decoder";
+  default: return rc >= 32 ? "panic" : "infrastructure error";
+  }
+}
+
+static uint32_t ents_digest(const go_entry *e, int64_t n) {
+  uint32_t h = 0;
+  for (int64_t i = 0; i < n; i++) {
+    uint8_t hd[32];
+    const int32_t nil = e[i].data == NULL;
+    memcpy(hd, &e[i].term, 8);
+    memcpy(hd + 8, &e[i].index, 8);
+    memcpy(hd + 16, &e[i].type, 4);
+    memcpy(hd + 20, &nil, 4);
+    memcpy(hd + 24, &e[i].len, 8);
+    h = ewal_crc32_update_host(h, 0x82F63B78u, hd, 32);
+    if (e[i].len) h = ewal_crc32_update_host(h, 0x82F63B78u, e[i].data, e[i].len);
+  }
+  return h;
+}
+
+int main(int argc, char **argv) {
+  if (argc < 3) {
+    fprintf(stderr, "usage: %s DIR INDEX\n", argv[0]);
+    return 2;
+  }
+  const uint64_t index = strtoull(argv[2], NULL, 0);
+  const double t0 = now_ms();
+  ewal_ctx *ctx = NULL;
+  int rc = ewal_ctx_create(0, &ctx);
+  if (rc) {
+    printf("{\"ok\": false, \"stage\": \"ctx\", \"rc\": %d, \"status\": \"%s\"}\n", rc, ewal_status_string(rc));
+    return 0;
+  }
+  const double t1 = now_ms();
+  ewal_wal *w = NULL;
+  rc = ewal_open_at_index(argv[1], index, &w);            /* wal.OpenAtIndex: select + read the files */
+  const double t2 = now_ms();
+  if (rc) {
+    printf("{\"ok\": true, \"rc\": %d, \"sentinel\": \"%s\"}\n", rc, go_sentinel(rc));
+    ewal_ctx_destroy(ctx);
+    return 0;
+  }
+  uint64_t len = 0;
+  const uint8_t *buf = ewal_wal_bytes(w, &len);
+  rc = ewal_ctx_reserve(ctx, len);                          /* a server overlaps this with the file reads */
+  const double t3 = now_ms();
+  if (rc) {
+    printf("{\"ok\": false, \"stage\": \"reserve\", \"rc\": %d}\n", rc);
+    return 0;
+  }
+  ewal_result r;
+  rc = ewal_wal_readall(w, ctx, &r);                       /* (*WAL).ReadAll */
+  const double t4 = now_ms();
+  /* materialise the Go return values */
+  go_entry *ents = NULL;
+  int64_t n = 0;
+  uint64_t md_len = 0;
+  const uint8_t *md = NULL;
+  if (rc == EWAL_OK) {
+    if (r.metadata_off >= 0) { md = buf + r.metadata_off; md_len = (uint64_t)r.metadata_len; }
+    if (r.n_ents > 0) {
+      ewal_entry *ds = (ewal_entry *)malloc(sizeof(ewal_entry) * (size_t)r.n_ents);
+      n = ewal_copy_entries(ctx, ds, r.n_ents);
+      ents = (go_entry *)malloc(sizeof(go_entry) * (size_t)(n > 0 ? n : 1));
+      for (int64_t i = 0; i < n; i++) {
+        ents[i].type = ds[i].type;
+        ents[i].term = ds[i].term;
+        ents[i].index = ds[i].index;
+        ents[i].data = ds[i].data_nil ? NULL : buf + ds[i].data_off;   /* zero-copy view */
+        ents[i].len = ds[i].data_len;
+      }
+      free(ds);
+    }
+  }
+  const double t5 = now_ms();
+  const uint32_t dg = ents_digest(ents, n);
+  printf("{\"ok\": true, \"rc\": %d, \"sentinel\": \"%s\", \"status_string\": \"%s\", \"fail_record\": %lld, "
+         "\"n_records\": %lld, \"n_ents\": %lld, \"enti\": %llu, \"last_crc\": %u, \"has_state\": %d, "
+         "\"state\": [%llu, %llu, %llu], \"metadata_len\": %lld, \"ents_digest\": %u, \"wal_bytes\": %llu, "
+         "\"ms\": {\"ctx_create\": %.3f, \"open_at_index\": %.3f, \"reserve\": %.3f, \"readall\": %.3f, "
+         "\"materialise\": %.3f, \"total\": %.3f}, \"device_ms\": %.3f}\n",
+         rc, go_sentinel(rc), ewal_status_string(rc), (long long)r.fail_record, (long long)r.n_records,
+         (long long)n, (unsigned long long)r.enti, (unsigned)r.last_crc, r.has_state,
+         (unsigned long long)r.state_term, (unsigned long long)r.state_vote, (unsigned long long)r.state_commit,
+         md ? (long long)md_len : -1LL, dg, (unsigned long long)len, t1 - t0, t2 - t1, t3 - t2, t4 - t3, t5 - t4,
+         t5 - t0, r.device_ms);
+  free(ents);
+  ewal_wal_close(w);
+  ewal_ctx_destroy(ctx);
+  return 0;
+}

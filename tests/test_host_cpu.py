@@ -207,3 +207,19 @@ def test_message_writer_matches_oracle():
                 rng.randrange(1 << 30), rng.randrange(1 << 40))
         rej = rng.random() < 0.5
         assert M.message_marshal(*args, mine, 77, snap, rej) == O.message_marshal(*args, mine, 77, snap, rej)
+
+
+def test_shim_harness_links_and_fails_loudly_without_gpu():
+    """tests/shim/readall_shim (the cgo shim's call sequence in C) links
+    against libewal.so; without a GPU it reports EWAL_E_NODEVICE at context
+    creation -- no CPU fallback."""
+    import json
+    import subprocess
+    shim = os.path.join(os.path.dirname(os.path.abspath(__file__)), "shim", "readall_shim")
+    if not os.path.exists(shim):
+        pytest.skip("build() not run")
+    p = subprocess.run([shim, "/nonexistent", "0"], capture_output=True, text=True, timeout=60)
+    assert p.returncode == 0
+    out = json.loads(p.stdout.strip().splitlines()[-1])
+    if L.lib.ewal_device_count() == 0:
+        assert out["ok"] is False and out["rc"] == L.E_NODEVICE
