@@ -111,7 +111,8 @@ _SIGS = {
     "ewal_ctx_create": (C.c_int, [C.c_int, C.POINTER(vp)]),
     "ewal_ctx_destroy": (None, [vp]),
     "ewal_ctx_set_stream": (C.c_int, [vp, vp]),
-    "ewal_ctx_reserve": (C.c_int, [vp, C.c_uint64]),
+    "ewal_ctx_reserve": (C.c_int, [vp, C.c_uint64, C.c_uint32]),
+    "ewal_wal_size": (C.c_uint64, [vp]),
     "ewal_status_string": (C.c_char_p, [C.c_int]),
     "ewal_last_device_ms": (C.c_float, [vp]),
     "ewal_device_count": (C.c_int, []),

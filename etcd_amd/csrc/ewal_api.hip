@@ -23,6 +23,7 @@
 #include "aux_kernels.hip"
 #include "msg_kernels.hip"
 #include "fused_kernels.hip"
+#include "ewal_stage.h"
 
 #define EW_CHECK(x)                                                          \
   do {                                                                       \
@@ -1383,8 +1384,12 @@ int ewal_ctx_set_stream(ewal_ctx *c, void *s) {
   return EWAL_OK;
 }
 
-int ewal_ctx_reserve(ewal_ctx *c, uint64_t wal_bytes) {
+int ewal_ctx_reserve(ewal_ctx *c, uint64_t wal_bytes, uint32_t flags) {
   if (!c) return EWAL_E_INVAL;
+  if (flags & EWAL_RESERVE_HOST_STAGING) {   // the HBM copy of host bytes (ewal_readall_host / ewal_wal_readall)
+    EW_CHECK(hipSetDevice(c->device));
+    EW_CHECK(c->hbuf_dev.ensure(wal_bytes + 16));
+  }
   EW_CHECK(hipSetDevice(c->device));
   DevTables *tb;
   int rc = get_tables(c, 0x82F63B78u, &tb);
@@ -1473,6 +1478,23 @@ int ewal_stage_to_device(ewal_ctx *c, const void *h_buf, uint64_t len, void **d_
   EW_CHECK(hipStreamSynchronize(c->stream));
   *d_out = c->hbuf_dev.p;
   return EWAL_OK;
+}
+
+int ewal_stage_begin(ewal_ctx *c, uint64_t len) {
+  if (!c) return EWAL_E_INVAL;
+  EW_CHECK(hipSetDevice(c->device));
+  EW_CHECK(c->hbuf_dev.ensure(len + 16));
+  return EWAL_OK;
+}
+int ewal_stage_put(ewal_ctx *c, uint64_t off, const void *h, uint64_t n) {
+  if (!c || (n && !h) || off + n + 16 > c->hbuf_dev.cap) return EWAL_E_INVAL;
+  if (n) EW_CHECK(hipMemcpyAsync(c->hbuf_dev.as<uint8_t>() + off, h, n, hipMemcpyHostToDevice, c->stream));
+  return EWAL_OK;
+}
+int ewal_stage_readall(ewal_ctx *c, uint64_t len, uint64_t ri, ewal_result *out) {
+  if (!c || !out || len + 16 > c->hbuf_dev.cap) return EWAL_E_INVAL;
+  EW_CHECK(hipSetDevice(c->device));
+  return readall_impl(c, c->hbuf_dev.as<uint8_t>(), len, ri, out);
 }
 
 int ewal_readall_host(ewal_ctx *c, const void *h_buf, uint64_t len, uint64_t ri, ewal_result *out) {

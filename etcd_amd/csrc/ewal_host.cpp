@@ -8,6 +8,7 @@
 // rec.Crc = Sum32), with the SSE4.2 crc32 instruction like Go's amd64 path.
 #include <dirent.h>
 #include <fcntl.h>
+#include <sys/mman.h>
 #include <sys/stat.h>
 #include <unistd.h>
 #include <nmmintrin.h>
@@ -16,6 +17,7 @@
 #include <atomic>
 #include <cerrno>
 #include <cmath>
+#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -28,6 +30,7 @@
 
 #include "../../include/ewal.h"
 #include "crc_math.h"
+#include "ewal_stage.h"
 
 namespace {
 
@@ -190,12 +193,105 @@ bool read_file(const std::string &path, std::vector<uint8_t> *out, size_t pad) {
 }  // namespace
 
 // ===========================================================================
+// An opened WAL (wal.OpenAtIndex): the selected files names[nameIndex:]; their
+// bytes are read by ReadAll (as MultiReadCloser is, wal/wal.go:126-134) into
+// one host buffer -- the buffer ReadAll's ents are views into.
 struct ewal_wal {
   std::string dir;
   uint64_t ri = 0;
   uint64_t seq = 0;
-  std::vector<uint8_t> bytes;
+  std::vector<std::string> paths;
+  std::vector<uint64_t> sizes;
+  uint64_t total = 0;
+  uint8_t *bytes = nullptr;           // total bytes once loaded (anonymous mapping, huge pages advised)
+  size_t map_len = 0;
+  bool loaded = false;
+  ~ewal_wal() {
+    if (bytes) munmap(bytes, map_len);
+  }
 };
+
+namespace {
+
+// The files' bytes in pieces of at most kPiece bytes, read by a small pool of
+// threads (pread) in piece order; `ready` is called for every piece in
+// order as soon as it and all earlier ones are in the buffer (ReadAll
+// uploads them while the later ones are still being read).
+const uint64_t kPiece = 64ull << 20;
+template <class F>
+int load_pieces(ewal_wal *w, F ready) {
+  struct Piece { size_t file; uint64_t foff, off, len; };
+  std::vector<Piece> pcs;
+  uint64_t off = 0;
+  for (size_t f = 0; f < w->paths.size(); ++f)
+    for (uint64_t o = 0; o < w->sizes[f]; o += kPiece) {
+      const uint64_t l = std::min<uint64_t>(kPiece, w->sizes[f] - o);
+      pcs.push_back(Piece{f, o, off, l});
+      off += l;
+    }
+  if (!w->bytes) {
+    // one anonymous mapping in 2 MiB huge pages where the kernel allows:
+    // first-touch faults per 4 KiB page otherwise dominate the read
+    const size_t hp = 2u << 20;
+    w->map_len = (size_t)((std::max<uint64_t>(w->total, 1) + hp - 1) / hp * hp);
+    void *m = mmap(nullptr, w->map_len, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+    if (m == MAP_FAILED) {
+      w->map_len = 0;
+      return EWAL_E_NOMEM;
+    }
+    (void)madvise(m, w->map_len, MADV_HUGEPAGE);
+    w->bytes = (uint8_t *)m;
+  }
+  std::vector<int> fds(w->paths.size(), -1);
+  for (size_t f = 0; f < w->paths.size(); ++f) {
+    fds[f] = open(w->paths[f].c_str(), O_RDONLY);
+    if (fds[f] < 0) {
+      for (int fd : fds) if (fd >= 0) close(fd);
+      return EWAL_E_IO;
+    }
+  }
+  std::vector<std::atomic<int>> done(pcs.size());   // 0 pending, 1 read, -1 failed
+  for (auto &d : done) d.store(0);
+  std::atomic<size_t> next(0);
+  std::mutex mu;
+  std::condition_variable cv;
+  auto reader = [&]() {
+    for (;;) {
+      const size_t k = next.fetch_add(1);
+      if (k >= pcs.size()) break;
+      const Piece &p = pcs[k];
+      uint64_t got = 0;
+      while (got < p.len) {
+        const ssize_t r = pread(fds[p.file], w->bytes + p.off + got, (size_t)(p.len - got), (off_t)(p.foff + got));
+        if (r <= 0) break;
+        got += (uint64_t)r;
+      }
+      {
+        std::lock_guard<std::mutex> lk(mu);
+        done[k].store(got == p.len ? 1 : -1);
+      }
+      cv.notify_all();
+    }
+  };
+  const unsigned nth = (unsigned)std::max<size_t>(1, std::min<size_t>(pcs.size(), std::max(1u, std::min(16u, std::thread::hardware_concurrency()))));
+  std::vector<std::thread> th;
+  for (unsigned t = 0; t < nth; ++t) th.emplace_back(reader);
+  int rc = EWAL_OK;
+  for (size_t k = 0; k < pcs.size(); ++k) {
+    std::unique_lock<std::mutex> lk(mu);
+    cv.wait(lk, [&] { return done[k].load() != 0; });
+    lk.unlock();
+    if (done[k].load() < 0) { rc = EWAL_E_IO; break; }
+    if ((rc = ready(pcs[k].off, pcs[k].len)) != 0) break;
+  }
+  if (rc) next.store(pcs.size());   // stop handing out pieces
+  for (auto &t : th) t.join();
+  for (int fd : fds) close(fd);
+  if (rc == EWAL_OK) w->loaded = true;
+  return rc;
+}
+
+}  // namespace
 
 struct ewal_encoder {
   std::vector<uint8_t> buf;
@@ -304,11 +400,16 @@ int ewal_open_at_index(const char *dirpath, uint64_t index, ewal_wal **out) {
   auto *w = new ewal_wal();
   w->dir = dirpath;
   w->ri = index;
-  for (size_t k = (size_t)ni; k < names.size(); ++k) {
-    if (!read_file(std::string(dirpath) + "/" + names[k], &w->bytes, 0)) {
+  for (size_t k = (size_t)ni; k < names.size(); ++k) {   // os.Open of each file (wal/wal.go:126-133)
+    const std::string p = std::string(dirpath) + "/" + names[k];
+    struct stat st;
+    if (stat(p.c_str(), &st) != 0 || access(p.c_str(), R_OK) != 0) {
       delete w;
       return EWAL_E_IO;
     }
+    w->paths.push_back(p);
+    w->sizes.push_back((uint64_t)st.st_size);
+    w->total += (uint64_t)st.st_size;
   }
   uint64_t s, i;
   parse_wal_name(names.back(), &s, &i);
@@ -317,14 +418,33 @@ int ewal_open_at_index(const char *dirpath, uint64_t index, ewal_wal **out) {
   return EWAL_OK;
 }
 
+uint64_t ewal_wal_size(ewal_wal *w) { return w ? w->total : 0; }
+
+// (*WAL).ReadAll over the opened files: the files are read in 64 MiB pieces
+// by a few threads while every finished piece is already on its way to HBM
+// (ewal_stage_put, asynchronous on the ctx stream), then the device pipeline
+// runs on the staged bytes.
 int ewal_wal_readall(ewal_wal *w, ewal_ctx *ctx, ewal_result *out) {
-  if (!w) return EWAL_E_INVAL;
-  return ewal_readall_host(ctx, w->bytes.data(), w->bytes.size(), w->ri, out);
+  if (!w || !out) return EWAL_E_INVAL;
+  int rc = ewal_stage_begin(ctx, w->total);
+  if (rc) return rc;
+  if (w->loaded) {
+    rc = w->total ? ewal_stage_put(ctx, 0, w->bytes, w->total) : 0;
+  } else {
+    rc = load_pieces(w, [&](uint64_t off, uint64_t len) { return ewal_stage_put(ctx, off, w->bytes + off, len); });
+  }
+  if (rc) return rc;
+  return ewal_stage_readall(ctx, w->total, w->ri, out);
 }
 
 const uint8_t *ewal_wal_bytes(ewal_wal *w, uint64_t *len) {
-  if (len) *len = w->bytes.size();
-  return w->bytes.data();
+  if (!w) return nullptr;
+  if (!w->loaded && load_pieces(w, [](uint64_t, uint64_t) { return 0; }) != EWAL_OK) {
+    if (len) *len = 0;
+    return nullptr;
+  }
+  if (len) *len = w->total;
+  return w->bytes;
 }
 uint64_t ewal_wal_seq(ewal_wal *w) { return w->seq; }
 void ewal_wal_close(ewal_wal *w) { delete w; }

@@ -126,7 +126,8 @@ int ewal_ctx_set_stream(ewal_ctx *ctx, void *hip_stream);
  * it reads the WAL files from disk: OpenAtIndex's directory listing gives
  * their total size first.  Optional: without it the first call sizes the
  * workspace itself. */
-int ewal_ctx_reserve(ewal_ctx *ctx, uint64_t wal_bytes);
+#define EWAL_RESERVE_HOST_STAGING 1u   /* also the HBM staging buffer of ewal_readall_host / ewal_wal_readall */
+int ewal_ctx_reserve(ewal_ctx *ctx, uint64_t wal_bytes, uint32_t flags);
 const char *ewal_status_string(int status);
 /* Device time (ms) of the last pipeline call on this ctx (HIP events). */
 float ewal_last_device_ms(ewal_ctx *ctx);
@@ -179,7 +180,9 @@ int64_t ewal_copy_unrec_bytes(ewal_ctx *ctx, uint8_t *out, int64_t cap);
 /* ---- directory-level API: wal.OpenAtIndex + ReadAll + writer ----------- */
 typedef struct ewal_wal ewal_wal;
 /* wal.OpenAtIndex(dirpath, index), wal/wal.go:108-159 (file selection:
- * wal/util.go:20-88).  Reads names[nameIndex:] into one buffer. */
+ * wal/util.go:20-88): selects and opens names[nameIndex:]; their bytes are
+ * read by ewal_wal_readall (pieces read by a few threads while the finished
+ * ones are already copied to HBM) or on demand by ewal_wal_bytes. */
 int ewal_open_at_index(const char *dirpath, uint64_t index, ewal_wal **out);
 /* The file-name helpers OpenAtIndex uses (host-only), wal/util.go:20-88:
  * parseWalName (1 = parsed), searchIndex over sorted names (the index, -1
@@ -189,6 +192,8 @@ int64_t ewal_search_index(const char *const *names, uint64_t n, uint64_t index);
 int ewal_is_valid_seq(const char *const *names, uint64_t n);
 void ewal_wal_name(uint64_t seq, uint64_t index, char *out);
 int ewal_wal_readall(ewal_wal *w, ewal_ctx *ctx, ewal_result *out);
+/* total bytes of the opened files (size ewal_ctx_reserve before ReadAll) */
+uint64_t ewal_wal_size(ewal_wal *w);
 const uint8_t *ewal_wal_bytes(ewal_wal *w, uint64_t *len);
 uint64_t ewal_wal_seq(ewal_wal *w);
 void ewal_wal_close(ewal_wal *w);

@@ -26,6 +26,9 @@ int esnap_verify_packed(ewal_ctx *, const void *, uint64_t, const uint64_t *, co
 }
 int esnap_copy_snapshot(ewal_ctx *, uint32_t, esnap_snapshot *) { return EWAL_E_NODEVICE; }
 int ewal_stage_to_device(ewal_ctx *, const void *, uint64_t, void **) { return EWAL_E_NODEVICE; }
+int ewal_stage_begin(ewal_ctx *, uint64_t) { return EWAL_E_NODEVICE; }
+int ewal_stage_put(ewal_ctx *, uint64_t, const void *, uint64_t) { return EWAL_E_NODEVICE; }
+int ewal_stage_readall(ewal_ctx *, uint64_t, uint64_t, ewal_result *) { return EWAL_E_NODEVICE; }
 }
 
 static int fails = 0;

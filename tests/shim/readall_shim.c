@@ -1,10 +1,11 @@
 /* readall_shim.c -- the cgo shim of INTEGRATION.md ("readAllGPU"), in C.
  *
  * What a Go maintainer's `wal.OpenAtIndex(dir, index).ReadAll()` drop-in does
- * through the C ABI, step for step: create a context, reserve its workspace
- * for the WAL's size while the files are read (ewal_ctx_reserve), select and
- * read the files (ewal_open_at_index: wal/wal.go:108-159), ReadAll on the GPU
- * (ewal_wal_readall: wal/wal.go:164-216), then map the status to the
+ * through the C ABI, step for step: create a context, select and open the
+ * files (ewal_open_at_index: wal/wal.go:108-159), reserve the workspace for
+ * their total size (ewal_ctx_reserve), ReadAll (ewal_wal_readall: the files
+ * read and copied to HBM piece by piece, then the device pipeline,
+ * wal/wal.go:164-216), then map the status to the
  * reference's sentinel / panic (the Go switch) and materialise the return
  * values the way the shim does: raftpb.Entry structs whose Data are
  * zero-copy views into the gathered WAL bytes, the metadata view, the
@@ -84,24 +85,24 @@ int main(int argc, char **argv) {
   }
   const double t1 = now_ms();
   ewal_wal *w = NULL;
-  rc = ewal_open_at_index(argv[1], index, &w);            /* wal.OpenAtIndex: select + read the files */
+  rc = ewal_open_at_index(argv[1], index, &w);            /* wal.OpenAtIndex: select + open the files */
   const double t2 = now_ms();
   if (rc) {
     printf("{\"ok\": true, \"rc\": %d, \"sentinel\": \"%s\"}\n", rc, go_sentinel(rc));
     ewal_ctx_destroy(ctx);
     return 0;
   }
-  uint64_t len = 0;
-  const uint8_t *buf = ewal_wal_bytes(w, &len);
-  rc = ewal_ctx_reserve(ctx, len);                          /* a server overlaps this with the file reads */
+  const uint64_t len = ewal_wal_size(w);
+  rc = ewal_ctx_reserve(ctx, len, EWAL_RESERVE_HOST_STAGING);   /* sized from the directory listing */
   const double t3 = now_ms();
   if (rc) {
     printf("{\"ok\": false, \"stage\": \"reserve\", \"rc\": %d}\n", rc);
     return 0;
   }
   ewal_result r;
-  rc = ewal_wal_readall(w, ctx, &r);                       /* (*WAL).ReadAll */
+  rc = ewal_wal_readall(w, ctx, &r);                       /* (*WAL).ReadAll: read the files + HBM + verify */
   const double t4 = now_ms();
+  const uint8_t *buf = ewal_wal_bytes(w, NULL);             /* the bytes ents are views into */
   /* materialise the Go return values */
   go_entry *ents = NULL;
   int64_t n = 0;

@@ -28,7 +28,7 @@ for name in ("first ctx, first call", "first ctx, 2nd call"):
 for i in range(2):
     c2 = W.Context(0)
     if i == 1 and hasattr(L.lib, "ewal_ctx_reserve"):
-        t = time.perf_counter(); L.lib.ewal_ctx_reserve(c2.handle, nb); print("reserve ms", round((time.perf_counter() - t) * 1e3, 3))
+        t = time.perf_counter(); L.lib.ewal_ctx_reserve(c2.handle, nb, 0); print("reserve ms", round((time.perf_counter() - t) * 1e3, 3))
     r = L.Result()
     t = time.perf_counter(); L.lib.ewal_readall_device(c2.handle, d.ptr, nb, 1, C.byref(r)); dt = time.perf_counter() - t
     print("fresh ctx%s, first call ms" % (" (reserved)" if i else ""), round(dt * 1e3, 3), "device_ms", round(r.device_ms, 3))
