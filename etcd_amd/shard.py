@@ -8,6 +8,9 @@ independently.  What crosses ranks is small:
 * `combine`   -- one all-reduce of {MIN first-corrupt key, SUM frames, SUM
   failing shards}; key = shard << 40 | frame, so the minimum names the first
   corrupt record of the lowest failing shard.
+* `split_verdict` -- ONE WAL split across ranks by file: ReadAll's verdict
+  (first failure, its global frame ordinal) from the per-range results,
+  with the crc seam and metadata rules across ranges (one all-gather).
 * `seam_check` -- for ONE WAL whose files were verified on different ranks:
   the only cross-file rule of ReadAll (wal/wal.go:184-192): file k+1's leading
   crcType record must carry file k's final running CRC whenever that CRC is
@@ -97,3 +100,59 @@ def seam_check(dist, world: int, rank: int, first_crc_record: int, last_crc: int
         if stored >= 0 and running != 0 and stored != running:
             return k
     return -1
+
+
+# ---- one WAL split across ranks by file -------------------------------------
+# Status numbers of the verdict (include/ewal.h)
+_OK, _UNEXPECTED_EOF, _WAL_CRC, _META_CONFLICT, _INDEX_NOT_FOUND = 0, 2, 4, 5, 6
+NIL = -2        # a metadata record whose Data is nil
+NONE = -1       # no metadata record in the range
+
+
+def split_verdict(dist, world: int, rank: int, status: int, fail_record: int, n_records: int, last_crc: int,
+                  first_crc_record: int, md_first: int, md_first_frame: int, md_last: int, device="cpu"):
+    """ReadAll's verdict for ONE WAL whose files were split into contiguous
+    ranges, range r verified by rank r (each range starts at a file boundary:
+    a crcType record carrying the running CRC, wal/wal.go:93,232-234).  Every
+    rank passes its own ReadAll result over its range (with w.ri = the first
+    entry index of its range, from the first file's name) plus:
+    first_crc_record (the Crc of the range's leading crcType record, -1 if it
+    does not start with one), md_first / md_first_frame (a digest of the
+    range's first metadata record's Data, NIL for nil Data, NONE when the
+    range has none; its frame ordinal in the range) and md_last (the digest
+    of the metadata value after the range, as ReadAll returns it).
+
+    One all-gather of 8 words per rank; every rank then walks the ranges in
+    file order applying ReadAll's two cross-file rules -- the crc seam
+    (wal/wal.go:184-192: running != 0 and stored != running ->
+    wal.ErrCRCMismatch) and the metadata rule (wal/wal.go:178-183: metadata !=
+    nil and not DeepEqual -> ErrMetadataConflict) -- before each range's own
+    first failure.  Returns (status, global frame ordinal of the first
+    failure or -1, frames verified, resplit); a range's ErrIndexNotFound (no
+    entry at or after its first file's index) is not a failure of the split
+    verify.  resplit = k >= 0 when range k (not the last) ends in a torn frame
+    (io.ErrUnexpectedEOF at its end): the reference reads on across the file
+    boundary (MultiReadCloser), so that frame's verdict depends on the next
+    range's bytes -- the caller verifies ranges k.. joined as one range and
+    calls again (status is then not final)."""
+    mine = torch.tensor([status, fail_record, n_records, last_crc, first_crc_record, md_first, md_first_frame,
+                         md_last], dtype=torch.int64, device=device)
+    allv = [torch.zeros(8, dtype=torch.int64, device=device) for _ in range(world)]
+    dist.all_gather(allv, mine)
+    rows = [[int(x) for x in v.tolist()] for v in allv]
+    before, running, md = 0, 0, NONE
+    for k, (st, fr, n, lc, fc, mf, mff, ml) in enumerate(rows):
+        own = fr if st not in (_OK, _INDEX_NOT_FOUND) else None
+        if k > 0 and fc >= 0 and running != 0 and fc != running:
+            return _WAL_CRC, before, before, -1
+        if k > 0 and md not in (NONE, NIL) and mf != NONE and mf != md and (own is None or mff < own):
+            return _META_CONFLICT, before + mff, before + mff, -1
+        if own is not None:
+            if st == _UNEXPECTED_EOF and k < world - 1 and fr == n:
+                return st, before + own, before + own, k
+            return st, before + own, before + own, -1
+        before += n
+        running = lc
+        if ml != NONE:
+            md = ml
+    return _OK, -1, before, -1
