@@ -121,7 +121,7 @@ struct ewal_ctx {
   std::map<uint32_t, DevTables> tables;
   std::map<uint32_t, std::unique_ptr<ewal::CrcTables>> host_tables;
   DevBuf encw, encs, lbstat, gagg, slow, mlist, pf, v, pwave, ux, tagg, tpx, wcnt, slots, cbase, ovf, cpos, clen, nxt, exc, E, rs, jl, vis, entry, on, rec_cand, rd, opf, ops, kk, kkrev, suf,
-      ents, recs, tmp, small, sdesc, snaps, hbuf_dev, xpos, walk, fpos, ulist, uitems, uarena, fstat, ftrec;
+      ents, recs, tmp, small, sdesc, snaps, hbuf_dev, xpos, walk, fpos, ulist, uitems, uarena, ftrec;
   HostBuf hsdesc;                  // esnap_verify_packed's per-file table (host-mapped)
   std::vector<ewal_unrec> unrec;   // XXX_unrecognized of the last ReadAll's result (side list)
   uint64_t unrec_bytes = 0;
@@ -139,7 +139,6 @@ struct ewal_ctx {
   uint64_t last_n = 0, last_nents = 0;
   uint64_t last_k = 0;     // candidates of the previous call (sizes k_frame's descriptors)
   uint32_t epoch = 0;      // k_check look-back epoch (24 bits)
-  uint32_t fepoch = 0;     // k_fc look-back epoch (24 bits)
   int fused = 1;           // the fused frame + check pass first (EWAL_FUSED=0: the general path only)
   bool rd_valid = false;   // c->rd holds the last call's per-frame descriptors
   const uint8_t *last_buf = nullptr;   // the last ReadAll's stream (materialise_records)
@@ -500,17 +499,10 @@ static int fused_pass(ewal_ctx *c, DevTables *tb, const uint8_t *d_buf, uint64_t
   Small *ds = c->small.as<Small>();
   *done = false;
   const uint64_t ntiles = ccap / FC_THREADS + 2;
-  const size_t had = c->fstat.cap;
-  EW_CHECK(c->fstat.ensure((size_t)ntiles * 8));
   EW_CHECK(c->ftrec.ensure((size_t)ntiles * sizeof(TileRec)));
   for (int pass = 0; pass < 2; ++pass) {
     EW_CHECK(c->ents.ensure((size_t)ecap * sizeof(ewal_entry)));
     EW_CHECK(c->mlist.ensure((size_t)ecap * 4));
-    c->fepoch = (c->fepoch + 1) & 0xffffffu;
-    if (c->fstat.cap != had || c->fepoch == 0 || pass) {
-      EW_CHECK(hipMemsetAsync(c->fstat.p, 0, c->fstat.cap, c->stream));
-      if (c->fepoch == 0) c->fepoch = 1;
-    }
     FcArgs a;
     a.buf = d_buf;
     a.B = B;
@@ -522,9 +514,7 @@ static int fused_pass(ewal_ctx *c, DevTables *tb, const uint8_t *d_buf, uint64_t
     a.g_slice = tb->slice;
     a.g_shift = tb->shift;
     a.ri = ri;
-    a.status = c->fstat.as<unsigned long long>();
     a.trec = c->ftrec.as<TileRec>();
-    a.epoch = c->fepoch;
     a.ents = c->ents.as<ewal_entry>();
     a.mlist = c->mlist.as<uint32_t>();
     a.ds = ds;
@@ -994,8 +984,6 @@ static int fused_batch(ewal_ctx *c, DevTables *tb, const uint8_t *d_buf, uint64_
   Small *ds = c->small.as<Small>();
   *done = false;
   const uint64_t ntiles = ccap / FC_THREADS + 2;
-  const size_t had = c->fstat.cap;
-  EW_CHECK(c->fstat.ensure((size_t)ntiles * 8));
   EW_CHECK(c->ftrec.ensure((size_t)ntiles * sizeof(TileRec)));
   EW_CHECK(c->bsoff.ensure((size_t)(ns + 1) * 8));
   EW_CHECK(c->bri.ensure((size_t)ns * 8));
@@ -1015,11 +1003,6 @@ static int fused_batch(ewal_ctx *c, DevTables *tb, const uint8_t *d_buf, uint64_
   for (int pass = 0; pass < 2; ++pass) {
     EW_CHECK(grow_keep(c->bents, (size_t)ecap * sizeof(ewal_entry), 0, c->stream));
     EW_CHECK(c->mlist.ensure((size_t)ecap * 4));
-    c->fepoch = (c->fepoch + 1) & 0xffffffu;
-    if (c->fstat.cap != had || c->fepoch == 0 || pass) {
-      EW_CHECK(hipMemsetAsync(c->fstat.p, 0, c->fstat.cap, c->stream));
-      if (c->fepoch == 0) c->fepoch = 1;
-    }
     FcArgs a;
     a.buf = d_buf;
     a.B = B;
@@ -1031,9 +1014,7 @@ static int fused_batch(ewal_ctx *c, DevTables *tb, const uint8_t *d_buf, uint64_
     a.g_slice = tb->slice;
     a.g_shift = tb->shift;
     a.ri = 0;
-    a.status = c->fstat.as<unsigned long long>();
     a.trec = c->ftrec.as<TileRec>();
-    a.epoch = c->fepoch;
     a.ents = c->bents.as<ewal_entry>();
     a.mlist = c->mlist.as<uint32_t>();
     a.ds = ds;
@@ -1401,10 +1382,7 @@ int ewal_ctx_reserve(ewal_ctx *c, uint64_t wal_bytes, uint32_t flags) {
   // the fused pass: look-back words, tile records, ents / mlist for the
   // first call's descriptor capacity (readall_impl's rdcap)
   const uint64_t ntiles = ccap / FC_THREADS + 2;
-  const size_t had = c->fstat.cap;
-  EW_CHECK(c->fstat.ensure((size_t)ntiles * 8));
   EW_CHECK(c->ftrec.ensure((size_t)ntiles * sizeof(TileRec)));
-  if (c->fstat.cap != had) EW_CHECK(hipMemsetAsync(c->fstat.p, 0, c->fstat.cap, c->stream));
   const uint64_t ecap = std::min<uint64_t>(ccap, B / 4096 + 1024);
   EW_CHECK(c->ents.ensure((size_t)ecap * sizeof(ewal_entry)));
   EW_CHECK(c->mlist.ensure((size_t)ecap * 4));

@@ -20,11 +20,14 @@
 // blockIdx.x + i * gridDim.x.  Within a tile the predecessor's stored CRC and
 // the successor's prefix come from the neighbouring lane (wave shuffles, LDS
 // across waves); the tile's first frame re-reads its predecessor's head, its
-// last frame computes its own data-end prefix.  Entry ops are numbered by a
-// decoupled look-back over the tiles' op counts (relaxed atomics on one word
-// per tile, like k_check's); the index-gap rule for a tile's FIRST op, whose
-// predecessor op lives in an earlier tile, is applied by k_fc_seam once every
-// op is in ents (ents[j - 1].Index is op j's predecessor).
+// last frame computes its own data-end prefix.  Entry ops need no global
+// numbering: in the regular case (no index gap -- a panic -- and no rewind --
+// the general path) op k of a WAL has Index - ri == k, so each op goes
+// straight to ents[Index - ri] (batched: the shard's region starts at its
+// first frame, fs[s], and never holds more ops than the shard has frames).
+// The index-gap rule for a tile's FIRST op, whose predecessor op lives in an
+// earlier tile, is applied by k_fc_seam from the tiles' records (the nearest
+// earlier tile with ops holds the predecessor's Index).
 #include "ewal_device.h"
 #include "ewal_internal.h"
 
@@ -32,12 +35,13 @@
 #define FC_WAVES (FC_THREADS / 64)
 #define FC_WGS 3          // resident workgroups per CU (LDS ~49 KiB each)
 
-// Per tile, for k_fc_seam: its op count and base, the frame of its first op,
-// and whether that op's predecessor lies before the tile (the seam to check).
+// Per tile, for k_fc_seam: its entry ops (count, frames and Index of the
+// first / last), the edge frames' CRC operands.
 struct TileRec {
-  uint32_t count, base;
+  uint32_t count;
   uint32_t first_frame, last_frame;   // of its first / last op
-  uint32_t seam;       // 1: the first op's predecessor op (if any) lies before the tile
+  uint32_t seam;       // 1: k_fc_seam applies the gap rule to the tile's first op
+  uint64_t first_index, last_index;   // Index of its first / last op
   uint32_t lastcrc;    // the stored CRC of the tile's last frame (the next tile's first seed)
   uint32_t pfo0;       // P at the tile's first frame start (the previous tile's last P(data end))
   // the CRC checks k_fc leaves to k_fc_seam: [0] the tile's first frame
@@ -98,14 +102,12 @@ struct FcArgs {
   uint64_t ecap;        // capacity of ents / mlist
   const uint32_t *pwave, *v, *g_slice, *g_shift;
   uint64_t ri;          // w.ri (single WAL)
-  unsigned long long *status;   // per tile look-back word (lookback_count)
   TileRec *trec;
-  uint32_t epoch;
   ewal_entry *ents;
   uint32_t *mlist;
   Small *ds;
   uint32_t ablate;      // EWAL_FC_ABLATE timing experiments only (results are wrong): 1 shift, 2 prefixes,
-                        // 4 look-back, 8 ents stores
+                        // 4 look-back, 8 ents stores, 16 no failure reports
 };
 
 // walpb.Record's stored Crc from a canonical frame head at p (08 type 10
@@ -198,10 +200,11 @@ __global__ __launch_bounds__(FC_THREADS, FC_WGS) void k_fc(FcArgs a, SegArgs sg)
   __shared__ uint32_t s_nib[FC_NIB_LEVELS * 128];   // S_{2^0} .. S_{2^16}, nibble tables (the seed shift)
   __shared__ uint32_t s_win[20 * FC_THREADS];  // frame heads, transposed (bank = thread & 31)
   __shared__ uint32_t s_wcrc[FC_WAVES], s_wpfo[FC_WAVES], s_wo[FC_WAVES];
-  __shared__ uint64_t s_wlast[FC_WAVES];       // per wave: its last op's index ...
+  __shared__ uint64_t s_wlast[FC_WAVES];       // per wave: its last op's Index ...
   __shared__ uint32_t s_wlastf[FC_WAVES];      // ... and frame (EW_NIL: no op)
-  __shared__ uint32_t s_wfirstf[FC_WAVES];     // per wave: its first op's frame (EW_NIL: no op)
-  __shared__ uint32_t s_base, s_seam, s_ff, s_shr[2];
+  __shared__ uint32_t s_wfirstf[FC_WAVES];     // per wave: its first op's frame (EW_NIL: no op) ...
+  __shared__ uint64_t s_wfirst[FC_WAVES];      // ... and Index
+  __shared__ uint32_t s_shr[2];
   __shared__ uint32_t s_red[4];                // last entry + 1, last state + 1, ~first meta, last op + 1
   __shared__ unsigned long long s_fail;        // min (frame << 8 | status)
   Small *ds = a.ds;
@@ -333,6 +336,7 @@ __global__ __launch_bounds__(FC_THREADS, FC_WGS) void k_fc(FcArgs a, SegArgs sg)
         tr->dlen[1] = d.dlen;
       }
     }
+    if (a.ablate & 16) st = 0;   // timing only: no failure reports (keeps the ablations' verdict path alike)
     if (dfirst || dlast) st = 0;
     else if (live && r + 1 == K32) ds->fc.last_chained = chained;
     // entry ops (wal/wal.go:170-176): the op's predecessor in the wave, else
@@ -346,12 +350,14 @@ __global__ __launch_bounds__(FC_THREADS, FC_WGS) void k_fc(FcArgs a, SegArgs sg)
     const int pl = bsh ? 63 - __clzll((long long)bsh) : lane;
     const uint64_t fprev = __shfl(d.f1, pl);
     const int wl = mo ? 63 - __clzll((long long)mo) : 0;
-    const uint64_t wli = __shfl(d.f1, wl);
+    const int wf = mo ? __ffsll((long long)mo) - 1 : 0;
+    const uint64_t wli = __shfl(d.f1, wl), wfi = __shfl(d.f1, wf);
     if (lane == 0) {
       s_wo[wv] = (uint32_t)__popcll(mo);
       s_wlastf[wv] = mo ? rw0 + (uint32_t)wl : EW_NIL;
-      s_wfirstf[wv] = mo ? rw0 + (uint32_t)(__ffsll((long long)mo) - 1) : EW_NIL;
+      s_wfirstf[wv] = mo ? rw0 + (uint32_t)wf : EW_NIL;
       s_wlast[wv] = wli;
+      s_wfirst[wv] = wfi;
     }
     // reductions (one LDS atomic per wave and quantity)
     const unsigned long long mf = __ballot(live && st != 0), me = __ballot(live && d.type == 2),
@@ -379,63 +385,55 @@ __global__ __launch_bounds__(FC_THREADS, FC_WGS) void k_fc(FcArgs a, SegArgs sg)
       if (op) atomicMax(&A->lastop, r + 1u);
     }
     __syncthreads();
-    if (wv == 0) {   // the tile's op base (decoupled look-back over op counts)
-      uint32_t cnt = 0, ff = EW_NIL, lf = EW_NIL;
+    // the tile's first op: its predecessor op (if any) lies before the tile
+    // unless the tile opens the op's shard -- k_fc_seam decides that one
+    uint32_t ff = EW_NIL;
+    uint64_t ffi = 0;
+#pragma unroll
+    for (int w = 0; w < FC_WAVES; ++w)
+      if (ff == EW_NIL && s_wfirstf[w] != EW_NIL) { ff = s_wfirstf[w]; ffi = s_wfirst[w]; }
+    const bool tseam = ff != EW_NIL && (!SEG || sg.fs[shard_of(sg.fs, sg.ns, ff)] < r0);
+    if (tid == 0) {
+      uint32_t cnt = 0, lf = EW_NIL;
+      uint64_t lfi = 0;
 #pragma unroll
       for (int w = 0; w < FC_WAVES; ++w) {
         cnt += s_wo[w];
-        if (ff == EW_NIL) ff = s_wfirstf[w];
-        if (s_wlastf[w] != EW_NIL) lf = s_wlastf[w];
+        if (s_wlastf[w] != EW_NIL) { lf = s_wlastf[w]; lfi = s_wlast[w]; }
       }
-      const uint32_t base = (a.ablate & 4) ? t * 64u : lookback_count(a.status, t, cnt, a.epoch, &ds->errflag);
-      if (lane == 0) {
-        // the tile's first op has its predecessor op (if any) before the tile:
-        // k_fc_seam applies the gap rule to it once ents holds every op
-        uint32_t seam = 0;
-        if (cnt) {
-          if (SEG) seam = sg.fs[shard_of(sg.fs, sg.ns, ff)] < r0;
-          else seam = base > 0;
-        }
-        s_base = base;
-        s_seam = seam;
-        s_ff = ff;
-        TileRec *tr = a.trec + t;
-        tr->count = cnt;
-        tr->base = base;
-        tr->first_frame = ff;
-        tr->last_frame = lf;
-        tr->seam = seam;
-        if (t == ntiles - 1) ds->nsel3 = base + cnt;
-        if (!SEG) {
-          if (s_fail != ~0ull) atomicMax(&ds->fc.fail_inv, ~s_fail);
-          if (s_red[0]) atomicMax(&ds->fc.last_entry1, s_red[0]);
-          if (s_red[1]) atomicMax(&ds->fc.last_state1, s_red[1]);
-          if (s_red[2]) atomicMax(&ds->fc.meta_inv, ~(unsigned long long)(uint32_t)~s_red[2]);
-          if (s_red[3]) atomicMax(&ds->lastop, s_red[3]);
-        } else if (s_shr[0] == s_shr[1]) {
-          ShardAgg *A = sg.sagg + s_shr[0];
-          if (s_fail != ~0ull) atomicMin(&A->first_fail, s_fail);
-          if (s_red[0]) atomicMax(&A->last_entry, (long long)(s_red[0] - 1));
-          if (s_red[1]) atomicMax(&A->last_state, (long long)(s_red[1] - 1));
-          if (s_red[2]) atomicMin(&A->first_meta, (unsigned long long)(uint32_t)~s_red[2]);
-          if (s_red[3]) atomicMax(&A->lastop, s_red[3]);
-        }
+      TileRec *tr = a.trec + t;
+      tr->count = cnt;
+      tr->first_frame = ff;
+      tr->last_frame = lf;
+      tr->first_index = ffi;
+      tr->last_index = lfi;
+      tr->seam = tseam;
+      if (cnt) atomicAdd(&ds->nsel3, cnt);
+      if (!SEG) {
+        if (s_fail != ~0ull) atomicMax(&ds->fc.fail_inv, ~s_fail);
+        if (s_red[0]) atomicMax(&ds->fc.last_entry1, s_red[0]);
+        if (s_red[1]) atomicMax(&ds->fc.last_state1, s_red[1]);
+        if (s_red[2]) atomicMax(&ds->fc.meta_inv, ~(unsigned long long)(uint32_t)~s_red[2]);
+        if (s_red[3]) atomicMax(&ds->lastop, s_red[3]);
+      } else if (s_shr[0] == s_shr[1]) {
+        ShardAgg *A = sg.sagg + s_shr[0];
+        if (s_fail != ~0ull) atomicMin(&A->first_fail, s_fail);
+        if (s_red[0]) atomicMax(&A->last_entry, (long long)(s_red[0] - 1));
+        if (s_red[1]) atomicMax(&A->last_state, (long long)(s_red[1] - 1));
+        if (s_red[2]) atomicMin(&A->first_meta, (unsigned long long)(uint32_t)~s_red[2]);
+        if (s_red[3]) atomicMax(&A->lastop, s_red[3]);
       }
     }
-    __syncthreads();
     if (op) {
-      uint32_t j = s_base + (uint32_t)__popcll(below);
-#pragma unroll
-      for (int w = 0; w < FC_WAVES; ++w) j += (w < wv) ? s_wo[w] : 0u;
       uint64_t kp = fprev;
       uint32_t pf = bsh ? 0u : EW_NIL;         // the predecessor op: in the wave, or an earlier wave
       for (int w = wv - 1; w >= 0 && pf == EW_NIL; --w)
         if (s_wlastf[w] != EW_NIL) { pf = s_wlastf[w]; kp = s_wlast[w]; }
       const bool has = pf != EW_NIL && (bsh || pf >= lo);   // SEG: in this shard
       const uint64_t k = d.f1 - ri;
-      // no predecessor in the tile: this is the tile's first op (or a shard's
-      // first op inside it); decided here unless k_fc_seam owns it
-      const bool seam_op = !has && s_seam && r == s_ff;
+      // no predecessor in the tile and the op's shard began before the tile:
+      // the tile's first op, k_fc_seam's
+      const bool seam_op = !has && tseam && r == ff;
       if (!seam_op) {
         bool gap;
         if (has) {
@@ -444,7 +442,6 @@ __global__ __launch_bounds__(FC_THREADS, FC_WGS) void k_fc(FcArgs a, SegArgs sg)
           gap = k > kq && k - kq > 1;
         } else {
           gap = k > 0;
-          if (SEG) sg.sagg[sh].ent_first = j;  // the shard's first op
         }
         if (gap) {
           const int gs = st ? st : EWAL_PANIC_INDEX_GAP;
@@ -452,14 +449,18 @@ __global__ __launch_bounds__(FC_THREADS, FC_WGS) void k_fc(FcArgs a, SegArgs sg)
           else atomicMax(&ds->fc.fail_inv, ~(((unsigned long long)r << 8) | (uint32_t)gs));
         }
       }
-      ewal_entry e;
-      e.term = d.f0;
-      e.index = d.f1;
-      e.data_off = SEG ? d.edoff - sg.soff[sh] : d.edoff;
-      e.data_len = d.edlen;
-      e.type = d.etype;
-      e.data_nil = d.enil;
-      if (!(a.ablate & 8)) a.ents[j] = e;
+      // op k is ents[k] (the shard's region: [fs[s], fs[s + 1]))
+      const uint64_t room = SEG ? (uint64_t)(sg.fs[sh + 1] - lo) : a.ecap;
+      if (k < room) {
+        ewal_entry e;
+        e.term = d.f0;
+        e.index = d.f1;
+        e.data_off = SEG ? d.edoff - sg.soff[sh] : d.edoff;
+        e.data_len = d.edlen;
+        e.type = d.etype;
+        e.data_nil = d.enil;
+        if (!(a.ablate & 8)) a.ents[(SEG ? lo : 0u) + k] = e;
+      }
     }
   }
   // flags of every lane, then one atomic per wave
@@ -470,9 +471,11 @@ __global__ __launch_bounds__(FC_THREADS, FC_WGS) void k_fc(FcArgs a, SegArgs sg)
 }
 
 // The index-gap rule (wal/wal.go:173) for each tile's first op whose
-// predecessor op lies in an earlier tile: ents[j - 1] is op j's predecessor
-// (ops are numbered in frame order) -- in the same shard when an op of the
-// shard precedes the tile.  One thread per tile.
+// predecessor op lies in an earlier tile: the nearest earlier tile with ops
+// holds it (its last op's Index) -- in the same shard when that tile's last
+// op lies at or after the shard's first frame.  One thread per tile; the
+// edge frames' CRC checks k_fc left to it too.
+#define FC_SEAM_SCAN 4096   // tiles scanned back for the predecessor (beyond: the general path)
 template <bool SEG>
 __global__ void k_fc_seam(const uint8_t *__restrict__ buf, uint64_t B, const uint64_t *__restrict__ cpos,
                           const uint32_t *__restrict__ g_shift, const TileRec *__restrict__ trec,
@@ -501,33 +504,38 @@ __global__ void k_fc_seam(const uint8_t *__restrict__ buf, uint64_t B, const uin
     }
     if (!SEG && r + 1 == K) ds->fc.last_chained = chained;
   }
-  if (!tr.seam) return;
-  const uint32_t j = tr.base, f = tr.first_frame;
-  if (j >= ecap || f >= K) return;
+  if (!tr.seam || !tr.count) return;
+  const uint32_t f = tr.first_frame;
+  if (f >= K) return;
   uint64_t ri = ri_one;
-  uint32_t sh = 0;
-  bool has = j > 0;
+  uint32_t sh = 0, lo = 0;
   if (SEG) {
     sh = shard_of(sg.fs, sg.ns, f);
     ri = sg.ri[sh];
-    const uint32_t lo = sg.fs[sh];
-    has = false;
-    for (int64_t u = (int64_t)t - 1; u >= 0 && (uint64_t)(u + 1) * FC_THREADS > lo; --u) {
-      const TileRec q = trec[u];
-      if (!q.count) continue;
-      has = q.last_frame >= lo;   // the nearest earlier tile with ops holds op j - 1
-      break;
-    }
+    lo = sg.fs[sh];
   }
-  const uint64_t k = ents[j].index - ri;
+  bool has = false;
+  uint64_t pidx = 0;
+  uint32_t scanned = 0;
+  for (int64_t u = (int64_t)t - 1; u >= 0 && (uint64_t)(u + 1) * FC_THREADS > lo; --u) {
+    if (++scanned > FC_SEAM_SCAN) {   // a very long run of tiles without entries: the general path
+      atomicOr(&ds->fc.rare, 8u);
+      return;
+    }
+    const TileRec q = trec[u];
+    if (!q.count) continue;
+    has = !SEG || q.last_frame >= lo;
+    pidx = q.last_index;
+    break;
+  }
+  const uint64_t k = tr.first_index - ri;
   bool gap;
   if (has) {
-    const uint64_t kq = ents[j - 1].index - ri;
+    const uint64_t kq = pidx - ri;
     if (k <= kq) atomicOr(&ds->fc.rare, 2u);
     gap = k > kq && k - kq > 1;
   } else {
     gap = k > 0;
-    if (SEG) sg.sagg[sh].ent_first = j;
   }
   if (gap) {
     if (SEG) atomicMin(&sg.sagg[sh].first_fail, ((unsigned long long)f << 8) | EWAL_PANIC_INDEX_GAP);
@@ -728,7 +736,7 @@ __global__ __launch_bounds__(256) void k_result_batch_fc(const uint8_t *__restri
         o.state_commit = D[4].f2;
       }
       o.n_ents = A.lastop ? (int64_t)(D[5].f1 - ri + 1) : 0;
-      ef = o.n_ents ? A.ent_first : 0;
+      ef = o.n_ents ? f0 : 0;   // op k of the shard is bents[fs[s] + k]
     }
   }
   out[s] = o;

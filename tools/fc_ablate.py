@@ -1,6 +1,6 @@
 """k_fc ablation timing (diagnostic; results are wrong under ablation):
 pipeline device ms of one ReadAll / one batched ReadAll per EWAL_FC_ABLATE
-value (1 shift, 2 prefixes, 4 look-back, 8 ents stores)."""
+value (1 shift, 2 prefixes, 4 look-back, 8 ents stores, 16 no failure reports)."""
 import ctypes as C
 import os
 import sys
@@ -9,7 +9,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: F401,E402
 from etcd_amd import wal as W, _lib as L  # noqa: E402
 
-variants = [0, 1, 2, 4, 8, 15]
+variants = [int(x) for x in sys.argv[1].split(',')] if len(sys.argv) > 1 else [0, 16, 17, 18, 20, 24, 31]
 blob, lens, _ = W.synth_shards(list(range(128)), 64 << 20, 128, 4096)
 wal, _ = W.synth_wal(8 << 30, 64, 65536, seed=2)
 for name, data in (("shards128", blob), ("wal8g", wal)):
