@@ -690,7 +690,7 @@ def main():
     # the one-shot restart (etcdserver/server.go:153-156) in a cold process: ewal_ctx_reserve first (device
     # code load + workspace; a server runs it while it reads the WAL files), then the first ReadAll
     tf = time.perf_counter()
-    rc0 = L.lib.ewal_ctx_reserve(ctx.handle, nb)
+    rc0 = L.lib.ewal_ctx_reserve(ctx.handle, nb, 0)
     reserve_ms = (time.perf_counter() - tf) * 1e3
     assert rc0 == 0, rc0
     tf = time.perf_counter()
