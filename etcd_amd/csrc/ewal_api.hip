@@ -498,7 +498,7 @@ static int fused_pass(ewal_ctx *c, DevTables *tb, const uint8_t *d_buf, uint64_t
                       uint64_t ecap, bool *done) {
   Small *ds = c->small.as<Small>();
   *done = false;
-  const uint64_t ntiles = ccap / FC_THREADS + 2;
+  const uint64_t ntiles = ccap / FC_TILE + 2;
   EW_CHECK(c->ftrec.ensure((size_t)ntiles * sizeof(TileRec)));
   for (int pass = 0; pass < 2; ++pass) {
     EW_CHECK(c->ents.ensure((size_t)ecap * sizeof(ewal_entry)));
@@ -983,7 +983,7 @@ static int fused_batch(ewal_ctx *c, DevTables *tb, const uint8_t *d_buf, uint64_
                        ewal_result *out, bool *done) {
   Small *ds = c->small.as<Small>();
   *done = false;
-  const uint64_t ntiles = ccap / FC_THREADS + 2;
+  const uint64_t ntiles = ccap / FC_TILE + 2;
   EW_CHECK(c->ftrec.ensure((size_t)ntiles * sizeof(TileRec)));
   EW_CHECK(c->bsoff.ensure((size_t)(ns + 1) * 8));
   EW_CHECK(c->bri.ensure((size_t)ns * 8));
@@ -1381,7 +1381,7 @@ int ewal_ctx_reserve(ewal_ctx *c, uint64_t wal_bytes, uint32_t flags) {
   EW_CHECK(c->cpos.ensure(ccap * 8));
   // the fused pass: look-back words, tile records, ents / mlist for the
   // first call's descriptor capacity (readall_impl's rdcap)
-  const uint64_t ntiles = ccap / FC_THREADS + 2;
+  const uint64_t ntiles = ccap / FC_TILE + 2;
   EW_CHECK(c->ftrec.ensure((size_t)ntiles * sizeof(TileRec)));
   const uint64_t ecap = std::min<uint64_t>(ccap, B / 4096 + 1024);
   EW_CHECK(c->ents.ensure((size_t)ecap * sizeof(ewal_entry)));

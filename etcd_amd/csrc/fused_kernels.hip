@@ -15,12 +15,15 @@
 // and the host runs the general path (k_frame, k_decode_slow, k_check, the
 // op-list passes) over the same stream pass -- nothing is guessed.
 //
-// Frames are processed in tiles of FC_THREADS consecutive frames, one frame
-// per thread, by a persistent grid of FC_WGS workgroups per CU: tile t =
-// blockIdx.x + i * gridDim.x.  Within a tile the predecessor's stored CRC and
-// the successor's prefix come from the neighbouring lane (wave shuffles, LDS
-// across waves); the tile's first frame re-reads its predecessor's head, its
-// last frame computes its own data-end prefix.  Entry ops need no global
+// Frames are processed in tiles of FC_TILE = 64 consecutive frames, one
+// frame per lane, each tile by ONE wave: a persistent grid of FC_WGS
+// workgroups per CU shares the LDS tables, and every wave then runs its own
+// tiles (wave w: tiles w, w + all waves, ...) with no workgroup barrier, so
+// the waves hide each other's memory latency.  Within a tile the
+// predecessor's stored CRC and the successor's prefix come from the
+// neighbouring lane (wave shuffles); the tile's edge frames are checked by
+// k_fc_seam from the neighbouring tiles' records, which also folds the
+// tiles' reductions.  Entry ops need no global
 // numbering: in the regular case (no index gap -- a panic -- and no rewind --
 // the general path) op k of a WAL has Index - ri == k, so each op goes
 // straight to ents[Index - ri] (batched: the shard's region starts at its
@@ -34,6 +37,7 @@
 #define FC_THREADS 256
 #define FC_WAVES (FC_THREADS / 64)
 #define FC_WGS 3          // resident workgroups per CU (LDS ~49 KiB each)
+#define FC_TILE 64        // frames per tile: one wave's, no workgroup barrier in the frame loop
 
 // Per tile, for k_fc_seam: its entry ops (count, frames and Index of the
 // first / last), the edge frames' CRC operands.
@@ -51,6 +55,9 @@ struct TileRec {
   uint32_t crc[2], pfd[2], seed1, pe0;
   int32_t type[2];
   uint64_t dlen[2];
+  // the tile's reductions (single WAL; k_fc_seam folds them)
+  unsigned long long fail;        // min (frame << 8 | status), ~0: none
+  uint32_t last_entry1, last_state1, meta1, lastop1;   // 1 + frame (0: none); meta1: the first metadata frame
 };
 
 // decoder.decode's check + ReadAll's crc-record rule for one frame (k_check's
@@ -199,14 +206,6 @@ __global__ __launch_bounds__(FC_THREADS, FC_WGS) void k_fc(FcArgs a, SegArgs sg)
   __shared__ uint32_t s_svp[1024];             // S_256 (prefix Horner step)
   __shared__ uint32_t s_nib[FC_NIB_LEVELS * 128];   // S_{2^0} .. S_{2^16}, nibble tables (the seed shift)
   __shared__ uint32_t s_win[20 * FC_THREADS];  // frame heads, transposed (bank = thread & 31)
-  __shared__ uint32_t s_wcrc[FC_WAVES], s_wpfo[FC_WAVES], s_wo[FC_WAVES];
-  __shared__ uint64_t s_wlast[FC_WAVES];       // per wave: its last op's Index ...
-  __shared__ uint32_t s_wlastf[FC_WAVES];      // ... and frame (EW_NIL: no op)
-  __shared__ uint32_t s_wfirstf[FC_WAVES];     // per wave: its first op's frame (EW_NIL: no op) ...
-  __shared__ uint64_t s_wfirst[FC_WAVES];      // ... and Index
-  __shared__ uint32_t s_shr[2];
-  __shared__ uint32_t s_red[4];                // last entry + 1, last state + 1, ~first meta, last op + 1
-  __shared__ unsigned long long s_fail;        // min (frame << 8 | status)
   Small *ds = a.ds;
   const uint64_t K = ds->total;
   if (K == 0 || K > a.ccap || ds->novf || K >= 0xffffff00ull) return;   // the host takes the general path
@@ -217,36 +216,29 @@ __global__ __launch_bounds__(FC_THREADS, FC_WGS) void k_fc(FcArgs a, SegArgs sg)
   stage_lds<FC_THREADS>(s_t4, 16 * 256, [&](int i) { return a.g_slice[i]; });
   stage_lds<FC_THREADS>(s_svp, 1024, [&](int i) { return a.g_shift[EW_VLOG * 1024 + i]; });
   stage_lds<FC_THREADS>(s_nib, FC_NIB_LEVELS * 128, [&](int i) { return nib_src(a.g_shift, i); });
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  __syncthreads();   // the only barrier: every wave runs its own tiles from here on
+  const int tid = threadIdx.x, lane = tid & 63;
   const uint32_t K32 = (uint32_t)K;
-  const uint32_t ntiles = (K32 + FC_THREADS - 1) / FC_THREADS;
+  const uint32_t ntiles = (K32 + FC_TILE - 1) / FC_TILE;
+  const uint32_t wid = blockIdx.x * FC_WAVES + (uint32_t)(tid >> 6), nwaves = gridDim.x * FC_WAVES;
   uint32_t rare = 0, irr = 0;
-  // this thread's candidate offsets, one tile ahead (their latency hides
-  // behind the previous tile's barriers and look-back)
+  // this lane's candidate offsets, one tile ahead
   auto cand = [&](uint32_t tt, uint64_t &pp, uint64_t &pq) {
-    const uint32_t rr = min(tt * FC_THREADS + (uint32_t)tid, K32 - 1);
+    const uint32_t rr = min(tt * FC_TILE + (uint32_t)lane, K32 - 1);
     pp = a.cpos[rr];
     pq = rr + 1 < K32 ? a.cpos[rr + 1] : ~0ull;
   };
   uint64_t p_nx = 0, pn_nx = 0;
-  if (blockIdx.x < ntiles) cand(blockIdx.x, p_nx, pn_nx);
-  for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
-    const uint32_t r0 = t * FC_THREADS;
-    const uint32_t rt = r0 + (uint32_t)tid;
+  if (wid < ntiles) cand(wid, p_nx, pn_nx);
+  if (wid == 0 && lane == 0) ds->pos0 = a.cpos[0];
+  for (uint32_t t = wid; t < ntiles; t += nwaves) {
+    const uint32_t r0 = t * FC_TILE;
+    const uint32_t rt = r0 + (uint32_t)lane;
     const bool live = rt < K32;
-    const uint32_t r = live ? rt : K32 - 1;    // the whole tile reaches every barrier; writes masked
-    __syncthreads();                           // the previous tile's LDS reads are done
-    if (tid == 0) {
-      s_red[0] = 0; s_red[1] = 0; s_red[2] = 0; s_red[3] = 0;
-      s_fail = ~0ull;
-      if (SEG) {
-        s_shr[0] = shard_of(sg.fs, sg.ns, r0);
-        s_shr[1] = shard_in(sg.fs, s_shr[0], sg.ns, min(r0 + FC_THREADS, K32) - 1);
-      }
-      if (t == 0) ds->pos0 = a.cpos[0];
-    }
+    const uint32_t r = live ? rt : K32 - 1;    // writes masked for lanes past the end
+    const uint32_t rl = min(r0 + FC_TILE, K32) - 1;   // the tile's last frame
     const uint64_t p = p_nx, pn = pn_nx;
-    if (t + gridDim.x < ntiles) cand(t + gridDim.x, p_nx, pn_nx);
+    if (t + nwaves < ntiles) cand(t + nwaves, p_nx, pn_nx);
     RecDesc d;
     int64_t L = 0;
     uint32_t Pfo = 0, Pfd = 0;
@@ -264,29 +256,28 @@ __global__ __launch_bounds__(FC_THREADS, FC_WGS) void k_fc(FcArgs a, SegArgs sg)
       ds->q = s;
       ds->qlen = (s <= a.B && a.B - s >= 8) ? (int64_t)ld_le64_b(a.buf, a.B, s) : 0;
     }
-    // neighbours: the predecessor's stored CRC, the successor's P at its frame start
-    uint32_t cprev = (uint32_t)__shfl_up((int)d.crc, 1);
-    uint32_t pnext = (uint32_t)__shfl_down((int)Pfo, 1);
-    if (lane == 63) s_wcrc[wv] = d.crc;
-    if (lane == 0) s_wpfo[wv] = Pfo;
-    __syncthreads();
-    if (lane == 0 && wv) cprev = s_wcrc[wv - 1];
-    if (lane == 63 && wv + 1 < FC_WAVES) pnext = s_wpfo[wv + 1];
+    // neighbours in the wave: the predecessor's stored CRC, the successor's
+    // P at its frame start; the tile's edge frames take theirs from the
+    // neighbouring tiles' records in k_fc_seam
+    const uint32_t cprev = (uint32_t)__shfl_up((int)d.crc, 1);
+    const uint32_t pnext = (uint32_t)__shfl_down((int)Pfo, 1);
     uint32_t sh = 0, lo = 0;                   // SEG: the frame's shard and its first frame
     uint64_t ri = a.ri;
-    if (SEG) {
-      sh = s_shr[0] == s_shr[1] ? s_shr[0] : shard_in(sg.fs, s_shr[0], s_shr[1] + 1, r);
+    uint32_t sh0 = 0, sh1 = 0;
+    if (SEG) {   // the tile's shard range, searched by one lane
+      if (lane == 0) {
+        sh0 = shard_of(sg.fs, sg.ns, r0);
+        sh1 = shard_in(sg.fs, sh0, sg.ns, rl);
+      }
+      sh0 = (uint32_t)__shfl((int)sh0, 0);
+      sh1 = (uint32_t)__shfl((int)sh1, 0);
+      sh = sh0 == sh1 ? sh0 : shard_in(sg.fs, sh0, sh1 + 1, r);
       lo = sg.fs[sh];
       ri = sg.ri[sh];
     }
-    // decoder.decode's check + ReadAll's crc-record rule (as k_check).  The
-    // tile's first frame takes its seed from the frame before the tile, its
-    // last frame P(data end) from the frame after it: k_fc_seam makes those
-    // checks with the neighbouring tiles' records (their verdict is
-    // provisionally 0 here; the frame's other reports carry larger keys, so a
-    // CRC failure still wins)
-    const bool dfirst = tid == 0 && r > lo;
-    const bool dlast = tid == FC_THREADS - 1 && r + 1 < K32;
+    // decoder.decode's check + ReadAll's crc-record rule (as k_check)
+    const bool dfirst = lane == 0 && r > lo;
+    const bool dlast = live && r == rl && r + 1 < K32;
     const uint32_t seed = r > lo ? cprev : 0u;
     int st = 0;
     uint32_t chained = seed;
@@ -314,10 +305,10 @@ __global__ __launch_bounds__(FC_THREADS, FC_WGS) void k_fc(FcArgs a, SegArgs sg)
       if (computed != d.crc) st = EWAL_ERR_RECORD_CRC;
       else if (d.type != 1 && d.type != 2 && d.type != 3) st = EWAL_ERR_UNEXPECTED_TYPE;
     }
-    if (live && (tid == 0 || tid == FC_THREADS - 1 || r + 1 == K32)) {
-      TileRec *tr = a.trec + t;
+    TileRec *tr = a.trec + t;
+    if (live && (lane == 0 || r == rl)) {
       const int32_t ty = (int32_t)(d.type < 0 || d.type > 1000 ? 1000 : d.type);
-      if (tid == 0) {
+      if (lane == 0) {
         tr->pfo0 = Pfo;
         tr->dfirst = dfirst;
         tr->crc[0] = d.crc;
@@ -326,7 +317,7 @@ __global__ __launch_bounds__(FC_THREADS, FC_WGS) void k_fc(FcArgs a, SegArgs sg)
         tr->type[0] = ty;
         tr->dlen[0] = d.dlen;
       }
-      if (tid == FC_THREADS - 1 || r + 1 == K32) {   // the tile's last frame
+      if (r == rl) {   // the tile's last frame
         tr->lastcrc = d.crc;
         tr->dlast = dlast;
         tr->crc[1] = d.crc;
@@ -339,27 +330,27 @@ __global__ __launch_bounds__(FC_THREADS, FC_WGS) void k_fc(FcArgs a, SegArgs sg)
     if (a.ablate & 16) st = 0;   // timing only: no failure reports (keeps the ablations' verdict path alike)
     if (dfirst || dlast) st = 0;
     else if (live && r + 1 == K32) ds->fc.last_chained = chained;
-    // entry ops (wal/wal.go:170-176): the op's predecessor in the wave, else
-    // in an earlier wave of the tile; the tile's first op is k_fc_seam's
-    const uint32_t rw0 = r0 + (uint32_t)(tid & ~63);
+    // entry ops (wal/wal.go:170-176): the op's predecessor in the tile; the
+    // tile's first op is k_fc_seam's unless the tile opens its shard
     const bool op = live && d.type == 2 && d.f1 >= ri;
     const unsigned long long mo = __ballot(op);
     const unsigned long long below = mo & ((1ull << lane) - 1ull);
     unsigned long long bsh = below;
-    if (SEG && lo > rw0) bsh = (lo - rw0 >= 64) ? 0ull : below & ~((1ull << (lo - rw0)) - 1ull);
+    if (SEG && lo > r0) bsh = (lo - r0 >= 64) ? 0ull : below & ~((1ull << (lo - r0)) - 1ull);
     const int pl = bsh ? 63 - __clzll((long long)bsh) : lane;
-    const uint64_t fprev = __shfl(d.f1, pl);
+    const uint64_t kp = __shfl(d.f1, pl);
     const int wl = mo ? 63 - __clzll((long long)mo) : 0;
     const int wf = mo ? __ffsll((long long)mo) - 1 : 0;
     const uint64_t wli = __shfl(d.f1, wl), wfi = __shfl(d.f1, wf);
-    if (lane == 0) {
-      s_wo[wv] = (uint32_t)__popcll(mo);
-      s_wlastf[wv] = mo ? rw0 + (uint32_t)wl : EW_NIL;
-      s_wfirstf[wv] = mo ? rw0 + (uint32_t)wf : EW_NIL;
-      s_wlast[wv] = wli;
-      s_wfirst[wv] = wfi;
+    const uint32_t ff = mo ? r0 + (uint32_t)wf : EW_NIL;
+    bool tseam = mo != 0;
+    if (SEG && mo) {   // the first op's shard began before the tile (one lane searches)
+      int b = 0;
+      if (lane == 0) b = sg.fs[shard_in(sg.fs, sh0, sh1 + 1, ff)] < r0;
+      tseam = __shfl(b, 0) != 0;
     }
-    // reductions (one LDS atomic per wave and quantity)
+    // reductions: per tile into its record (k_fc_seam folds the tiles'),
+    // batched: per shard (lane by lane where a shard starts inside the tile)
     const unsigned long long mf = __ballot(live && st != 0), me = __ballot(live && d.type == 2),
                              ms = __ballot(live && d.type == 3), mm = __ballot(live && d.type == 1 && d.dlen > 0);
     const int ffl = mf ? __ffsll((long long)mf) - 1 : 0;
@@ -368,72 +359,42 @@ __global__ __launch_bounds__(FC_THREADS, FC_WGS) void k_fc(FcArgs a, SegArgs sg)
       const uint32_t mi = atomicAdd(&ds->nmeta, 1u);
       if (mi < a.ecap) a.mlist[mi] = r; else rare |= 4u;
     }
-    const bool wg1 = !SEG || s_shr[0] == s_shr[1];
-    if (lane == 0 && wg1) {
-      if (mf) atomicMin(&s_fail, ((unsigned long long)(rw0 + (uint32_t)ffl) << 8) | fst);
-      if (me) atomicMax(&s_red[0], rw0 + (uint32_t)(63 - __clzll((long long)me)) + 1u);
-      if (ms) atomicMax(&s_red[1], rw0 + (uint32_t)(63 - __clzll((long long)ms)) + 1u);
-      if (mm) atomicMax(&s_red[2], ~(rw0 + (uint32_t)(__ffsll((long long)mm) - 1)));
-      if (mo) atomicMax(&s_red[3], rw0 + (uint32_t)wl + 1u);
-    }
-    if (SEG && !wg1 && live) {   // a shard boundary inside the tile (rare): lane by lane
-      ShardAgg *A = sg.sagg + sh;
-      if (st != 0) atomicMin(&A->first_fail, ((unsigned long long)r << 8) | (uint32_t)st);
-      if (d.type == 2) atomicMax(&A->last_entry, (long long)r);
-      if (d.type == 3) atomicMax(&A->last_state, (long long)r);
-      if (d.type == 1 && d.dlen > 0) atomicMin(&A->first_meta, (unsigned long long)r);
-      if (op) atomicMax(&A->lastop, r + 1u);
-    }
-    __syncthreads();
-    // the tile's first op: its predecessor op (if any) lies before the tile
-    // unless the tile opens the op's shard -- k_fc_seam decides that one
-    uint32_t ff = EW_NIL;
-    uint64_t ffi = 0;
-#pragma unroll
-    for (int w = 0; w < FC_WAVES; ++w)
-      if (ff == EW_NIL && s_wfirstf[w] != EW_NIL) { ff = s_wfirstf[w]; ffi = s_wfirst[w]; }
-    const bool tseam = ff != EW_NIL && (!SEG || sg.fs[shard_of(sg.fs, sg.ns, ff)] < r0);
-    if (tid == 0) {
-      uint32_t cnt = 0, lf = EW_NIL;
-      uint64_t lfi = 0;
-#pragma unroll
-      for (int w = 0; w < FC_WAVES; ++w) {
-        cnt += s_wo[w];
-        if (s_wlastf[w] != EW_NIL) { lf = s_wlastf[w]; lfi = s_wlast[w]; }
-      }
-      TileRec *tr = a.trec + t;
-      tr->count = cnt;
+    if (lane == 0) {
+      tr->count = (uint32_t)__popcll(mo);
       tr->first_frame = ff;
-      tr->last_frame = lf;
-      tr->first_index = ffi;
-      tr->last_index = lfi;
+      tr->last_frame = mo ? r0 + (uint32_t)wl : EW_NIL;
+      tr->first_index = wfi;
+      tr->last_index = wli;
       tr->seam = tseam;
-      if (cnt) atomicAdd(&ds->nsel3, cnt);
-      if (!SEG) {
-        if (s_fail != ~0ull) atomicMax(&ds->fc.fail_inv, ~s_fail);
-        if (s_red[0]) atomicMax(&ds->fc.last_entry1, s_red[0]);
-        if (s_red[1]) atomicMax(&ds->fc.last_state1, s_red[1]);
-        if (s_red[2]) atomicMax(&ds->fc.meta_inv, ~(unsigned long long)(uint32_t)~s_red[2]);
-        if (s_red[3]) atomicMax(&ds->lastop, s_red[3]);
-      } else if (s_shr[0] == s_shr[1]) {
-        ShardAgg *A = sg.sagg + s_shr[0];
-        if (s_fail != ~0ull) atomicMin(&A->first_fail, s_fail);
-        if (s_red[0]) atomicMax(&A->last_entry, (long long)(s_red[0] - 1));
-        if (s_red[1]) atomicMax(&A->last_state, (long long)(s_red[1] - 1));
-        if (s_red[2]) atomicMin(&A->first_meta, (unsigned long long)(uint32_t)~s_red[2]);
-        if (s_red[3]) atomicMax(&A->lastop, s_red[3]);
+      tr->fail = mf ? ((unsigned long long)(r0 + (uint32_t)ffl) << 8) | fst : ~0ull;
+      tr->last_entry1 = me ? r0 + (uint32_t)(63 - __clzll((long long)me)) + 1u : 0u;
+      tr->last_state1 = ms ? r0 + (uint32_t)(63 - __clzll((long long)ms)) + 1u : 0u;
+      tr->meta1 = mm ? r0 + (uint32_t)(__ffsll((long long)mm) - 1) + 1u : 0u;
+      tr->lastop1 = mo ? r0 + (uint32_t)wl + 1u : 0u;
+    }
+    if (SEG) {
+      if (sh0 == sh1) {
+        if (lane == 0) {
+          ShardAgg *A = sg.sagg + sh0;
+          if (mf) atomicMin(&A->first_fail, ((unsigned long long)(r0 + (uint32_t)ffl) << 8) | fst);
+          if (me) atomicMax(&A->last_entry, (long long)(r0 + (uint32_t)(63 - __clzll((long long)me))));
+          if (ms) atomicMax(&A->last_state, (long long)(r0 + (uint32_t)(63 - __clzll((long long)ms))));
+          if (mm) atomicMin(&A->first_meta, (unsigned long long)(r0 + (uint32_t)(__ffsll((long long)mm) - 1)));
+          if (mo) atomicMax(&A->lastop, r0 + (uint32_t)wl + 1u);
+        }
+      } else if (live) {   // a shard boundary inside the tile (rare): lane by lane
+        ShardAgg *A = sg.sagg + sh;
+        if (st != 0) atomicMin(&A->first_fail, ((unsigned long long)r << 8) | (uint32_t)st);
+        if (d.type == 2) atomicMax(&A->last_entry, (long long)r);
+        if (d.type == 3) atomicMax(&A->last_state, (long long)r);
+        if (d.type == 1 && d.dlen > 0) atomicMin(&A->first_meta, (unsigned long long)r);
+        if (op) atomicMax(&A->lastop, r + 1u);
       }
     }
     if (op) {
-      uint64_t kp = fprev;
-      uint32_t pf = bsh ? 0u : EW_NIL;         // the predecessor op: in the wave, or an earlier wave
-      for (int w = wv - 1; w >= 0 && pf == EW_NIL; --w)
-        if (s_wlastf[w] != EW_NIL) { pf = s_wlastf[w]; kp = s_wlast[w]; }
-      const bool has = pf != EW_NIL && (bsh || pf >= lo);   // SEG: in this shard
+      const bool has = bsh != 0;               // the predecessor op, in the tile (SEG: in this shard)
       const uint64_t k = d.f1 - ri;
-      // no predecessor in the tile and the op's shard began before the tile:
-      // the tile's first op, k_fc_seam's
-      const bool seam_op = !has && tseam && r == ff;
+      const bool seam_op = !has && tseam && r == ff;   // k_fc_seam's
       if (!seam_op) {
         bool gap;
         if (has) {
@@ -474,72 +435,113 @@ __global__ __launch_bounds__(FC_THREADS, FC_WGS) void k_fc(FcArgs a, SegArgs sg)
 // predecessor op lies in an earlier tile: the nearest earlier tile with ops
 // holds it (its last op's Index) -- in the same shard when that tile's last
 // op lies at or after the shard's first frame.  One thread per tile; the
-// edge frames' CRC checks k_fc left to it too.
+// edge frames' CRC checks k_fc left to it too, and (single WAL) the fold of
+// the tiles' reductions: one atomic per workgroup and quantity.
 #define FC_SEAM_SCAN 4096   // tiles scanned back for the predecessor (beyond: the general path)
 template <bool SEG>
-__global__ void k_fc_seam(const uint8_t *__restrict__ buf, uint64_t B, const uint64_t *__restrict__ cpos,
-                          const uint32_t *__restrict__ g_shift, const TileRec *__restrict__ trec,
-                          const ewal_entry *__restrict__ ents, uint64_t ri_one, uint64_t ccap, uint64_t ecap, Small *ds,
-                          SegArgs sg) {
+__global__ __launch_bounds__(256) void k_fc_seam(const uint8_t *__restrict__ buf, uint64_t B,
+                                                 const uint64_t *__restrict__ cpos,
+                                                 const uint32_t *__restrict__ g_shift,
+                                                 const TileRec *__restrict__ trec,
+                                                 const ewal_entry *__restrict__ ents, uint64_t ri_one, uint64_t ccap,
+                                                 uint64_t ecap, Small *ds, SegArgs sg) {
+  __shared__ unsigned long long s_fail;
+  __shared__ uint32_t s_red[5];   // last entry + 1, last state + 1, ~first meta, last op + 1, ops
   if (!fc_ran(ds, ccap, ecap)) return;
   const uint64_t K = ds->total;
-  const uint32_t ntiles = (uint32_t)((K + FC_THREADS - 1) / FC_THREADS);
+  const uint32_t ntiles = (uint32_t)((K + FC_TILE - 1) / FC_TILE);
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= ntiles) return;
-  const TileRec tr = trec[t];
-  const uint32_t r0 = t * FC_THREADS;
-  const uint32_t rl = min(r0 + FC_THREADS, (uint32_t)K) - 1;   // the tile's last frame
-  for (int w = 0; w < 2; ++w) {   // the edge frames' CRC checks k_fc left
-    const bool first = w == 0;
-    if (first ? !tr.dfirst : (!tr.dlast || (tr.dfirst && rl == r0))) continue;
-    const uint32_t r = first ? r0 : rl;
-    const uint32_t seed = first ? trec[t - 1].lastcrc : tr.seed1;
-    const bool next = !first || (tr.dlast && rl == r0);   // P(data end) from the next tile
-    const uint32_t pe = next ? trec[t + 1].pfo0 : tr.pe0;
-    uint32_t chained;
-    const int st = fc_check_one(g_shift, tr.type[w], tr.crc[w], seed, tr.pfd[w], pe, tr.dlen[w], &chained);
-    if (st) {
-      if (SEG) atomicMin(&sg.sagg[shard_of(sg.fs, sg.ns, r)].first_fail, ((unsigned long long)r << 8) | (uint32_t)st);
-      else atomicMax(&ds->fc.fail_inv, ~(((unsigned long long)r << 8) | (uint32_t)st));
+  if (!SEG) {
+    if (threadIdx.x == 0) {
+      s_fail = ~0ull;
+      s_red[0] = s_red[1] = s_red[3] = s_red[4] = 0;
+      s_red[2] = 0;
     }
-    if (!SEG && r + 1 == K) ds->fc.last_chained = chained;
+    __syncthreads();
   }
-  if (!tr.seam || !tr.count) return;
-  const uint32_t f = tr.first_frame;
-  if (f >= K) return;
-  uint64_t ri = ri_one;
-  uint32_t sh = 0, lo = 0;
-  if (SEG) {
-    sh = shard_of(sg.fs, sg.ns, f);
-    ri = sg.ri[sh];
-    lo = sg.fs[sh];
-  }
-  bool has = false;
-  uint64_t pidx = 0;
-  uint32_t scanned = 0;
-  for (int64_t u = (int64_t)t - 1; u >= 0 && (uint64_t)(u + 1) * FC_THREADS > lo; --u) {
-    if (++scanned > FC_SEAM_SCAN) {   // a very long run of tiles without entries: the general path
-      atomicOr(&ds->fc.rare, 8u);
-      return;
+  unsigned long long fail = ~0ull;
+  if (t < ntiles) {
+    const TileRec tr = trec[t];
+    const uint32_t r0 = t * FC_TILE;
+    const uint32_t rl = min(r0 + FC_TILE, (uint32_t)K) - 1;   // the tile's last frame
+    for (int w = 0; w < 2; ++w) {   // the edge frames' CRC checks k_fc left
+      const bool first = w == 0;
+      if (first ? !tr.dfirst : (!tr.dlast || (tr.dfirst && rl == r0))) continue;
+      const uint32_t r = first ? r0 : rl;
+      const uint32_t seed = first ? trec[t - 1].lastcrc : tr.seed1;
+      const bool next = !first || (tr.dlast && rl == r0);   // P(data end) from the next tile
+      const uint32_t pe = next ? trec[t + 1].pfo0 : tr.pe0;
+      uint32_t chained;
+      const int st = fc_check_one(g_shift, tr.type[w], tr.crc[w], seed, tr.pfd[w], pe, tr.dlen[w], &chained);
+      if (st) {
+        const unsigned long long key = ((unsigned long long)r << 8) | (uint32_t)st;
+        if (SEG) atomicMin(&sg.sagg[shard_of(sg.fs, sg.ns, r)].first_fail, key);
+        else fail = min(fail, key);
+      }
+      if (!SEG && r + 1 == K) ds->fc.last_chained = chained;
     }
-    const TileRec q = trec[u];
-    if (!q.count) continue;
-    has = !SEG || q.last_frame >= lo;
-    pidx = q.last_index;
-    break;
+    if (tr.seam && tr.count && tr.first_frame < K) {
+      const uint32_t f = tr.first_frame;
+      uint64_t ri = ri_one;
+      uint32_t sh = 0, lo = 0;
+      if (SEG) {
+        sh = shard_of(sg.fs, sg.ns, f);
+        ri = sg.ri[sh];
+        lo = sg.fs[sh];
+      }
+      bool has = false, far = false;
+      uint64_t pidx = 0;
+      uint32_t scanned = 0;
+      for (int64_t u = (int64_t)t - 1; u >= 0 && (uint64_t)(u + 1) * FC_TILE > lo; --u) {
+        if (++scanned > FC_SEAM_SCAN) {   // a very long run of tiles without entries: the general path
+          far = true;
+          break;
+        }
+        const TileRec q = trec[u];
+        if (!q.count) continue;
+        has = !SEG || q.last_frame >= lo;
+        pidx = q.last_index;
+        break;
+      }
+      if (far) {
+        atomicOr(&ds->fc.rare, 8u);
+      } else {
+        const uint64_t k = tr.first_index - ri;
+        bool gap;
+        if (has) {
+          const uint64_t kq = pidx - ri;
+          if (k <= kq) atomicOr(&ds->fc.rare, 2u);
+          gap = k > kq && k - kq > 1;
+        } else {
+          gap = k > 0;
+        }
+        if (gap) {
+          const unsigned long long key = ((unsigned long long)f << 8) | EWAL_PANIC_INDEX_GAP;
+          if (SEG) atomicMin(&sg.sagg[sh].first_fail, key);
+          else fail = min(fail, key);
+        }
+      }
+    }
+    if (!SEG) {
+      fail = min(fail, tr.fail);
+      if (tr.last_entry1) atomicMax(&s_red[0], tr.last_entry1);
+      if (tr.last_state1) atomicMax(&s_red[1], tr.last_state1);
+      if (tr.meta1) atomicMax(&s_red[2], ~(tr.meta1 - 1u));
+      if (tr.lastop1) atomicMax(&s_red[3], tr.lastop1);
+      if (tr.count) atomicAdd(&s_red[4], tr.count);
+    }
   }
-  const uint64_t k = tr.first_index - ri;
-  bool gap;
-  if (has) {
-    const uint64_t kq = pidx - ri;
-    if (k <= kq) atomicOr(&ds->fc.rare, 2u);
-    gap = k > kq && k - kq > 1;
-  } else {
-    gap = k > 0;
-  }
-  if (gap) {
-    if (SEG) atomicMin(&sg.sagg[sh].first_fail, ((unsigned long long)f << 8) | EWAL_PANIC_INDEX_GAP);
-    else atomicMax(&ds->fc.fail_inv, ~(((unsigned long long)f << 8) | EWAL_PANIC_INDEX_GAP));
+  if (!SEG) {
+    if (fail != ~0ull) atomicMin(&s_fail, fail);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      if (s_fail != ~0ull) atomicMax(&ds->fc.fail_inv, ~s_fail);
+      if (s_red[0]) atomicMax(&ds->fc.last_entry1, s_red[0]);
+      if (s_red[1]) atomicMax(&ds->fc.last_state1, s_red[1]);
+      if (s_red[2]) atomicMax(&ds->fc.meta_inv, ~(unsigned long long)(uint32_t)~s_red[2]);
+      if (s_red[3]) atomicMax(&ds->lastop, s_red[3]);
+      if (s_red[4]) atomicAdd(&ds->nsel3, s_red[4]);
+    }
   }
 }
 
