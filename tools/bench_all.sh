@@ -12,7 +12,7 @@ for w in $WS; do
   echo "== $w $(date +%T)"
   timeout -k 10 420 python3 -u bench.py --workload $w --cpu-seconds 8 > gpurun_out/bench_$w.json 2> gpurun_out/bench_$w.err
   tail -c 600 gpurun_out/bench_$w.json
-  if [ "$w" != snapstream ]; then
+  if [ "$w" != snapstream ] && [ "$w" != restart ]; then
     timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$w -o run -- \
       python3 bench.py --workload $w --steps 5 --warmup 1 --no-cpu-baseline --no-e2e > gpurun_out/prof_$w.log 2>&1
   fi
