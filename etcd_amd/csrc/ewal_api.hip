@@ -488,7 +488,7 @@ static int walk_chain(ewal_ctx *c, DevTables *tb, const uint8_t *d_buf, uint64_t
   return 0;
 }
 
-// The fused frame + check pass (k_fc + k_result_fc, fused_kernels.hip) over
+// The fused frame + check pass (k_fc + k_fc_seam / fc_result, fused_kernels.hip) over
 // the stream pass's candidates: ONE host sync.  *done when the regular case
 // held (ResultDev in c->h_res, ents in c->ents); otherwise the reductions are
 // reset and the caller runs the general path over the same stream pass.
@@ -521,9 +521,9 @@ static int fused_pass(ewal_ctx *c, DevTables *tb, const uint8_t *d_buf, uint64_t
     a.ablate = c->fc_ablate;
     hipLaunchKernelGGL(k_fc<false>, dim3((unsigned)std::max(1, c->num_cu) * FC_WGS), dim3(FC_THREADS), 0, c->stream,
                        a, SegArgs{});
+    // the seam pass; its last workgroup gathers the result (fc_result)
     hipLaunchKernelGGL(k_fc_seam<false>, dim3(grid_for(ntiles, 256)), dim3(256), 0, c->stream, d_buf, B, a.cpos,
-                       tb->shift, a.trec, a.ents, ri, ccap, ecap, ds, SegArgs{});
-    hipLaunchKernelGGL(k_result_fc, dim3(1), dim3(256), 0, c->stream, d_buf, B, a.cpos, ccap, ecap, ri, a.mlist, ds,
+                       tb->shift, a.trec, a.ents, ri, ccap, ecap, ds, SegArgs{}, (const uint32_t *)a.mlist,
                        c->h_res_dev, c->h_small_dev);
     EW_CHECK(hipGetLastError());
     EW_CHECK(hipStreamSynchronize(c->stream));
@@ -1024,7 +1024,8 @@ static int fused_batch(ewal_ctx *c, DevTables *tb, const uint8_t *d_buf, uint64_
     hipLaunchKernelGGL(k_fc<true>, dim3((unsigned)std::max(1, c->num_cu) * FC_WGS), dim3(FC_THREADS), 0, c->stream, a,
                        sg);
     hipLaunchKernelGGL(k_fc_seam<true>, dim3(grid_for(ntiles, 256)), dim3(256), 0, c->stream, d_buf, B, a.cpos,
-                       tb->shift, a.trec, a.ents, 0ull, ccap, ecap, ds, sg);
+                       tb->shift, a.trec, a.ents, 0ull, ccap, ecap, ds, sg, (const uint32_t *)nullptr,
+                       (ResultDev *)nullptr, (Small *)nullptr);
     hipLaunchKernelGGL(k_meta_batch_fc, dim3(64), dim3(256), 0, c->stream, d_buf, B, a.cpos, ccap, ecap, a.mlist, ds,
                        sg);
     hipLaunchKernelGGL(k_result_batch_fc, dim3(grid_for((uint64_t)ns * 8, 256)), dim3(256), 0, c->stream, d_buf, B, a.cpos, ccap,

@@ -133,7 +133,7 @@ struct Small {
   uint32_t segbad;                // k_shard_start: a shard does not start on a frame of the chain
   uint32_t spec_n;                // k_spec_gate: frames when k_frame's speculation holds, else 0
   uint32_t nunrec;                // k_check: entry ops carrying XXX_unrecognized (listed in ulist)
-  uint32_t pad2;
+  uint32_t fc_done;               // k_fc_seam workgroups done (the last one gathers the result)
   FcAgg fc;
 };
 

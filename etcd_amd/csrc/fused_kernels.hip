@@ -139,6 +139,53 @@ __device__ __forceinline__ uint32_t fc_head_crc(const uint8_t *__restrict__ buf,
   return (uint32_t)c;
 }
 
+// The canonical layout etcd's encoder writes (record.pb.go:175-196,
+// raft.pb.go:921-943, 1079-1097): every field once, in order, the last one
+// ending at the message end -- parsed straight from the frame's head bytes
+// h[0..n) (n >= 81: every canonical head fits).  false: not canonical.
+__device__ __forceinline__ bool fc_varint(const uint8_t *h, int n, int &o, uint64_t &v) {
+  uint64_t x = 0;
+  for (int s = 0; s < 64 && o < n; s += 7) {
+    const uint8_t b = h[o++];
+    x |= (uint64_t)(b & 0x7f) << s;
+    if (b < 0x80) { v = x; return true; }
+  }
+  return false;
+}
+__device__ __forceinline__ bool fc_tag_varint(const uint8_t *h, int n, int &o, uint8_t tag, uint64_t &v) {
+  return o < n && h[o++] == tag && fc_varint(h, n, o, v);
+}
+__device__ bool fc_canon_fields(const uint8_t *h, int n, uint64_t p, int64_t L, RecDesc &d) {
+  int o = 8;
+  uint64_t ty, cr, dl = 0;
+  if (!fc_tag_varint(h, n, o, 0x08, ty) || !fc_tag_varint(h, n, o, 0x10, cr)) return false;
+  const bool hasd = (int64_t)(o - 8) < L;
+  if (hasd && !fc_tag_varint(h, n, o, 0x1a, dl)) return false;
+  if ((int64_t)(o - 8) + (int64_t)dl != L) return false;
+  d.type = (int64_t)ty;
+  d.crc = (uint32_t)cr;
+  if (dl > 0) { d.doff = p + (uint64_t)o; d.dlen = dl; d.dnil = 0; }
+  if (dl == 0 || (d.type != 2 && d.type != 3)) return true;
+  const int e0 = o;
+  uint64_t f0, f1, f2;
+  if (!fc_tag_varint(h, n, o, 0x08, f0) || !fc_tag_varint(h, n, o, 0x10, f1) || !fc_tag_varint(h, n, o, 0x18, f2))
+    return false;
+  if (d.type == 3) {
+    if ((uint64_t)(o - e0) != dl) return false;
+    d.f0 = f0; d.f1 = f1; d.f2 = f2;
+    return true;
+  }
+  uint64_t el = 0;
+  const bool hase = (uint64_t)(o - e0) < dl;
+  if (hase && !fc_tag_varint(h, n, o, 0x22, el)) return false;
+  if ((uint64_t)(o - e0) + el != dl) return false;
+  d.etype = (int32_t)(uint32_t)f0;
+  d.f0 = f1;
+  d.f1 = f2;
+  if (el > 0) { d.edoff = p + (uint64_t)o; d.edlen = el; d.enil = 0; }
+  return true;
+}
+
 // Every field a later pass needs of one canonical frame, re-read from global
 // memory (the passes after k_fc touch a handful of frames): Record type /
 // crc / Data, Entry / HardState fields.  The first 96 bytes come in with six
@@ -170,6 +217,8 @@ __device__ RecDesc fc_frame_fields(const uint8_t *__restrict__ buf, uint64_t B, 
     }
     w[k] = x;
   }
+  if (fc_canon_fields((const uint8_t *)w + (p - p16), 96 - (int)(p - p16), p, L, d)) return d;
+  // not the canonical layout (a frame the general path also decodes): the walkers
   const WinReader R0{(const uint8_t *)w + (p - p16), (int64_t)(96 - (p - p16)), buf + p};
   const WinReader rb = R0 + 8;
   PbField a1, a2, a3, a4, a5;
@@ -431,6 +480,69 @@ __global__ __launch_bounds__(FC_THREADS, FC_WGS) void k_fc(FcArgs a, SegArgs sg)
   if (__ballot(irr) && lane == 0) atomicOr(&ds->irregular, 1u);
 }
 
+// After k_fc and the seam pass (one workgroup): does the regular case hold?
+// Then ReadAll's metadata rule (wal/wal.go:178-183) over the listed metadata
+// frames and the ResultDev gather k_result makes on the general path (the
+// few frames it needs re-read in parallel); spec_n = frames, or 0 (the host
+// takes the general path); Small -> host-mapped memory.
+__device__ void fc_result(const uint8_t *__restrict__ buf, uint64_t B, const uint64_t *__restrict__ cpos, uint64_t ccap,
+                          uint64_t ecap, uint64_t ri, const uint32_t *__restrict__ mlist, Small *ds, ResultDev *o,
+                          Small *h, uint4 (*s_w)[6], RecDesc *s_d) {
+  const uint64_t K = ds->total;
+  if (!fc_valid(ds, ccap, ecap)) {
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      ds->spec_n = 0;
+      *h = *ds;
+    }
+    return;
+  }
+  const uint32_t tid = threadIdx.x;
+  const uint64_t fm = ds->fc.meta_inv ? ~ds->fc.meta_inv : ~0ull;
+  if (fm != ~0ull && ds->nmeta > 1) {
+    const RecDesc m = fc_frame_fields(buf, B, cpos[fm], s_w[tid]);
+    for (uint32_t i = tid; i < ds->nmeta; i += blockDim.x) {
+      const uint32_t r = mlist[i];
+      if (r <= fm) continue;
+      const RecDesc d = fc_frame_fields(buf, B, cpos[r], s_w[tid]);
+      bool eq = d.dlen == m.dlen;
+      for (uint64_t k = 0; eq && k < d.dlen; ++k) eq = buf[d.doff + k] == buf[m.doff + k];
+      if (!eq) atomicMax(&ds->fc.fail_inv, ~(((unsigned long long)r << 8) | EWAL_ERR_METADATA_CONFLICT));
+    }
+  }
+  __threadfence();
+  __syncthreads();
+  // the frames the result needs: first failure, last entry, last state,
+  // first metadata, last op -- one thread each
+  const unsigned long long key = ds->fc.fail_inv ? ~ds->fc.fail_inv : ~0ull;
+  const long long le = (long long)ds->fc.last_entry1 - 1, ls = (long long)ds->fc.last_state1 - 1;
+  const long long lo = (long long)ds->lastop - 1;
+  const long long want[5] = {key != ~0ull ? (long long)(key >> 8) : -1, le, ls, fm != ~0ull ? (long long)fm : -1, lo};
+  if (tid < 5 && want[tid] >= 0) s_d[tid] = fc_frame_fields(buf, B, cpos[want[tid]], s_w[tid]);
+  __syncthreads();
+  if (tid != 0) return;
+  ResultDev res;
+  memset(&res, 0, sizeof(res));
+  res.agg.first_fail = key != ~0ull ? (key >> 8) : ~0ull;
+  res.agg.last_entry = le;
+  res.agg.last_state = ls;
+  res.agg.first_meta = fm;
+  if (key != ~0ull) {
+    res.fail = s_d[0];
+    res.fail.st = (int32_t)(key & 0xff);
+  }
+  if (le >= 0) res.lastent = s_d[1];
+  if (ls >= 0) res.sd = s_d[2];
+  if (fm != ~0ull) res.md = s_d[3];
+  res.last.chained = ds->fc.last_chained;
+  res.nops = ds->nsel3;
+  res.klast = lo >= 0 ? s_d[4].f1 - ri : 0;
+  res.errflag = ds->errflag;
+  *o = res;
+  ds->spec_n = (uint32_t)K;
+  *h = *ds;
+}
+
 // The index-gap rule (wal/wal.go:173) for each tile's first op whose
 // predecessor op lies in an earlier tile: the nearest earlier tile with ops
 // holds it (its last op's Index) -- in the same shard when that tile's last
@@ -444,12 +556,24 @@ __global__ __launch_bounds__(256) void k_fc_seam(const uint8_t *__restrict__ buf
                                                  const uint32_t *__restrict__ g_shift,
                                                  const TileRec *__restrict__ trec,
                                                  const ewal_entry *__restrict__ ents, uint64_t ri_one, uint64_t ccap,
-                                                 uint64_t ecap, Small *ds, SegArgs sg) {
+                                                 uint64_t ecap, Small *ds, SegArgs sg,
+                                                 const uint32_t *__restrict__ mlist, ResultDev *o, Small *h) {
   __shared__ unsigned long long s_fail;
   __shared__ uint32_t s_red[5];   // last entry + 1, last state + 1, ~first meta, last op + 1, ops
-  if (!fc_ran(ds, ccap, ecap)) return;
+  __shared__ uint32_t s_last;
+  __shared__ uint4 s_w[SEG ? 1 : 256][6];
+  __shared__ RecDesc s_d[SEG ? 1 : 6];
+  if (!fc_ran(ds, ccap, ecap)) {   // single WAL: the verdict "general path" to the host
+    if (!SEG && blockIdx.x == 0 && threadIdx.x == 0) {
+      ds->spec_n = 0;
+      *h = *ds;
+    }
+    return;
+  }
   const uint64_t K = ds->total;
   const uint32_t ntiles = (uint32_t)((K + FC_TILE - 1) / FC_TILE);
+  const uint32_t nblocks = (ntiles + blockDim.x - 1) / blockDim.x;   // the grid is sized for the capacity
+  if (blockIdx.x >= nblocks) return;
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   if (!SEG) {
     if (threadIdx.x == 0) {
@@ -541,74 +665,15 @@ __global__ __launch_bounds__(256) void k_fc_seam(const uint8_t *__restrict__ buf
       if (s_red[2]) atomicMax(&ds->fc.meta_inv, ~(unsigned long long)(uint32_t)~s_red[2]);
       if (s_red[3]) atomicMax(&ds->lastop, s_red[3]);
       if (s_red[4]) atomicAdd(&ds->nsel3, s_red[4]);
+      __threadfence();
+      s_last = atomicAdd(&ds->fc_done, 1u) == nblocks - 1;
     }
-  }
-}
-
-// After k_fc (one workgroup): does the regular case hold?  Then ReadAll's
-// metadata rule (wal/wal.go:178-183) over the listed metadata frames and the
-// ResultDev gather k_result makes on the general path (the few frames it
-// needs re-read in parallel); spec_n = frames, or 0 (the host takes the
-// general path); Small -> host-mapped memory.
-__global__ __launch_bounds__(256) void k_result_fc(const uint8_t *__restrict__ buf, uint64_t B,
-                                                   const uint64_t *__restrict__ cpos, uint64_t ccap, uint64_t ecap,
-                                                   uint64_t ri, const uint32_t *__restrict__ mlist, Small *ds,
-                                                   ResultDev *o, Small *h) {
-  __shared__ uint4 s_w[256][6];
-  __shared__ RecDesc s_d[6];
-  const uint64_t K = ds->total;
-  if (!fc_valid(ds, ccap, ecap)) {
     __syncthreads();
-    if (threadIdx.x == 0) {
-      ds->spec_n = 0;
-      *h = *ds;
-    }
-    return;
-  }
-  const uint32_t tid = threadIdx.x;
-  const uint64_t fm = ds->fc.meta_inv ? ~ds->fc.meta_inv : ~0ull;
-  if (fm != ~0ull && ds->nmeta > 1) {
-    const RecDesc m = fc_frame_fields(buf, B, cpos[fm], s_w[tid]);
-    for (uint32_t i = tid; i < ds->nmeta; i += blockDim.x) {
-      const uint32_t r = mlist[i];
-      if (r <= fm) continue;
-      const RecDesc d = fc_frame_fields(buf, B, cpos[r], s_w[tid]);
-      bool eq = d.dlen == m.dlen;
-      for (uint64_t k = 0; eq && k < d.dlen; ++k) eq = buf[d.doff + k] == buf[m.doff + k];
-      if (!eq) atomicMax(&ds->fc.fail_inv, ~(((unsigned long long)r << 8) | EWAL_ERR_METADATA_CONFLICT));
+    if (s_last) {   // the last workgroup: every tile's reductions are in
+      __threadfence();
+      fc_result(buf, B, cpos, ccap, ecap, ri_one, mlist, ds, o, h, s_w, s_d);
     }
   }
-  __threadfence();
-  __syncthreads();
-  // the frames the result needs: first failure, last entry, last state,
-  // first metadata, last op -- one thread each
-  const unsigned long long key = ds->fc.fail_inv ? ~ds->fc.fail_inv : ~0ull;
-  const long long le = (long long)ds->fc.last_entry1 - 1, ls = (long long)ds->fc.last_state1 - 1;
-  const long long lo = (long long)ds->lastop - 1;
-  const long long want[5] = {key != ~0ull ? (long long)(key >> 8) : -1, le, ls, fm != ~0ull ? (long long)fm : -1, lo};
-  if (tid < 5 && want[tid] >= 0) s_d[tid] = fc_frame_fields(buf, B, cpos[want[tid]], s_w[tid]);
-  __syncthreads();
-  if (tid != 0) return;
-  ResultDev res;
-  memset(&res, 0, sizeof(res));
-  res.agg.first_fail = key != ~0ull ? (key >> 8) : ~0ull;
-  res.agg.last_entry = le;
-  res.agg.last_state = ls;
-  res.agg.first_meta = fm;
-  if (key != ~0ull) {
-    res.fail = s_d[0];
-    res.fail.st = (int32_t)(key & 0xff);
-  }
-  if (le >= 0) res.lastent = s_d[1];
-  if (ls >= 0) res.sd = s_d[2];
-  if (fm != ~0ull) res.md = s_d[3];
-  res.last.chained = ds->fc.last_chained;
-  res.nops = ds->nsel3;
-  res.klast = lo >= 0 ? s_d[4].f1 - ri : 0;
-  res.errflag = ds->errflag;
-  *o = res;
-  ds->spec_n = (uint32_t)K;
-  *h = *ds;
 }
 
 // ---- batched ReadAll (ewal_readall_batch_device) on the fused pass --------

@@ -1371,6 +1371,7 @@ __global__ void k_reset_check(Small *ds) {
   ds->irregular = 0;
   ds->segbad = 0;
   ds->spec_n = 0;
+  ds->fc_done = 0;
   ds->fc.fail_inv = 0;
   ds->fc.meta_inv = 0;
   ds->fc.last_entry1 = 0;
