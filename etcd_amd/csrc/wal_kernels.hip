@@ -122,7 +122,10 @@ __device__ __forceinline__ uint32_t load_word_guarded(const uint8_t *buf, uint64
 __device__ __forceinline__ uint32_t cand_filter(const uint32_t (&D)[19]) {
   //   z   = (x ^ 08..) | y             bitop3 0xDE ((a ^ c) | b)
   //   acc = ((z - 01..) & ~z) | acc    bitop3 0xBA ((a & ~b) | c)
-  uint32_t acc0 = 0, acc1 = 0;
+  // One accumulator per group of four dwords (J = 4g .. 4g+3), packed at
+  // the end into bit 7 - g of every byte, so find_cands runs the exact test
+  // only on the groups that hit (+6 VALU here, ~3/4 of the exact tests gone).
+  uint32_t r = 0, acc = 0;
 #pragma unroll
   for (int J = 0; J < 16; J += 2) {
     const uint32_t y0 = __builtin_amdgcn_alignbyte(D[J + 2], D[J + 1], 3);
@@ -130,10 +133,14 @@ __device__ __forceinline__ uint32_t cand_filter(const uint32_t (&D)[19]) {
     const uint32_t z0 = __builtin_amdgcn_bitop3_b32(D[J + 2], y0, 0x08080808u, 0xDE);
     const uint32_t z1 = __builtin_amdgcn_bitop3_b32(D[J + 3], y1, 0x08080808u, 0xDE);
     const uint64_t s = (((uint64_t)z1 << 32) | z0) + 0xFEFEFEFEFEFEFEFFull;
-    acc0 = __builtin_amdgcn_bitop3_b32((uint32_t)s, z0, acc0, 0xBA);
-    acc1 = __builtin_amdgcn_bitop3_b32((uint32_t)(s >> 32), z1, acc1, 0xBA);
+    const uint32_t a0 = __builtin_amdgcn_bitop3_b32((uint32_t)s, z0, (J & 2) ? acc : 0u, 0xBA);
+    acc = __builtin_amdgcn_bitop3_b32((uint32_t)(s >> 32), z1, a0, 0xBA);
+    if (J & 2) {   // group g = J >> 2 complete: into bit 7 - g, (a & b) | c
+      const int g = J >> 2;
+      r = g == 0 ? (acc & 0x80808080u) : __builtin_amdgcn_bitop3_b32(acc >> g, 0x80808080u >> g, r, 0xEA);
+    }
   }
-  return (acc0 | acc1) & 0x80808080u;
+  return r;
 }
 
 __device__ __forceinline__ uint32_t count_cands(const uint32_t (&D)[19], uint64_t off, uint64_t B) {
@@ -251,8 +258,8 @@ __device__ __forceinline__ void crc_pieces(const uint8_t *s_slice, const uint32_
 
 // Exact test at every filter hit of a lane's piece; records the first two
 // candidate offsets (12-bit, inside the unit) in registers.
-__device__ __forceinline__ uint32_t find_cands(const uint32_t (&D)[19], uint64_t off, uint64_t B, uint32_t unit_off,
-                                               uint32_t &pa, uint32_t &pb) {
+__device__ __forceinline__ uint32_t find_cands(const uint32_t (&D)[19], uint32_t fm, uint64_t off, uint64_t B,
+                                               uint32_t unit_off, uint32_t &pa, uint32_t &pb) {
   uint32_t n = 0;
 #define CAND_ACTION                                                  \
   {                                                                  \
@@ -261,8 +268,11 @@ __device__ __forceinline__ uint32_t find_cands(const uint32_t (&D)[19], uint64_t
     pa = (n == 0) ? q_ : pa;                                         \
     ++n;                                                             \
   }
-  CAND_TEST(0) CAND_TEST(1) CAND_TEST(2) CAND_TEST(3) CAND_TEST(4) CAND_TEST(5) CAND_TEST(6) CAND_TEST(7)
-  CAND_TEST(8) CAND_TEST(9) CAND_TEST(10) CAND_TEST(11) CAND_TEST(12) CAND_TEST(13) CAND_TEST(14) CAND_TEST(15)
+  // only the dword groups cand_filter flagged (bit 7 - g of some byte of fm)
+  if (fm & 0x80808080u) { CAND_TEST(0) CAND_TEST(1) CAND_TEST(2) CAND_TEST(3) }
+  if (fm & 0x40404040u) { CAND_TEST(4) CAND_TEST(5) CAND_TEST(6) CAND_TEST(7) }
+  if (fm & 0x20202020u) { CAND_TEST(8) CAND_TEST(9) CAND_TEST(10) CAND_TEST(11) }
+  if (fm & 0x10101010u) { CAND_TEST(12) CAND_TEST(13) CAND_TEST(14) CAND_TEST(15) }
 #undef CAND_ACTION
   return n;
 }
@@ -296,6 +306,9 @@ __device__ __forceinline__ void row_transpose(uint32_t (&D)[19]) {
 // frame-start candidates -> slots[] / wcnt[] (the unit's candidate count,
 // from lane 63).  The 4 KiB aggregates are formed from v[] by k_uscan, where
 // one lane per unit does it with every lane busy.
+#ifndef EW_XS
+#define EW_XS 0   // timing-only k_stream ablations (tools/): 1 no CRC, 2 no candidates, 4 no v stores; results are wrong
+#endif
 template <int NU, bool FIND>
 __device__ __forceinline__ void stream_units(const StreamArgs &a, const uint8_t *s_slice, const uint32_t *s_s64,
                                              const uint32_t *s_s128, const uint32_t (&Lt)[4],
@@ -306,9 +319,14 @@ __device__ __forceinline__ void stream_units(const StreamArgs &a, const uint8_t 
   // place in the CRC chains' LDS shadows
   uint32_t fm[NU];
 #pragma unroll
-  for (int i = 0; i < NU; ++i) fm[i] = FIND ? cand_filter(D[i]) : 0u;
+  for (int i = 0; i < NU; ++i) fm[i] = (FIND && !(EW_XS & 2)) ? cand_filter(D[i]) : 0u;
   uint32_t c[NU];
-  crc_pieces<NU>(s_slice, Lt, D, c);
+  if (EW_XS & 1) {   // timing-only ablation: no CRC
+#pragma unroll
+    for (int i = 0; i < NU; ++i) c[i] = D[i][0] ^ D[i][5] ^ D[i][10] ^ D[i][15];
+  } else {
+    crc_pieces<NU>(s_slice, Lt, D, c);
+  }
   // lin of every 256-B super-piece (lanes 4m .. 4m+3) by a two-level tree,
   // branch-free: the lanes that do not combine look up entry 0 (one address,
   // a broadcast, no extra bank cycles).  Lane 4m+3 ends with the value.
@@ -328,14 +346,15 @@ __device__ __forceinline__ void stream_units(const StreamArgs &a, const uint8_t 
   // plain stores (measured a little faster than nontemporal ones here)
   if (top) {
 #pragma unroll
-    for (int i = 0; i < NU; ++i) a.v[(uint64_t)u[i] * EW_VPU + (lane >> 2)] = c[i];
+    for (int i = 0; i < NU; ++i)
+      if (!(EW_XS & 4) || c[i] == 0x12345678u) a.v[(uint64_t)u[i] * EW_VPU + (lane >> 2)] = c[i];
   }
   if (!FIND) return;
 #pragma unroll
   for (int i = 0; i < NU; ++i) {
     const uint64_t off = (uint64_t)u[i] * EW_WAVE_BYTES + (uint64_t)lane * EW_PIECE;
     uint32_t cnt = 0, pa = 0, pb = 0;
-    if (fm[i] && off < B) cnt = find_cands(D[i], off, B, (uint32_t)(lane * EW_PIECE), pa, pb);
+    if (fm[i] && off < B) cnt = find_cands(D[i], fm[i], off, B, (uint32_t)(lane * EW_PIECE), pa, pb);
     uint32_t ci = 0;
     if (__ballot(cnt != 0)) {   // wave-uniform: most 4 KiB units hold no frame start
       ci = wave_incl_sum(cnt);
