@@ -148,6 +148,36 @@ def test_noncanonical_frames_mid_wal(ctx, style):
     assert_parity(ctx, m2.buf[:-1], 1)
 
 
+@pytest.mark.parametrize("style", ["crc_first", "long_type", "data_first"])
+def test_noncanonical_frames_in_units_without_candidates(ctx, style):
+    """Large non-canonical frames (k_walk) whose frame and data starts lie in
+    4 KiB units holding no frame-start candidate: the stream pass writes no
+    super-piece lins there, so P comes from the unit start (prefix_slow).
+    A corruption inside such a frame's Data is found at the same frame."""
+    rng = random.Random(7 + len(style))
+    m = MixedWal()
+    m.canonical(4, None)
+    m.canonical(1, b"metadata")
+    idx = 1
+    walked = []
+    for seg in range(4):
+        for _ in range(3):
+            m.entry(idx, rng.randbytes(rng.randrange(5000, 14000)))
+            idx += 1
+        for _ in range(2):
+            walked.append((len(m.buf), rng.randrange(6000, 11000)))
+            m.entry(idx, rng.randbytes(walked[-1][1]), style)
+            idx += 1
+    m.canonical(3, O.hardstate_marshal(1, 1, idx - 1))
+    o, g = assert_parity(ctx, m.buf, 1)
+    assert o["status"] == O.OK and g["n_records"] == o["n_records"]
+    for at, n in walked[1::3]:
+        bad = bytearray(m.buf)
+        bad[at + 40 + n // 2] ^= 0x20        # inside the walked frame's Data
+        o, g = assert_parity(ctx, bad, 1)
+        assert o["status"] == O.ERR_RECORD_CRC
+
+
 def test_noncanonical_entry_payload_types(ctx):
     """A non-canonical walked frame whose payload fails mustUnmarshalEntry /
     has an unexpected type / fails its CRC: ReadAll stops at it."""

@@ -1,0 +1,6 @@
+# GPU suite on the v[]-only-where-read build, then A/B against HEAD
+set -e
+mkdir -p gpurun_out
+timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/pytest_gpu19.txt 2>&1
+bash tools/ab_quick.sh "ablibs/libewal_A.so ablibs/libewal_B.so" 3 "wal shards" > gpurun_out/ab19.log 2>&1
+timeout -k 10 600 python3 tools/ab_crcstream.py ablibs/libewal_A.so ablibs/libewal_B.so >> gpurun_out/ab19.log 2>&1
