@@ -1444,11 +1444,15 @@ __device__ __forceinline__ int pb_field_fast(const uint32_t *w, int o, uint32_t 
 // the data start (Pfd, when type != 4 and Data is not empty).  The frame
 // head and prefix_at's operands are loaded together, one memory round trip.
 // w: this thread's LDS window column (stride WS dwords).
-template <int WS>
+struct NoOp {
+  __device__ void operator()() const {}
+};
+template <int WS, class AfterIssue = NoOp>
 __device__ __forceinline__ bool decode_canon(const uint8_t *__restrict__ buf, uint64_t B, uint64_t p,
                                              const uint32_t *__restrict__ pwave, const uint32_t *__restrict__ v,
                                              const uint32_t *s_t4, const uint32_t *s_svp, uint32_t *w, RecDesc &d,
-                                             int64_t &L, uint32_t &Pfo, uint32_t &Pfd, bool noprefix = false) {
+                                             int64_t &L, uint32_t &Pfo, uint32_t &Pfd, bool noprefix = false,
+                                             AfterIssue after_issue = AfterIssue()) {
   const uint64_t p16 = p & ~15ull;
   uint4 hq[5];
 #pragma unroll
@@ -1465,6 +1469,7 @@ __device__ __forceinline__ bool decode_canon(const uint8_t *__restrict__ buf, ui
   }
   PrefixIn pin;
   prefix_load(p, pwave, v, buf, pin);
+  after_issue();   // the caller's stores: issued behind this frame's loads, so waiting for them never waits for those
 #pragma unroll
   for (int k = 0; k < 5; ++k) {
     w[(4 * k) * WS] = hq[k].x; w[(4 * k + 1) * WS] = hq[k].y;
