@@ -282,15 +282,15 @@ static int run_stream(ewal_ctx *c, DevTables *tb, const uint8_t *d_buf, uint64_t
   s.ovf = find_cand ? c->ovf.as<uint32_t>() : nullptr;
   s.novf = &ds->novf;
   // one wave per 1 MiB tile: k_uagg one 16-wave workgroup per CU (its S_256
-  // table fills the LDS), k_uapply four waves per workgroup
+  // table fills the LDS), k_uapply likewise (one staging of its tables per CU)
   const unsigned agrid = std::min<uint32_t>((nstiles + 15) / 16, (uint32_t)c->num_cu);
-  const unsigned sgrid = std::min<uint32_t>((nstiles + 3) / 4, 8u * (uint32_t)c->num_cu);
+  const unsigned sgrid = std::min<uint32_t>((nstiles + 15) / 16, (uint32_t)c->num_cu);
   hipLaunchKernelGGL(k_uagg, dim3(agrid), dim3(1024), 0, c->stream, s);
   const uint32_t ngroups = (nstiles + 1023) / 1024;
   if (ngroups > 1024) return EWAL_E_INVAL;   // k_tfix: at most 1024 tile groups (1 TiB)
   hipLaunchKernelGGL(k_tscan, dim3(ngroups), dim3(1024), 0, c->stream, s);
   hipLaunchKernelGGL(k_tfix, dim3(ngroups), dim3(1024), 0, c->stream, s, ngroups);
-  hipLaunchKernelGGL(k_uapply, dim3(sgrid), dim3(256), 0, c->stream, s);
+  hipLaunchKernelGGL(k_uapply, dim3(sgrid), dim3(1024), 0, c->stream, s);
   EW_CHECK(hipGetLastError());
   // units with more than EW_SLOTS candidates (ds->novf) are left out of cpos
   // here: k_frame then declines to speculate and the host runs k_rescan

@@ -262,10 +262,6 @@ __global__ __launch_bounds__(FC_THREADS, FC_WGS) void k_fc(FcArgs a, SegArgs sg)
     if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(&ds->fc.rare, 4u);
     return;
   }
-  stage_lds<FC_THREADS>(s_t4, 16 * 256, [&](int i) { return a.g_slice[i]; });
-  stage_lds<FC_THREADS>(s_svp, 1024, [&](int i) { return a.g_shift[EW_VLOG * 1024 + i]; });
-  stage_lds<FC_THREADS>(s_nib, FC_NIB_LEVELS * 128, [&](int i) { return nib_src(a.g_shift, i); });
-  __syncthreads();   // the only barrier: every wave runs its own tiles from here on
   const int tid = threadIdx.x, lane = tid & 63;
   const uint32_t K32 = (uint32_t)K;
   const uint32_t ntiles = (K32 + FC_TILE - 1) / FC_TILE;
@@ -286,7 +282,11 @@ __global__ __launch_bounds__(FC_THREADS, FC_WGS) void k_fc(FcArgs a, SegArgs sg)
   const uint32_t tbeg = SEG ? min(wid * chunk, ntiles) : wid;
   const uint32_t tend = SEG ? min(tbeg + chunk, ntiles) : ntiles;
   const uint32_t tstep = SEG ? 1u : nwaves;
-  if (tbeg < tend) cand(tbeg, p_nx, pn_nx);
+  if (tbeg < tend) cand(tbeg, p_nx, pn_nx);   // in flight while the tables are staged
+  stage_lds<FC_THREADS>(s_t4, 16 * 256, [&](int i) { return a.g_slice[i]; });
+  stage_lds<FC_THREADS>(s_svp, 1024, [&](int i) { return a.g_shift[EW_VLOG * 1024 + i]; });
+  stage_lds<FC_THREADS>(s_nib, FC_NIB_LEVELS * 128, [&](int i) { return nib_src(a.g_shift, i); });
+  __syncthreads();   // the only barrier: every wave runs its own tiles from here on
   uint32_t ash = EW_NIL, alo = 0;                 // SEG: the shard folded so far and its reductions
   unsigned long long aff = ~0ull, afm = ~0ull;
   long long ale = -1, als = -1;

@@ -389,10 +389,6 @@ __global__ __launch_bounds__(EW_THREADS, 1) void k_stream(StreamArgs a) {
   const int tid = threadIdx.x, lane = tid & 63;
   static_assert(sizeof(Small) % 4 == 0 && sizeof(Small) / 4 <= EW_THREADS, "Small is zeroed by one workgroup");
   if (blockIdx.x == 0 && tid < (int)(sizeof(Small) / 4)) ((uint32_t *)a.small)[tid] = 0u;   // the call's scratch
-  stage_lds<EW_THREADS>((uint32_t *)s_slice, EW_SLICE_DWORDS, [&](int i) { return a.g_slice[slice_src(i)]; });
-  stage_lds<EW_THREADS>(s_s64, 1024, [&](int i) { return a.g_shift[6 * 1024 + i]; });
-  stage_lds<EW_THREADS>(s_s128, 1024, [&](int i) { return a.g_shift[7 * 1024 + i]; });
-  __syncthreads();
   uint32_t Lt[4];
   lane_regs(lane, Lt);
   const uint64_t B = a.B;
@@ -445,10 +441,14 @@ __global__ __launch_bounds__(EW_THREADS, 1) void k_stream(StreamArgs a) {
   };
   uint32_t DA[2][19], DB[2][19], DC[2][19];
   ew_v3u nA, nB, nC;
-  if (npairs) {
+  if (npairs) {   // the first two pairs are in flight while the tables are staged
     load_pair(pair_at(0), DA, nA);
     load_pair(pair_at(1), DB, nB);
   }
+  stage_lds<EW_THREADS>((uint32_t *)s_slice, EW_SLICE_DWORDS, [&](int i) { return a.g_slice[slice_src(i)]; });
+  stage_lds<EW_THREADS>(s_s64, 1024, [&](int i) { return a.g_shift[6 * 1024 + i]; });
+  stage_lds<EW_THREADS>(s_s128, 1024, [&](int i) { return a.g_shift[7 * 1024 + i]; });
+  __syncthreads();
   // sched_barrier: each batch of loads stays ahead of the previous pair's arithmetic
   for (uint32_t k = 0; k < npairs; k += 3) {   // A is processed while B and C load, and so on
     load_pair(pair_at(k + 2), DC, nC);
@@ -509,17 +509,12 @@ __global__ __launch_bounds__(1024, 1) void k_uagg(ScanArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t s_s256[EW_SLICE_DWORDS * 4];   // S_256, perm layout
   __shared__ uint32_t s_sh[7 * 1024];             // S_{2^12} .. S_{2^18}
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  stage_lds<1024>((uint32_t *)s_s256, EW_SLICE_DWORDS, [&](int i) { return a.g_shift[shift_src(EW_VLOG, i)]; });
-  stage_lds<1024>(s_sh, 7 * 1024, [&](int i) { return a.g_shift[12 * 1024 + i]; });
-  __syncthreads();
-  uint32_t Lt[4];
-  lane_regs(lane, Lt);
-  for (uint32_t t = blockIdx.x * 16 + wv; t < a.ntiles; t += gridDim.x * 16) {
+  uint4 q[4][4];
+  uint32_t c[4];
+  auto load_tile = [&](uint32_t t) {   // every load of the tile up front
     const uint32_t u0 = t * EW_TILE_UNITS + lane;
-    uint4 q[4][4];
-    uint32_t c[4];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {   // every load of the tile up front
+    for (int r = 0; r < 4; ++r) {
       const uint32_t u = u0 + 64 * r;
       const bool in = u < a.nunits;
       const uint4 *vq = (const uint4 *)(a.v + (size_t)(in ? u : 0) * EW_VPU);
@@ -527,6 +522,17 @@ __global__ __launch_bounds__(1024, 1) void k_uagg(ScanArgs a) {
       for (int g = 0; g < 4; ++g) q[r][g] = in ? vq[g] : make_uint4(0, 0, 0, 0);
       c[r] = in ? a.wcnt[u] : 0u;
     }
+  };
+  const uint32_t t0 = blockIdx.x * 16 + wv, tstride = gridDim.x * 16;
+  if (t0 < a.ntiles) load_tile(t0);   // in flight while the tables are staged
+  stage_lds<1024>((uint32_t *)s_s256, EW_SLICE_DWORDS, [&](int i) { return a.g_shift[shift_src(EW_VLOG, i)]; });
+  stage_lds<1024>(s_sh, 7 * 1024, [&](int i) { return a.g_shift[12 * 1024 + i]; });
+  __syncthreads();
+  uint32_t Lt[4];
+  lane_regs(lane, Lt);
+  for (uint32_t t = t0; t < a.ntiles; t += tstride) {
+    const uint32_t u0 = t * EW_TILE_UNITS + lane;
+    if (t != t0) load_tile(t);
     uint32_t x[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) x[r] = q[r][0].x;
@@ -662,14 +668,17 @@ __global__ __launch_bounds__(1024) void k_tfix(ScanArgs a, uint32_t ngroups) {
 // Lane l owns units 4 l .. 4 l + 3 of the wave's tile: Horner over them
 // (S_4096), wave scan of the 64 lane spans (S_{2^(14+d)}), lane start =
 // S_{2^14 l}(P at the tile start) ^ exclusive span, replay.
-__global__ __launch_bounds__(256) void k_uapply(ScanArgs a) {
+// One persistent 16-wave workgroup per CU (each stages the 28 KiB of tables
+// once; four-wave workgroups, one per tile group, staged them 2048 times for
+// configs[1]).
+__global__ __launch_bounds__(1024) void k_uapply(ScanArgs a) {
   __shared__ uint32_t s_s12[1024];                // S_4096
   __shared__ uint32_t s_sh[6 * 1024];             // S_{2^14} .. S_{2^19}
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  stage_lds<256>(s_s12, 1024, [&](int i) { return a.g_shift[12 * 1024 + i]; });
-  stage_lds<256>(s_sh, 6 * 1024, [&](int i) { return a.g_shift[14 * 1024 + i]; });
+  stage_lds<1024>(s_s12, 1024, [&](int i) { return a.g_shift[12 * 1024 + i]; });
+  stage_lds<1024>(s_sh, 6 * 1024, [&](int i) { return a.g_shift[14 * 1024 + i]; });
   __syncthreads();
-  for (uint32_t t = blockIdx.x * 4 + wv; t < a.ntiles; t += gridDim.x * 4) {
+  for (uint32_t t = blockIdx.x * 16 + wv; t < a.ntiles; t += gridDim.x * 16) {
     const uint32_t u0 = t * EW_TILE_UNITS + 4 * lane;
     const bool full = u0 + 4 <= a.nunits;
     uint32_t x[4], c[4];
