@@ -753,10 +753,16 @@ __global__ __launch_bounds__(1024) void k_uapply(ScanArgs a) {
 #pragma unroll
           for (uint32_t m = 0; m < 8; ++m)
             if (m < cx && cbs[j] + m < a.ccap) a.cpos[cbs[j] + m] = ub + ((w4[m >> 1] >> (16 * (m & 1))) & 0xffffu);
-          if (cx > 8) {   // rare: more than 8 candidates in 4 KiB
-            const uint16_t *sl = a.slots + (size_t)u * EW_SLOTS;
-            for (uint32_t m = 8; m < cx; ++m)
-              if (cbs[j] + m < a.ccap) a.cpos[cbs[j] + m] = ub + sl[m];
+          if (cx > 8) {   // more than 8 candidates in 4 KiB (small records): the rest of the
+                          // slot line in three loads up front (a load / store loop here waits on
+                          // every load in turn: cpos may alias slots)
+            const uint4 *sq = (const uint4 *)(a.slots + (size_t)u * EW_SLOTS);
+            const uint4 t1 = sq[1], t2 = sq[2], t3 = sq[3];
+            const uint32_t w24[12] = {t1.x, t1.y, t1.z, t1.w, t2.x, t2.y, t2.z, t2.w, t3.x, t3.y, t3.z, t3.w};
+#pragma unroll
+            for (uint32_t m = 8; m < EW_SLOTS; ++m)
+              if (m < cx && cbs[j] + m < a.ccap)
+                a.cpos[cbs[j] + m] = ub + ((w24[(m - 8) >> 1] >> (16 * (m & 1))) & 0xffffu);
           }
         }
       }
