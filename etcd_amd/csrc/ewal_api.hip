@@ -1324,8 +1324,10 @@ int ewal_ctx_create(int device, ewal_ctx **out) {
     c->num_cu = prop.multiProcessorCount;
   EW_CHECK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
   c->own_stream = true;
+#ifdef EW_ABLATION_HOOKS   // timing experiments only (tools/fc_ablate.py): results are wrong under ablation
   if (const char *e = std::getenv("EWAL_STREAM_ABLATE")) c->ablate = std::atoi(e);
   if (const char *e = std::getenv("EWAL_FC_ABLATE")) c->fc_ablate = (uint32_t)std::atoi(e);
+#endif
   if (const char *e = std::getenv("EWAL_FRAME_WG")) c->frame_wg = std::max(1, std::min(16, std::atoi(e)));
   if (const char *e = std::getenv("EWAL_FUSED")) c->fused = std::atoi(e) != 0;
   EW_CHECK(hipEventCreate(&c->ev0));

@@ -1,6 +1,8 @@
 """k_fc ablation timing (diagnostic; results are wrong under ablation):
 pipeline device ms of one ReadAll / one batched ReadAll per EWAL_FC_ABLATE
-value (1 shift, 2 prefixes, 4 look-back, 8 ents stores, 16 no failure reports)."""
+value (1 shift, 2 prefixes, 4 look-back, 8 ents stores, 16 no failure reports).
+The product build ignores EWAL_FC_ABLATE: build the library with
+-DEW_ABLATION_HOOKS (etcd_amd/build.sh -DEW_ABLATION_HOOKS) for these runs."""
 import ctypes as C
 import os
 import sys
