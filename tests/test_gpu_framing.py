@@ -243,3 +243,24 @@ def test_pointer_jumping_64mib(ctx):
         assert (r.status, r.fail_record) == (ob["status"], ob["fail_record"])
         if ob["status"] == O.OK:
             assert (r.n_records, r.last_crc, r.enti) == (ob["n_records"], ob["last_crc"], ob["enti"])
+
+
+def test_entries_beyond_the_ternary_shift_span(ctx):
+    """Entries whose Data is 170-600 KB long: k_fc applies S_n for n below
+    3^11 = 177147 by ternary digits from LDS and the rest from the global
+    binary tables; every chained CRC and a corruption inside such an entry
+    must match the oracle (record.pb.go Data, pkg/crc chaining)."""
+    rng = random.Random(11)
+    e = O.WalEncoder(0)
+    e.save_crc(0)
+    e.encode(1, b"metadata")
+    sizes = [177147 - 40, 177147, 177147 + 5, 200000, 354294, 600000, 3, 65536, 531441]
+    for i, n in enumerate(sizes):
+        e.save_entry(0, 1, i + 1, rng.randbytes(n))
+    buf = e.getvalue()
+    o, g = assert_parity(ctx, buf, 1)
+    assert o["status"] == O.OK and g["n_records"] == o["n_records"]
+    bad = bytearray(buf)
+    bad[len(bad) * 2 // 3] ^= 0x01
+    o, g = assert_parity(ctx, bad, 1)
+    assert o["status"] != O.OK
