@@ -34,6 +34,19 @@
 #include "ewal_device.h"
 #include "ewal_internal.h"
 
+// The single WAL's ents are written with nontemporal stores (40 B per op,
+// read back only by the host's copy or the next call): configs[1]
+// post-stream -8 us; the batched path keeps plain stores (+1-2 % with
+// nontemporal ones, profiles/r02/ab_nt_ents.txt).
+__device__ __forceinline__ void store_entry_nt(ewal_entry *dst, const ewal_entry &e) {
+  uint64_t *q = (uint64_t *)dst;
+  __builtin_nontemporal_store(e.term, q);
+  __builtin_nontemporal_store(e.index, q + 1);
+  __builtin_nontemporal_store(e.data_off, q + 2);
+  __builtin_nontemporal_store(e.data_len, q + 3);
+  __builtin_nontemporal_store(((uint64_t)(uint32_t)e.data_nil << 32) | (uint32_t)e.type, q + 4);
+}
+
 #define FC_THREADS 256
 #define FC_WAVES (FC_THREADS / 64)
 #define FC_WGS 3          // resident workgroups per CU (LDS ~49 KiB each)
@@ -322,7 +335,10 @@ __global__ __launch_bounds__(FC_THREADS, FC_WGS) void k_fc(FcArgs a, SegArgs sg)
     // store issued before them would be waited for with them: vmcnt counts
     // loads and stores in order)
     auto flush = [&]() {
-      if (pend) a.ents[pidx] = pe;
+      if (pend) {
+        if (SEG) a.ents[pidx] = pe;
+        else store_entry_nt(a.ents + pidx, pe);
+      }
       pend = false;
     };
     const bool ok = decode_canon<FC_THREADS>(a.buf, a.B, p, a.pwave, a.v, s_t4, s_svp, s_win + tid, d, L, Pfo, Pfd,
@@ -512,7 +528,10 @@ __global__ __launch_bounds__(FC_THREADS, FC_WGS) void k_fc(FcArgs a, SegArgs sg)
       }
     }
   }
-  if (pend) a.ents[pidx] = pe;
+  if (pend) {
+    if (SEG) a.ents[pidx] = pe;
+    else store_entry_nt(a.ents + pidx, pe);
+  }
   if (SEG) aflush();
   // flags of every lane, then one atomic per wave
   uint32_t rr = rare;
