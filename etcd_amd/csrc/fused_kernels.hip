@@ -300,6 +300,9 @@ __global__ __launch_bounds__(FC_THREADS, FC_WGS) void k_fc(FcArgs a, SegArgs sg)
   stage_lds<FC_THREADS>(s_svp, 1024, [&](int i) { return a.g_shift[EW_VLOG * 1024 + i]; });
   stage_lds<FC_THREADS>(s_nib, FC_NIB_LEVELS * 128, [&](int i) { return nib_src(a.g_shift, i); });
   __syncthreads();   // the only barrier: every wave runs its own tiles from here on
+  // SEG: the shard of the run's first tile, one search per wave (binary
+  // searches per tile were chains of dependent loads on every tile)
+  uint32_t scur = (SEG && tbeg < tend) ? shard_of(sg.fs, sg.ns, tbeg * FC_TILE) : 0u;
   uint32_t ash = EW_NIL, alo = 0;                 // SEG: the shard folded so far and its reductions
   unsigned long long aff = ~0ull, afm = ~0ull;
   long long ale = -1, als = -1;
@@ -363,13 +366,11 @@ __global__ __launch_bounds__(FC_THREADS, FC_WGS) void k_fc(FcArgs a, SegArgs sg)
     uint32_t sh = 0, lo = 0;                   // SEG: the frame's shard and its first frame
     uint64_t ri = a.ri;
     uint32_t sh0 = 0, sh1 = 0;
-    if (SEG) {   // the tile's shard range, searched by one lane
-      if (lane == 0) {
-        sh0 = shard_of(sg.fs, sg.ns, r0);
-        sh1 = shard_in(sg.fs, sh0, sg.ns, rl);
-      }
-      sh0 = (uint32_t)__shfl((int)sh0, 0);
-      sh1 = (uint32_t)__shfl((int)sh1, 0);
+    if (SEG) {   // the tile's shard range: the wave's run of tiles walks the shards forward
+      while (scur + 1 < sg.ns && sg.fs[scur + 1] <= r0) ++scur;   // (uniform; usually no step)
+      sh0 = scur;
+      sh1 = sh0;
+      while (sh1 + 1 < sg.ns && sg.fs[sh1 + 1] <= rl) ++sh1;
       sh = sh0 == sh1 ? sh0 : shard_in(sg.fs, sh0, sh1 + 1, r);
       lo = sg.fs[sh];
       ri = sg.ri[sh];
