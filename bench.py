@@ -1,14 +1,21 @@
 #!/usr/bin/env python3
 """bench.py -- etcd WAL replay-and-verify on MI355X (BASELINE.json metric).
 
-One step = one (*WAL).ReadAll (wal/wal.go:164-216) over a GPU-resident
-synthetic WAL of configs[1]: 8 GiB of mixed 64 B - 64 KiB entries
-(log-uniform sizes, xorshift payload) with one corrupt record at frame
-k = 0.73 N, so every step must report walpb.ErrCRCMismatch at frame k.
-The whole WAL is read and verified each step (the GPU pipeline does not
-stop early).  With --gpus N (torchrun), every rank verifies its own
-independent WAL shard (weak scaling) and one RCCL all-reduce per step
-combines {MIN first-corrupt key, SUM frames, SUM mismatches}.
+Default line (value, ms_per_step, roofline, cpu_baseline): configs[1] -- one
+step = one (*WAL).ReadAll (wal/wal.go:164-216) over a GPU-resident synthetic
+WAL of 8 GiB of mixed 64 B - 64 KiB entries (log-uniform sizes, xorshift
+payload) with one corrupt record at frame k = 0.73 N, so every step must
+report walpb.ErrCRCMismatch at frame k.  The whole WAL is read and verified
+each step (the GPU pipeline does not stop early).  The same line carries
+`configs`: every other BASELINE config timed in the same run, each with its
+own ms_per_step, roofline and (N=1) cpu_baseline --
+  c1      configs[0]: the 1M x 256 B WAL (wal.Save) replayed on the GPU
+  shards  configs[2]: 512 per-raft-group WALs x 64 MiB per GPU (4096 over
+          8 GPUs), one batched ReadAll per step, one RCCL all-reduce
+  snap    configs[3]: a resident batch of snapshot files, loadSnap's CRC
+  commit  configs[4]: maybeCommit over 1M raft groups x 5/7 voters
+With --gpus N (torchrun) every rank verifies its own independent shards
+(weak scaling) and one RCCL all-reduce per step combines the verdicts.
 
 Prints ONE JSON line on rank 0 (value = GB/s over all ranks, 1 GB = 1e9 B).
 """
@@ -51,6 +58,10 @@ def parse():
                          "restart = OpenAtIndex + ReadAll + materialise through the C ABI (the cgo shim's calls)")
     ap.add_argument("--shards-per-gpu", type=int, default=512)
     ap.add_argument("--shard-mib", type=int, default=64)
+    ap.add_argument("--configs", default="c1,shards,snap,commit",
+                    help="default line: the other BASELINE configs timed in the same run ('none' to skip)")
+    ap.add_argument("--sub-cpu-seconds", type=float, default=6.0,
+                    help="CPU-baseline time per leg of each `configs` sub-result")
     return ap.parse_args()
 
 
@@ -67,10 +78,13 @@ def load_traffic():
 METRIC = "WAL verify GB/s (and records/s) per GPU + 8-GPU node, % of HBM roofline"
 
 
+CPU_SHARE = 16   # the GPU box's CPU share per GPU (nproc / the CPU set show the whole machine's)
+
+
 def cpu_threads():
     """The host cores the CPU baselines may use: the process's CPU set,
-    capped at the box's 16-CPU share (nproc shows the whole machine)."""
-    return max(1, min(16, len(os.sched_getaffinity(0))))
+    capped at the box's per-GPU share of 16 CPUs."""
+    return max(1, min(CPU_SHARE, len(os.sched_getaffinity(0))))
 
 
 def host_info():
@@ -87,6 +101,8 @@ def host_info():
         pass
     go = shutil.which("go")
     return {"cpu_model": model, "nproc": os.cpu_count(), "cpus_allowed": len(os.sched_getaffinity(0)),
+            "cores_note": "multi-core legs use min(cpus_allowed, %d): the GPU box's CPU share per GPU, not every "
+                          "CPU of the host" % CPU_SHARE,
             "gomaxprocs": "n/a (no Go toolchain on this host; the C restatement is timed instead)" if not go else
                           "n/a (go at %s not used: the reference is not built here)" % go}
 
@@ -120,23 +136,38 @@ def timed(dist, steps, fn):
     return elapsed
 
 
-def run_shards(a, dist, rank, world, local):
+def run_shards(a, dist, rank, world, local, cpu_seconds=None):
     """configs[2]: 4096 per-raft-group WAL shards x 64 MiB over the node --
     each GPU replays its 512 (at N=8) in ONE batched ReadAll
     (ewal_readall_batch_device); entries 128 B - 4 KiB log-uniform, seed =
     global shard id; one corrupt record in global shard 2749 mod (512 N).
-    The verdicts cross ranks in one all-reduce (etcd_amd/shard.py)."""
+    The verdicts cross ranks in one all-reduce (etcd_amd/shard.py).  The
+    shards are generated and copied to HBM 64 at a time (host memory stays
+    at ~4 GiB per rank)."""
     nsh, smib = a.shards_per_gpu, a.shard_mib
+    cpu_seconds = a.cpu_seconds if cpu_seconds is None else cpu_seconds
     first = rank * nsh
     bad_shard = 2749 % (nsh * world)
     t = time.time()
-    blob, lens, nrec = W.synth_shards([first + i for i in range(nsh)], smib << 20, 128, 4096,
-                                      corrupt={bad_shard - first: 1000} if first <= bad_shard < first + nsh else {})
-    gen_s = time.time() - t
-    nb = len(blob)
+    target = smib << 20
+    chunk = 64
     ctx = W.Context(local)
-    dbuf = ctx.alloc(nb + 64)
-    dbuf.upload_ptr(C.addressof((C.c_char * nb).from_buffer(blob)), nb)
+    dbuf = ctx.alloc(nsh * (target + 2 * 4096 + 4096) + 64)
+    lens, nrec, pos, keep = [], [], 0, None
+    for c0 in range(0, nsh, chunk):
+        ids = list(range(c0, min(nsh, c0 + chunk)))
+        blob, ls, nr = W.synth_shards([first + i for i in ids], target, 128, 4096,
+                                      corrupt={bad_shard - first - c0: 1000}
+                                      if first + c0 <= bad_shard < first + c0 + len(ids) else {})
+        dbuf.upload_ptr(C.addressof((C.c_char * len(blob)).from_buffer(blob)), len(blob), pos)
+        pos += len(blob)
+        lens += ls
+        nrec += nr
+        if c0 == 0:
+            keep = blob     # the CPU baseline's sample
+        del blob
+    gen_s = time.time() - t
+    nb = pos
     ris = [1] * nsh
     res = None
     for _ in range(max(a.warmup, 1)):
@@ -163,155 +194,160 @@ def run_shards(a, dist, rank, world, local):
     elapsed = timed(dist, a.steps, step)
     ms = elapsed / a.steps * 1e3
     r0 = last["r"][0]
+    assert all((x.status, x.fail_record) == ((L.ERR_RECORD_CRC, 1000) if first + i == bad_shard else (L.OK, -1))
+               for i, x in enumerate(c_out))
     frames = sum(nrec)
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         from oracle import oracle as O   # baseline only
         nth = cpu_threads()
-        offs = [0]
-        for x in lens[:-1]:
-            offs.append(offs[-1] + x)
-        addr = C.addressof((C.c_char * nb).from_buffer(blob))
-        k = max(nth, min(nsh, 4 * nth))          # a bounded sample: k shards per pass
-        so, sl = offs[:k], lens[:k]
+        k = min(chunk, nsh)              # a bounded sample: the first chunk of shards
+        so = [0]
+        for x in lens[:k - 1]:
+            so.append(so[-1] + x)
+        sl = lens[:k]
         sb = sum(sl)
-        it, cs = timed_cpu(a.cpu_seconds, lambda: O.fast_readall_batch(addr, so, sl, 1, nth, faithful=True))
-        it2, cs2 = timed_cpu(a.cpu_seconds / 2, lambda: O.fast_readall_batch(addr, so, sl, 1, nth))
+        addr = C.addressof((C.c_char * len(keep)).from_buffer(keep))
+        it, cs = timed_cpu(cpu_seconds, lambda: O.fast_readall_batch(addr, so, sl, 1, nth, faithful=True))
+        it2, cs2 = timed_cpu(cpu_seconds / 2, lambda: O.fast_readall_batch(addr, so, sl, 1, nth))
         st, fr = O.fast_readall_batch(addr, so, sl, 1, nth)
         assert all(x in (O.OK, O.ERR_RECORD_CRC) for x in st), st
         cpu = dict(host_info(), **{
             "value": round(sb * it / cs / 1e9, 4), "unit": "GB/s", "cores": nth, "kind": "port",
-            "sample": "oracle/ or_readall (the faithful C restatement of wal.ReadAll) on all %d cores, one shard per "
+            "sample": "oracle/ or_readall (the faithful C restatement of wal.ReadAll) on %d cores, one shard per "
                       "worker, over the first %d shards (%.2f GiB), %d passes, %.1f s" % (nth, k, sb / (1 << 30), it, cs),
             "optimised": {"value": round(sb * it2 / cs2 / 1e9, 4), "unit": "GB/s", "cores": nth,
                           "sample": "oracle/ewal_cpu_fast.c orf_readall (3-stream SSE4.2 CRC-32C, no per-record "
                                     "allocation) one shard per worker, same shards, %d passes, %.1f s" % (it2, cs2)}})
-    if rank == 0:
-        out = {
-            "metric": METRIC, "value": round(world * nb / (ms / 1e3) / 1e9, 3), "unit": "GB/s", "n_gpus": world,
-            "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(ms, 4), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
-            "config": {"workload": "configs[2]: %d per-raft-group WAL shards x %d MiB per GPU (%d on 8 GPUs), entry "
-                                   "Data log-uniform 128 B-4 KiB, seed = shard id, one corrupt record in shard %d; one "
-                                   "batched ReadAll per GPU per step" % (nsh, smib, nsh * 8, bad_shard),
-                       "wal_bytes_per_gpu": nb, "frames_per_gpu": frames, "shards_per_gpu": nsh, "ri": 1,
-                       "parallelism": "dp%d (independent shards, one all-reduce of verdicts)" % world},
-            "records_per_s": round(world * frames / (ms / 1e3), 1),
-            "roofline": {"bound": "hbm", "achieved": round(nb / (r0.stream_ms / 1e3) / 1e9, 2),
-                         "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                         "frac": round(nb / (r0.stream_ms / 1e3) / 1e9 / HBM_PEAK_GBPS, 4), "traffic": None,
-                         "kernel": "k_stream", "kernel_ms": round(r0.stream_ms, 4),
-                         "algorithmic_bytes_per_launch": nb,
-                         "pipeline_achieved": round(nb / (r0.device_ms / 1e3) / 1e9, 2),
-                         "pipeline_frac": round(nb / (r0.device_ms / 1e3) / 1e9 / HBM_PEAK_GBPS, 4)},
-            "pipeline_device_ms": round(r0.device_ms, 4),
-            "cpu_baseline": cpu,
-            "gen_seconds": round(gen_s, 2),
-        }
-        print(json.dumps(out), flush=True)
+    del keep
+    out = {
+        "metric": METRIC, "value": round(world * nb / (ms / 1e3) / 1e9, 3), "unit": "GB/s", "n_gpus": world,
+        "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(ms, 4), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
+        "config": {"workload": "configs[2]: %d per-raft-group WAL shards x %d MiB per GPU (%d on 8 GPUs), entry "
+                               "Data log-uniform 128 B-4 KiB, seed = shard id, one corrupt record in shard %d; one "
+                               "batched ReadAll per GPU per step" % (nsh, smib, nsh * 8, bad_shard),
+                   "wal_bytes_per_gpu": nb, "frames_per_gpu": frames, "shards_per_gpu": nsh, "ri": 1,
+                   "parallelism": "dp%d (independent shards, one all-reduce of verdicts)" % world},
+        "records_per_s": round(world * frames / (ms / 1e3), 1),
+        "roofline": {"bound": "hbm", "achieved": round(nb / (r0.stream_ms / 1e3) / 1e9, 2),
+                     "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                     "frac": round(nb / (r0.stream_ms / 1e3) / 1e9 / HBM_PEAK_GBPS, 4), "traffic": None,
+                     "kernel": "k_stream", "kernel_ms": round(r0.stream_ms, 4),
+                     "algorithmic_bytes_per_launch": nb,
+                     "pipeline_achieved": round(nb / (r0.device_ms / 1e3) / 1e9, 2),
+                     "pipeline_frac": round(nb / (r0.device_ms / 1e3) / 1e9 / HBM_PEAK_GBPS, 4),
+                     "step_frac": round(nb / (ms / 1e3) / 1e9 / HBM_PEAK_GBPS, 4)},
+        "pipeline_device_ms": round(r0.device_ms, 4),
+        "cpu_baseline": cpu,
+        "gen_seconds": round(gen_s, 2),
+    }
     dbuf.free()
     ctx.close()
+    return out
 
 
-def run_snap(a, dist, rank, world, local):
+def run_snap(a, dist, rank, world, local, cpu_seconds=None):
     """configs[3]: batch verification of snap/snapshotter snapshot files
     (loadSnap's CRC, snap/snapshotter.go:76-111): sizes log-uniform 1-256 MiB
     (seed 4), ~1 % corrupt (seed 5, at least one).  The 10k-file set is
     ~450 GiB, more than one GPU holds: each GPU verifies a resident batch of
-    --size-gib (default 16 GiB) per step in ONE esnap_verify_packed call (8
-    GPUs: ~56 GiB each)."""
+    16 GiB (--size-gib when given) per step in ONE esnap_verify_packed call
+    (8 GPUs: ~56 GiB each).  Files go to HBM as they are made (host memory
+    stays at one file plus the CPU baseline's ~1 GiB sample)."""
     import math
     import random
     import numpy as np
     from etcd_amd import snap as S
+    cpu_seconds = a.cpu_seconds if cpu_seconds is None else cpu_seconds
     rng, crng = random.Random(4 + 7919 * rank), random.Random(5 + 7919 * rank)
     budget = int((a.size_gib if a.size_gib != 8.0 else 16.0) * (1 << 30))
     t = time.time()
     pool = np.random.default_rng(4 + rank).integers(0, 256, size=(256 << 20) + 4096, dtype=np.uint8).tobytes()
-    files, bad, total = [], [], 0
+    ctx = W.Context(local)
+    dbuf = ctx.alloc(budget + (257 << 20))
+    lens, bad, total, sample = [], [], 0, {}
     while total < budget:
         n = int(math.exp(rng.uniform(math.log(1 << 20), math.log(256 << 20))))
         st = rng.randrange(0, len(pool) - n)
-        f = bytearray(S.snap_file(S.snapshot_marshal(pool[st:st + n], (1, 2, 3), len(files) + 1, 1)))
+        f = bytearray(S.snap_file(S.snapshot_marshal(pool[st:st + n], (1, 2, 3), len(lens) + 1, 1)))
         if crng.random() < 0.01 or (not bad and total + len(f) >= budget):
             f[len(f) // 2] ^= 0x10      # inside Data: snap.ErrCRCMismatch
-            bad.append(len(files))
-        files.append(bytes(f))
+            bad.append(len(lens))
+        dbuf.upload(f, total)
+        if len(f) <= (8 << 20) and sum(len(x) for x in sample.values()) < (1 << 30):
+            sample[len(lens)] = bytes(f)   # the CPU baseline's sample: the small files, up to 1 GiB
+        lens.append(len(f))
         total += len(f)
-    lens = [len(f) for f in files]
+    del pool
     offs = [0]
     for x in lens[:-1]:
         offs.append(offs[-1] + x)
-    blob = b"".join(files)
-    del files
     gen_s = time.time() - t
-    nb = len(blob)
-    ctx = W.Context(local)
-    dbuf = ctx.alloc(nb + 64)
-    dbuf.upload(blob)
+    nb = total
     for _ in range(max(a.warmup, 1)):
         stt, _, _ = S.verify_packed(dbuf, nb, offs, lens)
     assert [i for i, x in enumerate(stt) if x != L.OK] == bad and all(stt[i] == L.ERR_SNAP_CRC for i in bad), bad
-    elapsed = timed(dist, a.steps, lambda: S.verify_packed(dbuf, nb, offs, lens))
+    last = {}
+
+    def step():
+        last["st"] = S.verify_packed(dbuf, nb, offs, lens)[0]
+
+    elapsed = timed(dist, a.steps, step)
+    assert [i for i, x in enumerate(last["st"]) if x != L.OK] == bad
     ms = elapsed / a.steps * 1e3
     kms = float(L.lib.ewal_last_stream_ms(ctx.handle))
     dev_ms = float(L.lib.ewal_last_device_ms(ctx.handle))
-    e2e = None
-    if not a.no_e2e:   # host -> HBM copy of the batch included (pageable host memory), one pass
-        t1 = time.perf_counter()
-        dbuf.upload(blob)
-        S.verify_packed(dbuf, nb, offs, lens)
-        e2e = round(nb / (time.perf_counter() - t1) / 1e9, 3)
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         from oracle import oracle as O   # baseline only
-        small = sorted(range(len(lens)), key=lambda i: lens[i])
-        pick, acc = [], 0
-        for i in small:
-            if acc >= (1 << 30):
-                break
-            pick.append(i)
-            acc += lens[i]
-        views = [blob[offs[i]:offs[i] + lens[i]] for i in pick]
+        views = list(sample.values())
+        acc = sum(len(v) for v in views)
 
         def one_pass():
             for v in views:
                 O.loadsnap(v)
-        it, cs = timed_cpu(a.cpu_seconds, one_pass)
+        it, cs = timed_cpu(cpu_seconds, one_pass)
         nth = cpu_threads()
+        blob = b"".join(views)
+        so = [0]
+        for v in views[:-1]:
+            so.append(so[-1] + len(v))
+        sl = [len(v) for v in views]
         addr = C.cast(C.c_char_p(blob), C.c_void_p).value   # blob's own bytes (no copy)
-        it2, cs2 = timed_cpu(a.cpu_seconds / 2, lambda: O.fast_snap_verify_batch(addr, offs, lens, nth))
-        st2, _ = O.fast_snap_verify_batch(addr, offs, lens, nth)
-        assert [i for i, x in enumerate(st2) if x != O.OK] == bad
+        it2, cs2 = timed_cpu(cpu_seconds / 2, lambda: O.fast_snap_verify_batch(addr, so, sl, nth))
+        st2, _ = O.fast_snap_verify_batch(addr, so, sl, nth)
+        assert [k for k, x in zip(sample, st2) if x != O.OK] == [k for k in sample if k in bad]
         cpu = dict(host_info(), **{
             "value": round(acc * it / cs / 1e9, 4), "unit": "GB/s", "cores": 1, "kind": "port",
             "sample": "oracle/ or_loadsnap (snappb + raftpb.Snapshot Unmarshal, crc32.Update, 1 thread) over "
-                      "%d of the files (%.2f GiB), %d passes, %.1f s" % (len(pick), acc / (1 << 30), it, cs),
-            "optimised": {"value": round(nb * it2 / cs2 / 1e9, 4), "unit": "GB/s", "cores": nth,
+                      "%d of the files (<= 8 MiB each, %.2f GiB), %d passes, %.1f s" % (len(views), acc / (1 << 30),
+                                                                                       it, cs),
+            "optimised": {"value": round(acc * it2 / cs2 / 1e9, 4), "unit": "GB/s", "cores": nth,
                           "sample": "oracle/ewal_cpu_fast.c orf_snap_verify_batch (envelope + 3-stream SSE4.2 "
-                                    "CRC-32C) one file per worker over all %d files, %d passes, %.1f s"
-                                    % (len(lens), it2, cs2)}})
-    if rank == 0:
-        print(json.dumps({
-            "metric": METRIC, "value": round(world * nb / (ms / 1e3) / 1e9, 3), "unit": "GB/s", "n_gpus": world,
-            "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(ms, 4), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
-            "config": {"workload": "configs[3]: snapshot batch verify, %d files per GPU (%.2f GiB resident), sizes "
-                                   "log-uniform 1-256 MiB, %d corrupt (snap.ErrCRCMismatch)" %
-                                   (len(lens), nb / (1 << 30), len(bad)),
-                       "snapshot_bytes_per_gpu": nb, "files_per_gpu": len(lens),
-                       "parallelism": "dp%d (independent files)" % world},
-            "files_per_s": round(world * len(lens) / (ms / 1e3), 1),
-            "roofline": {"bound": "hbm", "achieved": round(nb / (kms / 1e3) / 1e9, 2), "peak": HBM_PEAK_GBPS,
-                         "unit": "GB/s", "frac": round(nb / (kms / 1e3) / 1e9 / HBM_PEAK_GBPS, 4), "traffic": None,
-                         "kernel": "k_stream<false>", "kernel_ms": round(kms, 4),
-                         "algorithmic_bytes_per_launch": nb,
-                         "pipeline_achieved": round(nb / (dev_ms / 1e3) / 1e9, 2),
-                         "pipeline_frac": round(nb / (dev_ms / 1e3) / 1e9 / HBM_PEAK_GBPS, 4)},
-            "pipeline_device_ms": round(dev_ms, 4), "e2e_gbps_incl_h2d": e2e,
-            "cpu_baseline": cpu, "gen_seconds": round(gen_s, 2)}), flush=True)
+                                    "CRC-32C) one file per worker over the same files, %d passes, %.1f s"
+                                    % (it2, cs2)}})
+    out = {
+        "metric": METRIC, "value": round(world * nb / (ms / 1e3) / 1e9, 3), "unit": "GB/s", "n_gpus": world,
+        "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(ms, 4), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
+        "config": {"workload": "configs[3]: snapshot batch verify, %d files per GPU (%.2f GiB resident), sizes "
+                               "log-uniform 1-256 MiB, %d corrupt (snap.ErrCRCMismatch)" %
+                               (len(lens), nb / (1 << 30), len(bad)),
+                   "snapshot_bytes_per_gpu": nb, "files_per_gpu": len(lens),
+                   "parallelism": "dp%d (independent files)" % world},
+        "files_per_s": round(world * len(lens) / (ms / 1e3), 1),
+        "roofline": {"bound": "hbm", "achieved": round(nb / (kms / 1e3) / 1e9, 2), "peak": HBM_PEAK_GBPS,
+                     "unit": "GB/s", "frac": round(nb / (kms / 1e3) / 1e9 / HBM_PEAK_GBPS, 4), "traffic": None,
+                     "kernel": "k_stream<false>", "kernel_ms": round(kms, 4),
+                     "algorithmic_bytes_per_launch": nb,
+                     "pipeline_achieved": round(nb / (dev_ms / 1e3) / 1e9, 2),
+                     "pipeline_frac": round(nb / (dev_ms / 1e3) / 1e9 / HBM_PEAK_GBPS, 4)},
+        "pipeline_device_ms": round(dev_ms, 4),
+        "cpu_baseline": cpu, "gen_seconds": round(gen_s, 2)}
     dbuf.free()
     ctx.close()
+    return out
 
 
 def run_snapstream(a, dist, rank, world, local):
@@ -420,8 +456,7 @@ def run_snapstream(a, dist, rank, world, local):
     assert stt_all == want, "verdict mismatch"
     nbad = sum(1 for x in want if x != L.OK)
     used_total = sum(sum((plens[fi] + 15) & ~15 for fi in bt) for bt in batches)
-    if rank == 0:
-        print(json.dumps({
+    out = ({
             "metric": METRIC, "value": round(world * sbytes / el / 1e9, 3), "unit": "GB/s", "n_gpus": world,
             "steps": 1, "warmup": 0, "ms_per_step": round(el * 1e3, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
@@ -443,8 +478,9 @@ def run_snapstream(a, dist, rank, world, local):
                          "pipeline_achieved": round(used_total / (sum(dms) / 1e3) / 1e9, 2),
                          "pipeline_frac": round(used_total / (sum(dms) / 1e3) / 1e9 / HBM_PEAK_GBPS, 4),
                          "note": "streamed value is PCIe-bound (host -> HBM); the roofline is the resident kernel"},
-            "cpu_baseline": None, "gen_seconds": round(gen_s, 2)}), flush=True)
+            "cpu_baseline": None, "gen_seconds": round(gen_s, 2)})
     ctx.close()
+    return out
 
 
 def run_restart(a, dist, rank, world, local):
@@ -479,8 +515,7 @@ def run_restart(a, dist, rank, world, local):
         shutil.rmtree(d, ignore_errors=True)
     best = min(runs, key=lambda g: g["ms"]["total"])
     med = sorted(runs, key=lambda g: g["ms"]["total"])[len(runs) // 2]
-    if rank == 0:
-        print(json.dumps({
+    out = ({
             "metric": METRIC, "value": round(world * nb / (med["ms"]["total"] / 1e3) / 1e9, 3), "unit": "GB/s",
             "n_gpus": world, "steps": len(runs), "warmup": 0, "ms_per_step": round(med["ms"]["total"], 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
@@ -491,10 +526,11 @@ def run_restart(a, dist, rank, world, local):
                        "wal_bytes": nb, "parallelism": "dp%d" % world},
             "steps_ms_median": med["ms"], "steps_ms_best": best["ms"], "device_ms": med["device_ms"],
             "readall_plus_materialise_ms": round(med["ms"]["readall"] + med["ms"]["materialise"], 3),
-            "cpu_baseline": None}), flush=True)
+            "cpu_baseline": None})
+    return out
 
 
-def run_commit(a, dist, rank, world, local):
+def run_commit(a, dist, rank, world, local, cpu_seconds=None):
     """configs[4]: batched raft.maybeCommit (raft/raft.go:248-258 +
     raft/log.go:148-154) over 1M raft groups per GPU, 5 or 7 voters (seed 6),
     SoA matchIndex, a 16-entry log-term window per group; one
@@ -520,6 +556,7 @@ def run_commit(a, dist, rank, world, local):
     d_st = torch.zeros(G, dtype=torch.uint8, device=dev)
     ctx = W.Context(local)
     ctx.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+    cpu_seconds = a.cpu_seconds if cpu_seconds is None else cpu_seconds
     summary = torch.zeros(3, dtype=torch.int64, device=dev) if dist is not None else None
     dms = C.c_double(0)
     kms = []
@@ -559,7 +596,7 @@ def run_commit(a, dist, rank, world, local):
             c[:] = committed0
             O.maybe_commit_batch(G, match.reshape(-1), nv, term, c, log_offset, log_ptr, log_terms, chc, stc)
             it += 1
-            if time.perf_counter() - t2 >= a.cpu_seconds:
+            if time.perf_counter() - t2 >= cpu_seconds:
                 break
         cs = time.perf_counter() - t2
         nth = cpu_threads()
@@ -567,7 +604,7 @@ def run_commit(a, dist, rank, world, local):
         def all_cores():
             c[:] = committed0
             O.fast_maybe_commit_batch(G, match.reshape(-1), nv, term, c, log_offset, log_ptr, log_terms, chc, stc, nth)
-        it2, cs2 = timed_cpu(a.cpu_seconds / 2, all_cores)
+        it2, cs2 = timed_cpu(cpu_seconds / 2, all_cores)
         cpu = dict(host_info(), **{
             "value": round(G * it / cs, 1), "unit": "groups/s", "cores": 1, "kind": "port",
             "sample": "oracle/ or_maybe_commit_batch (insertion sort + q-th largest + term check per group, 1 "
@@ -575,8 +612,7 @@ def run_commit(a, dist, rank, world, local):
             "optimised": {"value": round(G * it2 / cs2, 1), "unit": "groups/s", "cores": nth,
                           "sample": "the same per-group code on all %d cores over group ranges "
                                     "(orf_maybe_commit_batch), %d passes, %.1f s" % (nth, it2, cs2)}})
-    if rank == 0:
-        print(json.dumps({
+    out = {
             "metric": "maybeCommit groups/s (configs[4]); WAL verify GB/s is the headline metric",
             "value": round(world * G / (ms / 1e3), 1), "unit": "groups/s", "n_gpus": world, "steps": a.steps,
             "warmup": a.warmup, "ms_per_step": round(ms, 4), "higher_is_better": True, "scaling": "weak",
@@ -588,8 +624,9 @@ def run_commit(a, dist, rank, world, local):
                          "unit": "GB/s", "frac": round(abytes / (k_avg / 1e3) / 1e9 / HBM_PEAK_GBPS, 4),
                          "traffic": None, "kernel": "k_commit", "kernel_ms": round(k_avg, 4),
                          "algorithmic_bytes_per_launch": abytes},
-            "cpu_baseline": cpu}), flush=True)
+            "cpu_baseline": cpu}
     ctx.close()
+    return out
 
 
 def run_msg(a, dist, rank, world, local):
@@ -635,8 +672,7 @@ def run_msg(a, dist, rank, world, local):
     elapsed = timed(dist, a.steps, step)
     ms = elapsed / a.steps * 1e3
     dms = float(L.lib.ewal_last_device_ms(ctx.handle))
-    if rank == 0:
-        print(json.dumps({
+    out = ({
             "metric": "raftpb.Message decode messages/s (SURVEY 8(f) rank 4); WAL verify GB/s is the headline",
             "value": round(world * n / (ms / 1e3), 1), "unit": "messages/s", "n_gpus": world, "steps": a.steps,
             "warmup": a.warmup, "ms_per_step": round(ms, 4), "higher_is_better": True, "scaling": "weak",
@@ -645,9 +681,169 @@ def run_msg(a, dist, rank, world, local):
                                    "results copied to the host each step" % (n, nb / 1e6, tot.value),
                        "parallelism": "dp%d" % world},
             "gbps": round(world * nb / (ms / 1e3) / 1e9, 3), "device_ms": round(dms, 4),
-            "cpu_baseline": None}), flush=True)
+            "cpu_baseline": None})
     dbuf.free()
     ctx.close()
+    return out
+
+
+def run_wal(a, dist, rank, world, local, size, min_data, max_data, label, cpu_seconds, full=True):
+    """configs[1] (and configs[0]'s WAL as `c1`): one ReadAll per step over a
+    GPU-resident WAL per rank with one corrupt record at frame 0.73 N.  full:
+    the headline's extras -- the clean WAL timed in the loop too, first-call
+    and PCIe-inclusive (host -> HBM) rates."""
+    buf_t = time.time()
+    buf, n = W.synth_wal(size, min_data, max_data, seed=2 + rank)
+    nb = len(buf)
+    gen_s = time.time() - buf_t
+    ctx = W.Context(local)
+    dbuf = ctx.alloc(nb + 64)
+    dbuf.upload_ptr(C.addressof((C.c_char * nb).from_buffer(buf)), nb)
+    extra = {}
+    if full:
+        # the one-shot restart (etcdserver/server.go:153-156) in a cold process: ewal_ctx_reserve first (device
+        # code load + workspace; a server runs it while it reads the WAL files), then the first ReadAll
+        tf = time.perf_counter()
+        rc0 = L.lib.ewal_ctx_reserve(ctx.handle, nb, 0)
+        extra["reserve_ms_cold"] = round((time.perf_counter() - tf) * 1e3, 3)
+        assert rc0 == 0, rc0
+        tf = time.perf_counter()
+        r = W.readall_device(dbuf, nb, 1)
+        extra["first_call_reserved_ms"] = round((time.perf_counter() - tf) * 1e3, 3)
+        assert r.status == L.OK and r.n_records == n, (r.status, r.n_records, n)
+        # ... and on a fresh ctx without the reserve (it sizes its workspace itself; device code already loaded)
+        ctx2 = W.Context(local)
+        r2 = L.Result()
+        tf = time.perf_counter()
+        L.lib.ewal_readall_device(ctx2.handle, dbuf.ptr, nb, 1, C.byref(r2))
+        extra["first_call_ms"] = round((time.perf_counter() - tf) * 1e3, 3)
+        assert r2.status == L.OK and r2.n_records == n
+        ctx2.close()
+        extra["first_call_note"] = ("reserve_ms_cold: ewal_ctx_reserve in a cold process (device code load + "
+                                    "workspace), then first_call_reserved_ms; first_call_ms: a fresh ctx without "
+                                    "the reserve")
+    r = W.readall_device(dbuf, nb, 1)
+    assert r.status == L.OK and r.n_records == n, (r.status, r.n_records, n)
+    rs = L.Result()      # the C ABI straight into a preallocated result: no Python objects in the timed region
+    if full:
+        # the clean WAL (the common restart case: ents placed, the result gathered), timed in the loop
+        def clean_step():
+            rc = L.lib.ewal_readall_device(ctx.handle, dbuf.ptr, nb, 1, C.byref(rs))
+            assert rc == L.OK and rs.n_records == n, (rc, rs.n_records)
+        clean_step()
+        extra["clean_ms_per_step"] = round(timed(dist, a.steps, clean_step) / a.steps * 1e3, 4)
+        extra["clean_pipeline_device_ms"] = round(rs.device_ms, 4)
+    k = int(0.73 * n)
+    rec = W.records(ctx, n)[k]
+    p = rec["data_off"] + rec["data_len"] // 2
+    flip = bytearray(dbuf.download(1, p))
+    flip[0] ^= 0x5A
+    dbuf.upload(bytes(flip), p)
+    buf[p] ^= 0x5A     # keep the host copy identical (E2E and CPU legs)
+
+    # ---- warmup + correctness gate -----------------------------------------
+    for _ in range(max(a.warmup, 1)):
+        r = W.readall_device(dbuf, nb, 1)
+    assert r.status == L.ERR_RECORD_CRC and r.fail_record == k, (r.status, r.fail_record, k)
+
+    summary = torch.zeros(3, dtype=torch.int64, device="cuda") if dist is not None else None
+    stream_ms, dev_ms = [], []
+
+    def step():
+        rc = L.lib.ewal_readall_device(ctx.handle, dbuf.ptr, nb, 1, C.byref(rs))
+        assert rc == L.ERR_RECORD_CRC and rs.fail_record == k, (rc, rs.fail_record)
+        stream_ms.append(rs.stream_ms)
+        dev_ms.append(rs.device_ms)
+        if dist is not None:   # one all-reduce of the shard verdicts (etcd_amd/shard.py)
+            shard.combine(dist, rank, rs.fail_record, rs.n_records, rs.status != L.OK, out=summary)
+
+    elapsed = timed(dist, a.steps, step)
+    ms_per_step = elapsed / a.steps * 1e3
+    gbps = world * nb / (ms_per_step / 1e3) / 1e9
+    recs_per_s = world * n / (ms_per_step / 1e3)
+    stream_avg = sum(stream_ms) / len(stream_ms)
+    dev_avg = sum(dev_ms) / len(dev_ms)
+    achieved = nb / (stream_avg / 1e3) / 1e9
+
+    # ---- end-to-end variant (host -> device included), one pass -------------
+    if full and not a.no_e2e:
+        t1 = time.perf_counter()
+        rr = L.Result()
+        bptr = C.addressof((C.c_char * nb).from_buffer(buf))
+        rc = L.lib.ewal_readall_host(ctx.handle, C.c_void_p(bptr), nb, 1, C.byref(rr))
+        e2e_s = time.perf_counter() - t1
+        assert rc == L.ERR_RECORD_CRC and rr.fail_record == k
+        extra["e2e_gbps_incl_h2d"] = round(nb / e2e_s / 1e9, 3)
+
+    # ---- CPU baseline: oracle ReadAll (Go-faithful port) on a bounded sample -
+    cpu = None
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        from oracle import oracle as O   # checker / baseline only
+        # the sample: the frames before the first one at or past 1 GiB (or before the corrupt one)
+        r = W.readall_device(dbuf, nb, 1)
+        cutr = W.records(ctx, k)
+        cut = next((x["offset"] for x in cutr if x["offset"] >= (1 << 30)), cutr[-1]["offset"])
+        sample = bytes(buf[:cut])
+        iters, t2 = 0, time.perf_counter()
+        while True:
+            o = O.readall(sample, 1)
+            iters += 1
+            if time.perf_counter() - t2 >= cpu_seconds:
+                break
+        cpu_s = time.perf_counter() - t2
+        assert o["status"] == O.OK
+        # the optimised CPU ReadAll on the CPU share, over the whole WAL (its corrupt frame included)
+        nth = cpu_threads()
+        addr = C.addressof((C.c_char * nb).from_buffer(buf))
+        fst = O.fast_readall_status(addr, nb, 1, nth)
+        assert fst[0] == O.ERR_RECORD_CRC and fst[2] == k, fst
+        it2, cs2 = timed_cpu(cpu_seconds / 2, lambda: O.fast_readall_status(addr, nb, 1, nth))
+        it3, cs3 = timed_cpu(cpu_seconds / 4, lambda: O.fast_readall_status(addr, nb, 1, 1))
+        cpu = dict(host_info(), **{
+            "value": round(len(sample) * iters / cpu_s / 1e9, 4), "unit": "GB/s", "cores": 1, "kind": "port",
+            "sample": "oracle/ or_readall (C restatement of wal.ReadAll: per-record alloc+copy, SSE4.2 "
+                      "CRC-32C, 1 thread) over the first %.2f GiB (%d frames) of the same WAL, %d passes, "
+                      "%.1f s" % (len(sample) / (1 << 30), o["n_records"], iters, cpu_s),
+            "optimised": {"value": round(nb * it2 / cs2 / 1e9, 4), "unit": "GB/s", "cores": nth,
+                          "one_core_gbps": round(nb * it3 / cs3 / 1e9, 4),
+                          "sample": "oracle/ewal_cpu_fast.c orf_readall over the whole %.2f GiB WAL (stops at the "
+                                    "corrupt frame %d like the reference): serial framing walk, every frame's CRC "
+                                    "with the local-verify rule on %d cores (3-stream SSE4.2 CRC-32C), ReadAll's "
+                                    "dispatch over the frame table; %d passes, %.1f s" %
+                                    (nb / (1 << 30), k, nth, it2, cs2)}})
+    out = {
+        "metric": METRIC, "value": round(gbps, 3), "unit": "GB/s", "n_gpus": world, "steps": a.steps,
+        "warmup": a.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "u8", "data": "synthetic",
+        "config": {"workload": "%s: one %.3f GiB WAL per GPU, %d frames, entry Data log-uniform "
+                               "%d B-%d B, 1 corrupt record at frame %d (walpb.ErrCRCMismatch)"
+                               % (label, nb / (1 << 30), n, min_data, max_data, k),
+                   "wal_bytes_per_gpu": nb, "frames_per_gpu": n, "ri": 1,
+                   "parallelism": "dp%d (independent WAL shards)" % world},
+        "records_per_s": round(recs_per_s, 1),
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBPS, 4),
+                     "traffic": load_traffic() if label == "configs[1]" else None,
+                     "kernel": "k_stream", "kernel_ms": round(stream_avg, 4),
+                     "algorithmic_bytes_per_launch": nb,
+                     "pipeline_achieved": round(nb / (dev_avg / 1e3) / 1e9, 2),
+                     "pipeline_frac": round(nb / (dev_avg / 1e3) / 1e9 / HBM_PEAK_GBPS, 4),
+                     "step_frac": round(gbps / world / HBM_PEAK_GBPS, 4)},
+        "pipeline_device_ms": round(dev_avg, 4),
+    }
+    if label == "configs[1]":
+        out["roofline"]["traffic_source"] = ("profiles/k_stream_pmc.json: the committed rocprofv3 PMC pass of this "
+                                             "config (FETCH_SIZE x2 + WRITE_SIZE per launch), not measured in this run")
+    out.update(extra)
+    out["cpu_baseline"] = cpu
+    out["gen_seconds"] = round(gen_s, 2)
+    dbuf.free()
+    ctx.close()
+    del buf
+    return out
+
+
+SUBS = {"c1": None, "shards": run_shards, "snap": run_snap, "commit": run_commit}
 
 
 def main():
@@ -662,173 +858,35 @@ def main():
         torch.cuda.set_device(local)
         dist.init_process_group("nccl")
 
-    def barrier():
-        if dist is not None:
-            dist.barrier()
-
-    label = "configs[1]"
-    if a.workload == "c1":   # wal.Save of 1M x 256 B entries (~286 B per frame)
-        a.size_gib, a.min_data, a.max_data, label = 285e6 / (1 << 30), 256, 256, "configs[0] WAL on the GPU"
-    elif (a.size_gib, a.min_data, a.max_data) != (8.0, 64, 65536):
-        label = "configs[1]-shaped"
-    if a.workload not in ("wal", "c1"):
-        {"shards": run_shards, "snap": run_snap, "snapstream": run_snapstream, "commit": run_commit,
-         "msg": run_msg, "restart": run_restart}[a.workload](a, dist, rank, world, local)
-        if dist is not None:
-            dist.destroy_process_group()
-        return
-
-    # ---- input: an independent synthetic WAL shard per rank ----------------
-    size = int(a.size_gib * (1 << 30))
-    t = time.time()
-    buf, n = W.synth_wal(size, a.min_data, a.max_data, seed=2 + rank)
-    nb = len(buf)
-    gen_s = time.time() - t
-    ctx = W.Context(local)
-    dbuf = ctx.alloc(nb + 64)
-    dbuf.upload_ptr(C.addressof((C.c_char * nb).from_buffer(buf)), nb)
-    # the one-shot restart (etcdserver/server.go:153-156) in a cold process: ewal_ctx_reserve first (device
-    # code load + workspace; a server runs it while it reads the WAL files), then the first ReadAll
-    tf = time.perf_counter()
-    rc0 = L.lib.ewal_ctx_reserve(ctx.handle, nb, 0)
-    reserve_ms = (time.perf_counter() - tf) * 1e3
-    assert rc0 == 0, rc0
-    tf = time.perf_counter()
-    r = W.readall_device(dbuf, nb, 1)
-    first_reserved_ms = (time.perf_counter() - tf) * 1e3
-    assert r.status == L.OK and r.n_records == n, (r.status, r.n_records, n)
-    # ... and on a fresh ctx without the reserve (it sizes its workspace itself; device code already loaded)
-    ctx2 = W.Context(local)
-    r2 = L.Result()
-    tf = time.perf_counter()
-    L.lib.ewal_readall_device(ctx2.handle, dbuf.ptr, nb, 1, C.byref(r2))
-    first_ms = (time.perf_counter() - tf) * 1e3
-    assert r2.status == L.OK and r2.n_records == n
-    ctx2.close()
-    k = int(0.73 * n)
-    rec = W.records(ctx, n)[k]
-    p = rec["data_off"] + rec["data_len"] // 2
-    flip = bytearray(dbuf.download(1, p))
-    flip[0] ^= 0x5A
-    dbuf.upload(bytes(flip), p)
-    buf[p] ^= 0x5A     # keep the host copy identical (E2E and CPU legs)
-
-    # ---- warmup + correctness gate -----------------------------------------
-    for _ in range(max(a.warmup, 1)):
-        r = W.readall_device(dbuf, nb, 1)
-    assert r.status == L.ERR_RECORD_CRC and r.fail_record == k, (r.status, r.fail_record, k)
-
-    summary = None
-    if dist is not None:
-        summary = torch.zeros(3, dtype=torch.int64, device="cuda")
-
-    # ---- timed region --------------------------------------------------------
-    barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    stream_ms, dev_ms = [], []
-    rs = L.Result()      # the C ABI straight into a preallocated result: no Python objects in the timed region
-    for _ in range(a.steps):
-        rc = L.lib.ewal_readall_device(ctx.handle, dbuf.ptr, nb, 1, C.byref(rs))
-        assert rc == L.ERR_RECORD_CRC and rs.fail_record == k, (rc, rs.fail_record)
-        stream_ms.append(rs.stream_ms)
-        dev_ms.append(rs.device_ms)
-        if dist is not None:   # one all-reduce of the shard verdicts (etcd_amd/shard.py)
-            shard.combine(dist, rank, rs.fail_record, rs.n_records, rs.status != L.OK, out=summary)
-    torch.cuda.synchronize()
-    barrier()
-    elapsed = time.perf_counter() - t0
-    if dist is not None:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
-    ms_per_step = elapsed / a.steps * 1e3
-    gbps = world * nb / (ms_per_step / 1e3) / 1e9
-    recs_per_s = world * n / (ms_per_step / 1e3)
-
-    stream_avg = sum(stream_ms) / len(stream_ms)
-    dev_avg = sum(dev_ms) / len(dev_ms)
-    achieved = nb / (stream_avg / 1e3) / 1e9
-
-    # ---- end-to-end variant (host -> device included), one pass -------------
-    e2e = None
-    if not a.no_e2e:
-        t1 = time.perf_counter()
-        rr = L.Result()
-        bptr = C.addressof((C.c_char * nb).from_buffer(buf))
-        rc = L.lib.ewal_readall_host(ctx.handle, C.c_void_p(bptr), nb, 1, C.byref(rr))
-        e2e_s = time.perf_counter() - t1
-        assert rc == L.ERR_RECORD_CRC and rr.fail_record == k
-        e2e = round(nb / e2e_s / 1e9, 3)
-
-    # ---- CPU baseline: oracle ReadAll (Go-faithful port) on a bounded sample -
-    cpu = None
-    if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        from oracle import oracle as O   # checker / baseline only
-        recs = W.records(ctx, k)         # frames before the corrupt one
-        cut = next((x["offset"] for x in recs if x["offset"] >= (1 << 30)), recs[-1]["offset"])
-        sample = bytes(buf[:cut])
-        iters, t2 = 0, time.perf_counter()
-        while True:
-            o = O.readall(sample, 1)
-            iters += 1
-            if time.perf_counter() - t2 >= a.cpu_seconds:
-                break
-        cpu_s = time.perf_counter() - t2
-        assert o["status"] == O.OK
-        # the optimised CPU ReadAll on all cores, over the whole WAL (its corrupt frame included)
-        nth = cpu_threads()
-        addr = C.addressof((C.c_char * nb).from_buffer(buf))
-        fst = O.fast_readall_status(addr, nb, 1, nth)
-        assert fst[0] == O.ERR_RECORD_CRC and fst[2] == k, fst
-        it2, cs2 = timed_cpu(a.cpu_seconds / 2, lambda: O.fast_readall_status(addr, nb, 1, nth))
-        it3, cs3 = timed_cpu(a.cpu_seconds / 4, lambda: O.fast_readall_status(addr, nb, 1, 1))
-        cpu = dict(host_info(), **{
-            "value": round(len(sample) * iters / cpu_s / 1e9, 4), "unit": "GB/s", "cores": 1, "kind": "port",
-            "sample": "oracle/ or_readall (C restatement of wal.ReadAll: per-record alloc+copy, SSE4.2 "
-                      "CRC-32C, 1 thread) over the first %.2f GiB (%d frames) of the same WAL, %d passes, "
-                      "%.1f s" % (len(sample) / (1 << 30), o["n_records"], iters, cpu_s),
-            "optimised": {"value": round(nb * it2 / cs2 / 1e9, 4), "unit": "GB/s", "cores": nth,
-                          "one_core_gbps": round(nb * it3 / cs3 / 1e9, 4),
-                          "sample": "oracle/ewal_cpu_fast.c orf_readall over the whole %.2f GiB WAL (stops at the "
-                                    "corrupt frame %d like the reference): serial framing walk, every frame's CRC "
-                                    "with the local-verify rule on %d cores (3-stream SSE4.2 CRC-32C), ReadAll's "
-                                    "dispatch over the frame table; %d passes, %.1f s" %
-                                    (nb / (1 << 30), k, nth, it2, cs2)}})
-
+    c1 = dict(size=int(285e6), min_data=256, max_data=256, label="configs[0] WAL on the GPU")
+    if a.workload in ("wal", "c1"):
+        if a.workload == "c1":
+            out = run_wal(a, dist, rank, world, local, cpu_seconds=a.cpu_seconds, full=False, **c1)
+        else:
+            label = "configs[1]" if (a.size_gib, a.min_data, a.max_data) == (8.0, 64, 65536) else "configs[1]-shaped"
+            out = run_wal(a, dist, rank, world, local, int(a.size_gib * (1 << 30)), a.min_data, a.max_data, label,
+                          a.cpu_seconds)
+            subs = [x for x in a.configs.split(",") if x and x != "none"] if a.workload == "wal" else []
+            if subs:
+                out["configs"] = {}
+            for name in subs:
+                t0 = time.time()
+                if name == "c1":
+                    r = run_wal(a, dist, rank, world, local, cpu_seconds=a.sub_cpu_seconds, full=False, **c1)
+                else:
+                    r = SUBS[name](a, dist, rank, world, local, cpu_seconds=a.sub_cpu_seconds)
+                r["wall_seconds"] = round(time.time() - t0, 2)
+                for key in ("higher_is_better", "scaling", "vs_baseline", "data", "n_gpus"):
+                    r.pop(key, None)
+                out["configs"][name] = r
+                if rank == 0:
+                    print("bench: %s %.3f ms/step (%.1f s)" % (name, r["ms_per_step"], r["wall_seconds"]),
+                          file=sys.stderr, flush=True)
+    else:
+        out = {"shards": run_shards, "snap": run_snap, "snapstream": run_snapstream, "commit": run_commit,
+               "msg": run_msg, "restart": run_restart}[a.workload](a, dist, rank, world, local)
     if rank == 0:
-        out = {
-            "metric": "WAL verify GB/s (and records/s) per GPU + 8-GPU node, % of HBM roofline",
-            "value": round(gbps, 3), "unit": "GB/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
-            "ms_per_step": round(ms_per_step, 4), "higher_is_better": True, "scaling": "weak",
-            "vs_baseline": None, "dtype": "u8", "data": "synthetic",
-            "config": {"workload": "%s: one %.3f GiB WAL per GPU, %d frames, entry Data log-uniform "
-                                   "%d B-%d B, 1 corrupt record at frame %d (walpb.ErrCRCMismatch)"
-                                   % (label, nb / (1 << 30), n, a.min_data, a.max_data, k),
-                       "wal_bytes_per_gpu": nb, "frames_per_gpu": n, "ri": 1,
-                       "parallelism": "dp%d (independent WAL shards)" % world},
-            "records_per_s": round(recs_per_s, 1),
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": load_traffic() if label == "configs[1]" else None,
-                         "traffic_source": "profiles/k_stream_pmc.json: the committed rocprofv3 PMC pass of this "
-                                           "config (FETCH_SIZE x2 + WRITE_SIZE per launch), not measured in this run",
-                         "kernel": "k_stream", "kernel_ms": round(stream_avg, 4),
-                         "algorithmic_bytes_per_launch": nb,
-                         "pipeline_achieved": round(nb / (dev_avg / 1e3) / 1e9, 2),
-                         "pipeline_frac": round(nb / (dev_avg / 1e3) / 1e9 / HBM_PEAK_GBPS, 4),
-                         "step_frac": round(gbps / world / HBM_PEAK_GBPS, 4)},
-            "pipeline_device_ms": round(dev_avg, 4),
-            "first_call_ms": round(first_ms, 3),
-            "first_call_reserved_ms": round(first_reserved_ms, 3), "reserve_ms_cold": round(reserve_ms, 3),
-            "first_call_note": "reserve_ms_cold: ewal_ctx_reserve in a cold process (device code load + workspace), "
-                               "then first_call_reserved_ms; first_call_ms: a fresh ctx without the reserve",
-            "e2e_gbps_incl_h2d": e2e,
-            "cpu_baseline": cpu,
-            "gen_seconds": round(gen_s, 2),
-        }
         print(json.dumps(out), flush=True)
-    dbuf.free()
-    ctx.close()
     if dist is not None:
         dist.destroy_process_group()
 

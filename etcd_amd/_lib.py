@@ -99,6 +99,15 @@ class RecordDesc(C.Structure):
                 ("crc", C.c_uint32), ("chained_crc", C.c_uint32)]
 
 
+class RangeInfo(C.Structure):   # ewal_range_info
+    _fields_ = [("n_frames", C.c_int64), ("first_crc", C.c_int64), ("md_first_frame", C.c_int64),
+                ("md_first_off", C.c_int64), ("md_first_len", C.c_int64), ("md_value_frame", C.c_int64),
+                ("md_value_off", C.c_int64), ("md_value_len", C.c_int64), ("first_entry_frame", C.c_int64),
+                ("last_entry_frame", C.c_int64), ("first_entry_index", C.c_uint64),
+                ("min_entry_index", C.c_uint64), ("last_entry_index", C.c_uint64), ("last_op_frame", C.c_int64),
+                ("last_op_index", C.c_uint64)]
+
+
 class SnapshotDesc(C.Structure):
     _fields_ = [("index", C.c_uint64), ("term", C.c_uint64), ("data_off", C.c_uint64), ("data_len", C.c_uint64),
                 ("n_nodes", C.c_int64), ("n_removed", C.c_int64), ("nodes", C.c_uint64 * 64),
@@ -132,6 +141,7 @@ _SIGS = {
     "emsg_copy_entries": (C.c_int64, [vp, C.c_uint64, C.POINTER(EntryDesc), C.c_int64]),
     "ewal_batch_copy_entries": (C.c_int64, [vp, C.c_uint64, C.POINTER(EntryDesc), C.c_int64]),
     "ewal_copy_records": (C.c_int64, [vp, C.POINTER(RecordDesc), C.c_int64]),
+    "ewal_copy_range_info": (C.c_int, [vp, C.POINTER(RangeInfo)]),
     "ewal_copy_unrec": (C.c_int64, [vp, C.POINTER(UnrecDesc), C.c_int64]),
     "ewal_copy_unrec_bytes": (C.c_int64, [vp, vp, C.c_int64]),
     "ewal_open_at_index": (C.c_int, [C.c_char_p, C.c_uint64, C.POINTER(vp)]),

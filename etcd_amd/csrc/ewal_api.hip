@@ -141,11 +141,27 @@ struct ewal_ctx {
   uint32_t epoch = 0;      // k_check look-back epoch (24 bits)
   int fused = 1;           // the fused frame + check pass first (EWAL_FUSED=0: the general path only)
   bool rd_valid = false;   // c->rd holds the last call's per-frame descriptors
+  bool rec_valid = false;     // the last ReadAll's last_n frames can be described (ewal_copy_records,
+                              // ewal_range_info)
+  bool rec_rebuild = false;   // the last ReadAll was decided by the fused pass and the stream pass's
+                              // state (cpos, pwave, v) is still its own: ewal_copy_records can rebuild
+                              // the descriptors from it and the caller's stream bytes
   const uint8_t *last_buf = nullptr;   // the last ReadAll's stream (materialise_records)
   uint64_t last_B = 0, last_ri = 0;
   uint64_t pfcap = 0;      // pf = [P at data starts | P at frame starts], pfcap each
   bool last_ok = false;
 };
+
+// The HBM staging buffer of host bytes (ewal_readall_host, ewal_stage_*):
+// refilling or reallocating it takes away the stream the last ReadAll's
+// descriptors are rebuilt from when that ReadAll read it.
+static hipError_t stage_ensure(ewal_ctx *c, size_t n) {
+  if (c->last_buf && c->last_buf == c->hbuf_dev.as<uint8_t>()) {
+    c->rec_rebuild = false;
+    c->last_buf = nullptr;
+  }
+  return c->hbuf_dev.ensure(n);
+}
 
 static int get_tables(ewal_ctx *c, uint32_t poly, DevTables **out) {
   auto it = c->tables.find(poly);
@@ -233,7 +249,17 @@ static int stream_ensure(ewal_ctx *c, uint64_t B, int find_cand) {
   return 0;
 }
 
+// The per-frame descriptors of the last ReadAll live in (or are rebuilt from)
+// ctx state that any other pipeline call overwrites: forget them.
+static void forget_records(ewal_ctx *c) {
+  c->rec_valid = false;
+  c->rd_valid = false;
+  c->rec_rebuild = false;
+  c->last_n = 0;
+}
+
 static int run_stream(ewal_ctx *c, DevTables *tb, const uint8_t *d_buf, uint64_t B, int find_cand, uint64_t ccap) {
+  forget_records(c);   // cpos / pwave / v are about to change (readall_impl sets them again after)
   const uint64_t nunits64 = B / EW_WAVE_BYTES + 1;
   if (nunits64 >= 0xffff0000ull) return EWAL_E_INVAL;
   const uint32_t nunits = (uint32_t)nunits64;
@@ -951,6 +977,8 @@ static int readall_impl(ewal_ctx *c, const uint8_t *d_buf, uint64_t B, uint64_t 
     }
   }
   c->last_n = n;
+  c->rec_rebuild = n && !c->rd_valid;   // the fused pass decided: descriptors are rebuilt on demand
+  c->rec_valid = true;
   if (!ev1_final) EW_CHECK(hipEventRecord(c->ev1, c->stream));
   EW_CHECK(hipEventSynchronize(c->ev1));
   float ms = 0;
@@ -1256,6 +1284,7 @@ static int readall_batch_impl(ewal_ctx *c, const uint8_t *d_buf, uint32_t ns, co
   }
   EW_CHECK(hipStreamSynchronize(c->stream));
   c->last_ok = false;
+  forget_records(c);   // the descriptors of the last one-by-one shard are not a ReadAll of the batch
   return 0;
 }
 
@@ -1379,7 +1408,7 @@ int ewal_ctx_reserve(ewal_ctx *c, uint64_t wal_bytes, uint32_t flags) {
   if (!c) return EWAL_E_INVAL;
   if (flags & EWAL_RESERVE_HOST_STAGING) {   // the HBM copy of host bytes (ewal_readall_host / ewal_wal_readall)
     EW_CHECK(hipSetDevice(c->device));
-    EW_CHECK(c->hbuf_dev.ensure(wal_bytes + 16));
+    EW_CHECK(stage_ensure(c, wal_bytes + 16));
   }
   EW_CHECK(hipSetDevice(c->device));
   DevTables *tb;
@@ -1398,7 +1427,7 @@ int ewal_ctx_reserve(ewal_ctx *c, uint64_t wal_bytes, uint32_t flags) {
   EW_CHECK(c->mlist.ensure((size_t)ecap * 4));
   // load the device code: a ReadAll over a one-frame WAL (a crcType record)
   static const uint8_t tiny[16] = {4, 0, 0, 0, 0, 0, 0, 0, 0x08, 0x04, 0x10, 0x00};
-  EW_CHECK(c->hbuf_dev.ensure(64));
+  EW_CHECK(stage_ensure(c, 64));
   EW_CHECK(hipMemcpyAsync(c->hbuf_dev.p, tiny, sizeof(tiny), hipMemcpyHostToDevice, c->stream));
   ewal_result r;
   rc = readall_impl(c, c->hbuf_dev.as<uint8_t>(), 12, 0, &r);
@@ -1461,7 +1490,7 @@ int ewal_download(ewal_ctx *c, void *h, const void *d, uint64_t len) {
 int ewal_stage_to_device(ewal_ctx *c, const void *h_buf, uint64_t len, void **d_out) {
   if (!c || !d_out || (!h_buf && len)) return EWAL_E_INVAL;
   EW_CHECK(hipSetDevice(c->device));
-  EW_CHECK(c->hbuf_dev.ensure(len + 16));
+  EW_CHECK(stage_ensure(c, len + 16));
   if (len) EW_CHECK(hipMemcpyAsync(c->hbuf_dev.p, h_buf, len, hipMemcpyHostToDevice, c->stream));
   EW_CHECK(hipStreamSynchronize(c->stream));
   *d_out = c->hbuf_dev.p;
@@ -1471,12 +1500,17 @@ int ewal_stage_to_device(ewal_ctx *c, const void *h_buf, uint64_t len, void **d_
 int ewal_stage_begin(ewal_ctx *c, uint64_t len) {
   if (!c) return EWAL_E_INVAL;
   EW_CHECK(hipSetDevice(c->device));
-  EW_CHECK(c->hbuf_dev.ensure(len + 16));
+  EW_CHECK(stage_ensure(c, len + 16));
   return EWAL_OK;
 }
 int ewal_stage_put(ewal_ctx *c, uint64_t off, const void *h, uint64_t n) {
   if (!c || (n && !h) || off + n + 16 > c->hbuf_dev.cap) return EWAL_E_INVAL;
   if (n) EW_CHECK(hipMemcpyAsync(c->hbuf_dev.as<uint8_t>() + off, h, n, hipMemcpyHostToDevice, c->stream));
+  return EWAL_OK;
+}
+int ewal_stage_sync(ewal_ctx *c) {
+  if (!c) return EWAL_E_INVAL;
+  EW_CHECK(hipStreamSynchronize(c->stream));
   return EWAL_OK;
 }
 int ewal_stage_readall(ewal_ctx *c, uint64_t len, uint64_t ri, ewal_result *out) {
@@ -1488,7 +1522,7 @@ int ewal_stage_readall(ewal_ctx *c, uint64_t len, uint64_t ri, ewal_result *out)
 int ewal_readall_host(ewal_ctx *c, const void *h_buf, uint64_t len, uint64_t ri, ewal_result *out) {
   if (!c || !out || (!h_buf && len)) return EWAL_E_INVAL;
   EW_CHECK(hipSetDevice(c->device));
-  EW_CHECK(c->hbuf_dev.ensure(len + 16));
+  EW_CHECK(stage_ensure(c, len + 16));
   if (len) EW_CHECK(hipMemcpyAsync(c->hbuf_dev.p, h_buf, len, hipMemcpyHostToDevice, c->stream));
   return readall_impl(c, c->hbuf_dev.as<uint8_t>(), len, ri, out);
 }
@@ -1523,13 +1557,23 @@ int64_t ewal_copy_unrec_bytes(ewal_ctx *c, uint8_t *out, int64_t cap) {
   return n;
 }
 
+// The last ReadAll's per-frame descriptors in c->rd (rebuilt when the fused
+// pass decided it); EWAL_E_INVAL when another call took the state they come from.
+static int need_records(ewal_ctx *c) {
+  if (!c->rec_valid) return EWAL_E_INVAL;
+  if (c->last_n && !c->rd_valid) {   // the fused pass kept no descriptors: decode them now
+    if (!c->rec_rebuild) return EWAL_E_INVAL;
+    EW_CHECK(hipSetDevice(c->device));
+    return materialise_records(c);
+  }
+  return 0;
+}
+
 int64_t ewal_copy_records(ewal_ctx *c, ewal_record *out, int64_t cap) {
   if (!c || (!out && cap)) return EWAL_E_INVAL;
   int64_t n = std::min<int64_t>(cap, (int64_t)c->last_n);
-  if (n > 0 && !c->rd_valid) {   // the fused pass kept no descriptors: decode them now
-    EW_CHECK(hipSetDevice(c->device));
-    int rc = materialise_records(c);
-    if (rc) return rc;
+  if (n > 0) {
+    if (int rc = need_records(c)) return rc;
   }
   if (n > 0) {
     EW_CHECK(c->recs.ensure((size_t)n * sizeof(ewal_record)));
@@ -1539,6 +1583,65 @@ int64_t ewal_copy_records(ewal_ctx *c, ewal_record *out, int64_t cap) {
     EW_CHECK(hipStreamSynchronize(c->stream));
   }
   return n;
+}
+
+int ewal_copy_range_info(ewal_ctx *c, ewal_range_info *out) {
+  if (!c || !out) return EWAL_E_INVAL;
+  ewal_range_info o;
+  std::memset(&o, 0, sizeof(o));
+  o.first_crc = o.md_first_frame = o.md_value_frame = o.first_entry_frame = o.last_entry_frame = -1;
+  o.last_op_frame = -1;
+  o.md_first_off = o.md_value_off = -1;
+  if (int rc = need_records(c)) return rc;
+  const uint64_t n = c->last_n;
+  o.n_frames = (int64_t)n;
+  if (n) {
+    EW_CHECK(c->sdesc.ensure(sizeof(RangeDev)));
+    RangeDev h0{~0ull, ~0ull, ~0ull, ~0ull, 0ull, 0ull}, h;
+    EW_CHECK(hipMemcpyAsync(c->sdesc.p, &h0, sizeof(h0), hipMemcpyHostToDevice, c->stream));
+    const RecDesc *rd = c->rd.as<RecDesc>();
+    hipLaunchKernelGGL(k_range_info, dim3((unsigned)std::min<uint64_t>(grid_for(n, 256), 1024)), dim3(256), 0,
+                       c->stream, rd, (uint32_t)n, c->last_ri, c->sdesc.as<RangeDev>());
+    EW_CHECK(hipGetLastError());
+    EW_CHECK(hipMemcpyAsync(&h, c->sdesc.p, sizeof(h), hipMemcpyDeviceToHost, c->stream));
+    EW_CHECK(hipStreamSynchronize(c->stream));
+    auto frame = [&](uint64_t r, RecDesc *d) {
+      return hipMemcpy(d, rd + r, sizeof(RecDesc), hipMemcpyDeviceToHost);
+    };
+    RecDesc d;
+    EW_CHECK(frame(0, &d));
+    if (d.type == 4) o.first_crc = d.crc;
+    if (h.md_first != ~0ull) {
+      EW_CHECK(frame(h.md_first, &d));
+      o.md_first_frame = (int64_t)h.md_first;
+      if (!d.dnil && d.dlen) {
+        o.md_first_off = (int64_t)d.doff;
+        o.md_first_len = (int64_t)d.dlen;
+      }
+    }
+    if (h.md_value != ~0ull) {
+      EW_CHECK(frame(h.md_value, &d));
+      o.md_value_frame = (int64_t)h.md_value;
+      o.md_value_off = (int64_t)d.doff;
+      o.md_value_len = (int64_t)d.dlen;
+    }
+    if (h.ent_first != ~0ull) {
+      EW_CHECK(frame(h.ent_first, &d));
+      o.first_entry_frame = (int64_t)h.ent_first;
+      o.first_entry_index = d.f1;
+      o.min_entry_index = h.min_index;
+      EW_CHECK(frame(h.ent_last1 - 1, &d));
+      o.last_entry_frame = (int64_t)(h.ent_last1 - 1);
+      o.last_entry_index = d.f1;
+      if (h.op_last1) {
+        EW_CHECK(frame(h.op_last1 - 1, &d));
+        o.last_op_frame = (int64_t)(h.op_last1 - 1);
+        o.last_op_index = d.f1;
+      }
+    }
+  }
+  *out = o;
+  return EWAL_OK;
 }
 
 int ewal_encode_entries_device(ewal_ctx *c, const void *d_data, uint64_t data_len_total, const ewal_entry *d_ents,

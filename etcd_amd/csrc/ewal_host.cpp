@@ -433,7 +433,12 @@ int ewal_wal_readall(ewal_wal *w, ewal_ctx *ctx, ewal_result *out) {
   } else {
     rc = load_pieces(w, [&](uint64_t off, uint64_t len) { return ewal_stage_put(ctx, off, w->bytes + off, len); });
   }
-  if (rc) return rc;
+  if (rc) {
+    // copies already queued read w->bytes: let them land before the caller can
+    // unmap it (ewal_wal_close)
+    (void)ewal_stage_sync(ctx);
+    return rc;
+  }
   return ewal_stage_readall(ctx, w->total, w->ri, out);
 }
 
@@ -551,8 +556,9 @@ int ewal_writer_cut(ewal_writer *w) {
   ::close(w->fd);
   w->fd = nfd;
   w->seq = nseq;
-  const uint32_t prev = w->enc.crc;   // encoder re-created with prevCrc
-  w->enc.crc = prev;
+  // newEncoder(w.f, prevCrc): a fresh buffer (bytes a failed sync left
+  // behind belong to the old file and are dropped), the running CRC kept
+  w->enc.buf.clear();
   ewal_encoder_encode(&w->enc, EWAL_CRC, nullptr, 0, 1);          // saveCrc(prevCrc)
   return ewal_encoder_encode(&w->enc, EWAL_METADATA, w->md.data(), w->md.size(), w->md_nil);
 }

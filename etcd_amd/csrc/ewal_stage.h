@@ -13,6 +13,8 @@ int ewal_stage_begin(ewal_ctx *ctx, uint64_t len);
 /* host -> staging buffer [off, off + n), asynchronous on the ctx stream; h
  * must stay unchanged until ewal_stage_readall returns */
 int ewal_stage_put(ewal_ctx *ctx, uint64_t off, const void *h, uint64_t n);
+/* wait for the queued puts (their host bytes may be released afterwards) */
+int ewal_stage_sync(ewal_ctx *ctx);
 /* (*WAL).ReadAll over the staged len bytes (stream-ordered after the puts) */
 int ewal_stage_readall(ewal_ctx *ctx, uint64_t len, uint64_t ri, ewal_result *out);
 }

@@ -2223,6 +2223,37 @@ __global__ void k_records_out(const RecDesc *__restrict__ rd, uint32_t n, ewal_r
   out[r] = o;
 }
 
+// What one rank's range of ONE WAL split by file contributes to the joined
+// verdict (ewal_copy_range_info, etcd_amd/shard.py split_verdict): the first
+// metadata frame (any Data, then non-nil Data), the first / last entry frame,
+// the last entry op (Index >= ri, wal/wal.go:171) and the least Entry.Index,
+// over the chain's frames.  Maxima are folded as frame + 1 (0: none).
+struct RangeDev {
+  unsigned long long md_first, md_value, ent_first, min_index;   // min (~0: none)
+  unsigned long long ent_last1, op_last1;                        // max (0: none)
+};
+__global__ void k_range_info(const RecDesc *__restrict__ rd, uint32_t n, uint64_t ri, RangeDev *o) {
+  unsigned long long mf = ~0ull, mv = ~0ull, ef = ~0ull, mi = ~0ull, el = 0, ol = 0;
+  for (uint32_t r = blockIdx.x * blockDim.x + threadIdx.x; r < n; r += gridDim.x * blockDim.x) {
+    const RecDesc &d = rd[r];
+    if (d.type == 1) {
+      mf = min(mf, (unsigned long long)r);
+      if (!d.dnil && d.dlen) mv = min(mv, (unsigned long long)r);
+    } else if (d.type == 2) {
+      ef = min(ef, (unsigned long long)r);
+      el = max(el, (unsigned long long)r + 1);
+      if (d.f1 >= ri) ol = max(ol, (unsigned long long)r + 1);
+      mi = min(mi, (unsigned long long)d.f1);
+    }
+  }
+  if (mf != ~0ull) atomicMin(&o->md_first, mf);
+  if (mv != ~0ull) atomicMin(&o->md_value, mv);
+  if (ef != ~0ull) atomicMin(&o->ent_first, ef);
+  if (mi != ~0ull) atomicMin(&o->min_index, mi);
+  if (el) atomicMax(&o->ent_last1, el);
+  if (ol) atomicMax(&o->op_last1, ol);
+}
+
 __global__ void k_reverse_u64(const uint64_t *__restrict__ in, uint64_t *__restrict__ out, uint32_t n) {
   uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j < n) out[n - 1 - j] = in[j];

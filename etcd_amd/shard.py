@@ -104,55 +104,115 @@ def seam_check(dist, world: int, rank: int, first_crc_record: int, last_crc: int
 
 # ---- one WAL split across ranks by file -------------------------------------
 # Status numbers of the verdict (include/ewal.h)
-_OK, _UNEXPECTED_EOF, _WAL_CRC, _META_CONFLICT, _INDEX_NOT_FOUND = 0, 2, 4, 5, 6
-NIL = -2        # a metadata record whose Data is nil
-NONE = -1       # no metadata record in the range
+_OK, _UNEXPECTED_EOF, _WAL_CRC, _META_CONFLICT, _INDEX_NOT_FOUND, _INDEX_GAP = 0, 2, 4, 5, 6, 36
+_U64 = (1 << 64) - 1
+_ROW = 16
 
 
-def split_verdict(dist, world: int, rank: int, status: int, fail_record: int, n_records: int, last_crc: int,
-                  first_crc_record: int, md_first: int, md_first_frame: int, md_last: int, device="cpu"):
-    """ReadAll's verdict for ONE WAL whose files were split into contiguous
-    ranges, range r verified by rank r (each range starts at a file boundary:
-    a crcType record carrying the running CRC, wal/wal.go:93,232-234).  Every
-    rank passes its own ReadAll result over its range (with w.ri = the first
-    entry index of its range, from the first file's name) plus:
-    first_crc_record (the Crc of the range's leading crcType record, -1 if it
-    does not start with one), md_first / md_first_frame (a digest of the
-    range's first metadata record's Data, NIL for nil Data, NONE when the
-    range has none; its frame ordinal in the range) and md_last (the digest
-    of the metadata value after the range, as ReadAll returns it).
+def _s64(x):
+    """a uint64 in an int64 tensor slot (two's complement)"""
+    x &= _U64
+    return x - (1 << 64) if x >> 63 else x
 
-    One all-gather of 8 words per rank; every rank then walks the ranges in
-    file order applying ReadAll's two cross-file rules -- the crc seam
-    (wal/wal.go:184-192: running != 0 and stored != running ->
-    wal.ErrCRCMismatch) and the metadata rule (wal/wal.go:178-183: metadata !=
-    nil and not DeepEqual -> ErrMetadataConflict) -- before each range's own
-    first failure.  Returns (status, global frame ordinal of the first
-    failure or -1, frames verified, resplit); a range's ErrIndexNotFound (no
-    entry at or after its first file's index) is not a failure of the split
-    verify.  resplit = k >= 0 when range k (not the last) ends in a torn frame
-    (io.ErrUnexpectedEOF at its end): the reference reads on across the file
-    boundary (MultiReadCloser), so that frame's verdict depends on the next
-    range's bytes -- the caller verifies ranges k.. joined as one range and
-    calls again (status is then not final)."""
-    mine = torch.tensor([status, fail_record, n_records, last_crc, first_crc_record, md_first, md_first_frame,
-                         md_last], dtype=torch.int64, device=device)
-    allv = [torch.zeros(8, dtype=torch.int64, device=device) for _ in range(world)]
+
+def split_verdict(dist, world: int, rank: int, result, info, ri_range: int, ri_global: int, device="cpu"):
+    """ReadAll's verdict (wal/wal.go:164-216) for ONE WAL whose files were
+    split into contiguous ranges, range r verified by rank r.  Every range
+    but the first starts at a file boundary, so at a crcType record carrying
+    the running CRC (wal/wal.go:93,232-234); rank r ran ReadAll over its
+    range with w.ri = ri_range (its first file's index from the name) and
+    passes result = (status, fail_record, n_records, last_crc) plus info =
+    wal.range_info() of that ReadAll (ewal_range_info: first crc record,
+    first metadata frame and Data, the metadata value kept, first / last /
+    least entry Index, last entry op).
+
+    One all-gather of a 16-word row per rank and one of the metadata bytes;
+    every rank then walks the ranges in file order and applies ReadAll's
+    cross-file rules before each range's own first failure, frame by frame:
+    * crc seam (wal/wal.go:184-192): running != 0 and stored != running ->
+      wal.ErrCRCMismatch at the range's frame 0;
+    * metadata (wal/wal.go:178-183): metadata != nil and not DeepEqual ->
+      ErrMetadataConflict at the range's first metadata frame (exact bytes);
+    * ents (wal/wal.go:170-173): the range's first entry op against len(ents)
+      carried from the ranges before (the index-gap panic); entries of a
+      later range below its own w.ri (a leader change rewriting indexes
+      after a Cut) are ops of the global ReadAll that the range's read
+      skipped -- and a gap its read reports at its first op that the global
+      one does not have hides the rest of the range -- so both resplit;
+    * w.enti < w.ri (wal/wal.go:203-206): the global ErrIndexNotFound, from
+      the last entry Index over all ranges.
+    Returns (status, global frame ordinal of the first failure or -1, frames
+    verified, resplit).  resplit = k >= 0: the verdict needs ranges k..
+    joined into one range (a torn frame at the end of range k reads on into
+    the next file through MultiReadCloser; k = 0 for the rewind / gap cases
+    and a range that does not open with a crc record) -- the caller verifies
+    them joined and calls again; status is not final then."""
+    st, fr, n, lc = result
+    mdf, mdv = info.get("md_first"), info.get("md_value")
+    has_md = info["md_first_frame"] >= 0
+    row = [st, fr, n, lc, info["first_crc"], info["md_first_frame"],
+           (len(mdf) if mdf is not None else -1) if has_md else -2,
+           len(mdv) if (info["md_value_frame"] >= 0 and mdv is not None) else -1,
+           info["first_entry_frame"], _s64(info["first_entry_index"]), _s64(info["min_entry_index"]),
+           _s64(info["last_entry_index"]), _s64(ri_range), info["n_frames"], info["last_op_frame"],
+           _s64(info["last_op_index"])]
+    assert len(row) == _ROW
+    mine = torch.tensor(row, dtype=torch.int64, device=device)
+    allv = [torch.zeros(_ROW, dtype=torch.int64, device=device) for _ in range(world)]
     dist.all_gather(allv, mine)
     rows = [[int(x) for x in v.tolist()] for v in allv]
-    before, running, md = 0, 0, NONE
-    for k, (st, fr, n, lc, fc, mf, mff, ml) in enumerate(rows):
+    # the metadata bytes: first metadata Data + the value kept, padded to the longest
+    blob = (mdf or b"") + (mdv or b"")
+    width = max(1, max(max(r[6], 0) + max(r[7], 0) for r in rows))
+    t = torch.zeros(width, dtype=torch.uint8, device=device)
+    if blob:
+        t[:len(blob)] = torch.frombuffer(bytearray(blob), dtype=torch.uint8).to(device)
+    allb = [torch.zeros(width, dtype=torch.uint8, device=device) for _ in range(world)]
+    dist.all_gather(allb, t)
+    raw = [bytes(x.cpu().numpy().tobytes()) for x in allb]
+
+    before, running, md, last_op, enti = 0, 0, None, None, 0
+    rig = ri_global & _U64
+    for k, r in enumerate(rows):
+        st, fr, n, lc, fc, mff, mfl, mvl, fef, fei, mei, lei, rir, nfr, lof, loi = r
+        fei, mei, lei, rir, loi = fei & _U64, mei & _U64, lei & _U64, rir & _U64, loi & _U64
+        if nfr == 0 and n == 0 and st == _OK:
+            continue                        # an empty range (joined into an earlier one)
+        first_md = None if mfl < 0 else raw[k][:mfl]
+        value_md = None if mvl < 0 else raw[k][max(mfl, 0):max(mfl, 0) + mvl]
         own = fr if st not in (_OK, _INDEX_NOT_FOUND) else None
-        if k > 0 and fc >= 0 and running != 0 and fc != running:
-            return _WAL_CRC, before, before, -1
-        if k > 0 and md not in (NONE, NIL) and mf != NONE and mf != md and (own is None or mff < own):
-            return _META_CONFLICT, before + mff, before + mff, -1
-        if own is not None:
+        cross = []
+        if k > 0:
+            if fc < 0:
+                return st, -1, before, 0    # its CRCs depend on the range before: verify joined
+            if running != 0 and fc != running:
+                cross.append((0, _WAL_CRC))
+            if md is not None and mff >= 0 and first_md != md:
+                cross.append((mff, _META_CONFLICT))
+            if fef >= 0:
+                if mei < rir:
+                    return st, -1, before, 0
+                gap_g = fei > last_op + 1 if last_op is not None else fei > rig
+                gap_l = fei > rir
+                if gap_g and not gap_l:
+                    cross.append((fef, _INDEX_GAP))
+                if gap_l and not gap_g and (own is None or own >= fef):
+                    return st, -1, before, 0
+        first = min(cross) if cross else None
+        if own is not None and (first is None or own <= first[0]):
             if st == _UNEXPECTED_EOF and k < world - 1 and fr == n:
                 return st, before + own, before + own, k
             return st, before + own, before + own, -1
+        if first is not None:
+            return first[1], before + first[0], before + first[0], -1
         before += n
         running = lc
-        if ml != NONE:
-            md = ml
+        if value_md is not None:
+            md = value_md
+        if lof >= 0:
+            last_op = loi
+        if fef >= 0:
+            enti = lei
+    if enti < rig:
+        return _INDEX_NOT_FOUND, -1, before, -1
     return _OK, -1, before, -1

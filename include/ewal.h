@@ -169,13 +169,48 @@ int ewal_download(ewal_ctx *ctx, void *h_dst, const void *d_src, uint64_t len);
 /* Same, from host memory: staged to the device first (PCIe-inclusive). */
 int ewal_readall_host(ewal_ctx *ctx, const void *h_buf, uint64_t len, uint64_t ri, ewal_result *out);
 /* After a successful readall: copy the ents / per-frame descriptors out.
- * Return the number copied (<= cap) or a negative error. */
+ * Return the number copied (<= cap) or a negative error.  The descriptors
+ * are rebuilt on demand from the ctx's stream-pass state and the ReadAll's
+ * stream bytes: d_buf must still hold them (the same lifetime rule as the
+ * ents' Data views), and any later compute call on the ctx (another ReadAll,
+ * a batch, a CRC, snapshot or save call, a staging call that reuses the
+ * staging buffer) makes ewal_copy_records return EWAL_E_INVAL. */
 int64_t ewal_copy_entries(ewal_ctx *ctx, ewal_entry *out, int64_t cap);
 int64_t ewal_copy_records(ewal_ctx *ctx, ewal_record *out, int64_t cap);
 /* After a successful readall with n_unrec > 0: the side list (sorted by ent)
  * and its bytes. */
 int64_t ewal_copy_unrec(ewal_ctx *ctx, ewal_unrec *out, int64_t cap);
 int64_t ewal_copy_unrec_bytes(ewal_ctx *ctx, uint8_t *out, int64_t cap);
+
+/* What one rank's range of ONE WAL split by file contributes to the joined
+ * verdict (etcd_amd/shard.py split_verdict applies ReadAll's
+ * cross-file rules with it), from the last ReadAll on ctx over that range --
+ * all frames of its chain, those after a failure included.  Frames are
+ * ordinals in the range, offsets are into the range's stream (d_buf must
+ * still hold it, as for ewal_copy_records).  The rules it serves:
+ *   crc seam       wal/wal.go:184-192 (every file opens with crcType{running
+ *                  CRC}, wal/wal.go:93,232-234)
+ *   metadata       wal/wal.go:178-183
+ *   ents / enti    wal/wal.go:170-174, 203-206 (the index-gap rule across the
+ *                  range boundary, rewinds below the range's w.ri, and the
+ *                  global ErrIndexNotFound) */
+typedef struct ewal_range_info {
+  int64_t n_frames;              /* frames on the chain */
+  int64_t first_crc;             /* Crc of frame 0 when it is a crcType record, else -1 */
+  int64_t md_first_frame;        /* the first metadataType frame, -1: none */
+  int64_t md_first_off, md_first_len;   /* its Data; off -1 == nil */
+  int64_t md_value_frame;        /* the first metadataType frame with non-nil Data (the value ReadAll keeps), -1 */
+  int64_t md_value_off, md_value_len;
+  int64_t first_entry_frame;     /* the first entryType frame, -1: none */
+  int64_t last_entry_frame;
+  uint64_t first_entry_index;    /* its Entry.Index */
+  uint64_t min_entry_index;      /* the least Entry.Index of the range */
+  uint64_t last_entry_index;     /* the last entry frame's Index (w.enti after the range) */
+  int64_t last_op_frame;         /* the last entry frame with Index >= the ReadAll's ri (the last
+                                    append to ents, wal/wal.go:171-173), -1: none */
+  uint64_t last_op_index;
+} ewal_range_info;
+int ewal_copy_range_info(ewal_ctx *ctx, ewal_range_info *out);
 
 /* ---- directory-level API: wal.OpenAtIndex + ReadAll + writer ----------- */
 typedef struct ewal_wal ewal_wal;

@@ -29,6 +29,7 @@ int ewal_stage_to_device(ewal_ctx *, const void *, uint64_t, void **) { return E
 int ewal_stage_begin(ewal_ctx *, uint64_t) { return EWAL_E_NODEVICE; }
 int ewal_stage_put(ewal_ctx *, uint64_t, const void *, uint64_t) { return EWAL_E_NODEVICE; }
 int ewal_stage_readall(ewal_ctx *, uint64_t, uint64_t, ewal_result *) { return EWAL_E_NODEVICE; }
+int ewal_stage_sync(ewal_ctx *) { return EWAL_E_NODEVICE; }
 }
 
 static int fails = 0;

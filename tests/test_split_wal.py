@@ -4,9 +4,11 @@ runs ReadAll over its contiguous range of files, then shard.split_verdict's
 one all-gather applies ReadAll's cross-file rules (crc seam, metadata) in file
 order.  The global verdict must equal ReadAll over all the files.
 
-CPU (gloo, world_size 2 and 3): each range's result comes from the oracle's
-ReadAll of that range.  GPU (-m gpu, world_size 2 on one MI355X, gloo for the
-exchange): each range's result comes from the engine (libewal.so)."""
+CPU (gloo, world_size 2 and 3): each range's result and range info come from
+the oracle.  GPU (-m gpu, world_size 2 on one MI355X, gloo for the exchange):
+from the product alone -- ReadAll and ewal_copy_range_info (libewal.so); no
+oracle parser builds the per-range inputs (the oracle only judges the joined
+verdict)."""
 import os
 import random
 import socket
@@ -28,34 +30,33 @@ def _free_port():
     return p
 
 
-def md_digest(b):
-    return shard.NIL if b is None else (len(b) << 32) | O.crc32_update(0, b)
-
-
-def build_files(rng, nfiles, md=b"metadata", md_override=None, ents=(5, 60)):
+def build_files(rng, nfiles, md=b"metadata", md_override=None, ents=(5, 60), shift=None):
     """wal.Create + Save + Cut ... as the reference writes them: file k starts
-    with crcType{running CRC} and metadataType{md}; returns [(bytes, first
-    entry index)]."""
+    with crcType{running CRC} and metadataType{md}; returns [(bytes, the index
+    in the file's name)].  shift = {k: (name delta, entry delta)}: file k's
+    name index and its first entry Index moved (a leader change rewriting
+    indexes after a Cut, a gap, a name that disagrees with the entries)."""
     files, prev, idx = [], 0, 0
     for k in range(nfiles):
         e = O.WalEncoder(prev)
         e.save_crc(prev)
         e.encode(1, md_override.get(k, md) if md_override else md)
-        first = idx
+        dn, de = (shift or {}).get(k, (0, 0))
+        name = idx + dn
+        idx += de
         for _ in range(rng.randrange(*ents)):
             e.save_entry(0, 1, idx, rng.randbytes(rng.randrange(0, 2000)))
             idx += 1
         e.save_state(1, 1, idx)
-        files.append((e.getvalue(), first))
+        files.append((e.getvalue(), name))
         prev = e.crc
     return files
 
 
-def range_inputs(buf, ri, result):
-    """split_verdict's per-rank inputs from a range's ReadAll result and its
-    decoded records [(type, crc, data)]."""
-    st, fr, n, lc, md = result
-    recs, p = [], 0                      # the frames' records (int64 length + Record.Unmarshal), no CRC check
+def oracle_range_info(buf, ri):
+    """wal.range_info()'s fields from the oracle's record and entry decoders
+    over the range's framable frames (the CPU stand-in for ewal_range_info)."""
+    recs, p = [], 0
     while p + 8 <= len(buf):
         L = struct.unpack_from("<q", buf, p)[0]
         if L < 0 or p + 8 + L > len(buf):
@@ -63,18 +64,28 @@ def range_inputs(buf, ri, result):
         rs, r = O.record_unmarshal(buf[p + 8:p + 8 + L])
         if rs != O.OK:
             break
-        recs.append((r["type"], r["crc"], r["data"]))
+        recs.append(r)
         p += 8 + L
-    fc = recs[0][1] if recs and recs[0][0] == 4 else -1
-    mi = next((i for i, r in enumerate(recs) if r[0] == 1), None)
-    mf, mff = (shard.NONE, -1) if mi is None else (md_digest(recs[mi][2] if recs[mi][2] else None), mi)
-    ml = md_digest(md) if any(r[0] == 1 for r in recs[:n if st == O.OK else fr]) else shard.NONE
-    return st, fr, n, lc, fc, mf, mff, ml
-
-
-def oracle_result(buf, ri):
-    o = O.readall(buf, ri)
-    return o["status"], o["fail_record"], o["n_records"], o["last_crc"], o["metadata"]
+    info = dict(n_frames=len(recs), first_crc=recs[0]["crc"] if recs and recs[0]["type"] == 4 else -1,
+                md_first_frame=-1, md_first=None, md_value_frame=-1, md_value=None, first_entry_frame=-1,
+                first_entry_index=0, min_entry_index=0, last_entry_index=0, last_op_frame=-1, last_op_index=0)
+    idx = []
+    for i, r in enumerate(recs):
+        if r["type"] == 1:
+            if info["md_first_frame"] < 0:
+                info["md_first_frame"], info["md_first"] = i, r["data"] or None
+            if r["data"] and info["md_value_frame"] < 0:
+                info["md_value_frame"], info["md_value"] = i, r["data"]
+        elif r["type"] == 2:
+            est, e = O.entry_unmarshal(r["data"] or b"")
+            idx.append((i, e["index"]))
+    if idx:
+        info.update(first_entry_frame=idx[0][0], first_entry_index=idx[0][1],
+                    min_entry_index=min(x for _, x in idx), last_entry_index=idx[-1][1])
+        ops = [(i, x) for i, x in idx if x >= ri]
+        if ops:
+            info.update(last_op_frame=ops[-1][0], last_op_index=ops[-1][1])
+    return info
 
 
 def _worker(rank, world, port, cases, use_gpu, q):
@@ -87,19 +98,22 @@ def _worker(rank, world, port, cases, use_gpu, q):
             from etcd_amd import wal as W
             ctx = W.Context(0)
         out = []
-        for ranges in cases:
+        for ranges, rig in cases:
             ranges = list(ranges)
             while True:
                 buf, ri = ranges[rank]
-                if use_gpu:
+                if use_gpu:    # the product alone: ReadAll + ewal_range_info over the range
                     g = W.readall_bytes(buf, ri, ctx, with_ents=False)
-                    res = (g.status, g.fail_record, g.n_records, g.last_crc, g.metadata)
+                    res = (g.status, g.fail_record, g.n_records, g.last_crc)
+                    info = W.range_info(ctx, stream=buf)
                 else:
-                    res = oracle_result(buf, ri)
-                v = shard.split_verdict(dist, world, rank, *range_inputs(buf, ri, res))
+                    o = O.readall(buf, ri)
+                    res = (o["status"], o["fail_record"], o["n_records"], o["last_crc"])
+                    info = oracle_range_info(buf, ri)
+                v = shard.split_verdict(dist, world, rank, res, info, ri, rig)
                 if v[3] < 0:
                     break
-                # a torn frame at the end of range k: ranges k.. verified joined, on rank k
+                # ranges k.. verified joined, on rank k
                 k = v[3]
                 ranges = ranges[:k] + [(b"".join(b for b, _ in ranges[k:]), ranges[k][1])] + \
                     [(b"", 0)] * (world - k - 1)
@@ -112,14 +126,23 @@ def _worker(rank, world, port, cases, use_gpu, q):
         dist.destroy_process_group()
 
 
+KINDS = ("clean", "corrupt_late", "corrupt_both", "seam", "meta", "meta_nil", "torn", "rewind", "gap_cross",
+         "gap_name", "name_low", "index_not_found", "ri_mid")
+
+
 def _cases(rng, world):
-    """[(all bytes, [per-rank (range bytes, ri)])] over clean / corrupt /
-    seam / metadata-conflict WALs."""
+    """[(all bytes, w.ri of the whole ReadAll, [per-rank (range bytes, ri)])]
+    over clean / corrupt / seam / metadata-conflict / torn / index-rule WALs."""
     out = []
-    for kind in ("clean", "corrupt_late", "corrupt_both", "seam", "meta", "meta_nil", "torn"):
+    for kind in KINDS:
         nf = world * 2
+        per = nf // world
         over = {nf // 2: b"other"} if kind == "meta" else ({1: None} if kind == "meta_nil" else None)
-        files = build_files(rng, nf, md_override=over)
+        shift = {"rewind": {per: (0, -3)},          # a range's first entries rewrite indexes below its name
+                 "gap_cross": {per: (2, 2)},        # name and entries skip two indexes: a gap only globally
+                 "gap_name": {per: (0, 2)},         # entries skip two indexes after the name: a gap everywhere
+                 "name_low": {per: (-2, 0)}}.get(kind)   # the name lies below the entries: a gap only locally
+        files = build_files(rng, nf, md_override=over, shift=shift)
         blobs = [bytearray(b) for b, _ in files]
         if kind == "corrupt_late":
             blobs[-1][len(blobs[-1]) // 2] ^= 0x10
@@ -128,25 +151,22 @@ def _cases(rng, world):
             blobs[-1][len(blobs[-1]) // 2] ^= 0x10
         if kind == "seam":     # the crcType record of the file opening the last range carries a wrong CRC
             k = nf - 2
-            c = O.WalEncoder(12345)
-            c.save_crc(12345)
-            fixed = c.getvalue()
-            old = O.WalEncoder(0)
-            old.save_crc(0)
-            head = len(old.getvalue())    # 12-byte crc record when the CRC varint is short; rebuild the file
             b2 = O.WalEncoder(12345)
             b2.save_crc(12345)
             body = bytes(blobs[k])[8 + blobs[k][0]:]
             blobs[k] = bytearray(b2.getvalue() + body)
-            assert fixed and head
         if kind == "torn":          # the last file of range 0 torn: its frame reads on into range 1
-            blobs[nf // world - 1] = blobs[nf // world - 1][:-5]
-        per = nf // world
+            blobs[per - 1] = blobs[per - 1][:-5]
+        rig = 0
+        if kind == "index_not_found":    # OpenAtIndex past the last entry: the global ErrIndexNotFound
+            rig = files[-1][1] + 1000
+        if kind == "ri_mid":             # OpenAtIndex inside the first file
+            rig = 3
         ranges = []
         for r in range(world):
             part = b"".join(bytes(x) for x in blobs[r * per:(r + 1) * per])
-            ranges.append((part, 0 if r == 0 else files[r * per][1]))
-        out.append((b"".join(bytes(x) for x in blobs), ranges))
+            ranges.append((part, rig if r == 0 else max(rig, files[r * per][1])))
+        out.append((b"".join(bytes(x) for x in blobs), rig, ranges))
     return out
 
 
@@ -156,7 +176,7 @@ def _run(world, use_gpu):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    ps = [ctx.Process(target=_worker, args=(r, world, port, [c[1] for c in cases], use_gpu, q))
+    ps = [ctx.Process(target=_worker, args=(r, world, port, [(c[2], c[1]) for c in cases], use_gpu, q))
           for r in range(world)]
     for p in ps:
         p.start()
@@ -167,21 +187,42 @@ def _run(world, use_gpu):
         got = [x for x in res[r] if x[0] != "resplit"]
         assert len(got) == len(cases)
         assert any(x[0] == "resplit" for x in res[r])       # the torn-file case went through a resplit
-        for i, (allb, _) in enumerate(cases):
-            o = O.readall(allb, 0)
-            want = (o["status"], o["fail_record"] if o["status"] != O.OK else -1)
-            st, fr, _ = got[i]
-            assert (st, fr) == want, (i, r, (st, fr), want)
+        for i, (allb, rig, _) in enumerate(cases):
+            o = O.readall(allb, rig)
+            want = (o["status"], o["fail_record"] if o["status"] not in (O.OK, O.ERR_INDEX_NOT_FOUND) else -1,
+                    o["n_records"])
+            assert got[i] == want, (KINDS[i], r, got[i], want)
     return cases
 
 
 @pytest.mark.parametrize("world", [2, 3])
 def test_split_verdict_oracle_ranges(world):
     cases = _run(world, use_gpu=False)
-    kinds = [O.readall(c[0], 0)["status"] for c in cases]
-    assert O.ERR_WAL_CRC in kinds and O.ERR_METADATA_CONFLICT in kinds and O.ERR_RECORD_CRC in kinds
+    kinds = [O.readall(c[0], c[1])["status"] for c in cases]
+    for st in (O.ERR_WAL_CRC, O.ERR_METADATA_CONFLICT, O.ERR_RECORD_CRC, O.PANIC_INDEX_GAP, O.ERR_INDEX_NOT_FOUND):
+        assert st in kinds, st
 
 
 @pytest.mark.gpu
 def test_split_verdict_gpu_ranges():
     _run(2, use_gpu=True)
+
+
+@pytest.mark.gpu
+def test_range_info_gpu_matches_oracle(ctx):
+    """ewal_copy_range_info field by field against the oracle's decoders, on
+    every range of every split case (world 2 and 3)."""
+    from etcd_amd import wal as W
+    for world in (2, 3):
+        for allb, rig, ranges in _cases(random.Random(17 + world), world):
+            for buf, ri in ranges + [(allb, rig)]:
+                g = W.readall_bytes(buf, ri, ctx, with_ents=False)
+                o = O.readall(buf, ri)
+                assert (g.status, g.fail_record, g.n_records) == (o["status"], o["fail_record"], o["n_records"])
+                gi, oi = W.range_info(ctx, stream=buf), oracle_range_info(buf, ri)
+                if g.status == O.OK:      # every frame framable: the chain is the oracle's frame list
+                    assert gi == oi, (gi, oi)
+                else:                     # the fields split_verdict reads before the failure
+                    for key in ("first_crc", "md_first_frame", "md_first", "first_entry_frame", "first_entry_index"):
+                        if oi["md_first_frame"] < g.fail_record or not key.startswith("md"):
+                            assert gi[key] == oi[key], (key, gi[key], oi[key])
