@@ -143,7 +143,9 @@ def run_shards(a, dist, rank, world, local, cpu_seconds=None):
     global shard id; one corrupt record in global shard 2749 mod (512 N).
     The verdicts cross ranks in one all-reduce (etcd_amd/shard.py).  The
     shards are generated and copied to HBM 64 at a time (host memory stays
-    at ~4 GiB per rank)."""
+    at ~4 GiB per rank).  `torn5`: the same batch with the last frame of 5
+    shards torn (a crash mid-write): those 5 are replayed alone, the other
+    507 keep the batch's pass (wal/decoder.go:30-36)."""
     nsh, smib = a.shards_per_gpu, a.shard_mib
     cpu_seconds = a.cpu_seconds if cpu_seconds is None else cpu_seconds
     first = rank * nsh
@@ -152,14 +154,16 @@ def run_shards(a, dist, rank, world, local, cpu_seconds=None):
     target = smib << 20
     chunk = 64
     ctx = W.Context(local)
-    dbuf = ctx.alloc(nsh * (target + 2 * 4096 + 4096) + 64)
+    dev = torch.device("cuda", local)
+    dmem = torch.empty(nsh * (target + 2 * 4096 + 4096) + 64, dtype=torch.uint8, device=dev)
+    dbuf = W.DeviceBuffer(ctx, C.c_void_p(dmem.data_ptr()), dmem.numel())   # torch owns it
     lens, nrec, pos, keep = [], [], 0, None
     for c0 in range(0, nsh, chunk):
         ids = list(range(c0, min(nsh, c0 + chunk)))
         blob, ls, nr = W.synth_shards([first + i for i in ids], target, 128, 4096,
                                       corrupt={bad_shard - first - c0: 1000}
                                       if first + c0 <= bad_shard < first + c0 + len(ids) else {})
-        dbuf.upload_ptr(C.addressof((C.c_char * len(blob)).from_buffer(blob)), len(blob), pos)
+        dmem[pos:pos + len(blob)].copy_(torch.frombuffer(blob, dtype=torch.uint8))
         pos += len(blob)
         lens += ls
         nrec += nr
@@ -193,10 +197,40 @@ def run_shards(a, dist, rank, world, local, cpu_seconds=None):
 
     elapsed = timed(dist, a.steps, step)
     ms = elapsed / a.steps * 1e3
-    r0 = last["r"][0]
+    r0 = L.Result.from_buffer_copy(last["r"][0])   # (c_out is reused below)
     assert all((x.status, x.fail_record) == ((L.ERR_RECORD_CRC, 1000) if first + i == bad_shard else (L.OK, -1))
                for i, x in enumerate(c_out))
     frames = sum(nrec)
+    # ---- torn5: five shards end in a torn frame -----------------------------
+    torn = sorted({(nsh * j) // 5 + 7 for j in range(5)} - {bad_shard - first})[:5]
+    tlens = [x - (1000 + 37 * i) if i in torn else x for i, x in enumerate(lens)]
+    tmem = torch.empty(sum(tlens) + 64, dtype=torch.uint8, device=dev)
+    so, to = 0, 0
+    for x, y in zip(lens, tlens):
+        tmem[to:to + y].copy_(dmem[so:so + y])
+        so += x
+        to += y
+    tbuf = W.DeviceBuffer(ctx, C.c_void_p(tmem.data_ptr()), tmem.numel())
+    c_tlens = (C.c_uint64 * nsh)(*tlens)
+    torch.cuda.synchronize()
+
+    def tstep():
+        rc = L.lib.ewal_readall_batch_device(ctx.handle, tbuf.ptr, nsh, c_tlens, c_ris, c_out)
+        assert rc == 0, rc
+
+    for _ in range(max(a.warmup, 1)):
+        tstep()
+    for i, x in enumerate(c_out):
+        if i in torn:
+            assert x.status == L.ERR_UNEXPECTED_EOF and x.flags & L.FLAG_SHARD_FALLBACK, (i, x.status, x.flags)
+        else:
+            want = (L.ERR_RECORD_CRC, 1000) if first + i == bad_shard else (L.OK, -1)
+            assert (x.status, x.fail_record) == want and not x.flags & L.FLAG_SHARD_FALLBACK, (i, x.status)
+    tms = timed(dist, a.steps, tstep) / a.steps * 1e3
+    torn5 = {"ms_per_step": round(tms, 4), "vs_clean": round(tms / ms, 4), "torn_shards": torn,
+             "note": "the same batch with the last frame of 5 shards torn: they are replayed alone "
+                     "(EWAL_FLAG_SHARD_FALLBACK), every other shard keeps the batch's fused pass"}
+    del tmem
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         from oracle import oracle as O   # baseline only
@@ -239,10 +273,11 @@ def run_shards(a, dist, rank, world, local, cpu_seconds=None):
                      "pipeline_frac": round(nb / (r0.device_ms / 1e3) / 1e9 / HBM_PEAK_GBPS, 4),
                      "step_frac": round(nb / (ms / 1e3) / 1e9 / HBM_PEAK_GBPS, 4)},
         "pipeline_device_ms": round(r0.device_ms, 4),
+        "torn5": torn5,
         "cpu_baseline": cpu,
         "gen_seconds": round(gen_s, 2),
     }
-    dbuf.free()
+    del dmem
     ctx.close()
     return out
 

@@ -141,6 +141,8 @@ _SIGS = {
     "emsg_copy_entries": (C.c_int64, [vp, C.c_uint64, C.POINTER(EntryDesc), C.c_int64]),
     "ewal_batch_copy_entries": (C.c_int64, [vp, C.c_uint64, C.POINTER(EntryDesc), C.c_int64]),
     "ewal_copy_records": (C.c_int64, [vp, C.POINTER(RecordDesc), C.c_int64]),
+    "ewal_batch_copy_unrec": (C.c_int64, [vp, C.c_uint64, C.POINTER(UnrecDesc), C.c_int64]),
+    "ewal_batch_copy_unrec_bytes": (C.c_int64, [vp, C.c_uint64, vp, C.c_int64]),
     "ewal_copy_range_info": (C.c_int, [vp, C.POINTER(RangeInfo)]),
     "ewal_copy_unrec": (C.c_int64, [vp, C.POINTER(UnrecDesc), C.c_int64]),
     "ewal_copy_unrec_bytes": (C.c_int64, [vp, vp, C.c_int64]),

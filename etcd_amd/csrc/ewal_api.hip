@@ -131,6 +131,8 @@ struct ewal_ctx {
   DevBuf moff, mlen, mcnt, mfirst, mout, ments;
   uint64_t mtotal = 0;
   std::vector<uint64_t> bent_first, bnents;   // per shard: first ent in bents, count
+  std::vector<std::vector<ewal_unrec>> bunrec;       // per shard replayed alone: its XXX_unrecognized side list
+  std::vector<std::vector<uint8_t>> bunrec_bytes;
   Small *h_small = nullptr;        // host-mapped pinned mirrors (written by k_export_small / k_result)
   ResultDev *h_res = nullptr;
   Small *h_small_dev = nullptr;    // their device-side addresses
@@ -1098,6 +1100,64 @@ static int fused_batch(ewal_ctx *c, DevTables *tb, const uint8_t *d_buf, uint64_
   return 0;
 }
 
+// ReadAll of the listed shards of a batch, each alone (readall_impl over an
+// aligned scratch copy: the stream pass reads 16-B aligned): shards the
+// fused pass could not decide (torn or corrupt framing, index rewinds,
+// encodings the canonical parser declines, unknown fields) or the whole
+// batch when the general path could not decide it.  Their ents are appended
+// to bents after the first `have` entries; their XXX_unrecognized side lists
+// are kept per shard (ewal_batch_copy_unrec).  device_ms of every result
+// becomes the batch's plus the replays'.
+static int replay_shards(ewal_ctx *c, const uint8_t *d_buf, const std::vector<uint64_t> &soff, const uint64_t *lens,
+                         const uint64_t *ris, ewal_result *out, const std::vector<uint32_t> &which, uint64_t have) {
+  const uint32_t ns = (uint32_t)soff.size() - 1;
+  c->bunrec.assign(ns, {});
+  c->bunrec_bytes.assign(ns, {});
+  if (which.empty()) return 0;
+  const uint64_t keep_k = c->last_k;
+  const double batch_ms = ns ? out[0].device_ms : 0.0, batch_stream = ns ? out[0].stream_ms : 0.0;
+  double extra = 0;
+  for (uint32_t i : which) {
+    const uint8_t *p = d_buf;
+    if (lens[i]) {
+      EW_CHECK(c->bshard.ensure(lens[i] + 64));
+      EW_CHECK(hipMemcpyAsync(c->bshard.p, d_buf + soff[i], lens[i], hipMemcpyDeviceToDevice, c->stream));
+      p = c->bshard.as<uint8_t>();
+    }
+    ewal_result r;
+    int rc = readall_impl(c, p, lens[i], ris[i], &r);
+    if (rc < 0) return rc;
+    extra += r.device_ms;
+    r.flags |= EWAL_FLAG_SHARD_FALLBACK;
+    if (r.status == EWAL_OK && r.n_unrec) {
+      c->bunrec[i] = c->unrec;
+      c->bunrec_bytes[i].resize(c->unrec_bytes);
+      if (c->unrec_bytes)
+        EW_CHECK(hipMemcpy(c->bunrec_bytes[i].data(), c->uarena.p, c->unrec_bytes, hipMemcpyDeviceToHost));
+    }
+    const uint64_t ne = r.status == EWAL_OK ? (uint64_t)r.n_ents : 0;
+    c->bent_first[i] = 0;
+    c->bnents[i] = 0;
+    if (ne) {
+      EW_CHECK(grow_keep(c->bents, (size_t)(have + ne) * sizeof(ewal_entry), (size_t)have * sizeof(ewal_entry),
+                         c->stream));
+      EW_CHECK(hipMemcpyAsync(c->bents.as<ewal_entry>() + have, c->ents.p, (size_t)ne * sizeof(ewal_entry),
+                              hipMemcpyDeviceToDevice, c->stream));
+      c->bent_first[i] = have;
+      c->bnents[i] = ne;
+      have += ne;
+    }
+    out[i] = r;
+  }
+  EW_CHECK(hipStreamSynchronize(c->stream));
+  for (uint32_t i = 0; i < ns; ++i) {
+    out[i].device_ms = batch_ms + extra;
+    if (out[i].flags & EWAL_FLAG_SHARD_FALLBACK) out[i].stream_ms = batch_stream;
+  }
+  c->last_k = keep_k;
+  return 0;
+}
+
 // Batched ReadAll over many independent WALs (per-raft-group shards, SURVEY
 // §8(d) C3) laid end to end in one device buffer: ONE stream pass, ONE frame
 // pass and ONE segmented check (k_check<true>) for the whole batch, two host
@@ -1139,7 +1199,20 @@ static int readall_batch_impl(ewal_ctx *c, const uint8_t *d_buf, uint32_t ns, co
       bool done = false;
       rc = fused_batch(c, tb, d_buf, B, ns, soff, ris, ccap, rdcap, out, &done);
       if (rc) return rc;
-      if (done) return 0;
+      if (done) {   // every shard decided but those the fused pass flagged: they are replayed alone
+        std::vector<uint32_t> bad;
+        for (uint32_t i = 0; i < ns; ++i)
+          if (out[i].flags & EW_SHARD_BAD) bad.push_back(i);
+        if (bad.empty()) {
+          c->bunrec.assign(ns, {});
+          c->bunrec_bytes.assign(ns, {});
+          return 0;
+        }
+        rc = replay_shards(c, d_buf, soff, lens, ris, out, bad, c->h_small->total);
+        if (rc) return rc;
+        forget_records(c);
+        return 0;
+      }
     }
     uint32_t *pf = nullptr;
     bool rescanned = false;
@@ -1238,6 +1311,8 @@ static int readall_batch_impl(ewal_ctx *c, const uint8_t *d_buf, uint32_t ns, co
       if (fast) {
         EW_CHECK(hipEventElapsedTime(&dev_ms, c->ev0, c->ev1));
         EW_CHECK(hipEventElapsedTime(&str_ms, c->evs0, c->evs1));
+        c->bunrec.assign(ns, {});
+        c->bunrec_bytes.assign(ns, {});
         for (uint32_t i = 0; i < ns; ++i) {
           out[i].device_ms = dev_ms;
           out[i].stream_ms = str_ms;
@@ -1249,40 +1324,13 @@ static int readall_batch_impl(ewal_ctx *c, const uint8_t *d_buf, uint32_t ns, co
       }
     }
   }
-  // one shard at a time (a shard's bytes are copied to an aligned scratch
-  // buffer: the stream pass reads 16-B aligned)
+  // one shard at a time (the general path could not decide the batch)
   c->bent_first.assign(ns, 0);
   c->bnents.assign(ns, 0);
-  uint64_t have = 0;
-  for (uint32_t i = 0; i < ns; ++i) {
-    const uint8_t *p = d_buf;
-    if (lens[i]) {
-      EW_CHECK(c->bshard.ensure(lens[i] + 64));
-      EW_CHECK(hipMemcpyAsync(c->bshard.p, d_buf + soff[i], lens[i], hipMemcpyDeviceToDevice, c->stream));
-      p = c->bshard.as<uint8_t>();
-    }
-    rc = readall_impl(c, p, lens[i], ris[i], &out[i]);
-    if (rc < 0) return rc;
-    out[i].flags |= EWAL_FLAG_SHARD_FALLBACK;
-    if (out[i].status == EWAL_OK && out[i].n_unrec) {
-      // the batch keeps no per-shard side list: such a shard (unknown fields
-      // in its returned ents / HardState) is replayed alone for them
-      out[i].status = EWAL_UNSUPPORTED_ENCODING;
-      out[i].detail = 1;
-      out[i].n_unrec = 0;
-    }
-    const uint64_t ne = out[i].status == EWAL_OK ? (uint64_t)out[i].n_ents : 0;
-    if (ne) {
-      EW_CHECK(grow_keep(c->bents, (size_t)(have + ne) * sizeof(ewal_entry), (size_t)have * sizeof(ewal_entry),
-                         c->stream));
-      EW_CHECK(hipMemcpyAsync(c->bents.as<ewal_entry>() + have, c->ents.p, (size_t)ne * sizeof(ewal_entry),
-                              hipMemcpyDeviceToDevice, c->stream));
-      c->bent_first[i] = have;
-      c->bnents[i] = ne;
-      have += ne;
-    }
-  }
-  EW_CHECK(hipStreamSynchronize(c->stream));
+  std::vector<uint32_t> all(ns);
+  for (uint32_t i = 0; i < ns; ++i) all[i] = i;
+  rc = replay_shards(c, d_buf, soff, lens, ris, out, all, 0);
+  if (rc) return rc;
   c->last_ok = false;
   forget_records(c);   // the descriptors of the last one-by-one shard are not a ReadAll of the batch
   return 0;
@@ -1460,6 +1508,22 @@ int64_t ewal_batch_copy_entries(ewal_ctx *c, uint64_t shard, ewal_entry *out, in
   return n;
 }
 
+int64_t ewal_batch_copy_unrec(ewal_ctx *c, uint64_t shard, ewal_unrec *out, int64_t cap) {
+  if (!c || (!out && cap) || shard >= c->bunrec.size()) return EWAL_E_INVAL;
+  const std::vector<ewal_unrec> &u = c->bunrec[shard];
+  const int64_t n = std::min<int64_t>(cap, (int64_t)u.size());
+  if (n > 0) std::memcpy(out, u.data(), (size_t)n * sizeof(ewal_unrec));
+  return n;
+}
+
+int64_t ewal_batch_copy_unrec_bytes(ewal_ctx *c, uint64_t shard, uint8_t *out, int64_t cap) {
+  if (!c || (!out && cap) || shard >= c->bunrec_bytes.size()) return EWAL_E_INVAL;
+  const std::vector<uint8_t> &b = c->bunrec_bytes[shard];
+  const int64_t n = std::min<int64_t>(cap, (int64_t)b.size());
+  if (n > 0) std::memcpy(out, b.data(), (size_t)n);
+  return n;
+}
+
 int ewal_device_alloc(ewal_ctx *c, uint64_t len, void **d_out) {
   if (!c || !d_out) return EWAL_E_INVAL;
   EW_CHECK(hipSetDevice(c->device));
@@ -1570,7 +1634,7 @@ static int need_records(ewal_ctx *c) {
 }
 
 int64_t ewal_copy_records(ewal_ctx *c, ewal_record *out, int64_t cap) {
-  if (!c || (!out && cap)) return EWAL_E_INVAL;
+  if (!c || (!out && cap) || !c->rec_valid) return EWAL_E_INVAL;
   int64_t n = std::min<int64_t>(cap, (int64_t)c->last_n);
   if (n > 0) {
     if (int rc = need_records(c)) return rc;

@@ -78,8 +78,11 @@ struct ShardAgg {
   unsigned long long first_meta;  // min non-empty metadata frame (~0)
   unsigned long long ent_first;   // global op index of the shard's first entry op (~0)
   uint32_t lastop;                // 1 + the shard's last entry-op frame (0: none)
-  uint32_t pad;
+  uint32_t bad;                   // fused pass: the shard is not on the regular path (replayed alone)
 };
+// ewal_result.flags bit of a batched shard the fused pass could not decide
+// (internal: the host replays the shard alone and clears it)
+#define EW_SHARD_BAD 0x40000000
 
 struct SegArgs {
   uint2 *ulist;            // (frame, op index) of entry ops with XXX_unrecognized (both modes)

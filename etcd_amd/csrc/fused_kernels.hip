@@ -98,6 +98,12 @@ __device__ __forceinline__ bool fc_ran(const Small *ds, uint64_t ccap, uint64_t 
 __device__ __forceinline__ bool fc_valid(const Small *ds, uint64_t ccap, uint64_t ecap) {
   return fc_ran(ds, ccap, ecap) && ds->pos0 == 0 && !ds->irregular && !ds->fc.rare;
 }
+// Batched: the regular case is decided per shard (ShardAgg.bad: a shard whose
+// frames are not its candidates, or that needs a rare path, is replayed alone
+// by the host); what stays global is capacity.
+__device__ __forceinline__ bool fc_valid_seg(const Small *ds, uint64_t ccap, uint64_t ecap) {
+  return fc_ran(ds, ccap, ecap) && !ds->fc.rare;
+}
 
 // S_{2^m} as nibble tables: N[m][k][d] = S_{2^m}(d << 4k), 8 x 16 entries per
 // operator (512 B; m = 0..16 in 8.5 KiB of LDS instead of 68 KiB of byte
@@ -347,22 +353,6 @@ __global__ __launch_bounds__(FC_THREADS, FC_WGS) void k_fc(FcArgs a, SegArgs sg)
     const bool ok = decode_canon<FC_THREADS>(a.buf, a.B, p, a.pwave, a.v, s_t4, s_svp, s_win + tid, d, L, Pfo, Pfd,
                                              (a.ablate & 2) != 0, flush);
     const uint64_t s = p + 8 + (uint64_t)L;
-    if (live && !ok) rare |= 1u;
-    if (!ok) {   // not decoded (the pass is void): no field of it may address memory
-      d.type = 0;
-      d.dlen = 0;
-      d.doff = p + 8;
-    }
-    if (live && r + 1 < K32 && pn != s) irr = 1;
-    if (live && r + 1 == K32) {   // the chain's terminal
-      ds->q = s;
-      ds->qlen = (s <= a.B && a.B - s >= 8) ? (int64_t)ld_le64_b(a.buf, a.B, s) : 0;
-    }
-    // neighbours in the wave: the predecessor's stored CRC, the successor's
-    // P at its frame start; the tile's edge frames take theirs from the
-    // neighbouring tiles' records in k_fc_seam
-    const uint32_t cprev = (uint32_t)__shfl_up((int)d.crc, 1);
-    const uint32_t pnext = (uint32_t)__shfl_down((int)Pfo, 1);
     uint32_t sh = 0, lo = 0;                   // SEG: the frame's shard and its first frame
     uint64_t ri = a.ri;
     uint32_t sh0 = 0, sh1 = 0;
@@ -375,6 +365,31 @@ __global__ __launch_bounds__(FC_THREADS, FC_WGS) void k_fc(FcArgs a, SegArgs sg)
       lo = sg.fs[sh];
       ri = sg.ri[sh];
     }
+    bool bad = false;   // SEG: this frame takes its shard off the regular path (the host replays it alone)
+    if (live && !ok) {
+      if (SEG) bad = true;
+      else rare |= 1u;
+    }
+    if (!ok) {   // not decoded (the pass is void): no field of it may address memory
+      d.type = 0;
+      d.dlen = 0;
+      d.doff = p + 8;
+    }
+    if (SEG) {
+      // a shard's frames are its candidates, the last one ending at the shard's end
+      if (live && (r + 1 == sg.fs[sh + 1] ? s != sg.soff[sh + 1] : pn != s)) bad = true;
+    } else {
+      if (live && r + 1 < K32 && pn != s) irr = 1;
+      if (live && r + 1 == K32) {   // the chain's terminal
+        ds->q = s;
+        ds->qlen = (s <= a.B && a.B - s >= 8) ? (int64_t)ld_le64_b(a.buf, a.B, s) : 0;
+      }
+    }
+    // neighbours in the wave: the predecessor's stored CRC, the successor's
+    // P at its frame start; the tile's edge frames take theirs from the
+    // neighbouring tiles' records in k_fc_seam
+    const uint32_t cprev = (uint32_t)__shfl_up((int)d.crc, 1);
+    const uint32_t pnext = (uint32_t)__shfl_down((int)Pfo, 1);
     // decoder.decode's check + ReadAll's crc-record rule (as k_check)
     const bool dfirst = lane == 0 && r > lo;
     const bool dlast = live && r == rl && r + 1 < K32;
@@ -500,7 +515,10 @@ __global__ __launch_bounds__(FC_THREADS, FC_WGS) void k_fc(FcArgs a, SegArgs sg)
         bool gap;
         if (has) {
           const uint64_t kq = kp - ri;
-          if (k <= kq) rare |= 2u;             // an index rewind: the general path's survivor pass
+          if (k <= kq) {                       // an index rewind: the general path's survivor pass
+            if (SEG) bad = true;
+            else rare |= 2u;
+          }
           gap = k > kq && k - kq > 1;
         } else {
           gap = k > 0;
@@ -528,6 +546,7 @@ __global__ __launch_bounds__(FC_THREADS, FC_WGS) void k_fc(FcArgs a, SegArgs sg)
         }
       }
     }
+    if (SEG && bad) atomicOr(&sg.sagg[sh].bad, 1u);
   }
   if (pend) {
     if (SEG) a.ents[pidx] = pe;
@@ -689,13 +708,17 @@ __global__ __launch_bounds__(256) void k_fc_seam(const uint8_t *__restrict__ buf
         break;
       }
       if (far) {
-        atomicOr(&ds->fc.rare, 8u);
+        if (SEG) atomicOr(&sg.sagg[sh].bad, 1u);
+        else atomicOr(&ds->fc.rare, 8u);
       } else {
         const uint64_t k = tr.first_index - ri;
         bool gap;
         if (has) {
           const uint64_t kq = pidx - ri;
-          if (k <= kq) atomicOr(&ds->fc.rare, 2u);
+          if (k <= kq) {
+            if (SEG) atomicOr(&sg.sagg[sh].bad, 1u);
+            else atomicOr(&ds->fc.rare, 2u);
+          }
           gap = k > kq && k - kq > 1;
         } else {
           gap = k > 0;
@@ -757,7 +780,6 @@ __global__ void k_shard_start_fc(const uint64_t *__restrict__ cpos, uint64_t cca
     if (cpos[m] < o) a = m + 1; else b = m;
   }
   fs[s] = a;
-  if (soff[s + 1] > o && (a >= n || cpos[a] != o)) atomicOr(&ds->segbad, 1u);
   ShardAgg g;
   g.first_fail = ~0ull;
   g.last_entry = -1;
@@ -765,7 +787,7 @@ __global__ void k_shard_start_fc(const uint64_t *__restrict__ cpos, uint64_t cca
   g.first_meta = ~0ull;
   g.ent_first = ~0ull;
   g.lastop = 0;
-  g.pad = 0;
+  g.bad = soff[s + 1] > o && (a >= n || cpos[a] != o);   // the shard does not open on a candidate
   sagg[s] = g;
 }
 
@@ -775,7 +797,7 @@ __global__ void k_meta_batch_fc(const uint8_t *__restrict__ buf, uint64_t B, con
                                 uint64_t ccap, uint64_t ecap, const uint32_t *__restrict__ mlist, const Small *ds,
                                 SegArgs sg) {
   __shared__ uint4 s_w[256][6];
-  if (!fc_valid(ds, ccap, ecap)) return;
+  if (!fc_valid_seg(ds, ccap, ecap)) return;
   const uint32_t nm = ds->nmeta;
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nm; i += gridDim.x * blockDim.x) {
     const uint32_t r = mlist[i];
@@ -802,7 +824,7 @@ __global__ __launch_bounds__(256) void k_result_batch_fc(const uint8_t *__restri
   __shared__ uint4 s_w[256][6];
   __shared__ RecDesc s_d[256];
   const uint32_t s = (blockIdx.x * blockDim.x + threadIdx.x) >> 3, k = threadIdx.x & 7;
-  if (!fc_valid(ds, ccap, ecap)) return;   // (a void pass: the host discards out[])
+  if (!fc_valid_seg(ds, ccap, ecap)) return;   // (a void pass: the host discards out[])
   const bool in = s < sg.ns;
   ShardAgg A;
   uint32_t f0 = 0, f1 = 0;
@@ -867,16 +889,18 @@ __global__ __launch_bounds__(256) void k_result_batch_fc(const uint8_t *__restri
       ef = o.n_ents ? f0 : 0;   // op k of the shard is bents[fs[s] + k]
     }
   }
+  if (A.bad) o.flags = EW_SHARD_BAD;   // replayed alone by the host (its fields here are void)
   out[s] = o;
   ent_first[s] = ef;
 }
 
-// The batch's verdict on the fused pass (one thread): the regular case for
-// every shard -> spec_n = frames, else 0; Small -> host-mapped memory.
+// The batch's verdict on the fused pass (one thread): the pass ran over every
+// candidate -> spec_n = frames (shards it could not decide carry EW_SHARD_BAD
+// in their result), else 0; Small -> host-mapped memory.
 __global__ void k_batch_gate_fc(Small *ds, uint64_t ccap, uint64_t ecap, uint64_t B, Small *h) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   const uint64_t K = ds->total;
-  const bool ok = fc_valid(ds, ccap, ecap) && !ds->segbad && ds->q == B;
+  const bool ok = fc_valid_seg(ds, ccap, ecap);
   ds->spec_n = ok ? (uint32_t)K : 0u;
   *h = *ds;
 }

@@ -2078,7 +2078,7 @@ __global__ void k_shard_start(const RecDesc *__restrict__ rd, uint32_t n, const 
   g.first_meta = ~0ull;
   g.ent_first = ~0ull;
   g.lastop = 0;
-  g.pad = 0;
+  g.bad = 0;
   sagg[s] = g;
 }
 

@@ -167,8 +167,8 @@ def _collect(ctx, r, buf_view, with_ents=True, shard=None):
         for e in arr[:n]:
             data = None if e.data_nil else bytes(buf_view[e.data_off:e.data_off + e.data_len])
             ents.append(Entry(e.type, e.term, e.index, data))
-    if ok and r.n_unrec and shard is None:
-        for ent, b in unrecognized(ctx, r.n_unrec):
+    if ok and r.n_unrec:
+        for ent, b in unrecognized(ctx, r.n_unrec, shard):
             if ent < 0:
                 st.XXX_unrecognized = b
             elif ent < len(ents):
@@ -178,15 +178,22 @@ def _collect(ctx, r, buf_view, with_ents=True, shard=None):
                          r.flags)
 
 
-def unrecognized(ctx, n):
+def unrecognized(ctx, n, shard=None):
     """The last ReadAll's XXX_unrecognized side list: [(ent index or -1 for
-    the HardState, bytes)] (ewal_copy_unrec / ewal_copy_unrec_bytes)."""
+    the HardState, bytes)] (ewal_copy_unrec / ewal_copy_unrec_bytes; a
+    batched shard's: ewal_batch_copy_unrec / _bytes)."""
     arr = (L.UnrecDesc * max(n, 1))()
-    k = lib.ewal_copy_unrec(ctx.handle, arr, n)
+    if shard is None:
+        k = lib.ewal_copy_unrec(ctx.handle, arr, n)
+    else:
+        k = lib.ewal_batch_copy_unrec(ctx.handle, shard, arr, n)
     check(0 if k >= 0 else int(k))
     tot = max([a.off + a.len for a in arr[:k]] + [0])
     raw = (C.c_char * max(tot, 1))()
-    got = lib.ewal_copy_unrec_bytes(ctx.handle, raw, tot)
+    if shard is None:
+        got = lib.ewal_copy_unrec_bytes(ctx.handle, raw, tot)
+    else:
+        got = lib.ewal_batch_copy_unrec_bytes(ctx.handle, shard, raw, tot)
     check(0 if got >= 0 else int(got))
     return [(a.ent, raw.raw[a.off:a.off + a.len]) for a in arr[:k]]
 

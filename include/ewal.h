@@ -144,19 +144,28 @@ int ewal_readall_device(ewal_ctx *ctx, const void *d_buf, uint64_t len, uint64_t
  * names[nameIndex:] each) laid end to end in ONE device
  * buffer: shard s is the lens[s] bytes after shards 0..s-1; out[s] is exactly
  * ewal_readall_device's result for that shard alone with w.ri = ri[s]
- * (ordinals and offsets relative to the shard; device_ms / stream_ms are the
- * whole batch's).  One stream pass, one frame pass and one segmented check
- * cover the batch; shards that do not end on a frame boundary (torn or
- * corrupt framing) or need the rare op-list paths send the batch through the
- * one-by-one path (flags |= EWAL_FLAG_SHARD_FALLBACK).  Returns 0 or a
- * negative infrastructure error; per-shard verdicts are in out[].  Replaces,
- * per shard, wal.OpenAtIndex(...).ReadAll() (wal/wal.go:108,164). */
+ * (ordinals and offsets relative to the shard; stream_ms is the batch's
+ * k_stream, device_ms the batch's pipeline plus any shard replayed alone).
+ * One stream pass and one fused frame + check pass cover the batch; a shard
+ * that pass cannot decide -- torn or corrupt framing, an index rewind, an
+ * encoding the canonical parser declines, unknown fields -- is replayed alone
+ * (flags |= EWAL_FLAG_SHARD_FALLBACK) while every other shard keeps the
+ * batch's result.  Shards whose returned ents / HardState carry
+ * XXX_unrecognized have n_unrec > 0 and a side list per shard
+ * (ewal_batch_copy_unrec).  Returns 0 or a negative infrastructure error;
+ * per-shard verdicts are in out[].  Replaces, per shard,
+ * wal.OpenAtIndex(...).ReadAll() (wal/wal.go:108,164). */
 #define EWAL_FLAG_SHARD_FALLBACK 1
 int ewal_readall_batch_device(ewal_ctx *ctx, const void *d_buf, uint64_t n_shards, const uint64_t *lens,
                               const uint64_t *ri, ewal_result *out);
 /* After ewal_readall_batch_device: shard s's ents (Data offsets relative to
  * the shard).  Returns the number copied (<= cap) or a negative error. */
 int64_t ewal_batch_copy_entries(ewal_ctx *ctx, uint64_t shard, ewal_entry *out, int64_t cap);
+/* After ewal_readall_batch_device: shard s's XXX_unrecognized side list
+ * (ewal_unrec, ent = index into that shard's ents or -1 for its HardState)
+ * and the bytes it indexes.  Return the number copied (<= cap). */
+int64_t ewal_batch_copy_unrec(ewal_ctx *ctx, uint64_t shard, ewal_unrec *out, int64_t cap);
+int64_t ewal_batch_copy_unrec_bytes(ewal_ctx *ctx, uint64_t shard, uint8_t *out, int64_t cap);
 /* Copy host bytes into ctx-owned device memory (16-B aligned; valid until
  * the next staging call on this ctx). */
 int ewal_stage_to_device(ewal_ctx *ctx, const void *h_buf, uint64_t len, void **d_out);

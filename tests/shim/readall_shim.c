@@ -9,12 +9,16 @@
  * reference's sentinel / panic (the Go switch) and materialise the return
  * values the way the shim does: raftpb.Entry structs whose Data are
  * zero-copy views into the gathered WAL bytes, the metadata view, the
- * HardState, w.enti and the encoder seed (lastCRC).
+ * HardState, w.enti and the encoder seed (lastCRC), and every Entry's and
+ * the HardState's XXX_unrecognized (raft.pb.go:273,699; fresh copies out of
+ * the side list, as Go's Unmarshal appends them).
  *
  * Usage: readall_shim DIR INDEX      prints one JSON line: the sentinel, the
  * result, a digest of ents (CRC-32C over each entry's (term, index, type,
  * nil, len, Data), the oracle's or_ents_digest format) and the time of each
- * step.  Exit 0 whenever the call completed (whatever the sentinel).
+ * step, and a digest of the XXX_unrecognized bytes (CRC-32C over (entry
+ * index or ~0 for the HardState, len, bytes) of each non-nil one, in order).
+ * Exit 0 whenever the call completed (whatever the sentinel).
  */
 #include <stdio.h>
 #include <stdlib.h>
@@ -29,6 +33,8 @@ typedef struct {
   uint64_t term, index;
   const uint8_t *data;   /* NULL == nil; a view into the WAL bytes */
   uint64_t len;
+  uint8_t *unrec;        /* XXX_unrecognized: NULL == nil; its own copy */
+  uint64_t unrec_len;
 } go_entry;
 
 static double now_ms(void) {
@@ -52,6 +58,14 @@ static const char *go_sentinel(int rc) {
   case EWAL_UNSUPPORTED_ENCODING: return "fallback: Go decoder";
   default: return rc >= 32 ? "panic" : "infrastructure error";
   }
+}
+
+static uint32_t unrec_digest(uint32_t h, uint64_t who, const uint8_t *b, uint64_t n) {
+  uint8_t hd[16];
+  memcpy(hd, &who, 8);
+  memcpy(hd + 8, &n, 8);
+  h = ewal_crc32_update_host(h, 0x82F63B78u, hd, 16);
+  return n ? ewal_crc32_update_host(h, 0x82F63B78u, b, n) : h;
 }
 
 static uint32_t ents_digest(const go_entry *e, int64_t n) {
@@ -106,6 +120,9 @@ int main(int argc, char **argv) {
   /* materialise the Go return values */
   go_entry *ents = NULL;
   int64_t n = 0;
+  uint8_t *state_unrec = NULL;   /* HardState.XXX_unrecognized */
+  uint64_t state_unrec_len = 0;
+  uint32_t udg = 0;
   uint64_t md_len = 0;
   const uint8_t *md = NULL;
   if (rc == EWAL_OK) {
@@ -120,22 +137,54 @@ int main(int argc, char **argv) {
         ents[i].index = ds[i].index;
         ents[i].data = ds[i].data_nil ? NULL : buf + ds[i].data_off;   /* zero-copy view */
         ents[i].len = ds[i].data_len;
+        ents[i].unrec = NULL;
+        ents[i].unrec_len = 0;
       }
       free(ds);
     }
+    if (r.n_unrec > 0) {   /* the side list: fresh XXX_unrecognized slices */
+      ewal_unrec *u = (ewal_unrec *)malloc(sizeof(ewal_unrec) * r.n_unrec);
+      const int64_t nu = ewal_copy_unrec(ctx, u, r.n_unrec);
+      uint64_t tot = 0;
+      for (int64_t i = 0; i < nu; i++)
+        if (u[i].off + u[i].len > tot) tot = u[i].off + u[i].len;
+      uint8_t *side = (uint8_t *)malloc(tot ? tot : 1);
+      ewal_copy_unrec_bytes(ctx, side, (int64_t)tot);
+      for (int64_t i = 0; i < nu; i++) {
+        uint8_t *b = (uint8_t *)malloc(u[i].len ? u[i].len : 1);
+        memcpy(b, side + u[i].off, u[i].len);
+        if (u[i].ent < 0) {
+          state_unrec = b;
+          state_unrec_len = u[i].len;
+        } else if (u[i].ent < n) {
+          ents[u[i].ent].unrec = b;
+          ents[u[i].ent].unrec_len = u[i].len;
+        } else {
+          free(b);
+        }
+      }
+      free(side);
+      free(u);
+    }
+    for (int64_t i = 0; i < n; i++)
+      if (ents[i].unrec) udg = unrec_digest(udg, (uint64_t)i, ents[i].unrec, ents[i].unrec_len);
+    if (state_unrec) udg = unrec_digest(udg, ~0ull, state_unrec, state_unrec_len);
   }
   const double t5 = now_ms();
   const uint32_t dg = ents_digest(ents, n);
   printf("{\"ok\": true, \"rc\": %d, \"sentinel\": \"%s\", \"status_string\": \"%s\", \"fail_record\": %lld, "
          "\"n_records\": %lld, \"n_ents\": %lld, \"enti\": %llu, \"last_crc\": %u, \"has_state\": %d, "
-         "\"state\": [%llu, %llu, %llu], \"metadata_len\": %lld, \"ents_digest\": %u, \"wal_bytes\": %llu, "
+         "\"state\": [%llu, %llu, %llu], \"metadata_len\": %lld, \"ents_digest\": %u, \"n_unrec\": %u, "
+         "\"unrec_digest\": %u, \"wal_bytes\": %llu, "
          "\"ms\": {\"ctx_create\": %.3f, \"open_at_index\": %.3f, \"reserve\": %.3f, \"readall\": %.3f, "
          "\"materialise\": %.3f, \"total\": %.3f}, \"device_ms\": %.3f}\n",
          rc, go_sentinel(rc), ewal_status_string(rc), (long long)r.fail_record, (long long)r.n_records,
          (long long)n, (unsigned long long)r.enti, (unsigned)r.last_crc, r.has_state,
          (unsigned long long)r.state_term, (unsigned long long)r.state_vote, (unsigned long long)r.state_commit,
-         md ? (long long)md_len : -1LL, dg, (unsigned long long)len, t1 - t0, t2 - t1, t3 - t2, t4 - t3, t5 - t4,
+         md ? (long long)md_len : -1LL, dg, (unsigned)r.n_unrec, udg, (unsigned long long)len, t1 - t0, t2 - t1, t3 - t2, t4 - t3, t5 - t4,
          t5 - t0, r.device_ms);
+  for (int64_t i = 0; i < n; i++) free(ents[i].unrec);
+  free(state_unrec);
   free(ents);
   ewal_wal_close(w);
   ewal_ctx_destroy(ctx);

@@ -3,9 +3,11 @@ SURVEY.md §8(d) C3: thousands of per-raft-group WALs replayed together).
 
 Every shard's batched result must equal the oracle's ReadAll of that shard
 alone (status, failing frame and offset, lastCRC, enti, metadata, HardState,
-ents), whichever path the batch took: the segmented fast path (one stream
-pass for the whole batch) or the one-by-one fallback for batches whose
-shards do not all end on a frame boundary or need the op-list paths."""
+ents, XXX_unrecognized), whichever path each shard took: the batch's fused
+pass (one stream pass and one frame + check pass for the whole batch) or,
+for a shard that pass cannot decide (torn or corrupt framing, an index
+rewind, unknown fields), its replay alone -- which must not take any other
+shard off the batch's path."""
 import random
 import struct
 
@@ -19,7 +21,7 @@ from test_gpu_parity import build_wal
 pytestmark = pytest.mark.gpu
 
 
-def check_batch(ctx, shards, ris, expect_fast=None):
+def check_batch(ctx, shards, ris, expect_fast=None, fallback=None):
     res = W.readall_batch_bytes(shards, ris, ctx)
     assert len(res) == len(shards)
     for s, (buf, ri, g) in enumerate(zip(shards, ris, res)):
@@ -30,15 +32,18 @@ def check_batch(ctx, shards, ris, expect_fast=None):
             for k in ("n_records", "last_crc", "enti", "metadata", "state"):
                 assert gd[k] == o[k], (s, k, gd[k], o[k])
             assert gd["ents"] == o["ents"], s
+            assert gd["state"]["unrec"] == o["state"]["unrec"], s
         elif o["status"] == O.ERR_INDEX_NOT_FOUND:
             assert gd["enti"] == o["enti"], s
         else:
             assert (gd["fail_record"], gd["fail_offset"]) == (o["fail_record"], o["fail_offset"]), s
             if o["status"] == O.ERR_UNEXPECTED_TYPE:
                 assert gd["detail"] == o["detail"]
+    fb = [bool(g.flags & L.FLAG_SHARD_FALLBACK) for g in res]
     if expect_fast is not None:
-        fb = [bool(g.flags & L.FLAG_SHARD_FALLBACK) for g in res]
         assert not any(fb) if expect_fast else all(fb), fb
+    if fallback is not None:     # exactly these shards were replayed alone
+        assert {i for i, x in enumerate(fb) if x} == set(fallback), fb
     return res
 
 
@@ -112,12 +117,12 @@ def test_batch_fallback_torn_and_rewind(ctx):
     # a torn shard in the middle: its chain runs into the next shard
     torn = list(base)
     torn[2] = torn[2][:-5]
-    check_batch(ctx, torn, [0] * 6, expect_fast=False)
+    check_batch(ctx, torn, [0] * 6, fallback={2})
     # a trailing bare length prefix (io.EOF) and a negative length
     t2 = list(base)
     t2[1] = t2[1] + struct.pack("<q", 77)
     t2[4] = t2[4] + struct.pack("<q", -5) + b"zz"
-    check_batch(ctx, t2, [0] * 6, expect_fast=False)
+    check_batch(ctx, t2, [0] * 6, fallback={1, 4})
     # an index rewind (leader overwrite) needs the op-list path
     e = O.WalEncoder(0)
     e.save_crc(0)
@@ -126,7 +131,33 @@ def test_batch_fallback_torn_and_rewind(ctx):
         e.save_entry(0, i, i, bytes([i]) * i)
     rw = list(base)
     rw[3] = e.getvalue()
-    check_batch(ctx, rw, [0, 0, 0, 2, 0, 0], expect_fast=False)
+    check_batch(ctx, rw, [0, 0, 0, 2, 0, 0], fallback={3})
+    # all of them in one batch, plus a shard whose entries carry unknown fields
+    u = O.WalEncoder(0)
+    u.save_crc(0)
+    u.encode(1, b"m")
+    u.encode(2, O.entry_marshal(0, 1, 0, b"x") + bytes([0x38, 0x05]))
+    u.save_entry(0, 1, 1, b"plain")
+    u.encode(3, O.hardstate_marshal(1, 2, 3) + bytes([0x20, 0x07]))
+    mix = [base[0], torn[2], base[1], rw[3], t2[4], u.getvalue(), base[5]]
+    res = check_batch(ctx, mix, [0, 0, 0, 2, 0, 0, 0], fallback={1, 3, 4, 5})
+    assert res[5].ents[0].XXX_unrecognized == bytes([0x38, 0x05]) and res[5].state.XXX_unrecognized == bytes([0x20, 7])
+
+
+def test_batch_torn_shards_stay_local(ctx):
+    """C3-shaped shards with torn tails in a few of them (a crash mid-write):
+    only those shards are replayed alone; the others keep the batch's pass."""
+    shards, want = [], []
+    for s in range(24):
+        buf, n = W.synth_wal(1 << 20, 128, 4096, seed=40 + s)
+        b = bytes(buf)
+        if s in (3, 11, 17):
+            b = b[:-(100 + s)]          # the last frame torn
+        shards.append(b)
+        want.append(n)
+    res = check_batch(ctx, shards, [1] * 24, fallback={3, 11, 17})
+    for s in (3, 11, 17):
+        assert res[s].status == L.ERR_UNEXPECTED_EOF and res[s].fail_record == want[s] - 1
 
 
 @pytest.mark.parametrize("seed", range(6))

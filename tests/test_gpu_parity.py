@@ -209,9 +209,11 @@ def test_unknown_fields(ctx):
     e.encode(2, O.entry_marshal(0, 2, 2, b"c") + bytes([0x38, 9]))
     o, g = assert_parity(ctx, e.getvalue(), 0)
     assert [x["unrec"] for x in g["ents"]] == [None, None, bytes([0x38, 9])]
-    # the batch replays a shard with unknown fields alone (no per-shard side list)
+    # the batch replays a shard with unknown fields alone and keeps its side list
     r = W.readall_batch_bytes([e.getvalue(), build_wal(random.Random(2), 5, 10)], [0, 0], ctx)
-    assert r[0].status == L.UNSUPPORTED_ENCODING and r[1].status == L.OK
+    assert r[0].status == L.OK and r[1].status == L.OK
+    assert [x.XXX_unrecognized for x in r[0].ents] == [None, None, bytes([0x38, 9])]
+    assert r[0].flags & L.FLAG_SHARD_FALLBACK and not r[1].flags & L.FLAG_SHARD_FALLBACK
 
 
 def test_synth_medium_with_corruption(ctx):

@@ -7,6 +7,7 @@ TestOpenAtUncommittedIndex shapes, wal/wal_test.go:152-351)."""
 import json
 import os
 import random
+import struct
 import subprocess
 
 import pytest
@@ -100,3 +101,38 @@ def test_shim_large_and_corrupt(tmp_path):
     (d / W.walName(0, 0)).write_bytes(bytes(bad))
     g = check(d, 1)
     assert g["sentinel"] != "nil"
+
+
+def unrec_digest(o):
+    """The shim's XXX_unrecognized digest over the oracle's ReadAll result."""
+    h = 0
+    items = [(i, e["unrec"]) for i, e in enumerate(o["ents"]) if e["unrec"] is not None]
+    if o["state"]["unrec"] is not None:
+        items.append(((1 << 64) - 1, o["state"]["unrec"]))
+    for who, b in items:
+        h = O.crc32_update(h, struct.pack("<QQ", who, len(b)))
+        h = O.crc32_update(h, b)
+    return h, len(items)
+
+
+@pytest.mark.gpu
+def test_shim_unknown_fields(tmp_path):
+    """Entries and the HardState carrying unknown fields: the shim returns their
+    XXX_unrecognized (raft.pb.go:273,699) byte-exact, as reflect.DeepEqual in
+    wal_test.go:188 would see them."""
+    d = tmp_path / "wal"
+    os.makedirs(d)
+    e = O.WalEncoder(0)
+    e.save_crc(0)
+    e.encode(1, b"metadata")
+    for i in range(40):
+        tail = bytes([0x38, i]) if i % 3 == 0 else (bytes([0x45, 1, 2, 3, i]) if i % 7 == 0 else b"")
+        e.encode(2, O.entry_marshal(0, 1, i, bytes([i]) * (i * 13 % 300)) + tail)
+    e.encode(3, O.hardstate_marshal(1, 2, 30) + bytes([0x20, 0x07]))
+    buf = e.getvalue()
+    (d / W.walName(0, 0)).write_bytes(buf)
+    g = check(d, 0)
+    o = O.readall(buf, 0)
+    assert o["status"] == O.OK and g["sentinel"] == "nil"
+    assert (g["unrec_digest"], g["n_unrec"]) == unrec_digest(o)
+    assert g["n_unrec"] > 10

@@ -47,9 +47,11 @@ def test_records_match_oracle_then_invalidate(ctx):
         rs = W.readall_batch_device(d, [len(buf)], [1])
         assert rs[0].status == L.OK
         _records_fail(ctx, n)
-        # a ReadAll over host bytes stages them; staging new bytes takes its stream away
+        # a ReadAll over host bytes stages them; staging new bytes before the
+        # descriptors were rebuilt takes their stream away (once rebuilt they
+        # hold offsets and CRCs only and stay valid until the next pipeline call)
         g = W.readall_bytes(buf, 1, ctx, with_ents=False)
-        assert g.status == L.OK and len(W.records(ctx, n)) == n
+        assert g.status == L.OK
         p = C.c_void_p()
         L.check(L.lib.ewal_stage_to_device(ctx.handle, b"\0" * 64, 64, C.byref(p)))
         _records_fail(ctx, n)
