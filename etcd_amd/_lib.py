@@ -150,6 +150,7 @@ _SIGS = {
     "ewal_wal_readall": (C.c_int, [vp, vp, C.POINTER(Result)]),
     "ewal_wal_bytes": (u8p, [vp, C.POINTER(C.c_uint64)]),
     "ewal_wal_seq": (C.c_uint64, [vp]),
+    "ewal_wal_prefetch": (C.c_int, [vp]),
     "ewal_wal_close": (None, [vp]),
     "ewal_parse_wal_name": (C.c_int, [C.c_char_p, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
     "ewal_search_index": (C.c_int64, [C.POINTER(C.c_char_p), C.c_uint64, C.c_uint64]),

@@ -115,42 +115,65 @@ __device__ __noinline__ uint64_t quorum_select_any(const uint64_t *__restrict__ 
   return 0;
 }
 
-__global__ void k_commit(uint64_t G, const uint64_t *__restrict__ match, const uint8_t *__restrict__ nvoters,
-                         const uint64_t *__restrict__ term, uint64_t *__restrict__ committed,
-                         const uint64_t *__restrict__ log_offset, const uint64_t *__restrict__ log_ptr,
-                         const uint64_t *__restrict__ log_terms, uint8_t *__restrict__ changed,
-                         uint8_t *__restrict__ status) {
-  const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (g >= G) return;
-  const int n = nvoters[g];
-  uint8_t chg = 0, st = 0;
-  if (n <= 0) {
-    st = EWAL_PANIC_BOUNDS;   // mis[q-1] on an empty slice (raft/raft.go:255)
-  } else {
-    const uint64_t mci = n <= 8 ? quorum_select<8>(match, G, g, n)
-                         : n <= 16 ? quorum_select<16>(match, G, g, n) : quorum_select_any(match, G, g, n);
-    uint64_t c = committed[g];
-    if (mci > c) {
-      const uint64_t off = log_offset[g];
-      const uint64_t p0 = log_ptr[g];
-      const uint64_t nlog = log_ptr[g + 1] - p0;
-      const uint64_t last = nlog - 1 + off;    // lastIndex(), uint64 wrap
-      uint64_t t = 0;
-      bool panic = false;
-      if (!(mci < off || mci > last)) {
-        const uint64_t k = mci - off;
-        if (k >= nlog) panic = true; else t = log_terms[p0 + k];
-      }
-      if (panic) {
-        st = EWAL_PANIC_BOUNDS;
-      } else if (t == term[g]) {
-        committed[g] = mci;
-        chg = 1;
+// One lane per raft group, EW_COMMIT_ILP groups per lane (g, g + T, ...): the
+// loads that do not depend on the voter count (committed, term, the log
+// window bounds) are issued for every group of the lane before the first
+// match load, so a wave keeps 4x the independent requests in flight (the
+// kernel is a chain nvoters -> match -> select -> term gather -> store).
+#define EW_COMMIT_ILP 4
+__global__ __launch_bounds__(256) void k_commit(uint64_t G, const uint64_t *__restrict__ match,
+                                                const uint8_t *__restrict__ nvoters, const uint64_t *__restrict__ term,
+                                                uint64_t *__restrict__ committed,
+                                                const uint64_t *__restrict__ log_offset,
+                                                const uint64_t *__restrict__ log_ptr,
+                                                const uint64_t *__restrict__ log_terms, uint8_t *__restrict__ changed,
+                                                uint8_t *__restrict__ status) {
+  const uint64_t T = (uint64_t)gridDim.x * blockDim.x;
+  const uint64_t g0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  int n[EW_COMMIT_ILP];
+  uint64_t c[EW_COMMIT_ILP], tm[EW_COMMIT_ILP], off[EW_COMMIT_ILP], p0[EW_COMMIT_ILP], p1[EW_COMMIT_ILP];
+#pragma unroll
+  for (int k = 0; k < EW_COMMIT_ILP; ++k) {
+    const uint64_t g = g0 + (uint64_t)k * T;
+    const bool in = g < G;
+    n[k] = in ? nvoters[g] : 0;
+    c[k] = in ? committed[g] : 0;
+    tm[k] = in ? term[g] : 0;
+    off[k] = in ? log_offset[g] : 0;
+    p0[k] = in ? log_ptr[g] : 0;
+    p1[k] = in ? log_ptr[g + 1] : 0;
+  }
+#pragma unroll
+  for (int k = 0; k < EW_COMMIT_ILP; ++k) {
+    const uint64_t g = g0 + (uint64_t)k * T;
+    if (g >= G) break;
+    const int nv = n[k];
+    uint8_t chg = 0, st = 0;
+    if (nv <= 0) {
+      st = EWAL_PANIC_BOUNDS;   // mis[q-1] on an empty slice (raft/raft.go:255)
+    } else {
+      const uint64_t mci = nv <= 8 ? quorum_select<8>(match, G, g, nv)
+                           : nv <= 16 ? quorum_select<16>(match, G, g, nv) : quorum_select_any(match, G, g, nv);
+      if (mci > c[k]) {   // raftLog.maybeCommit: term(mci) == Term (raft/log.go:148-154)
+        const uint64_t nlog = p1[k] - p0[k];
+        const uint64_t last = nlog - 1 + off[k];    // lastIndex(), uint64 wrap
+        uint64_t t = 0;
+        bool panic = false;
+        if (!(mci < off[k] || mci > last)) {        // raftLog.at / isOutOfBounds (raft/log.go:194-217)
+          const uint64_t kk = mci - off[k];
+          if (kk >= nlog) panic = true; else t = log_terms[p0[k] + kk];
+        }
+        if (panic) {
+          st = EWAL_PANIC_BOUNDS;
+        } else if (t == tm[k]) {
+          committed[g] = mci;
+          chg = 1;
+        }
       }
     }
+    changed[g] = chg;
+    status[g] = st;
   }
-  changed[g] = chg;
-  status[g] = st;
 }
 
 // ===========================================================================

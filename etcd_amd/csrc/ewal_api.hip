@@ -1983,7 +1983,8 @@ int ecommit_batch_device(ewal_ctx *c, uint64_t G, const uint64_t *match, const u
   EW_CHECK(hipSetDevice(c->device));
   EW_CHECK(hipEventRecord(c->ev0, c->stream));
   if (G)
-    hipLaunchKernelGGL(k_commit, dim3((unsigned)((G + 255) / 256)), dim3(256), 0, c->stream, G, match, nvoters, term,
+    hipLaunchKernelGGL(k_commit, dim3((unsigned)((G + 256 * EW_COMMIT_ILP - 1) / (256 * EW_COMMIT_ILP))), dim3(256), 0,
+                       c->stream, G, match, nvoters, term,
                        committed, log_offset, log_ptr, log_terms, changed, status);
   EW_CHECK(hipGetLastError());
   EW_CHECK(hipEventRecord(c->ev1, c->stream));

@@ -194,8 +194,20 @@ bool read_file(const std::string &path, std::vector<uint8_t> *out, size_t pad) {
 
 // ===========================================================================
 // An opened WAL (wal.OpenAtIndex): the selected files names[nameIndex:]; their
-// bytes are read by ReadAll (as MultiReadCloser is, wal/wal.go:126-134) into
-// one host buffer -- the buffer ReadAll's ents are views into.
+// bytes are read (as MultiReadCloser streams them, wal/wal.go:126-134) into
+// one host buffer -- the buffer ReadAll's ents are views into -- by a small
+// pool of reader threads, in pieces of at most kPiece bytes.  The reading
+// starts at ewal_wal_prefetch (or at ReadAll), so it can run while the
+// caller creates the GPU context; ReadAll uploads every piece, in order, as
+// soon as it and all earlier ones are in the buffer.
+namespace {
+const uint64_t kPiece = 64ull << 20;
+struct Piece {
+  size_t file;
+  uint64_t foff, off, len;
+};
+}  // namespace
+
 struct ewal_wal {
   std::string dir;
   uint64_t ri = 0;
@@ -206,27 +218,39 @@ struct ewal_wal {
   uint8_t *bytes = nullptr;           // total bytes once loaded (anonymous mapping, huge pages advised)
   size_t map_len = 0;
   bool loaded = false;
+  // the reader pool (started once)
+  bool started = false;
+  std::vector<Piece> pcs;
+  std::vector<int> fds;
+  std::unique_ptr<std::atomic<int>[]> done;   // per piece: 0 pending, 1 read, -1 failed
+  std::atomic<size_t> next{0};
+  std::mutex mu;
+  std::condition_variable cv;
+  std::vector<std::thread> th;
+  void stop() {
+    next.store(pcs.size());   // no more pieces handed out
+    for (auto &t : th) t.join();
+    th.clear();
+    for (int fd : fds)
+      if (fd >= 0) close(fd);
+    fds.clear();
+  }
   ~ewal_wal() {
+    stop();
     if (bytes) munmap(bytes, map_len);
   }
 };
 
 namespace {
 
-// The files' bytes in pieces of at most kPiece bytes, read by a small pool of
-// threads (pread) in piece order; `ready` is called for every piece in
-// order as soon as it and all earlier ones are in the buffer (ReadAll
-// uploads them while the later ones are still being read).
-const uint64_t kPiece = 64ull << 20;
-template <class F>
-int load_pieces(ewal_wal *w, F ready) {
-  struct Piece { size_t file; uint64_t foff, off, len; };
-  std::vector<Piece> pcs;
+// Start reading every piece (idempotent): the buffer, the files, the pool.
+int start_load(ewal_wal *w) {
+  if (w->started || w->loaded) return EWAL_OK;
   uint64_t off = 0;
   for (size_t f = 0; f < w->paths.size(); ++f)
     for (uint64_t o = 0; o < w->sizes[f]; o += kPiece) {
       const uint64_t l = std::min<uint64_t>(kPiece, w->sizes[f] - o);
-      pcs.push_back(Piece{f, o, off, l});
+      w->pcs.push_back(Piece{f, o, off, l});
       off += l;
     }
   if (!w->bytes) {
@@ -237,56 +261,66 @@ int load_pieces(ewal_wal *w, F ready) {
     void *m = mmap(nullptr, w->map_len, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
     if (m == MAP_FAILED) {
       w->map_len = 0;
+      w->pcs.clear();
       return EWAL_E_NOMEM;
     }
     (void)madvise(m, w->map_len, MADV_HUGEPAGE);
     w->bytes = (uint8_t *)m;
   }
-  std::vector<int> fds(w->paths.size(), -1);
+  w->fds.assign(w->paths.size(), -1);
   for (size_t f = 0; f < w->paths.size(); ++f) {
-    fds[f] = open(w->paths[f].c_str(), O_RDONLY);
-    if (fds[f] < 0) {
-      for (int fd : fds) if (fd >= 0) close(fd);
+    w->fds[f] = open(w->paths[f].c_str(), O_RDONLY);
+    if (w->fds[f] < 0) {
+      w->stop();
+      w->pcs.clear();
       return EWAL_E_IO;
     }
   }
-  std::vector<std::atomic<int>> done(pcs.size());   // 0 pending, 1 read, -1 failed
-  for (auto &d : done) d.store(0);
-  std::atomic<size_t> next(0);
-  std::mutex mu;
-  std::condition_variable cv;
-  auto reader = [&]() {
+  w->done.reset(new std::atomic<int>[std::max<size_t>(1, w->pcs.size())]);
+  for (size_t k = 0; k < w->pcs.size(); ++k) w->done[k].store(0);
+  w->next.store(0);
+  auto reader = [w]() {
     for (;;) {
-      const size_t k = next.fetch_add(1);
-      if (k >= pcs.size()) break;
-      const Piece &p = pcs[k];
+      const size_t k = w->next.fetch_add(1);
+      if (k >= w->pcs.size()) break;
+      const Piece &p = w->pcs[k];
       uint64_t got = 0;
       while (got < p.len) {
-        const ssize_t r = pread(fds[p.file], w->bytes + p.off + got, (size_t)(p.len - got), (off_t)(p.foff + got));
+        const ssize_t r = pread(w->fds[p.file], w->bytes + p.off + got, (size_t)(p.len - got), (off_t)(p.foff + got));
         if (r <= 0) break;
         got += (uint64_t)r;
       }
       {
-        std::lock_guard<std::mutex> lk(mu);
-        done[k].store(got == p.len ? 1 : -1);
+        std::lock_guard<std::mutex> lk(w->mu);
+        w->done[k].store(got == p.len ? 1 : -1);
       }
-      cv.notify_all();
+      w->cv.notify_all();
     }
   };
-  const unsigned nth = (unsigned)std::max<size_t>(1, std::min<size_t>(pcs.size(), std::max(1u, std::min(16u, std::thread::hardware_concurrency()))));
-  std::vector<std::thread> th;
-  for (unsigned t = 0; t < nth; ++t) th.emplace_back(reader);
-  int rc = EWAL_OK;
-  for (size_t k = 0; k < pcs.size(); ++k) {
-    std::unique_lock<std::mutex> lk(mu);
-    cv.wait(lk, [&] { return done[k].load() != 0; });
+  const unsigned nth = (unsigned)std::max<size_t>(
+      1, std::min<size_t>(w->pcs.size(), std::max(1u, std::min(16u, std::thread::hardware_concurrency()))));
+  for (unsigned t = 0; t < nth; ++t) w->th.emplace_back(reader);
+  w->started = true;
+  return EWAL_OK;
+}
+
+// Every piece, in order, to `ready` as soon as it and all earlier ones are
+// in the buffer (ReadAll uploads them while the later ones are still read).
+template <class F>
+int load_pieces(ewal_wal *w, F ready) {
+  if (w->loaded) return w->total ? ready(0, w->total) : EWAL_OK;
+  int rc = start_load(w);
+  if (rc) return rc;
+  for (size_t k = 0; k < w->pcs.size(); ++k) {
+    std::unique_lock<std::mutex> lk(w->mu);
+    w->cv.wait(lk, [&] { return w->done[k].load() != 0; });
     lk.unlock();
-    if (done[k].load() < 0) { rc = EWAL_E_IO; break; }
-    if ((rc = ready(pcs[k].off, pcs[k].len)) != 0) break;
+    if (w->done[k].load() < 0) { rc = EWAL_E_IO; break; }
+    if ((rc = ready(w->pcs[k].off, w->pcs[k].len)) != 0) break;
   }
-  if (rc) next.store(pcs.size());   // stop handing out pieces
-  for (auto &t : th) t.join();
-  for (int fd : fds) close(fd);
+  w->stop();
+  w->started = false;
+  w->pcs.clear();
   if (rc == EWAL_OK) w->loaded = true;
   return rc;
 }
@@ -428,11 +462,7 @@ int ewal_wal_readall(ewal_wal *w, ewal_ctx *ctx, ewal_result *out) {
   if (!w || !out) return EWAL_E_INVAL;
   int rc = ewal_stage_begin(ctx, w->total);
   if (rc) return rc;
-  if (w->loaded) {
-    rc = w->total ? ewal_stage_put(ctx, 0, w->bytes, w->total) : 0;
-  } else {
-    rc = load_pieces(w, [&](uint64_t off, uint64_t len) { return ewal_stage_put(ctx, off, w->bytes + off, len); });
-  }
+  rc = load_pieces(w, [&](uint64_t off, uint64_t len) { return ewal_stage_put(ctx, off, w->bytes + off, len); });
   if (rc) {
     // copies already queued read w->bytes: let them land before the caller can
     // unmap it (ewal_wal_close)
@@ -450,6 +480,10 @@ const uint8_t *ewal_wal_bytes(ewal_wal *w, uint64_t *len) {
   }
   if (len) *len = w->total;
   return w->bytes;
+}
+int ewal_wal_prefetch(ewal_wal *w) {
+  if (!w) return EWAL_E_INVAL;
+  return start_load(w);
 }
 uint64_t ewal_wal_seq(ewal_wal *w) { return w->seq; }
 void ewal_wal_close(ewal_wal *w) { delete w; }

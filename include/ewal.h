@@ -238,6 +238,12 @@ void ewal_wal_name(uint64_t seq, uint64_t index, char *out);
 int ewal_wal_readall(ewal_wal *w, ewal_ctx *ctx, ewal_result *out);
 /* total bytes of the opened files (size ewal_ctx_reserve before ReadAll) */
 uint64_t ewal_wal_size(ewal_wal *w);
+/* Start reading the opened files into host memory in the background (reader
+ * threads, 64 MiB pieces) and return at once: a restarting server calls it
+ * right after OpenAtIndex so the reads overlap its GPU context creation;
+ * ewal_wal_readall then uploads the pieces already read and waits for the
+ * rest.  Optional (ReadAll starts the reads itself). */
+int ewal_wal_prefetch(ewal_wal *w);
 const uint8_t *ewal_wal_bytes(ewal_wal *w, uint64_t *len);
 uint64_t ewal_wal_seq(ewal_wal *w);
 void ewal_wal_close(ewal_wal *w);

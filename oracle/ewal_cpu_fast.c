@@ -24,7 +24,11 @@
 #include "ewal_cpu_fast.h"
 #include "ewal_oracle.h"
 
+#include <fcntl.h>
 #include <nmmintrin.h>
+#include <sys/stat.h>
+#include <time.h>
+#include <unistd.h>
 #include <pthread.h>
 #include <stdatomic.h>
 #include <stdlib.h>
@@ -422,4 +426,84 @@ void orf_maybe_commit_batch(uint64_t G, const uint64_t *match, const uint8_t *nv
   for (int t = 1; t < nthreads; t++) pthread_create(&th[t], NULL, commit_worker, &jobs[t]);
   commit_worker(&jobs[0]);
   for (int t = 1; t < nthreads; t++) pthread_join(th[t], NULL);
+}
+
+
+/* ---- the restart on the CPU, file reads included --------------------------
+ * OpenAtIndex(dir, ri).ReadAll() of a one-file WAL as a CPU process does it:
+ * read the file into memory (nthreads pread workers, 64 MiB pieces), then
+ * ReadAll -- faithful: or_readall (the Go restatement, 1 thread); optimised:
+ * orf_readall on nthreads cores.  The bench's restart cpu_baseline. */
+typedef struct {
+  int fd;
+  uint8_t *buf;
+  uint64_t size;
+  atomic_uint_fast64_t *next;
+  int err;
+} read_job;
+static void *read_worker(void *arg) {
+  read_job *j = (read_job *)arg;
+  const uint64_t piece = 64ull << 20;
+  for (;;) {
+    const uint64_t o = atomic_fetch_add(j->next, piece);
+    if (o >= j->size) break;
+    const uint64_t n = o + piece <= j->size ? piece : j->size - o;
+    uint64_t got = 0;
+    while (got < n) {
+      const ssize_t r = pread(j->fd, j->buf + o + got, (size_t)(n - got), (off_t)(o + got));
+      if (r <= 0) { j->err = 1; break; }
+      got += (uint64_t)r;
+    }
+  }
+  return NULL;
+}
+static double ms_now(void) {
+  struct timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return ts.tv_sec * 1e3 + ts.tv_nsec / 1e6;
+}
+int orf_restart_file(const char *path, uint64_t ri, int nthreads, int faithful, int64_t *frames, double *read_ms,
+                     double *total_ms) {
+  const double t0 = ms_now();
+  const int fd = open(path, O_RDONLY);
+  if (fd < 0) return -1;
+  struct stat st;
+  if (fstat(fd, &st) != 0) { close(fd); return -1; }
+  const uint64_t size = (uint64_t)st.st_size;
+  uint8_t *buf = (uint8_t *)malloc(size ? size : 1);
+  if (!buf) { close(fd); return -1; }
+  if (nthreads < 1) nthreads = 1;
+  if (nthreads > 256) nthreads = 256;
+  atomic_uint_fast64_t next;
+  atomic_init(&next, 0);
+  read_job jobs[256];
+  pthread_t th[256];
+  for (int t = 0; t < nthreads; t++) jobs[t] = (read_job){fd, buf, size, &next, 0};
+  for (int t = 1; t < nthreads; t++) pthread_create(&th[t], NULL, read_worker, &jobs[t]);
+  read_worker(&jobs[0]);
+  int err = jobs[0].err;
+  for (int t = 1; t < nthreads; t++) {
+    pthread_join(th[t], NULL);
+    err |= jobs[t].err;
+  }
+  close(fd);
+  const double t1 = ms_now();
+  int status;
+  if (err) {
+    status = -1;
+  } else if (faithful) {
+    or_readall_result r;
+    status = or_readall(buf, (int64_t)size, ri, &r);
+    *frames = status == OR_OK ? r.n_records : r.fail_record;
+    or_readall_free(&r);
+  } else {
+    orf_result r;
+    status = orf_readall(buf, (int64_t)size, ri, nthreads, &r);
+    *frames = status == OR_OK ? r.n_records : r.fail_record;
+    orf_result_free(&r);
+  }
+  free(buf);
+  *read_ms = t1 - t0;
+  *total_ms = ms_now() - t0;
+  return status;
 }

@@ -49,6 +49,12 @@ void orf_maybe_commit_batch(uint64_t G, const uint64_t *match, const uint8_t *nv
                             uint64_t *committed, const uint64_t *log_offset, const uint64_t *log_ptr,
                             const uint64_t *log_terms, uint8_t *changed, uint8_t *status, int nthreads);
 
+/* OpenAtIndex(dir, ri).ReadAll() of a one-file WAL on the CPU, file read
+ * included (nthreads readers; faithful: or_readall on 1 thread, else
+ * orf_readall on nthreads): the status; frames, read and total ms out */
+int orf_restart_file(const char *path, uint64_t ri, int nthreads, int faithful, int64_t *frames, double *read_ms,
+                     double *total_ms);
+
 #ifdef __cplusplus
 }
 #endif

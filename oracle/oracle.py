@@ -298,6 +298,14 @@ def fast_readall_status(buf_addr, n, ri=0, nthreads=1):
     return out
 
 
+def restart_file(path, ri, nthreads, faithful):
+    """orf_restart_file: (status, frames, read ms, total ms) of a CPU restart
+    (file read + ReadAll)."""
+    fr, rm, tm = C.c_int64(0), C.c_double(0), C.c_double(0)
+    st = lib.orf_restart_file(path.encode(), ri, nthreads, int(faithful), C.byref(fr), C.byref(rm), C.byref(tm))
+    return st, fr.value, rm.value, tm.value
+
+
 def _u64arr(x):
     return (C.c_uint64 * max(len(x), 1))(*x)
 

@@ -155,3 +155,45 @@ def test_configs3_snapshots_1_to_256mib(ctx):
         assert [i for i in range(len(files)) if st[i] != L.OK] == bad
     finally:
         d.free()
+
+
+@pytest.mark.gpu
+def test_configs4_1m_groups_against_oracle(ctx):
+    """configs[4] at its full size: maybeCommit (raft/raft.go:248-258 +
+    raft/log.go:148-154) over 1M raft groups x 5/7 voters with a 16-entry
+    log-term window (bench.py's generator, seed 6, plus groups whose quorum
+    index falls outside the window: no change / Go's bounds panic) -- every
+    committed index, changed flag and status against or_maybe_commit_batch."""
+    import numpy as np
+    import torch
+    G = 1 << 20
+    rng = np.random.default_rng(6)
+    nv = np.where(rng.random(G) < 0.5, 5, 7).astype(np.uint8)
+    committed0 = rng.integers(0, 1 << 20, size=G, dtype=np.uint64)
+    match = (committed0[None, :] + rng.integers(0, 24, size=(7, G), dtype=np.uint64) - np.uint64(4)).astype(np.uint64)
+    term = rng.integers(1, 4, size=G, dtype=np.uint64)
+    log_offset = committed0 + np.uint64(1) - rng.integers(0, 3, size=G, dtype=np.uint64)
+    # a slice of groups whose log window ends early (at() past the log: the bounds panic) or has no voters
+    short = rng.random(G) < 0.01
+    lens = np.where(short, rng.integers(0, 4, size=G), 16).astype(np.uint64)
+    log_ptr = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
+    log_terms = rng.integers(1, 4, size=int(lens.sum()), dtype=np.uint64)
+    nv[rng.random(G) < 0.001] = 0
+    dev = torch.device("cuda", 0)
+    T = lambda x: torch.from_numpy(x.view(np.int64) if x.dtype == np.uint64 else x).to(dev)   # noqa: E731
+    d = dict(m=T(match.reshape(-1)), n=T(nv), t=T(term), c=T(committed0.copy()), o=T(log_offset), p=T(log_ptr),
+             lt=T(log_terms))
+    ch = torch.zeros(G, dtype=torch.uint8, device=dev)
+    st = torch.zeros(G, dtype=torch.uint8, device=dev)
+    P = lambda t: C.c_void_p(t.data_ptr())   # noqa: E731
+    assert L.lib.ecommit_batch_device(ctx.handle, G, P(d["m"]), P(d["n"]), P(d["t"]), P(d["c"]), P(d["o"]), P(d["p"]),
+                                      P(d["lt"]), P(ch), P(st), None) == 0
+    c = committed0.copy()
+    chc, stc = np.zeros(G, np.uint8), np.zeros(G, np.uint8)
+    O.maybe_commit_batch(G, match.reshape(-1).copy(), nv, term, c, log_offset, log_ptr, log_terms, chc, stc)
+    got_c = d["c"].cpu().numpy().view(np.uint64)
+    assert (stc != 0).sum() > 0 and chc.sum() > G // 4
+    np.testing.assert_array_equal(st.cpu().numpy(), stc)
+    np.testing.assert_array_equal(ch.cpu().numpy(), chc)
+    ok = stc == 0
+    np.testing.assert_array_equal(got_c[ok], c[ok])
