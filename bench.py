@@ -14,6 +14,8 @@ own ms_per_step, roofline and (N=1) cpu_baseline --
           8 GPUs), one batched ReadAll per step, one RCCL all-reduce
   snap    configs[3]: a resident batch of snapshot files, loadSnap's CRC
   commit  configs[4]: maybeCommit over 1M raft groups x 5/7 voters
+  rewind  the configs[1]-shaped WAL after leader changes (1 % of the entries
+          rewrite the last 1-8 indexes): ReadAll's rewind path timed
 With --gpus N (torchrun) every rank verifies its own independent shards
 (weak scaling) and one RCCL all-reduce per step combines the verdicts.
 
@@ -49,7 +51,8 @@ def parse():
     ap.add_argument("--snap-files", type=int, default=10000)
     ap.add_argument("--pool-gib", type=float, default=24.0)
     ap.add_argument("--batch-gib", type=float, default=8.0)
-    ap.add_argument("--workload", choices=["wal", "c1", "shards", "snap", "snapstream", "commit", "msg", "restart"],
+    ap.add_argument("--workload", choices=["wal", "c1", "shards", "snap", "snapstream", "commit", "msg", "restart",
+                                           "rewind"],
                     default="wal",
                     help="wal = configs[1] (the headline, default); c1 = configs[0]'s WAL (1M x 256 B entries) on "
                          "the GPU; shards = configs[2] (4096 x 64 MiB per-group WALs over the node, 512 per GPU); "
@@ -58,7 +61,7 @@ def parse():
                          "restart = OpenAtIndex + ReadAll + materialise through the C ABI (the cgo shim's calls)")
     ap.add_argument("--shards-per-gpu", type=int, default=512)
     ap.add_argument("--shard-mib", type=int, default=64)
-    ap.add_argument("--configs", default="c1,shards,snap,commit",
+    ap.add_argument("--configs", default="c1,shards,snap,commit,rewind",
                     help="default line: the other BASELINE configs timed in the same run ('none' to skip)")
     ap.add_argument("--sub-cpu-seconds", type=float, default=6.0,
                     help="CPU-baseline time per leg of each `configs` sub-result")
@@ -902,7 +905,71 @@ def run_wal(a, dist, rank, world, local, size, min_data, max_data, label, cpu_se
     return out
 
 
-SUBS = {"c1": None, "shards": run_shards, "snap": run_snap, "commit": run_commit}
+def run_rewind(a, dist, rank, world, local, cpu_seconds=None):
+    """A configs[1]-shaped WAL (8 GiB, 64 B - 64 KiB entries) after leader
+    changes: 1 % of the entries open a new leader's term that rewrites the
+    last 1..8 indexes (wal/wal.go:170-176, ents = append(ents[:Index-ri], e)),
+    clean otherwise -- the irregular input a restart after an election sees.
+    One ReadAll per step; every step returns len(ents) == the last Index."""
+    cpu_seconds = a.cpu_seconds if cpu_seconds is None else cpu_seconds
+    t = time.time()
+    li = []
+    buf, n = W.synth_wal(8 << 30, 64, 65536, seed=22 + rank, rewind_per_mille=10, last_index=li)
+    nb = len(buf)
+    gen_s = time.time() - t
+    ctx = W.Context(local)
+    dbuf = ctx.alloc(nb + 64)
+    dbuf.upload_ptr(C.addressof((C.c_char * nb).from_buffer(buf)), nb)
+    rs = L.Result()
+
+    def step():
+        rc = L.lib.ewal_readall_device(ctx.handle, dbuf.ptr, nb, 1, C.byref(rs))
+        assert rc == L.OK and rs.n_records == n and rs.n_ents == li[0], (rc, rs.n_records, rs.n_ents, li[0])
+
+    for _ in range(max(a.warmup, 1)):
+        step()
+    ms = timed(dist, a.steps, step) / a.steps * 1e3
+    cpu = None
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        from oracle import oracle as O   # baseline only
+        cut = 1 << 30
+        p, last = 0, 0
+        while p + 8 <= nb and p < cut:      # the frames in the first GiB (length prefixes)
+            last = p
+            p += 8 + int.from_bytes(buf[p:p + 8], "little")
+        sample = bytes(buf[:p if p <= nb else last])
+        it, cs = timed_cpu(cpu_seconds, lambda: O.readall(sample, 1))
+        o = O.readall(sample, 1)
+        assert o["status"] == O.OK
+        cpu = dict(host_info(), **{
+            "value": round(len(sample) * it / cs / 1e9, 4), "unit": "GB/s", "cores": 1, "kind": "port",
+            "sample": "oracle/ or_readall (the faithful C restatement of wal.ReadAll, 1 thread) over the first "
+                      "%.2f GiB (%d frames) of the same WAL, %d passes, %.1f s" % (len(sample) / (1 << 30),
+                                                                                  o["n_records"], it, cs)})
+    out = {
+        "metric": METRIC, "value": round(world * nb / (ms / 1e3) / 1e9, 3), "unit": "GB/s",
+        "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(ms, 4), "dtype": "u8",
+        "config": {"workload": "configs[1]-shaped WAL after leader changes: %.3f GiB, %d frames, 1 %% of the entries "
+                               "rewrite the last 1-8 indexes (new term); clean, one ReadAll per step -> %d ents"
+                               % (nb / (1 << 30), n, li[0]),
+                   "wal_bytes_per_gpu": nb, "frames_per_gpu": n, "ri": 1},
+        "records_per_s": round(world * n / (ms / 1e3), 1),
+        "roofline": {"bound": "hbm", "achieved": round(nb / (rs.stream_ms / 1e3) / 1e9, 2), "peak": HBM_PEAK_GBPS,
+                     "unit": "GB/s", "frac": round(nb / (rs.stream_ms / 1e3) / 1e9 / HBM_PEAK_GBPS, 4),
+                     "traffic": None, "kernel": "k_stream", "kernel_ms": round(rs.stream_ms, 4),
+                     "algorithmic_bytes_per_launch": nb,
+                     "pipeline_achieved": round(nb / (rs.device_ms / 1e3) / 1e9, 2),
+                     "pipeline_frac": round(nb / (rs.device_ms / 1e3) / 1e9 / HBM_PEAK_GBPS, 4),
+                     "step_frac": round(nb / (ms / 1e3) / 1e9 / HBM_PEAK_GBPS, 4)},
+        "pipeline_device_ms": round(rs.device_ms, 4),
+        "cpu_baseline": cpu, "gen_seconds": round(gen_s, 2)}
+    dbuf.free()
+    ctx.close()
+    del buf
+    return out
+
+
+SUBS = {"c1": None, "shards": run_shards, "snap": run_snap, "commit": run_commit, "rewind": run_rewind}
 
 
 def main():
@@ -943,7 +1010,7 @@ def main():
                           file=sys.stderr, flush=True)
     else:
         out = {"shards": run_shards, "snap": run_snap, "snapstream": run_snapstream, "commit": run_commit,
-               "msg": run_msg, "restart": run_restart}[a.workload](a, dist, rank, world, local)
+               "msg": run_msg, "restart": run_restart, "rewind": run_rewind}[a.workload](a, dist, rank, world, local)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist is not None:

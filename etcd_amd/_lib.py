@@ -172,6 +172,8 @@ _SIGS = {
     "ewal_encoder_free": (None, [vp]),
     "ewal_synth_wal": (C.c_int64, [C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint32, C.c_int64, vp, C.c_uint64,
                                    C.POINTER(C.c_int64)]),
+    "ewal_synth_wal_ex": (C.c_int64, [C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint32, C.c_int64, C.c_uint32, vp,
+                                      C.c_uint64, C.POINTER(C.c_int64), C.POINTER(C.c_uint64)]),
     "ewal_encode_entries_device": (C.c_int, [vp, vp, C.c_uint64, vp, C.c_uint64, C.c_uint32, vp, C.c_uint64,
                                              C.POINTER(C.c_uint64), C.POINTER(C.c_uint32)]),
     "ewal_save_device": (C.c_int, [vp, vp, C.c_uint64, vp, C.c_uint64, C.c_uint32, vp, C.c_uint64,

@@ -13,13 +13,20 @@
 // Tables built here (per polynomial) and uploaded to the device:
 //   slice[4][256]      slicing-by-4 tables (slice[0] = MakeTable(poly))
 //   shift[m][4][256]   byte tables of S_{2^m}, m = 0..EW_SHIFT_LEVELS-1:
-//                      S_{2^m}(x) = ^_k shift[m][k][(x >> 8k) & 0xff]
+//                      S_{2^m}(x) = ^_k shift[m][k][(x >> 8k) & 0xff];
+//                      then EW_INV_LEVELS more: the inverses S_{2^m}^-1
+//                      (S_1 is x -> x * x^8 mod the polynomial, invertible
+//                      because the polynomial has a constant term), so that
+//                      P(x) = S_{b-x}^-1(P(b) ^ lin(stream[x, b))) reaches a
+//                      prefix from the NEXT boundary b
 #pragma once
 #include <cstdint>
 #include <cstring>
+#include <utility>
 #include <vector>
 
 #define EW_SHIFT_LEVELS 48  // S_{2^m} for m < 48: lengths up to 256 TiB
+#define EW_INV_LEVELS 8     // S_{2^m}^-1 for m < 8 (inverse shifts up to 255 bytes), after the forward levels
 
 namespace ewal {
 
@@ -29,7 +36,7 @@ struct CrcTables {
   uint32_t slice16[16][256];    // slicing-by-16 (slice16[t] = slice[t] for t < 4): the device table
   std::vector<uint32_t> shift;  // EW_SHIFT_LEVELS * 4 * 256
 
-  explicit CrcTables(uint32_t p) : poly(p), shift((size_t)EW_SHIFT_LEVELS * 1024) {
+  explicit CrcTables(uint32_t p) : poly(p), shift((size_t)(EW_SHIFT_LEVELS + EW_INV_LEVELS) * 1024) {
     for (uint32_t i = 0; i < 256; i++) {
       uint32_t c = i;
       for (int j = 0; j < 8; j++) c = (c & 1) ? (c >> 1) ^ poly : (c >> 1);
@@ -48,12 +55,48 @@ struct CrcTables {
       uint32_t x = 1u << j;
       m[j] = slice[0][x & 0xff] ^ (x >> 8);
     }
+    uint32_t m1[32];
+    std::memcpy(m1, m, sizeof(m1));
     for (int lvl = 0; lvl < EW_SHIFT_LEVELS; lvl++) {
       uint32_t *tb = &shift[(size_t)lvl * 1024];
       for (int k = 0; k < 4; k++)
         for (uint32_t b = 0; b < 256; b++) tb[k * 256 + b] = matvec(m, b << (8 * k));
       for (int j = 0; j < 32; j++) sq[j] = matvec(m, m[j]);
       std::memcpy(m, sq, sizeof(m));
+    }
+    // S_1^-1 by Gauss-Jordan over GF(2), then its powers S_{2^m}^-1
+    invert(m1, m);
+    for (int lvl = 0; lvl < EW_INV_LEVELS; lvl++) {
+      uint32_t *tb = &shift[(size_t)(EW_SHIFT_LEVELS + lvl) * 1024];
+      for (int k = 0; k < 4; k++)
+        for (uint32_t b = 0; b < 256; b++) tb[k * 256 + b] = matvec(m, b << (8 * k));
+      for (int j = 0; j < 32; j++) sq[j] = matvec(m, m[j]);
+      std::memcpy(m, sq, sizeof(m));
+    }
+  }
+
+  // inverse of the GF(2) matrix a (column j = a[j]) into r
+  static void invert(const uint32_t *a, uint32_t *r) {
+    // rows of [A | I]: row i holds bit i of every column
+    uint32_t ra[32], ri[32];
+    for (int i = 0; i < 32; i++) {
+      ra[i] = 0;
+      ri[i] = 1u << i;
+      for (int j = 0; j < 32; j++) ra[i] |= ((a[j] >> i) & 1u) << j;
+    }
+    for (int c = 0; c < 32; c++) {
+      int piv = c;
+      while (piv < 32 && !((ra[piv] >> c) & 1u)) piv++;
+      if (piv == 32) return;   // singular (not for a CRC polynomial with a constant term)
+      std::swap(ra[c], ra[piv]);
+      std::swap(ri[c], ri[piv]);
+      for (int i = 0; i < 32; i++)
+        if (i != c && ((ra[i] >> c) & 1u)) { ra[i] ^= ra[c]; ri[i] ^= ri[c]; }
+    }
+    // ri row i = row i of A^-1; back to columns
+    for (int j = 0; j < 32; j++) {
+      r[j] = 0;
+      for (int i = 0; i < 32; i++) r[j] |= ((ri[i] >> j) & 1u) << i;
     }
   }
 

@@ -220,6 +220,20 @@ static int compact_cands(ewal_ctx *c, const uint8_t *d_buf, uint64_t B, uint32_t
   return 0;
 }
 
+// The candidates of the units with more than EW_SLOTS of them (small
+// records) into cpos (k_rescan: each such unit scanned again, its candidates
+// written from its base); Small.novf cleared, so a pass over the candidate
+// list can run again.
+static int rescan_overflow(ewal_ctx *c, const uint8_t *d_buf, uint64_t B, uint64_t ccap) {
+  if (int rc = ensure_cand_aux(c, ccap)) return rc;
+  Small *ds = c->small.as<Small>();
+  hipLaunchKernelGGL(k_rescan, dim3(64), dim3(256), 0, c->stream, d_buf, B, c->ovf.as<uint32_t>(), &ds->novf,
+                     c->cbase.as<unsigned long long>(), c->cpos.as<uint64_t>(), c->clen.as<uint64_t>(), ccap);
+  EW_CHECK(hipGetLastError());
+  EW_CHECK(hipMemsetAsync(&ds->novf, 0, 4, c->stream));
+  return 0;
+}
+
 // Capacity of the dense candidate list for a B-byte stream: a frame is at
 // least 12 bytes, but candidates denser than one per 128 B only come from
 // tiny records; those calls grow the list (compact_cands) and run again.
@@ -528,7 +542,8 @@ static int fused_pass(ewal_ctx *c, DevTables *tb, const uint8_t *d_buf, uint64_t
   *done = false;
   const uint64_t ntiles = ccap / FC_TILE + 2;
   EW_CHECK(c->ftrec.ensure((size_t)ntiles * sizeof(TileRec)));
-  for (int pass = 0; pass < 2; ++pass) {
+  bool rescanned = false;
+  for (int pass = 0; pass < 3; ++pass) {
     EW_CHECK(c->ents.ensure((size_t)ecap * sizeof(ewal_entry)));
     EW_CHECK(c->mlist.ensure((size_t)ecap * 4));
     FcArgs a;
@@ -566,6 +581,12 @@ static int fused_pass(ewal_ctx *c, DevTables *tb, const uint8_t *d_buf, uint64_t
     hipLaunchKernelGGL(k_reset_check, dim3(1), dim3(64), 0, c->stream, ds);
     EW_CHECK(hipGetLastError());
     const uint64_t K = c->h_small->total;
+    if (c->h_small->novf && K <= ccap && !rescanned) {   // units with more than EW_SLOTS candidates
+      if (int rc = rescan_overflow(c, d_buf, B, ccap)) return rc;
+      rescanned = true;
+      if (K > ecap) ecap = K + K / 8 + 1024;
+      continue;
+    }
     // k_fc declined for capacity only: room for every candidate, once more
     if (c->h_small->fc.rare == 4u && K > ecap && K <= ccap && !c->h_small->novf) {
       ecap = K + K / 8 + 1024;
@@ -670,6 +691,17 @@ static int readall_impl(ewal_ctx *c, const uint8_t *d_buf, uint64_t B, uint64_t 
                                                                  B / 4096 + 1024));
     rc = run_stream(c, tb, d_buf, B, 1, ccap);
     if (rc) return rc;
+#if EW_XS
+    // timing-only ablation builds: the stream pass alone
+    EW_CHECK(hipEventRecord(c->ev1, c->stream));
+    EW_CHECK(hipStreamSynchronize(c->stream));
+    float xs_ms = 0;
+    EW_CHECK(hipEventElapsedTime(&xs_ms, c->ev0, c->ev1));
+    out->device_ms = xs_ms;
+    EW_CHECK(hipEventElapsedTime(&xs_ms, c->evs0, c->evs1));
+    out->stream_ms = xs_ms;
+    return 0;
+#endif
     bool fused_done = false;
     if (c->fused) {
       rc = fused_pass(c, tb, d_buf, B, ri, ccap, rdcap, &fused_done);
@@ -1037,7 +1069,8 @@ static int fused_batch(ewal_ctx *c, DevTables *tb, const uint8_t *d_buf, uint64_
   sg.ri = c->bri.as<uint64_t>();
   sg.soff = c->bsoff.as<uint64_t>();
   sg.sagg = c->bsagg.as<ShardAgg>();
-  for (int pass = 0; pass < 2; ++pass) {
+  bool rescanned = false;
+  for (int pass = 0; pass < 3; ++pass) {
     EW_CHECK(grow_keep(c->bents, (size_t)ecap * sizeof(ewal_entry), 0, c->stream));
     EW_CHECK(c->mlist.ensure((size_t)ecap * 4));
     FcArgs a;
@@ -1091,6 +1124,12 @@ static int fused_batch(ewal_ctx *c, DevTables *tb, const uint8_t *d_buf, uint64_
     }
     hipLaunchKernelGGL(k_reset_check, dim3(1), dim3(64), 0, c->stream, ds);
     EW_CHECK(hipGetLastError());
+    if (c->h_small->novf && K <= ccap && !rescanned) {   // units with more than EW_SLOTS candidates
+      if (int rc = rescan_overflow(c, d_buf, B, ccap)) return rc;
+      rescanned = true;
+      if (K > ecap) ecap = K + K / 8 + 1024;
+      continue;
+    }
     if (c->h_small->fc.rare == 4u && K > ecap && K <= ccap && !c->h_small->novf) {
       ecap = K + K / 8 + 1024;
       continue;
@@ -1195,10 +1234,30 @@ static int readall_batch_impl(ewal_ctx *c, const uint8_t *d_buf, uint32_t ns, co
                                                                  B / 1024 + 1024));
     rc = run_stream(c, tb, d_buf, B, 1, ccap);
     if (rc) return rc;
+#if EW_XS
+    // timing-only ablation builds (tools/build_ab.sh -DEW_XS=...): the stream pass alone
+    EW_CHECK(hipEventRecord(c->ev1, c->stream));
+    EW_CHECK(hipStreamSynchronize(c->stream));
+    EW_CHECK(hipEventElapsedTime(&dev_ms, c->ev0, c->ev1));
+    EW_CHECK(hipEventElapsedTime(&str_ms, c->evs0, c->evs1));
+    for (uint32_t i = 0; i < ns; ++i) {
+      std::memset(&out[i], 0, sizeof(out[i]));
+      out[i].device_ms = dev_ms;
+      out[i].stream_ms = str_ms;
+    }
+    return 0;
+#endif
     if (c->fused) {
       bool done = false;
       rc = fused_batch(c, tb, d_buf, B, ns, soff, ris, ccap, rdcap, out, &done);
       if (rc) return rc;
+      if (std::getenv("EWAL_DEBUG")) {
+        uint32_t nb = 0;
+        for (uint32_t i = 0; i < ns && done; ++i) nb += (out[i].flags & EW_SHARD_BAD) != 0;
+        std::fprintf(stderr, "ewal batch: fused done %d bad %u (K %llu ccap %llu ecap %llu novf %u rare %u err %u)\n",
+                     (int)done, nb, (unsigned long long)c->h_small->total, (unsigned long long)ccap,
+                     (unsigned long long)rdcap, c->h_small->novf, c->h_small->fc.rare, c->h_small->errflag);
+      }
       if (done) {   // every shard decided but those the fused pass flagged: they are replayed alone
         std::vector<uint32_t> bad;
         for (uint32_t i = 0; i < ns; ++i)

@@ -3,6 +3,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <cstdint>
+#include <type_traits>
 
 #define EW_PIECE 64                      // bytes per lane in the stream pass
 #define EW_WAVE_BYTES 4096               // 64 lanes x 64 B
@@ -30,6 +31,15 @@ __device__ __forceinline__ uint32_t gshift_n(const uint32_t *g, uint64_t n, uint
     x = gshift_pow2(g, m, x);
   }
   return x;
+}
+
+// A shift operator as eight nibble tables (t[k * 16 + d] = S(d << 4k)): 8
+// lookups per application, 512 B of LDS per operator.
+__device__ __forceinline__ uint32_t nib_apply(const uint32_t *t, uint32_t x) {
+  uint32_t r = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) r ^= t[k * 16 + ((x >> (4 * k)) & 15)];
+  return r;
 }
 
 // Copy n dwords into LDS: dst[i] = src(i).  Every thread issues 16 loads

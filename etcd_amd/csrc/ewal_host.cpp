@@ -609,6 +609,9 @@ void ewal_writer_close(ewal_writer *w) {
 // Create(Info{ID:1}) + Save(HardState{Term:1,Vote:1}, ents) where ents[i] =
 // Entry{Type:0, Term:1, Index:i+1, Data: len_i bytes}, len_i log-uniform in
 // [min_data, max_data] and the payload from xorshift64* seeded per entry.
+// With rewind_per_mille > 0, that share of the entries open a new leader's
+// term that rewrites the last 1..8 indexes (the uncommitted tail a new leader
+// overwrites: ReadAll's ents = append(ents[:Index-ri], e), wal/wal.go:173).
 // Two parallel passes: (1) CRC-32C of each entry's marshalled bytes,
 // (2) layout from the chained CRCs (varint widths), then bytes in place.
 static inline uint64_t mix64(uint64_t z) {
@@ -634,7 +637,13 @@ static void fill_payload(uint8_t *o, uint64_t n, uint64_t seed) {
 
 int64_t ewal_synth_wal(uint64_t seed, uint64_t target, uint32_t min_data, uint32_t max_data, int64_t corrupt_record,
                        uint8_t *out, uint64_t cap, int64_t *n_records) {
-  if (min_data == 0 || max_data < min_data) return EWAL_E_INVAL;
+  return ewal_synth_wal_ex(seed, target, min_data, max_data, corrupt_record, 0, out, cap, n_records, nullptr);
+}
+
+int64_t ewal_synth_wal_ex(uint64_t seed, uint64_t target, uint32_t min_data, uint32_t max_data,
+                          int64_t corrupt_record, uint32_t rewind_per_mille, uint8_t *out, uint64_t cap,
+                          int64_t *n_records, uint64_t *last_index) {
+  if (min_data == 0 || max_data < min_data || rewind_per_mille > 1000) return EWAL_E_INVAL;
   // entry sizes
   std::vector<uint32_t> sz;
   const double lo = std::log((double)min_data), hi = std::log((double)max_data + 1.0);
@@ -649,6 +658,22 @@ int64_t ewal_synth_wal(uint64_t seed, uint64_t target, uint32_t min_data, uint32
     approx += 8 + 2 + 5 + 1 + sov(s + 32) + entry_size(0, 1, sz.size(), s);
   }
   const size_t N = sz.size();
+  // each entry's Term and Index (a new leader's term rewinds the index)
+  std::vector<uint64_t> eterm(N), eidx(N);
+  {
+    uint64_t term = 1, idx = 0, r2 = mix64(seed ^ 0xBEEFull);
+    for (size_t j = 0; j < N; ++j) {
+      r2 = mix64(r2);
+      if (rewind_per_mille && j > 8 && (r2 % 1000) < rewind_per_mille) {
+        ++term;
+        const uint64_t back = 1 + ((r2 >> 20) & 7);
+        idx = idx > back ? idx - back : 0;
+      }
+      eterm[j] = term;
+      eidx[j] = ++idx;
+    }
+    if (last_index) *last_index = N ? eidx[N - 1] : 0;
+  }
   const uint8_t md[2] = {0x08, 0x01};   // etcdserverpb.Info{ID: 1}
   uint8_t st[40];
   const size_t stn = state_marshal(st, 1, 1, 0);
@@ -665,11 +690,11 @@ int64_t ewal_synth_wal(uint64_t seed, uint64_t target, uint32_t min_data, uint32
           size_t i = next.fetch_add(256);
           if (i >= N) break;
           for (size_t j = i; j < std::min(N, i + 256); ++j) {
-            tmp.resize(entry_size(0, 1, j + 1, sz[j]));
+            tmp.resize(entry_size(0, eterm[j], eidx[j], sz[j]));
             uint8_t *o = tmp.data();
             *o++ = 0x08; o = put_varint(o, 0);
-            *o++ = 0x10; o = put_varint(o, 1);
-            *o++ = 0x18; o = put_varint(o, j + 1);
+            *o++ = 0x10; o = put_varint(o, eterm[j]);
+            *o++ = 0x18; o = put_varint(o, eidx[j]);
             *o++ = 0x22; o = put_varint(o, sz[j]);
             fill_payload(o, sz[j], seed * 1000003ull + j);
             ecrc[j] = crc_update(0, kCastagnoli, tmp.data(), tmp.size());
@@ -695,7 +720,7 @@ int64_t ewal_synth_wal(uint64_t seed, uint64_t target, uint32_t min_data, uint32
   off += frame_size(3, c_st, stn, false);
   const uint64_t head = off;
   for (size_t j = 0; j < N; ++j) {
-    const uint64_t en = entry_size(0, 1, j + 1, sz[j]);
+    const uint64_t en = entry_size(0, eterm[j], eidx[j], sz[j]);
     c = T.combine(c, ecrc[j], en);
     fcrc[j] = c;
     foff[j] = off;
@@ -718,7 +743,7 @@ int64_t ewal_synth_wal(uint64_t seed, uint64_t target, uint32_t min_data, uint32
           size_t i = next.fetch_add(256);
           if (i >= N) break;
           for (size_t j = i; j < std::min(N, i + 256); ++j) {
-            const uint64_t en = entry_size(0, 1, j + 1, sz[j]);
+            const uint64_t en = entry_size(0, eterm[j], eidx[j], sz[j]);
             uint8_t *f = out + foff[j];
             int64_t L = (int64_t)frame_size(2, fcrc[j], en, false) - 8;
             std::memcpy(f, &L, 8);
@@ -727,8 +752,8 @@ int64_t ewal_synth_wal(uint64_t seed, uint64_t target, uint32_t min_data, uint32
             *p++ = 0x10; p = put_varint(p, fcrc[j]);
             *p++ = 0x1a; p = put_varint(p, en);
             *p++ = 0x08; p = put_varint(p, 0);
-            *p++ = 0x10; p = put_varint(p, 1);
-            *p++ = 0x18; p = put_varint(p, j + 1);
+            *p++ = 0x10; p = put_varint(p, eterm[j]);
+            *p++ = 0x18; p = put_varint(p, eidx[j]);
             *p++ = 0x22; p = put_varint(p, sz[j]);
             fill_payload(p, sz[j], seed * 1000003ull + j);
             if ((int64_t)(j + 3) == corrupt_record) p[sz[j] / 2] ^= 0x5a;

@@ -113,12 +113,7 @@ __device__ __forceinline__ uint32_t nib_src(const uint32_t *g_shift, int i) {
   const int m = i >> 7, k = (i >> 4) & 7, d = i & 15;
   return g_shift[m * 1024 + (k >> 1) * 256 + (d << (4 * (k & 1)))];
 }
-__device__ __forceinline__ uint32_t nib_apply(const uint32_t *t, uint32_t x) {
-  uint32_t r = 0;
-#pragma unroll
-  for (int k = 0; k < 8; ++k) r ^= t[k * 16 + ((x >> (4 * k)) & 15)];
-  return r;
-}
+
 
 struct FcArgs {
   const uint8_t *buf;
@@ -273,6 +268,7 @@ __global__ __launch_bounds__(FC_THREADS, FC_WGS) void k_fc(FcArgs a, SegArgs sg)
   __shared__ uint32_t s_t4[16 * 256];          // slicing-by-16
   __shared__ uint32_t s_svp[1024];             // S_256 (prefix Horner step)
   __shared__ uint32_t s_nib[FC_NIB_LEVELS * 128];   // S_{2^0} .. S_{2^16}, nibble tables (the seed shift)
+  __shared__ uint32_t s_inv[7 * 128];               // S_{2^0}^-1 .. S_{2^6}^-1 (prefixes from the next boundary)
   __shared__ uint32_t s_win[20 * FC_THREADS];  // frame heads, transposed (bank = thread & 31)
   Small *ds = a.ds;
   const uint64_t K = ds->total;
@@ -305,6 +301,7 @@ __global__ __launch_bounds__(FC_THREADS, FC_WGS) void k_fc(FcArgs a, SegArgs sg)
   stage_lds<FC_THREADS>(s_t4, 16 * 256, [&](int i) { return a.g_slice[i]; });
   stage_lds<FC_THREADS>(s_svp, 1024, [&](int i) { return a.g_shift[EW_VLOG * 1024 + i]; });
   stage_lds<FC_THREADS>(s_nib, FC_NIB_LEVELS * 128, [&](int i) { return nib_src(a.g_shift, i); });
+  stage_lds<FC_THREADS>(s_inv, 7 * 128, [&](int i) { return nib_src(a.g_shift + EW_SHIFT_LEVELS * 1024, i); });
   __syncthreads();   // the only barrier: every wave runs its own tiles from here on
   // SEG: the shard of the run's first tile, one search per wave (binary
   // searches per tile were chains of dependent loads on every tile)
@@ -350,8 +347,8 @@ __global__ __launch_bounds__(FC_THREADS, FC_WGS) void k_fc(FcArgs a, SegArgs sg)
       }
       pend = false;
     };
-    const bool ok = decode_canon<FC_THREADS>(a.buf, a.B, p, a.pwave, a.v, s_t4, s_svp, s_win + tid, d, L, Pfo, Pfd,
-                                             (a.ablate & 2) != 0, flush);
+    const bool ok = decode_canon<FC_THREADS, true>(a.buf, a.B, p, a.pwave, a.v, s_t4, s_svp, s_win + tid, d, L, Pfo,
+                                                   Pfd, (a.ablate & 2) != 0, flush, s_inv);
     const uint64_t s = p + 8 + (uint64_t)L;
     uint32_t sh = 0, lo = 0;                   // SEG: the frame's shard and its first frame
     uint64_t ri = a.ri;

@@ -307,7 +307,8 @@ __device__ __forceinline__ void row_transpose(uint32_t (&D)[19]) {
 // from lane 63).  The 4 KiB aggregates are formed from v[] by k_uscan, where
 // one lane per unit does it with every lane busy.
 #ifndef EW_XS
-#define EW_XS 0   // timing-only k_stream ablations (tools/): 1 no CRC, 2 no candidates, 4 no v stores; results are wrong
+#define EW_XS 0   // timing-only k_stream ablations (tools/): 1 no CRC, 2 no candidates, 4 no v stores,
+                  // 8 the candidate filter without the exact tests / slots; results are wrong
 #endif
 template <int NU, bool FIND>
 __device__ __forceinline__ void stream_units(const StreamArgs &a, const uint8_t *s_slice, const uint32_t *s_s64,
@@ -354,6 +355,10 @@ __device__ __forceinline__ void stream_units(const StreamArgs &a, const uint8_t 
   for (int i = 0; i < NU; ++i) {
     const uint64_t off = (uint64_t)u[i] * EW_WAVE_BYTES + (uint64_t)lane * EW_PIECE;
     uint32_t cnt = 0, pa = 0, pb = 0;
+    if (EW_XS & 8) {   // timing-only ablation: the filter's result kept, no exact tests / slots
+      if (lane == 63) a.wcnt[u[i]] = (uint32_t)__popcll(__ballot(fm[i] != 0));
+      continue;
+    }
     if (fm[i] && off < B) cnt = find_cands(D[i], fm[i], off, B, (uint32_t)(lane * EW_PIECE), pa, pb);
     uint32_t ci = 0;
     if (__ballot(cnt != 0)) {   // wave-uniform: most 4 KiB units hold no frame start
@@ -1080,6 +1085,91 @@ __device__ __forceinline__ uint32_t prefix_at(uint64_t x, const uint32_t *__rest
   return prefix_finish(in, t4, svp);
 }
 
+// P(x) from the NEARER super-piece boundary (the fused frame pass): x in the
+// upper half of its super-piece [x0, x1 = x0 + 256) takes P(x1) -- Horner over
+// one more v value -- and steps BACK over stream[x, x1) with the inverse
+// shift: P(x) = S_{x1-x}^-1(P(x1) ^ lin(stream[x, x1))) (lin(A||B) =
+// S_|B|(lin A) ^ lin B).  At most 128 tail bytes instead of 255 (half the
+// fetch and the slicing steps on average, 32 fewer VGPRs).  `inv`: nibble
+// tables of S_{2^m}^-1, m = 0..6.
+struct PrefixNear {
+  uint32_t pw, nk, n, up, lead, slow;   // slow: x in the upper half of the stream's last, partial
+                                        // super-piece (no next boundary): prefix_at instead
+  uint4 vv[EW_VPU / 4];
+  uint4 dd[9];
+};
+__device__ __forceinline__ void prefix_load_near(uint64_t x, uint64_t B, const uint32_t *__restrict__ pwave,
+                                                 const uint32_t *__restrict__ v, const uint8_t *__restrict__ buf,
+                                                 PrefixNear &in) {
+  const uint64_t w = x >> 12;
+  const uint64_t x0 = x & ~(uint64_t)(EW_VPIECE - 1);
+  const uint32_t k = (uint32_t)((x0 >> EW_VLOG) & (EW_VPU - 1));
+  const uint32_t tail = (uint32_t)(x - x0);
+  in.up = tail > EW_VPIECE / 2 && x0 + EW_VPIECE <= B;
+  in.slow = tail > EW_VPIECE / 2 && !in.up;
+  in.nk = k + in.up;
+  in.lead = (uint32_t)(x & 15);
+  const uint64_t base = in.up ? (x & ~15ull) : x0;
+  in.n = in.up ? (uint32_t)(x0 + EW_VPIECE - base) : (in.slow ? 0u : tail);   // bytes loaded from base
+  const uint4 *vq = (const uint4 *)(v + w * EW_VPU);
+#pragma unroll
+  for (int q = 0; q < EW_VPU / 4; ++q) in.vv[q] = (4u * q < in.nk) ? vq[q] : make_uint4(0, 0, 0, 0);
+  const uint4 *dq = (const uint4 *)(buf + base);
+#pragma unroll
+  for (int q = 0; q < 9; ++q) in.dd[q] = (16u * q < in.n) ? dq[q] : make_uint4(0, 0, 0, 0);
+  in.pw = pwave[w];
+}
+__device__ __forceinline__ uint32_t prefix_finish_near(const PrefixNear &in, const uint32_t *t16, const uint32_t *svp,
+                                                       const uint32_t *inv) {
+  uint32_t acc = in.pw;
+#pragma unroll
+  for (int q = 0; q < EW_VPU / 4; ++q) {
+    if (4u * q + 0 < in.nk) acc = tab_apply(svp, acc) ^ in.vv[q].x;
+    if (4u * q + 1 < in.nk) acc = tab_apply(svp, acc) ^ in.vv[q].y;
+    if (4u * q + 2 < in.nk) acc = tab_apply(svp, acc) ^ in.vv[q].z;
+    if (4u * q + 3 < in.nk) acc = tab_apply(svp, acc) ^ in.vv[q].w;
+  }
+  if (!in.up) {   // forward over the n <= 128 bytes after x0
+    const uint32_t nq = in.n >> 4;
+    uint4 pc = in.dd[0];
+#pragma unroll
+    for (int q = 0; q < 9; ++q) {
+      if ((uint32_t)q < nq) acc = step16(t16, acc, in.dd[q]);
+      if (q && (uint32_t)q == nq) pc = in.dd[q];
+    }
+    const uint32_t nd = (in.n & 15) >> 2;
+    if (nd > 0) acc = step4_flat(t16, acc ^ pc.x);
+    if (nd > 1) acc = step4_flat(t16, acc ^ pc.y);
+    if (nd > 2) acc = step4_flat(t16, acc ^ pc.z);
+    uint32_t wd = nd == 0 ? pc.x : nd == 1 ? pc.y : nd == 2 ? pc.z : pc.w;
+    for (uint32_t b = 0; b < (in.n & 3); ++b, wd >>= 8) acc = t16[(acc ^ wd) & 0xff] ^ (acc >> 8);
+    return acc;
+  }
+  // lin(stream[x, x1)) from register 0: chunk 0 from byte `lead` on, then whole chunks
+  uint32_t c = 0;
+  const uint32_t lead = in.lead;
+  const uint32_t w0[4] = {in.dd[0].x, in.dd[0].y, in.dd[0].z, in.dd[0].w};
+#pragma unroll
+  for (uint32_t j = 0; j < 4; ++j) {
+    if (4 * j >= lead) {
+      c = step4_flat(t16, c ^ w0[j]);
+    } else if (4 * j + 4 > lead) {
+      uint32_t t = w0[j] >> (8 * (lead & 3));
+      for (uint32_t b = lead & 3; b < 4; ++b, t >>= 8) c = t16[(c ^ t) & 0xff] ^ (c >> 8);
+    }
+  }
+  const uint32_t nq = in.n >> 4;   // in.n is a multiple of 16 here
+#pragma unroll
+  for (int q = 1; q < 9; ++q)
+    if ((uint32_t)q < nq) c = step16(t16, c, in.dd[q]);
+  uint32_t x = acc ^ c;
+  const uint32_t m = in.n - lead;   // x1 - x, 1..127
+#pragma unroll
+  for (int l = 0; l < 7; ++l)
+    if ((m >> l) & 1) x = nib_apply(inv + l * 128, x);
+  return x;
+}
+
 // lin of the concatenation of every non-empty segment of bytes field fnum
 // of a message pb_walk accepted (Go's `m.Data = append(m.Data, ...)` over
 // repeats), the message read at stream offset base:
@@ -1462,12 +1552,12 @@ __device__ __forceinline__ int pb_field_fast(const uint32_t *w, int o, uint32_t 
 struct NoOp {
   __device__ void operator()() const {}
 };
-template <int WS, class AfterIssue = NoOp>
+template <int WS, bool NEAR = false, class AfterIssue = NoOp>
 __device__ __forceinline__ bool decode_canon(const uint8_t *__restrict__ buf, uint64_t B, uint64_t p,
                                              const uint32_t *__restrict__ pwave, const uint32_t *__restrict__ v,
                                              const uint32_t *s_t4, const uint32_t *s_svp, uint32_t *w, RecDesc &d,
                                              int64_t &L, uint32_t &Pfo, uint32_t &Pfd, bool noprefix = false,
-                                             AfterIssue after_issue = AfterIssue()) {
+                                             AfterIssue after_issue = AfterIssue(), const uint32_t *s_inv = nullptr) {
   const uint64_t p16 = p & ~15ull;
   uint4 hq[5];
 #pragma unroll
@@ -1482,8 +1572,9 @@ __device__ __forceinline__ bool decode_canon(const uint8_t *__restrict__ buf, ui
       hq[k] = make_uint4(x[0], x[1], x[2], x[3]);
     }
   }
-  PrefixIn pin;
-  prefix_load(p, pwave, v, buf, pin);
+  typename std::conditional<NEAR, PrefixNear, PrefixIn>::type pin;
+  if constexpr (NEAR) prefix_load_near(p, B, pwave, v, buf, pin);
+  else prefix_load(p, pwave, v, buf, pin);
   after_issue();   // the caller's stores: issued behind this frame's loads, so waiting for them never waits for those
 #pragma unroll
   for (int k = 0; k < 5; ++k) {
@@ -1529,7 +1620,10 @@ __device__ __forceinline__ bool decode_canon(const uint8_t *__restrict__ buf, ui
     }
   }
   if (!ok) return false;
-  Pfo = noprefix ? pin.pw : prefix_finish16(pin, s_t4, s_svp);
+  if constexpr (NEAR)
+    Pfo = noprefix ? pin.pw
+                   : (pin.slow ? prefix_at(p, pwave, v, buf, s_t4, s_svp) : prefix_finish_near(pin, s_t4, s_svp, s_inv));
+  else Pfo = noprefix ? pin.pw : prefix_finish16(pin, s_t4, s_svp);
   if (d.type != 4 && d.dlen > 0) {    // P(data start): the header bytes after P(frame start)
     uint32_t c = Pfo;
     const int nh = ho - base;

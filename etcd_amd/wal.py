@@ -504,16 +504,23 @@ def save_device(ctx: Context, ops, prev_crc: int = 0):
             b.free()
 
 
-def synth_wal(target_bytes, min_data=64, max_data=65536, seed=2, corrupt_record=-1):
-    """Synthetic WAL (bench/test input); returns (bytearray, n_records)."""
+def synth_wal(target_bytes, min_data=64, max_data=65536, seed=2, corrupt_record=-1, rewind_per_mille=0,
+              last_index=None):
+    """Synthetic WAL (bench/test input); returns (bytearray, n_records).
+    rewind_per_mille: that share of the entries open a new leader's term that
+    rewrites the last 1..8 indexes; last_index (a list) receives the last
+    entry's Index."""
     cap = target_bytes + max_data * 2 + (1 << 20)
     out = bytearray(cap)
     nrec = C.c_int64(0)
-    n = lib.ewal_synth_wal(seed, target_bytes, min_data, max_data, corrupt_record,
-                           (C.c_char * cap).from_buffer(out), cap, C.byref(nrec))
+    li = C.c_uint64(0)
+    n = lib.ewal_synth_wal_ex(seed, target_bytes, min_data, max_data, corrupt_record, rewind_per_mille,
+                              (C.c_char * cap).from_buffer(out), cap, C.byref(nrec), C.byref(li))
     if n < 0:
         check(int(n))
     del out[n:]
+    if last_index is not None:
+        last_index.append(li.value)
     return out, nrec.value
 
 

@@ -276,6 +276,12 @@ void ewal_encoder_free(ewal_encoder *e);
  * Returns bytes written; *n_records receives the frame count. */
 int64_t ewal_synth_wal(uint64_t seed, uint64_t target_bytes, uint32_t min_data, uint32_t max_data,
                        int64_t corrupt_record, uint8_t *out, uint64_t cap, int64_t *n_records);
+/* The same with rewind_per_mille / 1000 of the entries opening a new
+ * leader's term that rewrites the last 1..8 indexes (leader changes);
+ * *last_index (nullable) = the last entry's Index. */
+int64_t ewal_synth_wal_ex(uint64_t seed, uint64_t target_bytes, uint32_t min_data, uint32_t max_data,
+                          int64_t corrupt_record, uint32_t rewind_per_mille, uint8_t *out, uint64_t cap,
+                          int64_t *n_records, uint64_t *last_index);
 
 /* ---- batched write path: (*WAL).SaveEntry / encoder.encode on the GPU ---- */
 /* encoder.encode(&walpb.Record{Type: entryType, Data: pbutil.MustMarshal(e)})

@@ -47,11 +47,12 @@ def check_batch(ctx, shards, ris, expect_fast=None, fallback=None):
     return res
 
 
-def _variety(rng):
+def _variety(rng, big_terms=True):
     """Shards covering ReadAll's outcomes, each framed cleanly (fast path)."""
     out = []
     for i in range(24):
-        w = build_wal(rng, rng.randrange(1, 120), rng.choice([50, 2000, 20000]), cuts=rng.randrange(0, 3))
+        w = build_wal(rng, rng.randrange(1, 120), rng.choice([50, 2000, 20000]), cuts=rng.randrange(0, 3),
+                      big_terms=big_terms)
         kind = i % 6
         ri = 0
         if kind == 1:     # payload byte flip -> walpb.ErrCRCMismatch
@@ -98,6 +99,11 @@ def _variety(rng):
 def test_batch_fast_path_outcomes(ctx):
     rng = random.Random(7)
     sh = _variety(rng)
+    # (Terms up to 2^63: 9-byte varints the fused pass's canonical parser
+    # declines -- those shards are replayed alone, exactly)
+    check_batch(ctx, [w for w, _ in sh], [ri for _, ri in sh])
+    rng = random.Random(7)
+    sh = _variety(rng, big_terms=False)
     check_batch(ctx, [w for w, _ in sh], [ri for _, ri in sh], expect_fast=True)
 
 
@@ -106,14 +112,15 @@ def test_batch_random(ctx, seed):
     rng = random.Random(300 + seed)
     shards, ris = [], []
     for _ in range(rng.randrange(1, 40)):
-        shards.append(build_wal(rng, rng.randrange(0, 80), rng.choice([100, 3000]), cuts=rng.randrange(0, 3)))
+        shards.append(build_wal(rng, rng.randrange(0, 80), rng.choice([100, 3000]), cuts=rng.randrange(0, 3),
+                                big_terms=seed % 2 == 0))
         ris.append(rng.choice([0, 0, 0, 3, 50]))
-    check_batch(ctx, shards, ris, expect_fast=True)
+    check_batch(ctx, shards, ris, expect_fast=None if seed % 2 == 0 else True)
 
 
 def test_batch_fallback_torn_and_rewind(ctx):
     rng = random.Random(11)
-    base = [build_wal(rng, 30, 500) for _ in range(6)]
+    base = [build_wal(rng, 30, 500, big_terms=False) for _ in range(6)]
     # a torn shard in the middle: its chain runs into the next shard
     torn = list(base)
     torn[2] = torn[2][:-5]
@@ -200,11 +207,11 @@ def test_batch_edges_and_ctx_reuse(ctx):
     assert W.readall_batch_bytes([], [], ctx) == []
     check_batch(ctx, [b"", b"", b""], [0, 1, 0])
     rng = random.Random(21)
-    one = build_wal(rng, 40, 3000, cuts=1)
+    one = build_wal(rng, 40, 3000, cuts=1, big_terms=False)
     r = check_batch(ctx, [one], [0], expect_fast=True)[0]
     g = W.readall_bytes(one, 0, ctx)
     assert g.as_dict() == r.as_dict()
-    big = [build_wal(rng, 200, 20000) for _ in range(5)]
+    big = [build_wal(rng, 200, 20000, big_terms=False) for _ in range(5)]
     check_batch(ctx, big, [0] * 5, expect_fast=True)
     g2 = W.readall_bytes(one, 0, ctx)           # a single ReadAll after a larger batch
     assert g2.as_dict() == g.as_dict()

@@ -197,3 +197,33 @@ def test_configs4_1m_groups_against_oracle(ctx):
     np.testing.assert_array_equal(ch.cpu().numpy(), chc)
     ok = stc == 0
     np.testing.assert_array_equal(got_c[ok], c[ok])
+
+
+@pytest.mark.gpu
+def test_configs1_shaped_with_leader_changes(ctx):
+    """A configs[1]-shaped WAL (64 B - 64 KiB entries) where 1 % of the entries
+    open a new leader's term that rewrites the last 1..8 indexes (wal/wal.go:173
+    truncate-and-overwrite): every ents Index / Term / Data view against the
+    oracle's ReadAll, single WAL and as one shard of a batch beside clean ones."""
+    li = []
+    buf, n = W.synth_wal(96 << 20, 64, 65536, seed=12, rewind_per_mille=10, last_index=li)
+    b = bytes(buf)
+    d = ctx.alloc(len(b) + 64)
+    try:
+        d.upload(b)
+        g = _readall(ctx, d, len(b), 1, memoryview(b))
+        o = O.readall_digest(b, 1)
+        assert o["status"] == O.OK and o["n_ents"] == li[0]
+        _assert_result(ctx, g, o, b)
+    finally:
+        d.free()
+    clean = [bytes(W.synth_wal(8 << 20, 64, 16384, seed=30 + i)[0]) for i in range(3)]
+    small = bytes(W.synth_wal(16 << 20, 64, 16384, seed=13, rewind_per_mille=10)[0])
+    shards = [clean[0], small, clean[1], clean[2]]
+    res = W.readall_batch_bytes(shards, [1] * 4, ctx, with_ents=True)
+    for s, (sb, r) in enumerate(zip(shards, res)):
+        o = O.readall(sb, 1)
+        assert r.status == o["status"] == O.OK and (r.n_records, r.last_crc, r.enti) == \
+            (o["n_records"], o["last_crc"], o["enti"])
+        assert [(e.Index, e.Term, e.Data) for e in r.ents] == [(e["index"], e["term"], e["data"]) for e in o["ents"]]
+        assert bool(r.flags & L.FLAG_SHARD_FALLBACK) == (s == 1)
