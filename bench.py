@@ -158,7 +158,7 @@ def run_shards(a, dist, rank, world, local, cpu_seconds=None):
     chunk = 64
     ctx = W.Context(local)
     dev = torch.device("cuda", local)
-    dmem = torch.empty(nsh * (target + 2 * 4096 + 4096) + 64, dtype=torch.uint8, device=dev)
+    dmem = torch.empty(nsh * (target + (1 << 20)) + 64, dtype=torch.uint8, device=dev)   # (the generator overshoots)
     dbuf = W.DeviceBuffer(ctx, C.c_void_p(dmem.data_ptr()), dmem.numel())   # torch owns it
     lens, nrec, pos, keep = [], [], 0, None
     for c0 in range(0, nsh, chunk):

@@ -126,7 +126,7 @@ struct ewal_ctx {
   std::vector<ewal_unrec> unrec;   // XXX_unrecognized of the last ReadAll's result (side list)
   uint64_t unrec_bytes = 0;
   // batched ReadAll (ewal_readall_batch_device): shard tables, results, ents
-  DevBuf bfs, bsoff, bri, bsagg, bres, bef, bents, bshard;
+  DevBuf bfs, bsoff, bri, bsagg, bres, bef, bents, bshard, hmask;
   // batched raftpb.Message decode (emsg_decode_batch_device)
   DevBuf moff, mlen, mcnt, mfirst, mout, ments;
   uint64_t mtotal = 0;
@@ -257,6 +257,7 @@ static int stream_ensure(ewal_ctx *c, uint64_t B, int find_cand) {
   if (find_cand) {
     EW_CHECK(c->slots.ensure((size_t)nunits * EW_SLOTS * 2));
     EW_CHECK(c->ovf.ensure((size_t)nunits * 4));
+    if (EW_SPLIT_CAND) EW_CHECK(c->hmask.ensure((size_t)nunits * 8));
   }
   EW_CHECK(c->ux.ensure((size_t)nunits * 4));
   EW_CHECK(c->tagg.ensure((size_t)nstiles * 16));
@@ -293,6 +294,7 @@ static int run_stream(ewal_ctx *c, DevTables *tb, const uint8_t *d_buf, uint64_t
   a.v = c->v.as<uint32_t>();
   a.wcnt = c->wcnt.as<uint32_t>();
   a.slots = find_cand ? c->slots.as<uint16_t>() : nullptr;
+  a.hmask = find_cand && EW_SPLIT_CAND ? c->hmask.as<unsigned long long>() : nullptr;
   a.small = ds;
   const unsigned grid = (unsigned)std::min<uint64_t>((nunits + 2 * EW_WAVES - 1) / (2 * EW_WAVES), (uint64_t)c->num_cu);
   EW_CHECK(hipEventRecord(c->evs0, c->stream));
@@ -302,6 +304,10 @@ static int run_stream(ewal_ctx *c, DevTables *tb, const uint8_t *d_buf, uint64_t
     hipLaunchKernelGGL(k_stream<false>, dim3(grid), dim3(EW_THREADS), 0, c->stream, a);
   EW_CHECK(hipGetLastError());
   EW_CHECK(hipEventRecord(c->evs1, c->stream));
+  if (find_cand && EW_SPLIT_CAND && !(EW_XS & 8))   // the exact tests on the flagged pieces -> slots, wcnt
+    hipLaunchKernelGGL(k_cand, dim3(grid_for(nunits, 64 * EW_CAND_WAVES)), dim3(64 * EW_CAND_WAVES), 0, c->stream,
+                       d_buf, B, nunits, c->hmask.as<unsigned long long>(), c->slots.as<uint16_t>(),
+                       c->wcnt.as<uint32_t>());
   ScanArgs s;
   s.nunits = nunits;
   s.ntiles = nstiles;

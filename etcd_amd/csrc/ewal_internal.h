@@ -17,6 +17,7 @@ struct StreamArgs {
   uint32_t *v;             // lin of every 64-B piece        [nunits*64]
   uint32_t *wcnt;          // candidates in the unit         [nunits]
   uint16_t *slots;         // first EW_SLOTS candidate offsets per unit
+  unsigned long long *hmask;   // EW_SPLIT_CAND: per unit, the lanes (64-B pieces) the candidate filter flagged
   Small *small;            // the call's device scratch, zeroed by k_stream's workgroup 0
 };
 

@@ -306,6 +306,15 @@ __device__ __forceinline__ void row_transpose(uint32_t (&D)[19]) {
 // frame-start candidates -> slots[] / wcnt[] (the unit's candidate count,
 // from lane 63).  The 4 KiB aggregates are formed from v[] by k_uscan, where
 // one lane per unit does it with every lane busy.
+// EW_SPLIT_CAND: k_stream runs only the branch-free candidate filter and
+// records which 64-B pieces it flagged (one 64-bit mask per unit); k_cand
+// then runs the exact frame-start tests and writes the slots for those
+// pieces alone.  In the stream pass the exact tests were divergent VALU and
+// scattered slot stores on every unit of a record-dense WAL (28 % of
+// k_stream on configs[2]-shaped shards, ablation EW_XS=2, r03).
+#ifndef EW_SPLIT_CAND
+#define EW_SPLIT_CAND 1
+#endif
 #ifndef EW_XS
 #define EW_XS 0   // timing-only k_stream ablations (tools/): 1 no CRC, 2 no candidates, 4 no v stores,
                   // 8 the candidate filter without the exact tests / slots; results are wrong
@@ -351,6 +360,15 @@ __device__ __forceinline__ void stream_units(const StreamArgs &a, const uint8_t 
       if (!(EW_XS & 4) || c[i] == 0x12345678u) a.v[(uint64_t)u[i] * EW_VPU + (lane >> 2)] = c[i];
   }
   if (!FIND) return;
+  if (EW_SPLIT_CAND && !(EW_XS & 8)) {   // the flagged pieces, for k_cand
+#pragma unroll
+    for (int i = 0; i < NU; ++i) {
+      const uint64_t off = (uint64_t)u[i] * EW_WAVE_BYTES + (uint64_t)lane * EW_PIECE;
+      const unsigned long long hm = __ballot(fm[i] != 0 && off < B);
+      if (lane == 0) a.hmask[u[i]] = hm;
+    }
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < NU; ++i) {
     const uint64_t off = (uint64_t)u[i] * EW_WAVE_BYTES + (uint64_t)lane * EW_PIECE;
@@ -476,6 +494,103 @@ __global__ __launch_bounds__(EW_THREADS, 1) void k_stream(StreamArgs a) {
     const uint32_t uu[1] = {u};
     stream_units<1, FIND>(a, s_slice, s_s64, s_s128, Lt, uu, D1);
   }
+}
+
+// ===========================================================================
+// k_cand (EW_SPLIT_CAND): the exact frame-start test on the 64-B pieces
+// k_stream's filter flagged, and every unit's slots and candidate count.
+// One wave per 64 units: lane l reads unit l's mask, the wave lists the
+// flagged pieces (unit, piece) in order in LDS, then takes them 64 at a
+// time -- each lane loads its piece plus the 12 bytes after it (80 B), runs
+// the filter and the exact tests, and places its candidates after those of
+// the unit's earlier pieces (a segmented scan over the round, the unit's
+// running count in LDS), so every unit's slots stay position-sorted.
+// ===========================================================================
+#define EW_CAND_WAVES 4
+__device__ __forceinline__ void load_piece80(const uint8_t *buf, uint64_t B, uint64_t off, uint32_t (&D)[19]) {
+  if (off + 80 <= B) {
+    const uint4 *q = (const uint4 *)(buf + off);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint4 x = q[k];
+      D[4 * k] = x.x; D[4 * k + 1] = x.y; D[4 * k + 2] = x.z; D[4 * k + 3] = x.w;
+    }
+    const uint4 x = q[4];
+    D[16] = x.x; D[17] = x.y; D[18] = x.z;
+  } else {
+#pragma unroll
+    for (int k = 0; k < 19; ++k) D[k] = load_word_guarded(buf, B, off + 4 * k);
+  }
+}
+__global__ __launch_bounds__(EW_CAND_WAVES * 64) void k_cand(const uint8_t *__restrict__ buf, uint64_t B,
+                                                             uint32_t nunits,
+                                                             const unsigned long long *__restrict__ hmask,
+                                                             uint16_t *__restrict__ slots,
+                                                             uint32_t *__restrict__ wcnt) {
+  __shared__ uint16_t s_list[EW_CAND_WAVES][64 * 64];
+  __shared__ uint32_t s_ucnt[EW_CAND_WAVES][64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const uint32_t u0 = (blockIdx.x * EW_CAND_WAVES + (uint32_t)wv) * 64;
+  const bool active = u0 < nunits;   // wave-uniform
+  uint16_t *list = s_list[wv];
+  uint32_t *ucnt = s_ucnt[wv];
+  const uint32_t ul = u0 + (uint32_t)lane;
+  const unsigned long long hm = (active && ul < nunits) ? hmask[ul] : 0ull;
+  const uint32_t pc = (uint32_t)__popcll(hm);
+  const uint32_t incl0 = wave_incl_sum(pc);
+  const uint32_t T = (uint32_t)__shfl((int)incl0, 63);
+  ucnt[lane] = 0;
+  {
+    uint32_t k = incl0 - pc;
+    unsigned long long m = hm;
+    while (m) {
+      const int b = __ffsll((long long)m) - 1;
+      m &= m - 1;
+      list[k++] = (uint16_t)((lane << 6) | b);
+    }
+  }
+  __syncthreads();
+  for (uint32_t r0 = 0; r0 < T; r0 += 64) {
+    const uint32_t i = r0 + (uint32_t)lane;
+    const bool live = i < T;
+    const uint32_t e = live ? list[i] : 0xffffu;
+    const uint32_t ulo = e >> 6, pcs = e & 63;
+    const uint64_t off = (uint64_t)(u0 + ulo) * EW_WAVE_BYTES + (uint64_t)pcs * EW_PIECE;
+    uint32_t D[19];
+    if (live) {
+      load_piece80(buf, B, off, D);
+    } else {
+#pragma unroll
+      for (int k = 0; k < 19; ++k) D[k] = 0u;
+    }
+    uint32_t pa = 0, pb = 0, cnt = 0;
+    if (live) {
+      const uint32_t fm = cand_filter(D);
+      if (fm) cnt = find_cands(D, fm, off, B, pcs * EW_PIECE, pa, pb);
+    }
+    // segmented exclusive scan of cnt over the round (a unit's pieces are contiguous)
+    const uint32_t incl = wave_incl_sum(cnt);
+    const uint32_t prev = (uint32_t)__shfl_up((int)e, 1);
+    const bool head = lane == 0 || (prev >> 6) != ulo;
+    const unsigned long long H = __ballot(head);
+    const int hl = 63 - __clzll((long long)(H & (lane == 63 ? ~0ull : ((2ull << lane) - 1ull))));
+    const uint32_t before = (uint32_t)__shfl((int)incl, hl > 0 ? hl - 1 : 0);
+    const uint32_t base = (live ? ucnt[ulo] : 0u) + (incl - cnt - (hl > 0 ? before : 0u));
+    const uint32_t nxt = (uint32_t)__shfl_down((int)e, 1);
+    const bool last = live && (lane == 63 || i + 1 >= T || (nxt >> 6) != ulo);
+    if (last) ucnt[ulo] = base + cnt;
+    if (cnt) {
+      uint16_t *sl = slots + (size_t)(u0 + ulo) * EW_SLOTS;
+      if (cnt > 2) {
+        slot_cands(D, off, B, base, sl, pcs * EW_PIECE);
+      } else {
+        if (base < EW_SLOTS) sl[base] = (uint16_t)pa;
+        if (cnt >= 2 && base + 1 < EW_SLOTS) sl[base + 1] = (uint16_t)pb;
+      }
+    }
+  }
+  __syncthreads();
+  if (active && ul < nunits) wcnt[ul] = ucnt[lane];
 }
 
 // ===========================================================================
