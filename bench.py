@@ -494,6 +494,35 @@ def run_snapstream(a, dist, rank, world, local):
     assert stt_all == want, "verdict mismatch"
     nbad = sum(1 for x in want if x != L.OK)
     used_total = sum(sum((plens[fi] + 15) & ~15 for fi in bt) for bt in batches)
+    cpu = None
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        from oracle import oracle as O   # baseline only
+        base_addr = pool.data_ptr()
+        pick, acc = [], 0                 # a sample of the pool: the first files up to 2 GiB
+        for i in range(len(plens)):
+            if acc >= (2 << 30):
+                break
+            pick.append(i)
+            acc += plens[i]
+        so, sl = [poffs[i] for i in pick], [plens[i] for i in pick]
+        small = [i for i in pick if plens[i] <= (8 << 20)][:64]
+        views = [bytes(pv[poffs[i]:poffs[i] + plens[i]]) for i in small]
+        vb = sum(len(v) for v in views)
+
+        def one_pass():
+            for v in views:
+                O.loadsnap(v)
+        it, cs = timed_cpu(a.cpu_seconds, one_pass)
+        nth = cpu_threads()
+        it2, cs2 = timed_cpu(a.cpu_seconds / 2, lambda: O.fast_snap_verify_batch(base_addr, so, sl, nth))
+        cpu = dict(host_info(), **{
+            "value": round(vb * it / cs / 1e9, 4), "unit": "GB/s", "cores": 1, "kind": "port",
+            "sample": "oracle/ or_loadsnap (1 thread) over %d of the pool's files (<= 8 MiB each, %.2f GiB), %d "
+                      "passes, %.1f s -- host-resident bytes, no PCIe" % (len(views), vb / (1 << 30), it, cs),
+            "optimised": {"value": round(acc * it2 / cs2 / 1e9, 4), "unit": "GB/s", "cores": nth,
+                          "sample": "orf_snap_verify_batch on %d cores over the pool's first %d files (%.2f GiB, "
+                                    "pinned host memory), %d passes, %.1f s" % (nth, len(pick), acc / (1 << 30),
+                                                                              it2, cs2)}})
     out = ({
             "metric": METRIC, "value": round(world * sbytes / el / 1e9, 3), "unit": "GB/s", "n_gpus": world,
             "steps": 1, "warmup": 0, "ms_per_step": round(el * 1e3, 3), "higher_is_better": True,
@@ -516,7 +545,7 @@ def run_snapstream(a, dist, rank, world, local):
                          "pipeline_achieved": round(used_total / (sum(dms) / 1e3) / 1e9, 2),
                          "pipeline_frac": round(used_total / (sum(dms) / 1e3) / 1e9 / HBM_PEAK_GBPS, 4),
                          "note": "streamed value is PCIe-bound (host -> HBM); the roofline is the resident kernel"},
-            "cpu_baseline": None, "gen_seconds": round(gen_s, 2)})
+            "cpu_baseline": cpu, "gen_seconds": round(gen_s, 2)})
     ctx.close()
     return out
 
@@ -734,6 +763,21 @@ def run_msg(a, dist, rank, world, local):
     elapsed = timed(dist, a.steps, step)
     ms = elapsed / a.steps * 1e3
     dms = float(L.lib.ewal_last_device_ms(ctx.handle))
+    cpu = None
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        from oracle import oracle as O   # baseline only
+        addr = C.cast(C.c_char_p(blob), C.c_void_p).value
+        stc = O.fast_message_batch(addr, offs, lens, 1)
+        assert all(x == O.OK for x in stc)
+        it, cs = timed_cpu(a.cpu_seconds, lambda: O.fast_message_batch(addr, offs, lens, 1))
+        nth = cpu_threads()
+        it2, cs2 = timed_cpu(a.cpu_seconds / 2, lambda: O.fast_message_batch(addr, offs, lens, nth))
+        cpu = dict(host_info(), **{
+            "value": round(n * it / cs, 1), "unit": "messages/s", "cores": 1, "kind": "port",
+            "sample": "oracle/ or_message_unmarshal (the C restatement of raftpb.Message.Unmarshal, a fresh message "
+                      "per body) over all %d bodies, 1 thread, %d passes, %.1f s" % (n, it, cs),
+            "optimised": {"value": round(n * it2 / cs2, 1), "unit": "messages/s", "cores": nth,
+                          "sample": "the same per message on %d cores, %d passes, %.1f s" % (nth, it2, cs2)}})
     out = ({
             "metric": "raftpb.Message decode messages/s (SURVEY 8(f) rank 4); WAL verify GB/s is the headline",
             "value": round(world * n / (ms / 1e3), 1), "unit": "messages/s", "n_gpus": world, "steps": a.steps,
@@ -743,7 +787,7 @@ def run_msg(a, dist, rank, world, local):
                                    "results copied to the host each step" % (n, nb / 1e6, tot.value),
                        "parallelism": "dp%d" % world},
             "gbps": round(world * nb / (ms / 1e3) / 1e9, 3), "device_ms": round(dms, 4),
-            "cpu_baseline": None})
+            "cpu_baseline": cpu})
     dbuf.free()
     ctx.close()
     return out
@@ -997,16 +1041,21 @@ def main():
                 out["configs"] = {}
             for name in subs:
                 t0 = time.time()
-                if name == "c1":
-                    r = run_wal(a, dist, rank, world, local, cpu_seconds=a.sub_cpu_seconds, full=False, **c1)
-                else:
-                    r = SUBS[name](a, dist, rank, world, local, cpu_seconds=a.sub_cpu_seconds)
+                try:
+                    if name == "c1":
+                        r = run_wal(a, dist, rank, world, local, cpu_seconds=a.sub_cpu_seconds, full=False, **c1)
+                    else:
+                        r = SUBS[name](a, dist, rank, world, local, cpu_seconds=a.sub_cpu_seconds)
+                except Exception as ex:   # the headline line still prints; the failure is in it
+                    import traceback
+                    traceback.print_exc()
+                    r = {"error": "%s: %s" % (type(ex).__name__, ex), "ms_per_step": None}
                 r["wall_seconds"] = round(time.time() - t0, 2)
                 for key in ("higher_is_better", "scaling", "vs_baseline", "data", "n_gpus"):
                     r.pop(key, None)
                 out["configs"][name] = r
                 if rank == 0:
-                    print("bench: %s %.3f ms/step (%.1f s)" % (name, r["ms_per_step"], r["wall_seconds"]),
+                    print("bench: %s %s ms/step (%.1f s)" % (name, r["ms_per_step"], r["wall_seconds"]),
                           file=sys.stderr, flush=True)
     else:
         out = {"shards": run_shards, "snap": run_snap, "snapstream": run_snapstream, "commit": run_commit,

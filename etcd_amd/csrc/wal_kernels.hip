@@ -507,6 +507,7 @@ __global__ __launch_bounds__(EW_THREADS, 1) void k_stream(StreamArgs a) {
 // running count in LDS), so every unit's slots stay position-sorted.
 // ===========================================================================
 #define EW_CAND_WAVES 4
+#define EW_CAND_PF 4      // rounds of 64 flagged pieces whose loads are in flight together
 __device__ __forceinline__ void load_piece80(const uint8_t *buf, uint64_t B, uint64_t off, uint32_t (&D)[19]) {
   if (off + 80 <= B) {
     const uint4 *q = (const uint4 *)(buf + off);
@@ -550,42 +551,53 @@ __global__ __launch_bounds__(EW_CAND_WAVES * 64) void k_cand(const uint8_t *__re
     }
   }
   __syncthreads();
-  for (uint32_t r0 = 0; r0 < T; r0 += 64) {
-    const uint32_t i = r0 + (uint32_t)lane;
-    const bool live = i < T;
-    const uint32_t e = live ? list[i] : 0xffffu;
-    const uint32_t ulo = e >> 6, pcs = e & 63;
-    const uint64_t off = (uint64_t)(u0 + ulo) * EW_WAVE_BYTES + (uint64_t)pcs * EW_PIECE;
-    uint32_t D[19];
-    if (live) {
-      load_piece80(buf, B, off, D);
-    } else {
+  // up to EW_CAND_PF rounds of pieces in flight at once, then processed in order
+  for (uint32_t rb = 0; rb < T; rb += 64 * EW_CAND_PF) {
+    uint32_t D[EW_CAND_PF][19], E[EW_CAND_PF];
 #pragma unroll
-      for (int k = 0; k < 19; ++k) D[k] = 0u;
-    }
-    uint32_t pa = 0, pb = 0, cnt = 0;
-    if (live) {
-      const uint32_t fm = cand_filter(D);
-      if (fm) cnt = find_cands(D, fm, off, B, pcs * EW_PIECE, pa, pb);
-    }
-    // segmented exclusive scan of cnt over the round (a unit's pieces are contiguous)
-    const uint32_t incl = wave_incl_sum(cnt);
-    const uint32_t prev = (uint32_t)__shfl_up((int)e, 1);
-    const bool head = lane == 0 || (prev >> 6) != ulo;
-    const unsigned long long H = __ballot(head);
-    const int hl = 63 - __clzll((long long)(H & (lane == 63 ? ~0ull : ((2ull << lane) - 1ull))));
-    const uint32_t before = (uint32_t)__shfl((int)incl, hl > 0 ? hl - 1 : 0);
-    const uint32_t base = (live ? ucnt[ulo] : 0u) + (incl - cnt - (hl > 0 ? before : 0u));
-    const uint32_t nxt = (uint32_t)__shfl_down((int)e, 1);
-    const bool last = live && (lane == 63 || i + 1 >= T || (nxt >> 6) != ulo);
-    if (last) ucnt[ulo] = base + cnt;
-    if (cnt) {
-      uint16_t *sl = slots + (size_t)(u0 + ulo) * EW_SLOTS;
-      if (cnt > 2) {
-        slot_cands(D, off, B, base, sl, pcs * EW_PIECE);
+    for (int k = 0; k < EW_CAND_PF; ++k) {
+      const uint32_t i = rb + 64 * k + (uint32_t)lane;
+      E[k] = i < T ? list[i] : 0xffffu;
+      if (i < T) {
+        load_piece80(buf, B, (uint64_t)(u0 + (E[k] >> 6)) * EW_WAVE_BYTES + (uint64_t)(E[k] & 63) * EW_PIECE, D[k]);
       } else {
-        if (base < EW_SLOTS) sl[base] = (uint16_t)pa;
-        if (cnt >= 2 && base + 1 < EW_SLOTS) sl[base + 1] = (uint16_t)pb;
+#pragma unroll
+        for (int q = 0; q < 19; ++q) D[k][q] = 0u;
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < EW_CAND_PF; ++k) {
+      const uint32_t r0 = rb + 64 * k;
+      if (r0 >= T) break;   // wave-uniform
+      const uint32_t i = r0 + (uint32_t)lane;
+      const bool live = i < T;
+      const uint32_t e = E[k];
+      const uint32_t ulo = e >> 6, pcs = e & 63;
+      const uint64_t off = (uint64_t)(u0 + ulo) * EW_WAVE_BYTES + (uint64_t)pcs * EW_PIECE;
+      uint32_t pa = 0, pb = 0, cnt = 0;
+      if (live) {
+        const uint32_t fm = cand_filter(D[k]);
+        if (fm) cnt = find_cands(D[k], fm, off, B, pcs * EW_PIECE, pa, pb);
+      }
+      // segmented exclusive scan of cnt over the round (a unit's pieces are contiguous)
+      const uint32_t incl = wave_incl_sum(cnt);
+      const uint32_t prev = (uint32_t)__shfl_up((int)e, 1);
+      const bool head = lane == 0 || (prev >> 6) != ulo;
+      const unsigned long long H = __ballot(head);
+      const int hl = 63 - __clzll((long long)(H & (lane == 63 ? ~0ull : ((2ull << lane) - 1ull))));
+      const uint32_t before = (uint32_t)__shfl((int)incl, hl > 0 ? hl - 1 : 0);
+      const uint32_t base = (live ? ucnt[ulo] : 0u) + (incl - cnt - (hl > 0 ? before : 0u));
+      const uint32_t nxt = (uint32_t)__shfl_down((int)e, 1);
+      const bool last = live && (lane == 63 || i + 1 >= T || (nxt >> 6) != ulo);
+      if (last) ucnt[ulo] = base + cnt;
+      if (cnt) {
+        uint16_t *sl = slots + (size_t)(u0 + ulo) * EW_SLOTS;
+        if (cnt > 2) {
+          slot_cands(D[k], off, B, base, sl, pcs * EW_PIECE);
+        } else {
+          if (base < EW_SLOTS) sl[base] = (uint16_t)pa;
+          if (cnt >= 2 && base + 1 < EW_SLOTS) sl[base + 1] = (uint16_t)pb;
+        }
       }
     }
   }

@@ -510,7 +510,7 @@ def synth_wal(target_bytes, min_data=64, max_data=65536, seed=2, corrupt_record=
     rewind_per_mille: that share of the entries open a new leader's term that
     rewrites the last 1..8 indexes; last_index (a list) receives the last
     entry's Index."""
-    cap = target_bytes + max_data * 2 + (1 << 20)
+    cap = target_bytes + max_data * 2 + (1 << 20) + target_bytes // 128   # (term varints grow with rewinds)
     out = bytearray(cap)
     nrec = C.c_int64(0)
     li = C.c_uint64(0)

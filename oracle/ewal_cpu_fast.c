@@ -507,3 +507,35 @@ int orf_restart_file(const char *path, uint64_t ri, int nthreads, int faithful, 
   *total_ms = ms_now() - t0;
   return status;
 }
+
+
+/* ---- raftpb.Message.Unmarshal over a batch (the msg bench's cpu_baseline):
+ * or_message_unmarshal + or_message_free per message, like Go's Unmarshal
+ * into a fresh Message per POST /raft; messages strided over nthreads. */
+typedef struct {
+  const uint8_t *buf;
+  const uint64_t *offs, *lens;
+  int64_t n;
+  int t, nt;
+  int32_t *status;
+} msg_job;
+static void *msg_worker(void *arg) {
+  msg_job *j = (msg_job *)arg;
+  for (int64_t i = j->t; i < j->n; i += j->nt) {
+    or_message m;
+    j->status[i] = or_message_unmarshal(j->buf + j->offs[i], (int64_t)j->lens[i], &m);
+    or_message_free(&m);
+  }
+  return NULL;
+}
+void orf_message_batch(const uint8_t *buf, const uint64_t *offs, const uint64_t *lens, int64_t n, int nthreads,
+                       int32_t *status) {
+  if (nthreads < 1) nthreads = 1;
+  if (nthreads > 256) nthreads = 256;
+  msg_job jobs[256];
+  pthread_t th[256];
+  for (int t = 0; t < nthreads; t++) jobs[t] = (msg_job){buf, offs, lens, n, t, nthreads, status};
+  for (int t = 1; t < nthreads; t++) pthread_create(&th[t], NULL, msg_worker, &jobs[t]);
+  msg_worker(&jobs[0]);
+  for (int t = 1; t < nthreads; t++) pthread_join(th[t], NULL);
+}

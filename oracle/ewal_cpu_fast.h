@@ -55,6 +55,10 @@ void orf_maybe_commit_batch(uint64_t G, const uint64_t *match, const uint8_t *nv
 int orf_restart_file(const char *path, uint64_t ri, int nthreads, int faithful, int64_t *frames, double *read_ms,
                      double *total_ms);
 
+/* raftpb.Message.Unmarshal (or_message_unmarshal) over n messages, strided over nthreads */
+void orf_message_batch(const uint8_t *buf, const uint64_t *offs, const uint64_t *lens, int64_t n, int nthreads,
+                       int32_t *status);
+
 #ifdef __cplusplus
 }
 #endif

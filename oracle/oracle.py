@@ -306,6 +306,14 @@ def restart_file(path, ri, nthreads, faithful):
     return st, fr.value, rm.value, tm.value
 
 
+def fast_message_batch(buf_addr, offs, lens, nthreads):
+    """orf_message_batch: the status of every message's Unmarshal."""
+    n = len(offs)
+    st = (C.c_int32 * max(n, 1))()
+    lib.orf_message_batch(C.c_void_p(buf_addr), _u64arr(offs), _u64arr(lens), n, nthreads, st)
+    return list(st[:n])
+
+
 def _u64arr(x):
     return (C.c_uint64 * max(len(x), 1))(*x)
 
