@@ -64,7 +64,14 @@ class MessageDesc(C.Structure):   # emsg_message
                 ("commit", C.c_uint64), ("ents_first", C.c_uint64), ("n_ents", C.c_uint64),
                 ("snap_index", C.c_uint64), ("snap_term", C.c_uint64), ("snap_data_off", C.c_int64),
                 ("snap_data_len", C.c_int64), ("snap_n_nodes", C.c_uint64), ("snap_n_removed", C.c_uint64),
-                ("unrec_len", C.c_int64)]
+                ("unrec_len", C.c_int64), ("segs_first", C.c_uint64), ("n_segs", C.c_uint64)]
+
+
+class SegmentDesc(C.Structure):   # emsg_segment
+    _fields_ = [("kind", C.c_int32), ("pad", C.c_int32), ("ent", C.c_int64), ("off", C.c_uint64), ("len", C.c_uint64)]
+
+
+SEG_UNREC, SEG_ENTRY_UNREC, SEG_ENTRY_DATA, SEG_SNAP_UNREC, SEG_SNAP_DATA, SEG_SNAP_NODE, SEG_SNAP_REMOVED = range(7)
 
 
 class Result(C.Structure):
@@ -139,6 +146,7 @@ _SIGS = {
     "emsg_decode_batch_device": (C.c_int, [vp, vp, C.c_uint64, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64),
                                            C.c_uint32, C.POINTER(MessageDesc), C.POINTER(C.c_uint64)]),
     "emsg_copy_entries": (C.c_int64, [vp, C.c_uint64, C.POINTER(EntryDesc), C.c_int64]),
+    "emsg_copy_segments": (C.c_int64, [vp, C.c_uint64, C.POINTER(SegmentDesc), C.c_int64]),
     "ewal_batch_copy_entries": (C.c_int64, [vp, C.c_uint64, C.POINTER(EntryDesc), C.c_int64]),
     "ewal_copy_records": (C.c_int64, [vp, C.POINTER(RecordDesc), C.c_int64]),
     "ewal_batch_copy_unrec": (C.c_int64, [vp, C.c_uint64, C.POINTER(UnrecDesc), C.c_int64]),

@@ -128,8 +128,8 @@ struct ewal_ctx {
   // batched ReadAll (ewal_readall_batch_device): shard tables, results, ents
   DevBuf bfs, bsoff, bri, bsagg, bres, bef, bents, bshard, hmask;
   // batched raftpb.Message decode (emsg_decode_batch_device)
-  DevBuf moff, mlen, mcnt, mfirst, mout, ments;
-  uint64_t mtotal = 0;
+  DevBuf moff, mlen, mcnt, mfirst, mout, ments, mscnt, msfirst, msegs;
+  uint64_t mtotal = 0, mstotal = 0;
   std::vector<uint64_t> bent_first, bnents;   // per shard: first ent in bents, count
   std::vector<std::vector<ewal_unrec>> bunrec;       // per shard replayed alone: its XXX_unrecognized side list
   std::vector<std::vector<uint8_t>> bunrec_bytes;
@@ -1987,35 +1987,56 @@ int emsg_decode_batch_device(ewal_ctx *c, const void *d_buf, uint64_t buf_len, c
   EW_CHECK(c->mlen.ensure((size_t)n * 8));
   EW_CHECK(c->mcnt.ensure((size_t)n * 8));
   EW_CHECK(c->mfirst.ensure((size_t)n * 8));
+  EW_CHECK(c->mscnt.ensure((size_t)n * 8));
+  EW_CHECK(c->msfirst.ensure((size_t)n * 8));
   EW_CHECK(c->mout.ensure((size_t)n * sizeof(emsg_message)));
   EW_CHECK(hipMemcpyAsync(c->moff.p, offs, (size_t)n * 8, hipMemcpyHostToDevice, c->stream));
   EW_CHECK(hipMemcpyAsync(c->mlen.p, lens, (size_t)n * 8, hipMemcpyHostToDevice, c->stream));
   EW_CHECK(hipEventRecord(c->ev0, c->stream));
   const uint8_t *b = (const uint8_t *)d_buf;
   unsigned long long *cnt = c->mcnt.as<unsigned long long>(), *first = c->mfirst.as<unsigned long long>();
+  unsigned long long *scnt = c->mscnt.as<unsigned long long>(), *sfirst = c->msfirst.as<unsigned long long>();
   hipLaunchKernelGGL(k_msg<false>, dim3(grid_for(n, 256)), dim3(256), 0, c->stream, b, c->moff.as<uint64_t>(),
-                     c->mlen.as<uint64_t>(), n, cnt, (const unsigned long long *)nullptr, (emsg_message *)nullptr,
-                     (ewal_entry *)nullptr);
+                     c->mlen.as<uint64_t>(), n, cnt, (const unsigned long long *)nullptr, scnt,
+                     (const unsigned long long *)nullptr, (emsg_message *)nullptr, (ewal_entry *)nullptr,
+                     (emsg_segment *)nullptr);
   size_t bytes = 0;
   EW_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, cnt, first, (int)n, c->stream));
   EW_CHECK(c->tmp.ensure(bytes));
   EW_CHECK(hipcub::DeviceScan::ExclusiveSum(c->tmp.p, bytes, cnt, first, (int)n, c->stream));
-  unsigned long long tail[2];
+  EW_CHECK(hipcub::DeviceScan::ExclusiveSum(c->tmp.p, bytes, scnt, sfirst, (int)n, c->stream));
+  unsigned long long tail[4];
   EW_CHECK(hipMemcpyAsync(&tail[0], first + (n - 1), 8, hipMemcpyDeviceToHost, c->stream));
   EW_CHECK(hipMemcpyAsync(&tail[1], cnt + (n - 1), 8, hipMemcpyDeviceToHost, c->stream));
+  EW_CHECK(hipMemcpyAsync(&tail[2], sfirst + (n - 1), 8, hipMemcpyDeviceToHost, c->stream));
+  EW_CHECK(hipMemcpyAsync(&tail[3], scnt + (n - 1), 8, hipMemcpyDeviceToHost, c->stream));
   EW_CHECK(hipStreamSynchronize(c->stream));
-  const uint64_t total = tail[0] + tail[1];
+  const uint64_t total = tail[0] + tail[1], stotal = tail[2] + tail[3];
   EW_CHECK(c->ments.ensure((size_t)std::max<uint64_t>(total, 1) * sizeof(ewal_entry)));
+  EW_CHECK(c->msegs.ensure((size_t)std::max<uint64_t>(stotal, 1) * sizeof(emsg_segment)));
   hipLaunchKernelGGL(k_msg<true>, dim3(grid_for(n, 256)), dim3(256), 0, c->stream, b, c->moff.as<uint64_t>(),
-                     c->mlen.as<uint64_t>(), n, cnt, (const unsigned long long *)first, c->mout.as<emsg_message>(),
-                     c->ments.as<ewal_entry>());
+                     c->mlen.as<uint64_t>(), n, cnt, (const unsigned long long *)first, scnt,
+                     (const unsigned long long *)sfirst, c->mout.as<emsg_message>(), c->ments.as<ewal_entry>(),
+                     c->msegs.as<emsg_segment>());
   EW_CHECK(hipGetLastError());
   EW_CHECK(hipEventRecord(c->ev1, c->stream));
   EW_CHECK(hipMemcpyAsync(out, c->mout.p, (size_t)n * sizeof(emsg_message), hipMemcpyDeviceToHost, c->stream));
   EW_CHECK(hipStreamSynchronize(c->stream));
   c->mtotal = total;
+  c->mstotal = stotal;
   if (n_entries) *n_entries = total;
   return EWAL_OK;
+}
+
+int64_t emsg_copy_segments(ewal_ctx *c, uint64_t first, emsg_segment *out, int64_t cap) {
+  if (!c || (!out && cap) || first > c->mstotal) return EWAL_E_INVAL;
+  const int64_t n = std::min<int64_t>(cap, (int64_t)(c->mstotal - first));
+  if (n > 0) {
+    EW_CHECK(hipMemcpyAsync(out, c->msegs.as<emsg_segment>() + first, (size_t)n * sizeof(emsg_segment),
+                            hipMemcpyDeviceToHost, c->stream));
+    EW_CHECK(hipStreamSynchronize(c->stream));
+  }
+  return n;
 }
 
 int64_t emsg_copy_entries(ewal_ctx *c, uint64_t first, ewal_entry *out, int64_t cap) {

@@ -39,8 +39,18 @@ def message_marshal(type_=0, to=0, from_=0, term=0, log_term=0, index=0, entries
     return b"".join(parts)
 
 
+def _fetch(copy, handle, desc, total):
+    arr = (desc * max(total, 1))()
+    if total:
+        k = copy(handle, 0, arr, total)
+        check(0 if k >= 0 else int(k))
+    return arr
+
+
 def decode_messages(ctx, bodies):
-    """Decode message bodies (bytes each): one dict per body."""
+    """Decode message bodies (bytes each): one dict per body, with every
+    XXX_unrecognized, split bytes field and the Snapshot's Nodes /
+    RemovedNodes assembled from the message's segments (include/ewal.h)."""
     n = len(bodies)
     if n == 0:
         return []
@@ -57,20 +67,37 @@ def decode_messages(ctx, bodies):
         tot = C.c_uint64(0)
         check(lib.emsg_decode_batch_device(ctx.handle, d.ptr, len(blob), (C.c_uint64 * n)(*offs),
                                            (C.c_uint64 * n)(*[len(b) for b in bodies]), n, out, C.byref(tot)))
-        ents = (L.EntryDesc * max(tot.value, 1))()
-        if tot.value:
-            k = lib.emsg_copy_entries(ctx.handle, 0, ents, tot.value)
-            check(0 if k >= 0 else int(k))
+        ents = _fetch(lib.emsg_copy_entries, ctx.handle, L.EntryDesc, tot.value)
+        nseg = out[n - 1].segs_first + out[n - 1].n_segs
+        segs = _fetch(lib.emsg_copy_segments, ctx.handle, L.SegmentDesc, nseg)
     finally:
         d.free()
     res = []
     for m in out:
-        es = [dict(type=e.type, term=e.term, index=e.index,
-                   data=None if e.data_nil else blob[e.data_off:e.data_off + e.data_len])
-              for e in ents[m.ents_first:m.ents_first + m.n_ents]]
-        sd = None if m.snap_data_off < 0 else blob[m.snap_data_off:m.snap_data_off + m.snap_data_len]
+        bykind = {}
+        for g in segs[m.segs_first:m.segs_first + m.n_segs]:
+            bykind.setdefault((g.kind, g.ent), []).append(g)
+
+        def cat(kind, ent=-1):
+            gs = bykind.get((kind, ent))
+            return b"".join(blob[g.off:g.off + g.len] for g in gs) if gs else None
+
+        es = []
+        for j, e in enumerate(ents[m.ents_first:m.ents_first + m.n_ents]):
+            ei = j   # segments name the entry by its index within the message
+            data = (cat(L.SEG_ENTRY_DATA, ei) if e.data_nil == 2 else
+                    None if e.data_nil else blob[e.data_off:e.data_off + e.data_len])
+            ur = cat(L.SEG_ENTRY_UNREC, ei)
+            es.append(dict(type=e.type, term=e.term, index=e.index, data=data, unrec=ur,
+                           unrec_len=len(ur) if ur else 0))
+        sd = (cat(L.SEG_SNAP_DATA) if m.snap_data_off == -2 else
+              None if m.snap_data_off < 0 else blob[m.snap_data_off:m.snap_data_off + m.snap_data_len])
+        su = cat(L.SEG_SNAP_UNREC)
         res.append(dict(status=m.status, type=m.type, to=m.to, from_=m.from_, term=m.term, log_term=m.log_term,
                         index=m.index, commit=m.commit, reject=bool(m.reject), ents=es, unrec_len=m.unrec_len,
+                        unrec=cat(L.SEG_UNREC),
                         snap=dict(data=sd, index=m.snap_index, term=m.snap_term, n_nodes=m.snap_n_nodes,
-                                  n_removed=m.snap_n_removed)))
+                                  n_removed=m.snap_n_removed, unrec=su, unrec_len=len(su) if su else 0,
+                                  nodes=[g.off for g in bykind.get((L.SEG_SNAP_NODE, -1), [])],
+                                  removed=[g.off for g in bykind.get((L.SEG_SNAP_REMOVED, -1), [])])))
     return res

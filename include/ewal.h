@@ -380,25 +380,55 @@ int ecommit_batch_device(ewal_ctx *ctx, uint64_t G, const uint64_t *match, const
  * (called per POST /raft in etcdserver/etcdhttp/http.go:119-146), batched
  * over n messages resident in one device buffer at offs[i], lens[i] (host
  * arrays).  status = EWAL_OK / EWAL_ERR_UNEXPECTED_EOF / EWAL_ERR_WRONG_TYPE /
- * EWAL_PANIC_BOUNDS / EWAL_NONTERMINATING as Unmarshal returns or panics, or
- * EWAL_UNSUPPORTED_ENCODING when the message would carry unrecognized
- * fields / a split bytes field this layout does not return.  The fields hold
- * what Go leaves in the struct (partial on error).  Entries go to a ctx-owned
- * array: message i's are [ents_first, ents_first + n_ents), fetched with
- * emsg_copy_entries (Data offsets are offsets into d_buf). */
+ * EWAL_PANIC_BOUNDS / EWAL_NONTERMINATING as Unmarshal returns or panics
+ * (EWAL_UNSUPPORTED_ENCODING only for protobuf groups nested deeper than the
+ * device walker's stack).  The fields hold what Go leaves in the struct
+ * (partial on error).  Entries go to a ctx-owned array: message i's are
+ * [ents_first, ents_first + n_ents), fetched with emsg_copy_entries (Data
+ * offsets are offsets into d_buf; data_nil == 2: Data is the concatenation
+ * of that entry's EMSG_SEG_ENTRY_DATA segments).  The byte values Go builds
+ * by append and the Snapshot's repeated fields are message i's segments
+ * [segs_first, segs_first + n_segs) (emsg_copy_segments), in order:
+ *   EMSG_SEG_UNREC         Message.XXX_unrecognized  (raft.pb.go:612-616)
+ *   EMSG_SEG_ENTRY_UNREC   Entries[ent].XXX_unrecognized
+ *   EMSG_SEG_ENTRY_DATA    Entries[ent].Data, repeated non-empty segments
+ *   EMSG_SEG_SNAP_UNREC    Snapshot.XXX_unrecognized
+ *   EMSG_SEG_SNAP_DATA     Snapshot.Data's segments (used when
+ *                          snap_data_off == -2: a split field)
+ *   EMSG_SEG_SNAP_NODE     one Snapshot.Nodes value (in off)
+ *   EMSG_SEG_SNAP_REMOVED  one Snapshot.RemovedNodes value (in off)
+ * a byte value is the concatenation of its kind's [off, off + len) ranges of
+ * d_buf (none: nil). */
 typedef struct emsg_message {
   int32_t status;
   int32_t reject;
   uint64_t type, to, from, term, log_term, index, commit;
   uint64_t ents_first, n_ents;
   uint64_t snap_index, snap_term;
-  int64_t snap_data_off, snap_data_len;   /* Snapshot.Data in d_buf; off -1 == nil */
+  int64_t snap_data_off, snap_data_len;   /* Snapshot.Data in d_buf; off -1 == nil, -2: split (segments) */
   uint64_t snap_n_nodes, snap_n_removed;
   int64_t unrec_len;                       /* len(XXX_unrecognized) */
+  uint64_t segs_first, n_segs;
 } emsg_message;
+enum {
+  EMSG_SEG_UNREC = 0,
+  EMSG_SEG_ENTRY_UNREC = 1,
+  EMSG_SEG_ENTRY_DATA = 2,
+  EMSG_SEG_SNAP_UNREC = 3,
+  EMSG_SEG_SNAP_DATA = 4,
+  EMSG_SEG_SNAP_NODE = 5,
+  EMSG_SEG_SNAP_REMOVED = 6
+};
+typedef struct emsg_segment {
+  int32_t kind;            /* EMSG_SEG_* */
+  int32_t pad;
+  int64_t ent;             /* the entry, counted within its message (EMSG_SEG_ENTRY_*), else -1 */
+  uint64_t off, len;       /* a range of d_buf, or (value, 0) */
+} emsg_segment;
 int emsg_decode_batch_device(ewal_ctx *ctx, const void *d_buf, uint64_t buf_len, const uint64_t *offs,
                              const uint64_t *lens, uint32_t n, emsg_message *out, uint64_t *n_entries);
 int64_t emsg_copy_entries(ewal_ctx *ctx, uint64_t first, ewal_entry *out, int64_t cap);
+int64_t emsg_copy_segments(ewal_ctx *ctx, uint64_t first, emsg_segment *out, int64_t cap);
 
 #ifdef __cplusplus
 }

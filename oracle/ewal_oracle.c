@@ -275,7 +275,7 @@ int or_snapshot_unmarshal(const uint8_t *d, int64_t l, or_snapshot *m) {
   fspec fs[5] = {{1, F_BYTES, &m->data, &m->data_len}, {2, F_U64REP, &m->nodes, &m->n_nodes},
                  {3, F_U64, &m->index, 0}, {4, F_U64, &m->term, 0},
                  {5, F_U64REP, &m->removed, &m->n_removed}};
-  return pb_unmarshal(d, l, fs, 5, &m->unrec_len, NULL);
+  return pb_unmarshal(d, l, fs, 5, &m->unrec_len, &m->unrec);
 }
 int or_snappb_unmarshal(const uint8_t *d, int64_t l, or_snappb *m) {
   fspec fs[2] = {{1, F_U32, &m->crc, 0}, {2, F_BYTES, &m->data, &m->data_len}};
@@ -356,12 +356,13 @@ int or_message_unmarshal(const uint8_t *d, int64_t l, or_message *m) {
     if (hi > l) return OR_ERR_UNEXPECTED_EOF;
     if (hi < index) return OR_PANIC_BOUNDS;
     if (skippy == 0) return OR_NONTERMINATING;
-    m->unrec_len += skippy;
+    bytes_append(&m->unrec, &m->unrec_len, d + index, skippy);   /* m.XXX_unrecognized = append(...) */
     index = hi;
   }
   return OR_OK;
 }
 void or_message_free(or_message *m) {
+  free(m->unrec);
   for (int64_t i = 0; i < m->n_ents; i++) or_entry_free(&m->ents[i]);
   free(m->ents);
   or_snapshot_free(&m->snap);
@@ -371,7 +372,10 @@ void or_message_free(or_message *m) {
 void or_record_free(or_record *m) { free(m->data); memset(m, 0, sizeof(*m)); }
 void or_entry_free(or_entry *m) { free(m->data); free(m->unrec); memset(m, 0, sizeof(*m)); }
 void or_hardstate_free(or_hardstate *m) { free(m->unrec); memset(m, 0, sizeof(*m)); }
-void or_snapshot_free(or_snapshot *m) { free(m->data); free(m->nodes); free(m->removed); memset(m, 0, sizeof(*m)); }
+void or_snapshot_free(or_snapshot *m) {
+  free(m->data); free(m->nodes); free(m->removed); free(m->unrec);
+  memset(m, 0, sizeof(*m));
+}
 void or_snappb_free(or_snappb *m) { free(m->data); memset(m, 0, sizeof(*m)); }
 
 /* ===================================================================== */

@@ -89,6 +89,7 @@ typedef struct {
   uint64_t index, term;
   uint64_t *removed; int64_t n_removed;
   int64_t unrec_len;
+  uint8_t *unrec;     /* XXX_unrecognized (NULL == nil) */
 } or_snapshot;
 
 typedef struct {
@@ -104,6 +105,7 @@ typedef struct {
   or_entry *ents; int64_t n_ents;
   or_snapshot snap;
   int64_t unrec_len;
+  uint8_t *unrec;     /* XXX_unrecognized (NULL == nil) */
 } or_message;
 
 /* Unmarshal: return OR_OK, OR_ERR_UNEXPECTED_EOF, OR_ERR_WRONG_TYPE,

@@ -51,7 +51,7 @@ class HardState(C.Structure):
 class Snapshot(C.Structure):
     _fields_ = [("data", u8p), ("data_len", C.c_int64), ("nodes", C.POINTER(C.c_uint64)), ("n_nodes", C.c_int64),
                 ("index", C.c_uint64), ("term", C.c_uint64), ("removed", C.POINTER(C.c_uint64)),
-                ("n_removed", C.c_int64), ("unrec_len", C.c_int64)]
+                ("n_removed", C.c_int64), ("unrec_len", C.c_int64), ("unrec", u8p)]
 
 
 class ReadAllResult(C.Structure):
@@ -422,7 +422,8 @@ def maybe_commit_batch(G, match, nvoters, term, committed, log_offset, log_ptr, 
 class Message(C.Structure):
     _fields_ = [("type", C.c_uint64), ("to", C.c_uint64), ("from_", C.c_uint64), ("term", C.c_uint64),
                 ("log_term", C.c_uint64), ("index", C.c_uint64), ("commit", C.c_uint64), ("reject", C.c_int),
-                ("ents", C.POINTER(Entry)), ("n_ents", C.c_int64), ("snap", Snapshot), ("unrec_len", C.c_int64)]
+                ("ents", C.POINTER(Entry)), ("n_ents", C.c_int64), ("snap", Snapshot), ("unrec_len", C.c_int64),
+                ("unrec", u8p)]
 
 
 lib.or_message_unmarshal.argtypes = [C.c_char_p, C.c_int64, C.POINTER(Message)]
@@ -449,13 +450,16 @@ def message_marshal(type_=0, to=0, from_=0, term=0, log_term=0, index=0, entries
 def message_unmarshal(b):
     m = Message()
     st = lib.or_message_unmarshal(b, len(b), C.byref(m))
-    ents = [dict(type=e.type, term=e.term, index=e.index, data=_bytes(e.data, e.data_len), unrec_len=e.unrec_len)
-            for e in m.ents[:m.n_ents]]
+    ents = [dict(type=e.type, term=e.term, index=e.index, data=_bytes(e.data, e.data_len), unrec_len=e.unrec_len,
+                 unrec=_bytes(e.unrec, e.unrec_len)) for e in m.ents[:m.n_ents]]
     s = m.snap
     out = dict(status=st, type=m.type, to=m.to, from_=m.from_, term=m.term, log_term=m.log_term, index=m.index,
                commit=m.commit, reject=bool(m.reject), ents=ents, unrec_len=m.unrec_len,
+               unrec=_bytes(m.unrec, m.unrec_len),
                snap=dict(data=_bytes(s.data, s.data_len), index=s.index, term=s.term, n_nodes=s.n_nodes,
-                         n_removed=s.n_removed, unrec_len=s.unrec_len))
+                         n_removed=s.n_removed, unrec_len=s.unrec_len, unrec=_bytes(s.unrec, s.unrec_len),
+                         nodes=[s.nodes[i] for i in range(s.n_nodes)],
+                         removed=[s.removed[i] for i in range(s.n_removed)]))
     lib.or_message_free(C.byref(m))
     return out
 

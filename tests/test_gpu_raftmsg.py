@@ -31,16 +31,12 @@ def _check(ctx, bodies):
     got = M.decode_messages(ctx, bodies)
     for b, g in zip(bodies, got):
         o = O.message_unmarshal(bytes(b))
-        if g["status"] == L.UNSUPPORTED_ENCODING:
-            assert o["status"] == O.OK and (o["unrec_len"] or any(e["unrec_len"] for e in o["ents"])
-                                            or o["snap"]["unrec_len"]), o
-            continue
         assert g["status"] == o["status"], (g["status"], o["status"], bytes(b).hex())
-        for k in ("type", "to", "from_", "term", "log_term", "index", "commit", "reject"):
+        for k in ("type", "to", "from_", "term", "log_term", "index", "commit", "reject", "unrec", "unrec_len"):
             assert g[k] == o[k], k
-        assert [(e["type"], e["term"], e["index"], e["data"]) for e in g["ents"]] == \
-            [(e["type"], e["term"], e["index"], e["data"]) for e in o["ents"]]
-        for k in ("data", "index", "term", "n_nodes", "n_removed"):
+        assert [(e["type"], e["term"], e["index"], e["data"], e["unrec"]) for e in g["ents"]] == \
+            [(e["type"], e["term"], e["index"], e["data"], e["unrec"]) for e in o["ents"]]
+        for k in ("data", "index", "term", "n_nodes", "n_removed", "unrec", "nodes", "removed"):
             assert g["snap"][k] == o["snap"][k], k
     return got
 
@@ -82,7 +78,7 @@ def test_message_quirks(ctx):
     # repeated Snapshot fields accumulate into one struct
     m3 = O.message_marshal(0, 0, 0, 0, 0, 0, [], 0, O.snapshot_marshal(b"", [1], 5, 0), False) + \
         bytes([0x4a, 0x02, 0x20, 0x07])
-    # unknown message field -> XXX_unrecognized (reported as unsupported)
+    # unknown message field -> XXX_unrecognized
     m4 = O.message_marshal(1, 1, 1, 1, 1, 1, [], 1, b"", False) + bytes([0x60, 0x05])
     # wrong wire type / empty body
     m5 = bytes([0x0a, 0x00])
@@ -90,5 +86,66 @@ def test_message_quirks(ctx):
     assert got[0]["status"] == L.OK and len(got[0]["ents"]) == 2
     assert got[1]["reject"] is False
     assert got[2]["snap"]["index"] == 5 and got[2]["snap"]["term"] == 7
-    assert got[3]["status"] == L.UNSUPPORTED_ENCODING
+    assert got[3]["status"] == L.OK and got[3]["unrec"] == bytes([0x60, 0x05])
     assert got[4]["status"] == L.ERR_WRONG_TYPE and got[5]["status"] == L.OK
+
+
+def test_message_residual_encodings(ctx):
+    """Values Go assembles by append: every XXX_unrecognized, Entry.Data and
+    Snapshot.Data repeated with several non-empty segments, Nodes /
+    RemovedNodes over repeated Snapshot fields and packed-free repeats."""
+    unk = bytes([0x78, 0x2a]) + bytes([0x82, 0x01, 0x03]) + b"abc"       # fields 15 (varint), 16 (bytes)
+    e_split = O.entry_marshal(0, 3, 7, b"head") + bytes([0x22, 0x04]) + b"tail" + unk
+    e_empty_rep = O.entry_marshal(1, 3, 8, b"x") + bytes([0x22, 0x00])  # an empty repeat keeps the value
+    snap = O.snapshot_marshal(b"part1", [4, 5], 9, 2) + bytes([0x0a, 0x05]) + b"part2" + unk
+    snap2 = bytes([0x28, 0x0b, 0x10, 0x06, 0x0a, 0x00]) + unk           # RemovedNodes, another node, empty Data
+    m = O.message_marshal(3, 1, 2, 4, 5, 6, [e_split, e_empty_rep], 7, snap, True) + \
+        bytes([0x4a, len(snap2)]) + snap2 + unk + bytes([0x3a, len(e_split)]) + e_split
+    many = O.snapshot_marshal(b"d", list(range(1, 200)), 1, 1)          # > 64 nodes
+    m2 = O.message_marshal(1, 1, 1, 1, 1, 1, [], 1, many, False)
+    got = _check(ctx, [m, m2])
+    assert all(g["status"] == L.OK for g in got)
+    g = got[0]
+    assert g["ents"][0]["data"] == b"headtail" and g["ents"][0]["unrec"] == unk
+    assert g["snap"]["data"] == b"part1part2" and g["snap"]["nodes"] == [4, 5, 6] and g["snap"]["removed"] == [11]
+    assert g["unrec"] == unk and len(g["ents"]) == 3
+    assert got[1]["snap"]["nodes"] == list(range(1, 200))
+
+
+def test_message_residual_random(ctx):
+    """Random bodies with unknown fields spliced in at field boundaries of
+    the Message, its Entries and its Snapshot, and bytes fields repeated."""
+    rng = random.Random(43)
+
+    def unk():
+        f = rng.choice([11, 12, 15, 100, 1000])
+        wt = rng.choice([0, 1, 2, 5])
+        tag = M._varint((f << 3) | wt)
+        if wt == 0:
+            return tag + M._varint(rng.randrange(1 << 40))
+        if wt == 1:
+            return tag + bytes(rng.getrandbits(8) for _ in range(8))
+        if wt == 5:
+            return tag + bytes(rng.getrandbits(8) for _ in range(4))
+        d = bytes(rng.getrandbits(8) for _ in range(rng.randrange(0, 20)))
+        return tag + M._varint(len(d)) + d
+
+    bodies = []
+    for _ in range(300):
+        ents = []
+        for _ in range(rng.choice([0, 1, 3])):
+            e = O.entry_marshal(0, rng.randrange(1 << 20), rng.randrange(1 << 20), b"a" * rng.randrange(0, 5))
+            while rng.random() < 0.4:
+                e += rng.choice([unk(), b"\x22" + M._varint(3) + b"xyz"])
+            ents.append(e)
+        sn = O.snapshot_marshal(b"s" * rng.randrange(0, 4), [rng.randrange(1, 99) for _ in range(rng.randrange(3))],
+                                rng.randrange(99), rng.randrange(9))
+        while rng.random() < 0.4:
+            sn += rng.choice([unk(), b"\x0a\x02zz", b"\x10" + M._varint(rng.randrange(1, 1 << 30)),
+                              b"\x28" + M._varint(rng.randrange(1, 1 << 30))])
+        b = O.message_marshal(rng.randrange(16), 1, 2, 3, 4, 5, ents, 6, sn, False)
+        while rng.random() < 0.5:
+            b += unk()
+        bodies.append(b)
+    got = _check(ctx, bodies)
+    assert all(g["status"] == L.OK for g in got)
