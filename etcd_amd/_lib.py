@@ -71,6 +71,7 @@ class SegmentDesc(C.Structure):   # emsg_segment
     _fields_ = [("kind", C.c_int32), ("pad", C.c_int32), ("ent", C.c_int64), ("off", C.c_uint64), ("len", C.c_uint64)]
 
 
+SNAP_FIELD_DATA, SNAP_FIELD_UNREC, SNAP_FIELD_NODES, SNAP_FIELD_REMOVED = range(4)
 SEG_UNREC, SEG_ENTRY_UNREC, SEG_ENTRY_DATA, SEG_SNAP_UNREC, SEG_SNAP_DATA, SEG_SNAP_NODE, SEG_SNAP_REMOVED = range(7)
 
 
@@ -147,6 +148,7 @@ _SIGS = {
                                            C.c_uint32, C.POINTER(MessageDesc), C.POINTER(C.c_uint64)]),
     "emsg_copy_entries": (C.c_int64, [vp, C.c_uint64, C.POINTER(EntryDesc), C.c_int64]),
     "emsg_copy_segments": (C.c_int64, [vp, C.c_uint64, C.POINTER(SegmentDesc), C.c_int64]),
+    "esnap_copy_field": (C.c_int64, [vp, C.c_uint32, C.c_int32, vp, C.c_int64]),
     "ewal_batch_copy_entries": (C.c_int64, [vp, C.c_uint64, C.POINTER(EntryDesc), C.c_int64]),
     "ewal_copy_records": (C.c_int64, [vp, C.POINTER(RecordDesc), C.c_int64]),
     "ewal_batch_copy_unrec": (C.c_int64, [vp, C.c_uint64, C.POINTER(UnrecDesc), C.c_int64]),

@@ -48,7 +48,7 @@ __global__ __launch_bounds__(256) void k_snap(const uint8_t *__restrict__ buf, c
     if (d.computed != d.stored) {
       st = EWAL_ERR_SNAP_CRC;
     } else if (a2.split) {
-      st = EWAL_UNSUPPORTED_ENCODING;   // raftpb.Snapshot over the concatenation: not decoded here
+      d.resid = 2;   // raftpb.Snapshot over the concatenation: gathered, then k_snap_resid
     } else {
       PbField s1, s2, s3, s4, s5;
       pbf_init(s1); pbf_init(s2); pbf_init(s3); pbf_init(s4); pbf_init(s5);
@@ -57,9 +57,9 @@ __global__ __launch_bounds__(256) void k_snap(const uint8_t *__restrict__ buf, c
       int st2 = d.dlen ? pb_walk<PB_BYTES, PB_REP64, PB_VAR64, PB_VAR64, PB_REP64>(
                              buf + d.doff, (int64_t)d.dlen, s1, s2, s3, s4, s5, ur, o->nodes, o->removed, 64)
                        : 0;
-      // Snapshot.XXX_unrecognized is returned; Data in several segments / more
-      // Nodes or RemovedNodes than esnap_snapshot holds: not decoded here
-      if (st2 == 0 && (ur || s1.split || s2.split || s5.split)) st2 = EWAL_UNSUPPORTED_ENCODING;
+      // Snapshot.XXX_unrecognized, Data in several segments, more Nodes or
+      // RemovedNodes than esnap_snapshot holds: k_snap_resid lists them
+      if (st2 == 0 && (ur || s1.split || s2.split || s5.split)) d.resid = 1;
       st = st2;
       o->index = s3.v;
       o->term = s4.v;
@@ -69,6 +69,92 @@ __global__ __launch_bounds__(256) void k_snap(const uint8_t *__restrict__ buf, c
       o->n_removed = (int64_t)s5.v;
     }
   }
+  d.st = st;
+  sd[f] = d;
+}
+
+// ---- residual snapshot encodings (rare; include/ewal.h esnap_copy_field)
+// k_snap_gather: one block per listed file whose envelope Data came in
+// several segments: the concatenation Go's append builds, into scratch.
+__global__ __launch_bounds__(256) void k_snap_gather(const uint8_t *__restrict__ buf, const SnapDesc *__restrict__ sd,
+                                                     const uint32_t *__restrict__ rlist,
+                                                     const uint64_t *__restrict__ goff, uint8_t *__restrict__ scratch,
+                                                     uint32_t nr) {
+  const uint32_t r = blockIdx.x;
+  if (r >= nr) return;
+  const SnapDesc d = sd[rlist[r]];
+  if (d.resid != 2) return;
+  uint8_t *dst = scratch + goff[r];
+  uint64_t pos = 0;
+  // snappb.Snapshot: Crc (1) varint, Data (2) bytes
+  pb_each(buf + d.off, (int64_t)d.len, 2, 0x2u, 0x4u, [&](bool b, uint64_t o, uint64_t n) {
+    if (!b) return;
+    const uint8_t *src = buf + d.off + o;
+    for (uint64_t j = threadIdx.x; j < n; j += blockDim.x) dst[pos + j] = src[j];
+    pos += n;
+  });
+}
+
+// k_snap_resid: one lane per listed file, raftpb.Snapshot Unmarshal over
+// the file's Data (or its gathered concatenation): the FILL pass writes the
+// status, esnap_snapshot's fields and the file's segments (emsg_segment:
+// offsets into d_buf, or into scratch for a gathered file); the count pass
+// only counts the segments.
+template <bool FILL>
+__global__ __launch_bounds__(256) void k_snap_resid(const uint8_t *__restrict__ buf, const uint8_t *__restrict__ scratch,
+                                                    SnapDesc *__restrict__ sd, const uint32_t *__restrict__ rlist,
+                                                    const uint64_t *__restrict__ goff, uint32_t nr,
+                                                    uint64_t *__restrict__ cnt, const uint64_t *__restrict__ first,
+                                                    emsg_segment *__restrict__ segs,
+                                                    esnap_snapshot *__restrict__ snaps) {
+  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= nr) return;
+  const uint32_t f = rlist[r];
+  SnapDesc d = sd[f];
+  const bool gathered = d.resid == 2;
+  const uint64_t base = gathered ? goff[r] : d.doff;
+  const uint8_t *p = (gathered ? scratch : buf) + base;
+  const int64_t l = (int64_t)d.dlen;
+  uint64_t ns = 0;
+  auto emit = [&](int32_t kind, uint64_t off, uint64_t len) {
+    if (FILL) {
+      emsg_segment g;
+      g.kind = kind;
+      g.pad = gathered ? 1 : 0;
+      g.ent = -1;
+      g.off = off;
+      g.len = len;
+      segs[first[r] + ns] = g;
+    }
+    ++ns;
+  };
+  PbField s1, s2, s3, s4, s5;
+  pbf_init(s1); pbf_init(s2); pbf_init(s3); pbf_init(s4); pbf_init(s5);
+  esnap_snapshot *o = snaps + f;
+  int ur = 0;
+  const int st = pb_walk<PB_BYTES, PB_REP64, PB_VAR64, PB_VAR64, PB_REP64>(
+      p, l, s1, s2, s3, s4, s5, ur, FILL ? o->nodes : nullptr, FILL ? o->removed : nullptr, 64,
+      [&](int64_t u0, int64_t u1) { emit(EMSG_SEG_SNAP_UNREC, base + (uint64_t)u0, (uint64_t)(u1 - u0)); });
+  pb_each(p, l, 1, 0x3cu, 0x2u, [&](bool b, uint64_t o2, uint64_t n) {
+    if (b) emit(EMSG_SEG_SNAP_DATA, base + o2, n);
+  });
+  if (s2.split) pb_each(p, l, 2, 0x3cu, 0x2u, [&](bool b, uint64_t v, uint64_t) {
+    if (!b) emit(EMSG_SEG_SNAP_NODE, v, 0);
+  });
+  if (s5.split) pb_each(p, l, 5, 0x3cu, 0x2u, [&](bool b, uint64_t v, uint64_t) {
+    if (!b) emit(EMSG_SEG_SNAP_REMOVED, v, 0);
+  });
+  if (!FILL) {
+    cnt[r] = ns;
+    return;
+  }
+  o->index = s3.v;
+  o->term = s4.v;
+  // one contiguous range of the file, else ~0: esnap_copy_field assembles it
+  o->data_off = (gathered || s1.split) ? ~0ull : (s1.blen > 0 ? d.doff + (uint64_t)s1.boff : d.doff);
+  o->data_len = s1.blen > 0 ? (uint64_t)s1.blen : 0;
+  o->n_nodes = (int64_t)s2.v;
+  o->n_removed = (int64_t)s5.v;
   d.st = st;
   sd[f] = d;
 }

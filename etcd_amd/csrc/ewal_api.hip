@@ -123,6 +123,13 @@ struct ewal_ctx {
   DevBuf encw, encs, lbstat, gagg, slow, mlist, pf, v, pwave, ux, tagg, tpx, wcnt, slots, cbase, ovf, cpos, clen, nxt, exc, E, rs, jl, vis, entry, on, rec_cand, rd, opf, ops, kk, kkrev, suf,
       ents, recs, tmp, small, sdesc, snaps, hbuf_dev, xpos, walk, fpos, ulist, uitems, uarena, ftrec;
   HostBuf hsdesc;                  // esnap_verify_packed's per-file table (host-mapped)
+  // esnap_verify_packed's residual decode (esnap_copy_field): the batch's
+  // buffer, per file its residual slot (-1: none), per slot its segments
+  const uint8_t *snap_buf = nullptr;
+  uint32_t snap_n = 0;
+  std::vector<int32_t> snap_rmap;
+  std::vector<uint64_t> snap_rfirst, snap_rcnt;
+  DevBuf sgather, ssegs, srlist, sgoff, srcnt, srfirst;
   std::vector<ewal_unrec> unrec;   // XXX_unrecognized of the last ReadAll's result (side list)
   uint64_t unrec_bytes = 0;
   // batched ReadAll (ewal_readall_batch_device): shard tables, results, ents
@@ -1927,6 +1934,62 @@ int ewal_crc32_update_device(ewal_ctx *c, uint32_t crc, uint32_t poly, const voi
   return EWAL_OK;
 }
 
+// The files k_snap left to the residual decode (h[i].resid): gather split
+// envelope Data, count and place the segments, decode.  Rare: the extents
+// come back to the host between the steps.
+static int snap_residuals(ewal_ctx *c, const uint8_t *buf, uint32_t n, SnapDesc *h) {
+  c->snap_buf = buf;
+  c->snap_n = n;
+  c->snap_rmap.assign(n, -1);
+  c->snap_rfirst.clear();
+  c->snap_rcnt.clear();
+  std::vector<uint32_t> rl;
+  std::vector<uint64_t> goff;
+  uint64_t gtot = 0;
+  for (uint32_t i = 0; i < n; ++i) {
+    if (h[i].st != EWAL_OK || !h[i].resid) continue;
+    c->snap_rmap[i] = (int32_t)rl.size();
+    rl.push_back(i);
+    goff.push_back(gtot);
+    if (h[i].resid == 2) gtot += h[i].dlen;
+  }
+  const uint32_t nr = (uint32_t)rl.size();
+  if (!nr) return EWAL_OK;
+  EW_CHECK(c->srlist.ensure((size_t)nr * 4));
+  EW_CHECK(c->sgoff.ensure((size_t)nr * 8));
+  EW_CHECK(c->srcnt.ensure((size_t)nr * 8));
+  EW_CHECK(c->srfirst.ensure((size_t)nr * 8));
+  EW_CHECK(c->sgather.ensure((size_t)std::max<uint64_t>(gtot, 1)));
+  EW_CHECK(hipMemcpyAsync(c->srlist.p, rl.data(), (size_t)nr * 4, hipMemcpyHostToDevice, c->stream));
+  EW_CHECK(hipMemcpyAsync(c->sgoff.p, goff.data(), (size_t)nr * 8, hipMemcpyHostToDevice, c->stream));
+  SnapDesc *sd = c->hsdesc.dev<SnapDesc>();
+  esnap_snapshot *snaps = c->snaps.as<esnap_snapshot>();
+  if (gtot)
+    hipLaunchKernelGGL(k_snap_gather, dim3(nr), dim3(256), 0, c->stream, buf, (const SnapDesc *)sd,
+                       c->srlist.as<uint32_t>(), c->sgoff.as<uint64_t>(), c->sgather.as<uint8_t>(), nr);
+  hipLaunchKernelGGL(k_snap_resid<false>, dim3(grid_for(nr, 256)), dim3(256), 0, c->stream, buf,
+                     (const uint8_t *)c->sgather.as<uint8_t>(), sd, c->srlist.as<uint32_t>(), c->sgoff.as<uint64_t>(), nr,
+                     c->srcnt.as<uint64_t>(), (const uint64_t *)nullptr, (emsg_segment *)nullptr, snaps);
+  EW_CHECK(hipGetLastError());
+  c->snap_rcnt.resize(nr);
+  EW_CHECK(hipMemcpyAsync(c->snap_rcnt.data(), c->srcnt.p, (size_t)nr * 8, hipMemcpyDeviceToHost, c->stream));
+  EW_CHECK(hipStreamSynchronize(c->stream));
+  c->snap_rfirst.resize(nr);
+  uint64_t tot = 0;
+  for (uint32_t r = 0; r < nr; ++r) {
+    c->snap_rfirst[r] = tot;
+    tot += c->snap_rcnt[r];
+  }
+  EW_CHECK(c->ssegs.ensure((size_t)std::max<uint64_t>(tot, 1) * sizeof(emsg_segment)));
+  EW_CHECK(hipMemcpyAsync(c->srfirst.p, c->snap_rfirst.data(), (size_t)nr * 8, hipMemcpyHostToDevice, c->stream));
+  hipLaunchKernelGGL(k_snap_resid<true>, dim3(grid_for(nr, 256)), dim3(256), 0, c->stream, buf,
+                     (const uint8_t *)c->sgather.as<uint8_t>(), sd, c->srlist.as<uint32_t>(), c->sgoff.as<uint64_t>(), nr,
+                     (uint64_t *)nullptr, (const uint64_t *)c->srfirst.as<uint64_t>(), c->ssegs.as<emsg_segment>(),
+                     snaps);
+  EW_CHECK(hipGetLastError());
+  return EWAL_OK;
+}
+
 int esnap_verify_packed(ewal_ctx *c, const void *d_buf, uint64_t buf_len, const uint64_t *offs, const uint64_t *lens,
                         uint32_t n, uint32_t poly, int32_t *status, uint32_t *stored_crc, uint32_t *computed_crc) {
   if (!c || (!d_buf && buf_len) || (n && (!offs || !lens || !status))) return EWAL_E_INVAL;
@@ -1959,6 +2022,9 @@ int esnap_verify_packed(ewal_ctx *c, const void *d_buf, uint64_t buf_len, const 
                        c->snaps.as<esnap_snapshot>(), n);
     EW_CHECK(hipGetLastError());
   }
+  EW_CHECK(hipStreamSynchronize(c->stream));
+  rc = snap_residuals(c, (const uint8_t *)d_buf, n, h);
+  if (rc) return rc;
   EW_CHECK(hipEventRecord(c->ev1, c->stream));
   EW_CHECK(hipStreamSynchronize(c->stream));
   for (uint32_t i = 0; i < n; ++i) {
@@ -1973,6 +2039,53 @@ int esnap_copy_snapshot(ewal_ctx *c, uint32_t i, esnap_snapshot *out) {
   if (!c || !out) return EWAL_E_INVAL;
   EW_CHECK(hipMemcpy(out, c->snaps.as<esnap_snapshot>() + i, sizeof(*out), hipMemcpyDeviceToHost));
   return EWAL_OK;
+}
+
+int64_t esnap_copy_field(ewal_ctx *c, uint32_t i, int32_t field, void *out, int64_t cap) {
+  if (!c || i >= c->snap_n || cap < 0 || (!out && cap) || field < ESNAP_FIELD_DATA || field > ESNAP_FIELD_REMOVED)
+    return EWAL_E_INVAL;
+  EW_CHECK(hipSetDevice(c->device));
+  esnap_snapshot s;
+  EW_CHECK(hipMemcpy(&s, c->snaps.as<esnap_snapshot>() + i, sizeof(s), hipMemcpyDeviceToHost));
+  const int32_t r = c->snap_rmap[i];
+  std::vector<emsg_segment> sg;
+  if (r >= 0 && c->snap_rcnt[r]) {
+    sg.resize(c->snap_rcnt[r]);
+    EW_CHECK(hipMemcpy(sg.data(), c->ssegs.as<emsg_segment>() + c->snap_rfirst[r], sg.size() * sizeof(emsg_segment),
+                       hipMemcpyDeviceToHost));
+  }
+  uint8_t *ob = (uint8_t *)out;
+  uint64_t *ov = (uint64_t *)out;
+  if (field == ESNAP_FIELD_NODES || field == ESNAP_FIELD_REMOVED) {
+    const bool nodes = field == ESNAP_FIELD_NODES;
+    const int64_t total = nodes ? s.n_nodes : s.n_removed;
+    if (total <= 64) {
+      const int64_t k = std::min(cap, total);
+      if (k > 0) std::memcpy(ov, nodes ? s.nodes : s.removed, (size_t)k * 8);
+      return total;
+    }
+    int64_t k = 0;
+    const int32_t kind = nodes ? EMSG_SEG_SNAP_NODE : EMSG_SEG_SNAP_REMOVED;
+    for (auto &g : sg)
+      if (g.kind == kind && k < cap) ov[k++] = g.off;
+    return total;
+  }
+  if (r < 0) {   // the common layout: Data is one range of the file, no XXX_unrecognized
+    if (field == ESNAP_FIELD_UNREC) return 0;
+    const int64_t k = std::min<int64_t>(cap, (int64_t)s.data_len);
+    if (k > 0) EW_CHECK(hipMemcpy(ob, c->snap_buf + s.data_off, (size_t)k, hipMemcpyDeviceToHost));
+    return (int64_t)s.data_len;
+  }
+  const int32_t kind = field == ESNAP_FIELD_DATA ? EMSG_SEG_SNAP_DATA : EMSG_SEG_SNAP_UNREC;
+  int64_t total = 0;
+  for (auto &g : sg) {
+    if (g.kind != kind) continue;
+    const int64_t k = std::min<int64_t>(std::max<int64_t>(cap - total, 0), (int64_t)g.len);
+    const uint8_t *src = (g.pad ? c->sgather.as<uint8_t>() : c->snap_buf) + g.off;
+    if (k > 0) EW_CHECK(hipMemcpy(ob + total, src, (size_t)k, hipMemcpyDeviceToHost));
+    total += (int64_t)g.len;
+  }
+  return total;
 }
 
 int emsg_decode_batch_device(ewal_ctx *c, const void *d_buf, uint64_t buf_len, const uint64_t *offs,

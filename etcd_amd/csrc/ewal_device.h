@@ -299,3 +299,41 @@ __device__ inline int pb_walk(const P &p, int64_t l, PbField &f1, PbField &f2, P
   }
   return 0;
 }
+
+// Every occurrence of field fnum that pb_walk consumed over the same bytes,
+// in order: f(true, off, len) for a non-empty bytes occurrence, f(false,
+// value, 0) for a varint one.  Other fields are stepped over by proto.Skip
+// from their tag; kvar / kbytes (bit fn) name the message's varint / bytes
+// fields, so a known field with the wrong wire type ends the walk where
+// Unmarshal's ErrWrongType does (a message whose error is discarded keeps
+// what came before it).
+template <class F>
+__device__ void pb_each(const uint8_t *p, int64_t l, uint32_t fnum, uint32_t kvar, uint32_t kbytes, F f) {
+  int64_t i = 0;
+  while (i < l) {
+    const int64_t tag = i;
+    uint64_t wire = 0;
+    if (rd_varint(p, i, l, wire, 64)) return;
+    const uint32_t fn = (uint32_t)(wire >> 3);
+    const int wt = (int)(wire & 7);
+    if (fn < 32 && ((((kvar >> fn) & 1) && wt != 0) || (((kbytes >> fn) & 1) && wt != 2))) return;
+    if (fn == fnum && wt == 0) {
+      uint64_t v = 0;
+      if (rd_varint(p, i, l, v, 64)) return;
+      f(false, v, 0ull);
+      continue;
+    }
+    if (fn == fnum && wt == 2) {
+      uint64_t bl = 0;
+      if (rd_varint(p, i, l, bl, 64)) return;
+      const int64_t post = (int64_t)((uint64_t)i + bl);
+      if (post > l || post < i) return;
+      if (post > i) f(true, (uint64_t)i, (uint64_t)(post - i));
+      i = post;
+      continue;
+    }
+    int64_t sk;
+    if (pb_skip(p + tag, l - tag, sk) || sk <= 0) return;
+    i = tag + sk;
+  }
+}

@@ -99,7 +99,8 @@ struct SnapDesc {
   uint64_t off, len;       // file within the packed buffer
   uint64_t doff, dlen;     // snappb.Snapshot.Data
   uint32_t stored, computed;
-  int32_t st, pad;
+  int32_t st;
+  int32_t resid;           // 1: raftpb.Snapshot needs k_snap_resid, 2: envelope Data split (gather first)
 };
 
 // The fused frame + check pass's reductions (k_fc).  Zero means none, so

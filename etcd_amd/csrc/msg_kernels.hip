@@ -23,39 +23,11 @@
 #include "ewal_device.h"
 #include "ewal_internal.h"
 
-// Every occurrence of field fnum of a message pb_walk accepted, in order:
-// f(true, off, len) for a non-empty bytes occurrence, f(false, value, 0)
-// for a varint one; every other field is stepped over by proto.Skip from
-// its tag (the extent Go's Unmarshal consumed).
-template <class F>
-__device__ void pb_each(const uint8_t *p, int64_t l, uint32_t fnum, F f) {
-  int64_t i = 0;
-  while (i < l) {
-    const int64_t tag = i;
-    uint64_t wire = 0;
-    if (rd_varint(p, i, l, wire, 64)) return;
-    const uint32_t fn = (uint32_t)(wire >> 3);
-    const int wt = (int)(wire & 7);
-    if (fn == fnum && wt == 0) {
-      uint64_t v = 0;
-      if (rd_varint(p, i, l, v, 64)) return;
-      f(false, v, 0ull);
-      continue;
-    }
-    if (fn == fnum && wt == 2) {
-      uint64_t bl = 0;
-      if (rd_varint(p, i, l, bl, 64)) return;
-      const int64_t post = (int64_t)((uint64_t)i + bl);
-      if (post > l || post < i) return;
-      if (post > i) f(true, (uint64_t)i, (uint64_t)(post - i));
-      i = post;
-      continue;
-    }
-    int64_t sk;
-    if (pb_skip(p + tag, l - tag, sk) || sk <= 0) return;
-    i = tag + sk;
-  }
-}
+// raftpb.Entry / raftpb.Snapshot field sets (bit = field number) for pb_each
+#define EMSG_ENTRY_VAR 0x0eu      // Type, Term, Index
+#define EMSG_ENTRY_BYTES 0x10u    // Data
+#define EMSG_SNAP_VAR 0x3cu       // Nodes, Index, Term, RemovedNodes
+#define EMSG_SNAP_BYTES 0x02u     // Data
 
 template <bool FILL>
 __device__ int msg_walk(const uint8_t *p, int64_t l, uint64_t base, emsg_message &m, ewal_entry *ents, uint64_t &ne,
@@ -119,7 +91,7 @@ __device__ int msg_walk(const uint8_t *p, int64_t l, uint64_t base, emsg_message
         if (es == 33 || es == 37) { st = es; break; }   // panics propagate, errors do not
         if (es == 48) unsup = 1;
         if (a4.split)   // Data = the concatenation of its segments
-          pb_each(p + i, post - i, 4, [&](bool b, uint64_t o, uint64_t n) {
+          pb_each(p + i, post - i, 4, EMSG_ENTRY_VAR, EMSG_ENTRY_BYTES, [&](bool b, uint64_t o, uint64_t n) {
             if (b) emit(EMSG_SEG_ENTRY_DATA, ei, at + o, n);
           });
         if (FILL) {
@@ -141,13 +113,13 @@ __device__ int msg_walk(const uint8_t *p, int64_t l, uint64_t base, emsg_message
         if (had == 0 && s1.blen > 0) m.snap_data_off = (int64_t)(at + (uint64_t)s1.boff);
         if (ss == 48) unsup = 1;
         // Nodes, RemovedNodes and the Data segments of this occurrence (they accumulate over repeats)
-        if (s2.v) pb_each(p + i, post - i, 2, [&](bool b, uint64_t v, uint64_t) {
+        if (s2.v) pb_each(p + i, post - i, 2, EMSG_SNAP_VAR, EMSG_SNAP_BYTES, [&](bool b, uint64_t v, uint64_t) {
           if (!b) emit(EMSG_SEG_SNAP_NODE, -1, v, 0);
         });
-        if (s5.v) pb_each(p + i, post - i, 5, [&](bool b, uint64_t v, uint64_t) {
+        if (s5.v) pb_each(p + i, post - i, 5, EMSG_SNAP_VAR, EMSG_SNAP_BYTES, [&](bool b, uint64_t v, uint64_t) {
           if (!b) emit(EMSG_SEG_SNAP_REMOVED, -1, v, 0);
         });
-        if (s1.blen > had) pb_each(p + i, post - i, 1, [&](bool b, uint64_t o, uint64_t n) {
+        if (s1.blen > had) pb_each(p + i, post - i, 1, EMSG_SNAP_VAR, EMSG_SNAP_BYTES, [&](bool b, uint64_t o, uint64_t n) {
           if (b) emit(EMSG_SEG_SNAP_DATA, -1, at + o, n);
         });
         if (ss) { st = ss; break; }

@@ -9,6 +9,8 @@
   (esnap_verify_packed; snap/snapshotter.go:76-111).
 * `load_dir` -- Snapshotter.Load (newest first, tried failures renamed
   .broken; snap/snapshotter.go:62-74); `snap_names` -- snapNames.
+* `snapshot` / `copy_field` -- the full decoded raftpb.Snapshot (Data over
+  repeated fields, Nodes / RemovedNodes past 64, XXX_unrecognized).
 """
 import ctypes as C
 
@@ -51,6 +53,35 @@ def verify_packed(dbuf, buf_len, offs, lens, poly=L.CASTAGNOLI):
                                  (C.c_uint64 * max(n, 1))(*lens), n, poly, st, sc, cc)
     check(rc)
     return list(st[:n]), list(sc[:n]), list(cc[:n])
+
+
+def copy_field(ctx, i, field):
+    """esnap_copy_field: the full value of one raftpb.Snapshot field of file i
+    of the last verify_packed / load_dir -- bytes (None when Go leaves it
+    nil) for SNAP_FIELD_DATA / SNAP_FIELD_UNREC, a list of uint64 for
+    SNAP_FIELD_NODES / SNAP_FIELD_REMOVED."""
+    n = lib.esnap_copy_field(ctx.handle, i, field, None, 0)
+    if n < 0:
+        check(int(n))
+    if field in (L.SNAP_FIELD_NODES, L.SNAP_FIELD_REMOVED):
+        buf = (C.c_uint64 * max(n, 1))()
+        check(min(0, int(lib.esnap_copy_field(ctx.handle, i, field, buf, n))))
+        return list(buf[:n])
+    if n == 0:
+        return None
+    buf = C.create_string_buffer(n)
+    check(min(0, int(lib.esnap_copy_field(ctx.handle, i, field, buf, n))))
+    return buf.raw[:n]
+
+
+def snapshot(ctx, i):
+    """The decoded raftpb.Snapshot of file i (status OK) as a dict shaped like
+    the oracle's loadsnap()["snap"], plus its XXX_unrecognized bytes."""
+    s = L.SnapshotDesc()
+    check(lib.esnap_copy_snapshot(ctx.handle, i, C.byref(s)))
+    return dict(data=copy_field(ctx, i, L.SNAP_FIELD_DATA), nodes=copy_field(ctx, i, L.SNAP_FIELD_NODES),
+                index=s.index, term=s.term, removed=copy_field(ctx, i, L.SNAP_FIELD_REMOVED),
+                unrec=copy_field(ctx, i, L.SNAP_FIELD_UNREC))
 
 
 def load_dir(ctx, dirpath, poly=L.CASTAGNOLI):

@@ -347,8 +347,9 @@ int esnap_verify_packed(ewal_ctx *ctx, const void *d_buf, uint64_t buf_len, cons
  * tried failures renamed *.broken.  On success *out_name (malloc'd, caller
  * frees with free()) names the snapshot file loaded; snapshot fields out.
  * Only the errors Go's loadSnap returns rename a file .broken; a Go panic
- * class or EWAL_UNSUPPORTED_ENCODING (a valid file this layout cannot
- * return in full) stops Load with *out_name naming that file, not renamed. */
+ * class (or EWAL_UNSUPPORTED_ENCODING: protobuf groups nested deeper than
+ * the device walker's stack) stops Load with *out_name naming that file,
+ * not renamed. */
 typedef struct esnap_snapshot {
   uint64_t index, term;
   uint64_t data_off, data_len;   /* raftpb.Snapshot.Data within the file */
@@ -356,8 +357,18 @@ typedef struct esnap_snapshot {
   uint64_t nodes[64], removed[64];
 } esnap_snapshot;
 /* After esnap_verify_packed: the decoded raftpb.Snapshot of file i (only
- * meaningful when status[i] == EWAL_OK). */
+ * meaningful when status[i] == EWAL_OK).  data_off == ~0: Data is not one
+ * range of the file (several segments); n_nodes / n_removed > 64: only the
+ * first 64 are held -- esnap_copy_field returns the full values. */
 int esnap_copy_snapshot(ewal_ctx *ctx, uint32_t i, esnap_snapshot *out);
+/* The full value of one raftpb.Snapshot field of file i of the last
+ * esnap_verify_packed (d_buf still alive) or esnap_load_dir (i = 0): the
+ * bytes of Data (the concatenation Go's append builds over repeated fields,
+ * raft.pb.go:279-406) or of Snapshot.XXX_unrecognized, or the uint64 values
+ * of Nodes / RemovedNodes.  Copies min(cap, full) bytes / values to out;
+ * returns the full count or a negative error. */
+enum { ESNAP_FIELD_DATA = 0, ESNAP_FIELD_UNREC = 1, ESNAP_FIELD_NODES = 2, ESNAP_FIELD_REMOVED = 3 };
+int64_t esnap_copy_field(ewal_ctx *ctx, uint32_t i, int32_t field, void *out, int64_t cap);
 int esnap_load_dir(ewal_ctx *ctx, const char *dirpath, uint32_t poly, esnap_snapshot *out, char **out_name);
 /* Snapshotter.snapNames (snap/snapshotter.go:115-131): the *.snap names,
  * newest first, NUL-separated into out (cap bytes; *len = bytes needed).

@@ -394,7 +394,8 @@ def loadsnap(b, poly=CASTAGNOLI):
     out = dict(status=st, stored_crc=r.stored_crc, computed_crc=r.computed_crc)
     if st == OK:
         out["snap"] = dict(data=_bytes(s.data, s.data_len), nodes=[s.nodes[i] for i in range(s.n_nodes)],
-                           index=s.index, term=s.term, removed=[s.removed[i] for i in range(s.n_removed)])
+                           index=s.index, term=s.term, removed=[s.removed[i] for i in range(s.n_removed)],
+                           unrec=_bytes(s.unrec, s.unrec_len))
     lib.or_loadsnap_free(C.byref(r))
     return out
 

@@ -9,6 +9,7 @@ import pytest
 
 from oracle import oracle as O
 from etcd_amd import _lib as L
+from etcd_amd import snap as S
 from etcd_amd import wal as W
 
 pytestmark = pytest.mark.gpu
@@ -503,25 +504,82 @@ def test_commit_large_voter_counts(ctx):
         assert (got, ch, s) == (want, 1 if rc == 1 else 0, 0)
 
 
-def test_snapshotter_load_dir_engine_limit_not_renamed(ctx, tmp_path):
-    """A valid snapshot the device decoder does not return in full (more than
-    64 RemovedNodes) is never renamed to .broken: Go's loadSnap loads it
-    (snap/snapshotter.go:76-111), so Load stops there with
-    EWAL_UNSUPPORTED_ENCODING and the file in place."""
+def test_snapshotter_load_dir_residual_encodings(ctx, tmp_path):
+    """A valid snapshot past esnap_snapshot's inline layout (more than 64
+    RemovedNodes, Data in two segments, unknown fields) loads like Go's
+    loadSnap (snap/snapshotter.go:76-111) and esnap_copy_field returns the
+    full values."""
     rng = random.Random(44)
     dd = tmp_path / "snap"
     dd.mkdir()
-    body = O.snapshot_marshal(rng.randbytes(100), [1, 2, 3], 9, 2, removed=list(range(1, 71)))
+    body = O.snapshot_marshal(rng.randbytes(100), [1, 2, 3], 9, 2, removed=list(range(1, 71))) + \
+        bytes([0x0a, 0x03]) + b"xyz" + bytes([0x30, 0x07])
     f = O.snappb_marshal(O.crc32_update(0, body), body)
-    assert O.loadsnap(f)["status"] == O.OK
+    o = O.loadsnap(f)
+    assert o["status"] == O.OK
     newest = "%016x-%016x.snap" % (2, 9)
     (dd / newest).write_bytes(f)
     (dd / ("%016x-%016x.snap" % (1, 1))).write_bytes(_snap_file(rng, 13, [1, 2, 3], 1, 1))
     s = L.SnapshotDesc()
     name = C.c_char_p()
     rc = L.lib.esnap_load_dir(ctx.handle, str(dd).encode(), L.CASTAGNOLI, C.byref(s), C.byref(name))
-    assert rc == L.UNSUPPORTED_ENCODING and name.value.decode() == newest
-    assert (dd / newest).exists() and not (dd / (newest + ".broken")).exists()
+    assert rc == 0 and name.value.decode() == newest and s.index == 9
+    assert S.snapshot(ctx, 0) == o["snap"]
+    assert o["snap"]["removed"] == list(range(1, 71)) and o["snap"]["unrec"] == bytes([0x30, 0x07])
+
+
+def _residual_snap_files(rng):
+    """snappb envelopes whose raftpb.Snapshot needs the residual decode, with
+    the oracle's verdicts."""
+    out = []
+    unk = bytes([0x30, 0x05, 0x3a, 0x02]) + b"hi"                    # fields 6 (varint), 7 (bytes)
+    for k in range(12):
+        body = O.snapshot_marshal(rng.randbytes(rng.choice([0, 5, 300])), list(range(1, rng.choice([2, 65, 130]))),
+                                  k, 3, removed=list(range(7, 7 + rng.choice([0, 64, 65, 200]))))
+        if k % 3 == 0:
+            body += bytes([0x0a, 0x04]) + rng.randbytes(4)               # Data in two segments
+        if k % 2 == 0:
+            body += unk
+        if k % 4 == 1:
+            body += bytes([0x0a, 0x02, 0x01])                            # truncated: ErrUnexpectedEOF
+        crc = O.crc32_update(0, body)
+        if k % 5 == 4:
+            # the envelope's Data in several segments: raftpb.Snapshot over the concatenation
+            cut = rng.randrange(1, len(body))
+            f = O.snappb_marshal(crc, body[:cut]) + b"\x12" + M_varint(len(body) - cut) + body[cut:]
+        else:
+            f = O.snappb_marshal(crc, body)
+        out.append(bytes(f))
+    return out
+
+
+def M_varint(v):
+    from etcd_amd import raftmsg
+    return raftmsg._varint(v)
+
+
+def test_snapshot_batch_residual(ctx):
+    rng = random.Random(45)
+    files = _residual_snap_files(rng) + [_snap_file(rng, 50, [1, 2], 3, 4)]
+    offs, packed = [], bytearray()
+    for f in files:
+        offs.append(len(packed))
+        packed += f
+        packed += b"\0" * rng.randrange(0, 40)
+    d = ctx.alloc(len(packed) + 64)
+    d.upload(bytes(packed))
+    try:
+        st, sc, cc = S.verify_packed(d, len(packed), offs, [len(f) for f in files])
+        seen = set()
+        for i, f in enumerate(files):
+            o = O.loadsnap(f)
+            assert st[i] == o["status"], (i, st[i], o["status"])
+            seen.add(o["status"])
+            if o["status"] == O.OK:
+                assert S.snapshot(ctx, i) == o["snap"], i
+        assert O.OK in seen and len(seen) >= 2
+    finally:
+        d.free()
 
 
 def _oracle_save(ops, prev):

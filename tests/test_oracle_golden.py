@@ -161,7 +161,8 @@ def test_snapshot_save_load_and_bad_crc():
     f = O.snappb_marshal(O.crc32_update(0, body), body)
     r = O.loadsnap(f)
     assert r["status"] == O.OK
-    assert r["snap"] == dict(data=g["data"].encode(), nodes=g["nodes"], index=g["index"], term=g["term"], removed=[])
+    assert r["snap"] == dict(data=g["data"].encode(), nodes=g["nodes"], index=g["index"], term=g["term"], removed=[],
+                             unrec=None)
     # TestBadCRC: the table swapped to Koopman makes the stored CRC mismatch
     assert O.loadsnap(f, O.KOOPMAN)["status"] == O.ERR_SNAP_CRC
     # TestFailback: "bad data" is not a snappb.Snapshot
