@@ -54,6 +54,7 @@ UNSUPPORTED_ENCODING = 48
 E_HIP, E_INVAL, E_NOMEM, E_NODEVICE, E_TIMEOUT, E_IO = -1, -2, -3, -4, -5, -6
 
 FLAG_SHARD_FALLBACK = 1   # ewal_readall_batch_device verified this shard on its own
+FLAG_METADATA_SPLIT = 2   # metadata_off / _len index the split bytes (ewal_copy_split_bytes)
 
 CASTAGNOLI, IEEE, KOOPMAN = 0x82F63B78, 0xEDB88320, 0xEB31D82E
 
@@ -113,7 +114,7 @@ class RangeInfo(C.Structure):   # ewal_range_info
                 ("md_value_off", C.c_int64), ("md_value_len", C.c_int64), ("first_entry_frame", C.c_int64),
                 ("last_entry_frame", C.c_int64), ("first_entry_index", C.c_uint64),
                 ("min_entry_index", C.c_uint64), ("last_entry_index", C.c_uint64), ("last_op_frame", C.c_int64),
-                ("last_op_index", C.c_uint64)]
+                ("last_op_index", C.c_uint64), ("md_split", C.c_int32), ("pad", C.c_int32)]
 
 
 class SnapshotDesc(C.Structure):
@@ -156,6 +157,8 @@ _SIGS = {
     "ewal_copy_range_info": (C.c_int, [vp, C.POINTER(RangeInfo)]),
     "ewal_copy_unrec": (C.c_int64, [vp, C.POINTER(UnrecDesc), C.c_int64]),
     "ewal_copy_unrec_bytes": (C.c_int64, [vp, vp, C.c_int64]),
+    "ewal_copy_split_bytes": (C.c_int64, [vp, vp, C.c_int64]),
+    "ewal_batch_copy_split_bytes": (C.c_int64, [vp, C.c_uint64, vp, C.c_int64]),
     "ewal_open_at_index": (C.c_int, [C.c_char_p, C.c_uint64, C.POINTER(vp)]),
     "ewal_wal_readall": (C.c_int, [vp, vp, C.POINTER(Result)]),
     "ewal_wal_bytes": (u8p, [vp, C.POINTER(C.c_uint64)]),

@@ -132,6 +132,13 @@ struct ewal_ctx {
   DevBuf sgather, ssegs, srlist, sgoff, srcnt, srfirst;
   std::vector<ewal_unrec> unrec;   // XXX_unrecognized of the last ReadAll's result (side list)
   uint64_t unrec_bytes = 0;
+  // the side arena of split byte fields (Record.Data / Entry.Data repeated
+  // with several non-empty segments): the general path gathers their
+  // concatenations here (ewal_copy_split_bytes)
+  DevBuf cat;
+  uint64_t cat_bytes = 0;
+  bool cat_retry = false;
+  std::vector<std::vector<uint8_t>> bsplit_bytes;   // per shard replayed alone: its split bytes
   // batched ReadAll (ewal_readall_batch_device): shard tables, results, ents
   DevBuf bfs, bsoff, bri, bsagg, bres, bef, bents, bshard, hmask;
   // batched raftpb.Message decode (emsg_decode_batch_device)
@@ -643,7 +650,7 @@ static int gather_unrec(ewal_ctx *c, const uint8_t *d_buf, const ResultDev &res,
   EW_CHECK(c->uitems.ensure((size_t)m * sizeof(UnrecItem)));
   EW_CHECK(hipMemcpyAsync(c->uitems.p, items.data(), (size_t)m * sizeof(UnrecItem), hipMemcpyHostToDevice, c->stream));
   hipLaunchKernelGGL(k_unrec<0>, dim3(grid_for(m, 64)), dim3(64), 0, c->stream, d_buf, c->rd.as<RecDesc>(),
-                     c->uitems.as<UnrecItem>(), m, (uint8_t *)nullptr);
+                     c->uitems.as<UnrecItem>(), m, (uint8_t *)nullptr, (const uint8_t *)c->cat.as<uint8_t>());
   EW_CHECK(hipMemcpyAsync(items.data(), c->uitems.p, (size_t)m * sizeof(UnrecItem), hipMemcpyDeviceToHost, c->stream));
   EW_CHECK(hipStreamSynchronize(c->stream));
   uint64_t tot = 0;
@@ -654,7 +661,7 @@ static int gather_unrec(ewal_ctx *c, const uint8_t *d_buf, const ResultDev &res,
   EW_CHECK(c->uarena.ensure(tot + 16));
   EW_CHECK(hipMemcpyAsync(c->uitems.p, items.data(), (size_t)m * sizeof(UnrecItem), hipMemcpyHostToDevice, c->stream));
   hipLaunchKernelGGL(k_unrec<1>, dim3(grid_for(m, 64)), dim3(64), 0, c->stream, d_buf, c->rd.as<RecDesc>(),
-                     c->uitems.as<UnrecItem>(), m, c->uarena.as<uint8_t>());
+                     c->uitems.as<UnrecItem>(), m, c->uarena.as<uint8_t>(), (const uint8_t *)c->cat.as<uint8_t>());
   EW_CHECK(hipGetLastError());
   EW_CHECK(hipStreamSynchronize(c->stream));
   for (const UnrecItem &it : items) c->unrec.push_back(ewal_unrec{it.ent, it.off, it.len});
@@ -676,6 +683,7 @@ static int readall_impl(ewal_ctx *c, const uint8_t *d_buf, uint64_t B, uint64_t 
   c->last_nents = 0;
   c->unrec.clear();
   c->unrec_bytes = 0;
+  c->cat_bytes = 0;
   c->rd_valid = false;
   c->last_buf = d_buf;
   c->last_B = B;
@@ -685,6 +693,7 @@ static int readall_impl(ewal_ctx *c, const uint8_t *d_buf, uint64_t B, uint64_t 
   int rc = get_tables(c, 0x82F63B78u, &tb);
   if (rc) return rc;
   EW_CHECK(c->small.ensure(sizeof(Small)));
+  EW_CHECK(c->cat.ensure((size_t)1 << 20));   // the split-field side arena (grown on demand, below)
   EW_CHECK(hipEventRecord(c->ev0, c->stream));
   Small *ds = c->small.as<Small>();
 
@@ -742,7 +751,8 @@ static int readall_impl(ewal_ctx *c, const uint8_t *d_buf, uint64_t B, uint64_t 
         hipLaunchKernelGGL(k_spec_gate, dim3(1), dim3(64), 0, c->stream, ds, ccap, rdcap, c->h_small_dev);
         hipLaunchKernelGGL(k_decode_slow, dim3(64), dim3(256), 0, c->stream, d_buf, B, c->cpos.as<uint64_t>(),
                            (const uint32_t *)nullptr, c->slow.as<uint32_t>(), ds, c->pwave.as<uint32_t>(),
-                           c->v.as<uint32_t>(), tb->slice, tb->shift, c->rd.as<RecDesc>(), pf, pf + rdcap, 0u);
+                           c->v.as<uint32_t>(), tb->slice, tb->shift, c->rd.as<RecDesc>(), pf, pf + rdcap, 0u,
+                           c->cat.as<uint8_t>(), (uint64_t)c->cat.cap);
         const uint32_t nbs = grid_for(rdcap, 1024);
         const size_t had = c->lbstat.cap;
         EW_CHECK(c->lbstat.ensure((size_t)nbs * 8));
@@ -763,7 +773,8 @@ static int readall_impl(ewal_ctx *c, const uint8_t *d_buf, uint64_t B, uint64_t 
                            c->ents.as<ewal_entry>(), c->mlist.as<uint32_t>(), ds, useg,
                            (const uint32_t *)&ds->spec_n);
         hipLaunchKernelGGL(k_result, dim3(1), dim3(256), 0, c->stream, d_buf, c->rd.as<RecDesc>(),
-                           c->mlist.as<uint32_t>(), 0u, ri, ds, c->h_res_dev, (const uint32_t *)&ds->spec_n);
+                           c->mlist.as<uint32_t>(), 0u, ri, ds, c->h_res_dev, (const uint32_t *)&ds->spec_n,
+                           (const uint8_t *)c->cat.as<uint8_t>());
         EW_CHECK(hipGetLastError());
         EW_CHECK(hipStreamSynchronize(c->stream));
         if (c->h_small->errflag) return EWAL_E_TIMEOUT;
@@ -802,7 +813,8 @@ static int readall_impl(ewal_ctx *c, const uint8_t *d_buf, uint64_t B, uint64_t 
         hipLaunchKernelGGL(k_decode_slow, dim3(std::min<uint64_t>(grid_for(c->h_small->nslow, 256), 1024)),
                            dim3(256), 0, c->stream, d_buf, B, c->cpos.as<uint64_t>(), (const uint32_t *)nullptr,
                            c->slow.as<uint32_t>(), ds, c->pwave.as<uint32_t>(), c->v.as<uint32_t>(), tb->slice,
-                           tb->shift, c->rd.as<RecDesc>(), pf, pf + rdcap, 0u);
+                           tb->shift, c->rd.as<RecDesc>(), pf, pf + rdcap, 0u, c->cat.as<uint8_t>(),
+                           (uint64_t)c->cat.cap);
         EW_CHECK(hipGetLastError());
       }
     } else {
@@ -907,7 +919,7 @@ static int readall_impl(ewal_ctx *c, const uint8_t *d_buf, uint64_t B, uint64_t 
       hipLaunchKernelGGL(k_decode_slow, dim3(std::min<uint64_t>(grid_for(n, 256), 64)), dim3(256), 0, c->stream,
                          d_buf, B, plist, rc_list, c->slow.as<uint32_t>(), ds,
                          c->pwave.as<uint32_t>(), c->v.as<uint32_t>(), tb->slice, tb->shift, c->rd.as<RecDesc>(), pf,
-                         pf + c->pfcap, n32);
+                         pf + c->pfcap, n32, c->cat.as<uint8_t>(), (uint64_t)c->cat.cap);
     }
     RecDesc *rd = c->rd.as<RecDesc>();
     const uint32_t *pfd = c->pf.as<uint32_t>(), *pfo = pfd + c->pfcap;
@@ -934,7 +946,7 @@ static int readall_impl(ewal_ctx *c, const uint8_t *d_buf, uint64_t B, uint64_t 
                          c->lbstat.as<unsigned long long>(), c->epoch, c->opf.as<uint32_t>(),
                          c->ents.as<ewal_entry>(), c->mlist.as<uint32_t>(), ds, useg, (const uint32_t *)nullptr);
       hipLaunchKernelGGL(k_result, dim3(1), dim3(256), 0, c->stream, d_buf, rd, c->mlist.as<uint32_t>(), n32, ri, ds,
-                         c->h_res_dev, (const uint32_t *)nullptr);
+                         c->h_res_dev, (const uint32_t *)nullptr, (const uint8_t *)c->cat.as<uint8_t>());
       EW_CHECK(hipGetLastError());
       EW_CHECK(hipStreamSynchronize(c->stream));
     }
@@ -948,12 +960,22 @@ static int readall_impl(ewal_ctx *c, const uint8_t *d_buf, uint64_t B, uint64_t 
       hipLaunchKernelGGL(k_gap, dim3(ggrid), dim3(256), 0, c->stream, rd, c->ops.as<uint32_t>(),
                          c->kk.as<uint64_t>(), ds);
       hipLaunchKernelGGL(k_result, dim3(1), dim3(256), 0, c->stream, d_buf, rd, c->mlist.as<uint32_t>(), n32, ri, ds,
-                         c->h_res_dev, (const uint32_t *)nullptr);
+                         c->h_res_dev, (const uint32_t *)nullptr, (const uint8_t *)c->cat.as<uint8_t>());
       EW_CHECK(hipGetLastError());
       EW_CHECK(hipStreamSynchronize(c->stream));
       std::memcpy(&res, c->h_res, sizeof(ResultDev));
     }
     out->n_slow = (int32_t)res.nslow;
+    if (res.ncatfail && !c->cat_retry) {
+      // a split byte field found no room in the side arena: grow it to what
+      // the frames asked for and run the call again (once)
+      EW_CHECK(c->cat.ensure((size_t)std::min<uint64_t>(2 * res.cat_need + (1 << 20), 2 * B + (1 << 20))));
+      c->cat_retry = true;
+      const int r2 = readall_impl(c, d_buf, B, ri, out);
+      c->cat_retry = false;
+      return r2;
+    }
+    c->cat_bytes = std::min<uint64_t>(res.cat_used, c->cat.cap);
   }
   const ReadAllAgg &hagg = res.agg;
   out->n_records = (int64_t)n;
@@ -980,8 +1002,9 @@ static int readall_impl(ewal_ctx *c, const uint8_t *d_buf, uint64_t B, uint64_t 
       if (n) {
         out->last_crc = res.last.chained;
         if (hagg.first_meta != ~0ull) {
-          out->metadata_off = (int64_t)res.md.doff;
+          out->metadata_off = (int64_t)(res.md.pad0 == 2 ? rd_cat_off(res.md) : res.md.doff);
           out->metadata_len = (int64_t)res.md.dlen;
+          if (res.md.pad0 == 2) out->flags |= EWAL_FLAG_METADATA_SPLIT;   // a range of the split bytes
         }
         if (hagg.last_state >= 0) {
           out->has_state = 1;
@@ -1165,6 +1188,7 @@ static int replay_shards(ewal_ctx *c, const uint8_t *d_buf, const std::vector<ui
   const uint32_t ns = (uint32_t)soff.size() - 1;
   c->bunrec.assign(ns, {});
   c->bunrec_bytes.assign(ns, {});
+  c->bsplit_bytes.assign(ns, {});
   if (which.empty()) return 0;
   const uint64_t keep_k = c->last_k;
   const double batch_ms = ns ? out[0].device_ms : 0.0, batch_stream = ns ? out[0].stream_ms : 0.0;
@@ -1186,6 +1210,10 @@ static int replay_shards(ewal_ctx *c, const uint8_t *d_buf, const std::vector<ui
       c->bunrec_bytes[i].resize(c->unrec_bytes);
       if (c->unrec_bytes)
         EW_CHECK(hipMemcpy(c->bunrec_bytes[i].data(), c->uarena.p, c->unrec_bytes, hipMemcpyDeviceToHost));
+    }
+    if (r.status == EWAL_OK && c->cat_bytes) {   // split byte fields: the ents / metadata views index these
+      c->bsplit_bytes[i].resize(c->cat_bytes);
+      EW_CHECK(hipMemcpy(c->bsplit_bytes[i].data(), c->cat.p, c->cat_bytes, hipMemcpyDeviceToHost));
     }
     const uint64_t ne = r.status == EWAL_OK ? (uint64_t)r.n_ents : 0;
     c->bent_first[i] = 0;
@@ -1278,6 +1306,7 @@ static int readall_batch_impl(ewal_ctx *c, const uint8_t *d_buf, uint32_t ns, co
         if (bad.empty()) {
           c->bunrec.assign(ns, {});
           c->bunrec_bytes.assign(ns, {});
+          c->bsplit_bytes.assign(ns, {});
           return 0;
         }
         rc = replay_shards(c, d_buf, soff, lens, ris, out, bad, c->h_small->total);
@@ -1332,7 +1361,7 @@ static int readall_batch_impl(ewal_ctx *c, const uint8_t *d_buf, uint32_t ns, co
         hipLaunchKernelGGL(k_decode_slow, dim3(std::min<uint64_t>(grid_for(c->h_small->nslow, 256), 1024)),
                            dim3(256), 0, c->stream, d_buf, B, c->cpos.as<uint64_t>(), (const uint32_t *)nullptr,
                            c->slow.as<uint32_t>(), ds, c->pwave.as<uint32_t>(), c->v.as<uint32_t>(), tb->slice,
-                           tb->shift, c->rd.as<RecDesc>(), pf, pf + rdcap, 0u);
+                           tb->shift, c->rd.as<RecDesc>(), pf, pf + rdcap, 0u, (uint8_t *)nullptr, 0ull);
         EW_CHECK(hipGetLastError());
       }
       EW_CHECK(c->bsoff.ensure((size_t)(ns + 1) * 8));
@@ -1376,7 +1405,9 @@ static int readall_batch_impl(ewal_ctx *c, const uint8_t *d_buf, uint32_t ns, co
       EW_CHECK(hipMemcpyAsync(c->bent_first.data(), c->bef.p, (size_t)ns * 8, hipMemcpyDeviceToHost, c->stream));
       EW_CHECK(hipEventRecord(c->ev1, c->stream));
       if ((rc = sync_small(c))) return rc;
-      fast = !c->h_small->segbad && !c->h_small->gapslow && !c->h_small->nonmono && !c->h_small->nunrec;
+      // split byte fields (no side arena in the batch) go one by one too
+      fast = !c->h_small->segbad && !c->h_small->gapslow && !c->h_small->nonmono && !c->h_small->nunrec &&
+             !c->h_small->ncatfail;
       if (!fast && std::getenv("EWAL_DEBUG"))
         std::fprintf(stderr, "ewal batch: one by one (segbad %u gapslow %u nonmono %u nunrec %u)\n",
                      c->h_small->segbad, c->h_small->gapslow, c->h_small->nonmono, c->h_small->nunrec);
@@ -1385,6 +1416,7 @@ static int readall_batch_impl(ewal_ctx *c, const uint8_t *d_buf, uint32_t ns, co
         EW_CHECK(hipEventElapsedTime(&str_ms, c->evs0, c->evs1));
         c->bunrec.assign(ns, {});
         c->bunrec_bytes.assign(ns, {});
+        c->bsplit_bytes.assign(ns, {});
         for (uint32_t i = 0; i < ns; ++i) {
           out[i].device_ms = dev_ms;
           out[i].stream_ms = str_ms;
@@ -1693,6 +1725,24 @@ int64_t ewal_copy_unrec_bytes(ewal_ctx *c, uint8_t *out, int64_t cap) {
   return n;
 }
 
+int64_t ewal_copy_split_bytes(ewal_ctx *c, uint8_t *out, int64_t cap) {
+  if (!c || (!out && cap) || cap < 0) return EWAL_E_INVAL;
+  const int64_t n = std::min<int64_t>(cap, (int64_t)c->cat_bytes);
+  if (n > 0) {
+    EW_CHECK(hipSetDevice(c->device));
+    EW_CHECK(hipMemcpy(out, c->cat.p, (size_t)n, hipMemcpyDeviceToHost));
+  }
+  return (int64_t)c->cat_bytes;
+}
+
+int64_t ewal_batch_copy_split_bytes(ewal_ctx *c, uint64_t shard, uint8_t *out, int64_t cap) {
+  if (!c || (!out && cap) || cap < 0 || shard >= c->bsplit_bytes.size()) return EWAL_E_INVAL;
+  const std::vector<uint8_t> &b = c->bsplit_bytes[shard];
+  const int64_t n = std::min<int64_t>(cap, (int64_t)b.size());
+  if (n > 0) std::memcpy(out, b.data(), (size_t)n);
+  return (int64_t)b.size();
+}
+
 // The last ReadAll's per-frame descriptors in c->rd (rebuilt when the fused
 // pass decided it); EWAL_E_INVAL when another call took the state they come from.
 static int need_records(ewal_ctx *c) {
@@ -1751,15 +1801,17 @@ int ewal_copy_range_info(ewal_ctx *c, ewal_range_info *out) {
       EW_CHECK(frame(h.md_first, &d));
       o.md_first_frame = (int64_t)h.md_first;
       if (!d.dnil && d.dlen) {
-        o.md_first_off = (int64_t)d.doff;
+        o.md_first_off = (int64_t)(d.pad0 == 2 ? rd_cat_off(d) : d.doff);
         o.md_first_len = (int64_t)d.dlen;
+        if (d.pad0 == 2) o.md_split |= 1;
       }
     }
     if (h.md_value != ~0ull) {
       EW_CHECK(frame(h.md_value, &d));
       o.md_value_frame = (int64_t)h.md_value;
-      o.md_value_off = (int64_t)d.doff;
+      o.md_value_off = (int64_t)(d.pad0 == 2 ? rd_cat_off(d) : d.doff);
       o.md_value_len = (int64_t)d.dlen;
+      if (d.pad0 == 2) o.md_split |= 2;
     }
     if (h.ent_first != ~0ull) {
       EW_CHECK(frame(h.ent_first, &d));

@@ -54,9 +54,14 @@ struct RecDesc {
   uint64_t edoff, edlen;   // Entry.Data
   int32_t etype;           // Entry.Type
   uint8_t dnil, enil;
-  uint8_t pad0;            // Record.Data in several segments (their concatenation)
-  uint8_t pad1;            // the Entry / HardState carries XXX_unrecognized
+  uint8_t pad0;            // Record.Data in several segments: 1 not decoded (no room in the side arena),
+                           // 2 decoded from their concatenation in the side arena (rd_cat_off)
+  uint8_t pad1;            // bit 0: the Entry / HardState carries XXX_unrecognized;
+                           // bit 1: Entry.Data lives in the side arena at edoff (a concatenation)
 };
+// Where the side arena holds a split Record.Data (pad0 == 2): entries keep
+// it in f2 (unused by Entry), metadata / HardState frames in edoff.
+__host__ __device__ inline uint64_t rd_cat_off(const RecDesc &d) { return d.type == 2 ? d.f2 : d.edoff; }
 
 struct ChainInfo {
   uint32_t last_cand;      // candidate index of the chain's last frame
@@ -140,6 +145,12 @@ struct Small {
   uint32_t nunrec;                // k_check: entry ops carrying XXX_unrecognized (listed in ulist)
   uint32_t fc_done;               // k_fc_seam workgroups done (the last one gathers the result)
   FcAgg fc;
+  // the side arena of split byte fields (Go's append over repeated
+  // Record.Data / Entry.Data segments, record.pb.go:112, raft.pb.go:254)
+  unsigned long long cat_used;    // bytes handed out
+  unsigned long long cat_need;    // bytes a frame wanted past the arena's capacity
+  uint32_t ncatfail;              // frames left undecoded for want of room (the host grows the arena, reruns)
+  uint32_t pad_cat;
 };
 
 // A returned Entry (ent = its index in ents) or the HardState (ent = -1)
@@ -159,4 +170,6 @@ struct ResultDev {
   uint64_t klast;
   uint32_t nslow, gapslow;
   uint32_t errflag, nunrec;
+  unsigned long long cat_used, cat_need;
+  uint32_t ncatfail, pad;
 };

@@ -47,9 +47,14 @@ __device__ __forceinline__ void store_entry_nt(ewal_entry *dst, const ewal_entry
   __builtin_nontemporal_store(((uint64_t)(uint32_t)e.data_nil << 32) | (uint32_t)e.type, q + 4);
 }
 
+#ifndef FC_THREADS
 #define FC_THREADS 256
+#endif
 #define FC_WAVES (FC_THREADS / 64)
+#ifndef FC_WGS
 #define FC_WGS 3          // resident workgroups per CU (LDS ~49 KiB each)
+#endif
+#define FC_OCC (FC_WGS * FC_WAVES / 4)   // waves per SIMD (the VGPR budget: 512 / FC_OCC)
 #define FC_TILE 64        // frames per tile: one wave's, no workgroup barrier in the frame loop
 
 // Per tile, for k_fc_seam: its entry ops (count, frames and Index of the
@@ -264,7 +269,7 @@ __device__ RecDesc fc_frame_fields(const uint8_t *__restrict__ buf, uint64_t B, 
 }
 
 template <bool SEG>
-__global__ __launch_bounds__(FC_THREADS, FC_WGS) void k_fc(FcArgs a, SegArgs sg) {
+__global__ __launch_bounds__(FC_THREADS, FC_OCC) void k_fc(FcArgs a, SegArgs sg) {
   __shared__ uint32_t s_t4[16 * 256];          // slicing-by-16
   __shared__ uint32_t s_svp[1024];             // S_256 (prefix Horner step)
   __shared__ uint32_t s_nib[FC_NIB_LEVELS * 128];   // S_{2^0} .. S_{2^16}, nibble tables (the seed shift)

@@ -1332,6 +1332,79 @@ __device__ uint32_t bytes_field_lin(const P &p, int64_t l, uint32_t fnum, uint64
   return lin;
 }
 
+// ---- split byte fields: the side arena ------------------------------------
+// A bytes field repeated with several non-empty segments is, in Go, their
+// concatenation (`m.Data = append(m.Data, data[i:post]...)`, record.pb.go:112,
+// raft.pb.go:254).  Such frames (crafted: etcd's encoder writes each field
+// once) get the concatenation gathered into a ctx-owned side arena, and every
+// view into it is an offset there.  ~0: no room (Small.ncatfail, cat_need:
+// the host grows the arena and runs the call again).
+__device__ __forceinline__ uint64_t cat_alloc(uint8_t *cat, uint64_t catcap, Small *ds, uint64_t n) {
+  const uint64_t co = atomicAdd(&ds->cat_used, (unsigned long long)n);
+  if (cat == nullptr || co + n > catcap) {
+    atomicMax(&ds->cat_need, (unsigned long long)(co + n));
+    atomicAdd(&ds->ncatfail, 1u);
+    return ~0ull;
+  }
+  return co;
+}
+// Every non-empty segment of bytes field fnum of message m (l bytes), in
+// order, to dst (one thread; rare).  kvar / kbytes: the message's varint /
+// bytes fields (pb_each's wire-type rule).
+__device__ __forceinline__ void cat_gather(uint8_t *dst, const uint8_t *m, int64_t l, uint32_t fnum, uint32_t kvar,
+                                           uint32_t kbytes) {
+  uint64_t w = 0;
+  pb_each(m, l, fnum, kvar, kbytes, [&](bool b, uint64_t off, uint64_t len) {
+    if (!b) return;
+    for (uint64_t k = 0; k < len; ++k) dst[w + k] = m[off + k];
+    w += len;
+  });
+}
+// Entry.Data split inside an Entry message at m (l bytes): its concatenation
+// (total bytes) to the side arena; edoff then indexes the arena (pad1 bit 1).
+__device__ __forceinline__ void entry_data_cat(const uint8_t *m, int64_t l, uint64_t total, uint8_t *cat,
+                                               uint64_t catcap, Small *ds, RecDesc &d) {
+  const uint64_t co = cat_alloc(cat, catcap, ds, total);
+  if (co == ~0ull) {
+    d.sub_st = 48;
+    return;
+  }
+  cat_gather(cat + co, m, l, 4, 0xeu, 0x10u);
+  d.edoff = co;
+  d.edlen = total;
+  d.enil = 0;
+  d.pad1 |= 2;
+}
+// The metadata / Entry / HardState of a Record whose Data is the n bytes at
+// arena offset co (mustUnmarshalEntry / mustUnmarshalState, wal/decoder.go:61-77);
+// the Entry's Data is then a range of the arena too.
+__device__ __forceinline__ void decode_inner(const uint8_t *m, int64_t n, uint64_t co, uint8_t *cat,
+                                             uint64_t catcap, Small *ds, RecDesc &d) {
+  if (d.type == 2) {
+    PbField e1, e2, e3, e4, e5;
+    pbf_init(e1); pbf_init(e2); pbf_init(e3); pbf_init(e4); pbf_init(e5);
+    int ur = 0;
+    const int s2 = pb_walk<PB_VAR32, PB_VAR64, PB_VAR64, PB_BYTES, PB_NONE>(m, n, e1, e2, e3, e4, e5, ur, nullptr,
+                                                                          nullptr, 0);
+    d.pad1 = (s2 == 0 && ur) ? 1 : 0;
+    d.sub_st = s2;
+    d.etype = (int32_t)(uint32_t)e1.v;
+    d.f0 = e2.v;
+    d.f1 = e3.v;
+    if (e4.blen > 0) { d.edoff = co + (uint64_t)e4.boff; d.edlen = (uint64_t)e4.blen; d.enil = 0; d.pad1 |= 2; }
+    if (s2 == 0 && e4.split) entry_data_cat(m, n, (uint64_t)e4.blen, cat, catcap, ds, d);
+  } else if (d.type == 3) {
+    PbField h1, h2, h3, h4, h5;
+    pbf_init(h1); pbf_init(h2); pbf_init(h3); pbf_init(h4); pbf_init(h5);
+    int ur = 0;
+    const int s2 = pb_walk<PB_VAR64, PB_VAR64, PB_VAR64, PB_NONE, PB_NONE>(m, n, h1, h2, h3, h4, h5, ur, nullptr,
+                                                                         nullptr, 0);
+    d.pad1 = (s2 == 0 && ur) ? 1 : 0;
+    d.sub_st = s2;
+    d.f0 = h1.v; d.f1 = h2.v; d.f2 = h3.v;
+  }
+}
+
 // General decode of frame r (any encoding the reference accepts): the
 // gogoprotobuf walkers over an LDS copy of the frame head, and P at its frame
 // start and data start:
@@ -1344,7 +1417,8 @@ __device__ __forceinline__ void decode_general(const uint8_t *__restrict__ buf, 
                                                const uint32_t *__restrict__ v, const uint32_t *s_t4,
                                                const uint32_t *s_svp, const uint32_t *__restrict__ g_shift,
                                                uint4 (&win)[5], RecDesc *__restrict__ rd,
-                                               uint32_t *__restrict__ pfd, uint32_t *__restrict__ pfo) {
+                                               uint32_t *__restrict__ pfd, uint32_t *__restrict__ pfo,
+                                               uint8_t *__restrict__ cat, uint64_t catcap, Small *ds) {
   const uint64_t p16 = p & ~15ull;
 #pragma unroll
   for (int k = 0; k < 5; ++k) {
@@ -1383,9 +1457,19 @@ __device__ __forceinline__ void decode_general(const uint8_t *__restrict__ buf, 
     pfo[r] = prefix_at(p, pwave, v, buf, s_t4, s_svp);
     pfd[r] = 0;
     d.chained = bytes_field_lin(R + 8, L, 3, p + 8, buf, pwave, v, s_t4, s_svp, g_shift);
-    // metadata / Entry / HardState over the concatenation are not decoded
-    // here: reported (EWAL_UNSUPPORTED_ENCODING) when the CRC holds
-    d.sub_st = 48;
+    // Go's Data is the concatenation (`m.Data = append(m.Data, ...)`,
+    // record.pb.go:112): gathered into the side arena, and the metadata /
+    // Entry / HardState decoded from it there
+    const uint64_t co = cat_alloc(cat, catcap, ds, (uint64_t)a3.blen);
+    if (co == ~0ull) {   // no room: left undecoded (the host grows the arena and runs the call again)
+      d.sub_st = 48;
+      rd[r] = d;
+      return;
+    }
+    cat_gather(cat + co, buf + p + 8, L, 3, 0x6u, 0x8u);
+    decode_inner(cat + co, (int64_t)a3.blen, co, cat, catcap, ds, d);
+    d.pad0 = 2;
+    if (d.type == 2) d.f2 = co; else d.edoff = co;   // rd_cat_off
     rd[r] = d;
     return;
   }
@@ -1404,6 +1488,7 @@ __device__ __forceinline__ void decode_general(const uint8_t *__restrict__ buf, 
       d.f0 = e2.v;                  // Term
       d.f1 = e3.v;                  // Index
       if (e4.blen > 0) { d.edoff = d.doff + e4.boff; d.edlen = e4.blen; d.enil = 0; }
+      if (s2 == 0 && e4.split) entry_data_cat(buf + d.doff, (int64_t)d.dlen, (uint64_t)e4.blen, cat, catcap, ds, d);
     } else if (d.type == 3) {    // stateType: mustUnmarshalState
       PbField h1, h2, h3, h4, h5;
       pbf_init(h1); pbf_init(h2); pbf_init(h3); pbf_init(h4); pbf_init(h5);
@@ -1435,10 +1520,12 @@ __device__ __forceinline__ void decode_general(const uint8_t *__restrict__ buf, 
 // count (rec_cand == nullptr: frame r is candidate r).
 __global__ __launch_bounds__(256) void k_decode_slow(const uint8_t *__restrict__ buf, uint64_t B,
                          const uint64_t *__restrict__ pos, const uint32_t *__restrict__ rec_cand,
-                         const uint32_t *__restrict__ slow, const Small *ds, const uint32_t *__restrict__ pwave,
+                         const uint32_t *__restrict__ slow, Small *dsw, const uint32_t *__restrict__ pwave,
                          const uint32_t *__restrict__ v, const uint32_t *__restrict__ g_slice,
                          const uint32_t *__restrict__ g_shift, RecDesc *__restrict__ rd, uint32_t *__restrict__ pfd,
-                         uint32_t *__restrict__ pfo, uint32_t n_host) {
+                         uint32_t *__restrict__ pfo, uint32_t n_host, uint8_t *__restrict__ cat,
+                         uint64_t catcap) {
+  Small *ds = dsw;
   const uint32_t ns = ds->nslow;
   if (ns == 0) return;
   // frames on the chain: the host's count, or the device's candidate count (k_frame)
@@ -1453,7 +1540,7 @@ __global__ __launch_bounds__(256) void k_decode_slow(const uint8_t *__restrict__
     const uint32_t r = slow[j];
     const uint64_t p = pos[rec_cand ? rec_cand[r] : r];
     decode_general(buf, B, p, (int64_t)ld_le64_b(buf, B, p), r, n, pwave, v, s_t4, s_svp, g_shift, s_win[threadIdx.x],
-                   rd, pfd, pfo);
+                   rd, pfd, pfo, cat, catcap, ds);
   }
 }
 
@@ -1499,7 +1586,10 @@ __device__ bool walk_passes(const uint8_t *__restrict__ buf, uint64_t x, int64_t
     computed = gshift_n(g_shift, (uint64_t)a3.blen, seed ^ 0xffffffffu ^ Ps) ^ Pe ^ 0xffffffffu;
   }
   if (computed != *crc) return false;                   // walpb.ErrCRCMismatch
-  if (a3.split) return false;                           // k_check reports it (not decoded here)
+  // Data in several segments: the frame is listed and decoded from their
+  // concatenation later (k_decode_slow); walking on past it costs only walk
+  // steps when its Entry / HardState then fails (k_check finds the first failure)
+  if (a3.split) return type == 1 || type == 2 || type == 3;
   if (type == 1) return true;
   if (type != 2 && type != 3) return false;             // unexpected block type
   if (a3.blen <= 0) return true;                        // Unmarshal(nil): the zero message
@@ -2141,13 +2231,14 @@ __global__ __launch_bounds__(1024) void k_check(const uint32_t *__restrict__ g_s
     ewal_entry e;
     e.term = d.f0;
     e.index = d.f1;
-    e.data_off = SEG ? d.edoff - sg.soff[sh] : d.edoff;
+    const bool side = (d.pad1 & 2) != 0;   // Data is a range of the side arena (split segments)
+    e.data_off = (SEG && !side) ? d.edoff - sg.soff[sh] : d.edoff;
     e.data_len = d.edlen;
     e.type = d.etype;
-    e.data_nil = d.enil;
+    e.data_nil = side ? 2 : d.enil;
     ents[j] = e;
     if (SEG && !wg1 && bsh == 0) atomicMin(&sg.sagg[sh].ent_first, (unsigned long long)j);   // the shard's first op in the wave
-    if (d.pad1) sg.ulist[atomicAdd(&ds->nunrec, 1u)] = make_uint2(r, j);   // rare: Entry.XXX_unrecognized
+    if (d.pad1 & 1) sg.ulist[atomicAdd(&ds->nunrec, 1u)] = make_uint2(r, j);   // rare: Entry.XXX_unrecognized
   }
 }
 
@@ -2227,7 +2318,7 @@ __global__ void k_export_small(const Small *ds, Small *h) {
 // gathers the result.
 __global__ __launch_bounds__(256) void k_result(const uint8_t *__restrict__ buf, RecDesc *__restrict__ rd,
                                                 const uint32_t *__restrict__ mlist, uint32_t n, uint64_t ri, Small *ds,
-                                                ResultDev *o, const uint32_t *n_dev = nullptr) {
+                                                ResultDev *o, const uint32_t *n_dev, const uint8_t *__restrict__ cat) {
   if (n_dev) {   // speculative launch (see k_check): nothing to gather when it failed
     n = *n_dev;
     if (n == 0) return;
@@ -2241,7 +2332,10 @@ __global__ __launch_bounds__(256) void k_result(const uint8_t *__restrict__ buf,
       RecDesc &d = rd[r];
       const RecDesc &m = rd[fm];
       bool eq = (d.dlen == m.dlen);
-      for (uint64_t k = 0; eq && k < d.dlen; ++k) eq = buf[d.doff + k] == buf[m.doff + k];
+      // a split Data is its concatenation in the side arena
+      const uint8_t *da = d.pad0 == 2 ? cat + rd_cat_off(d) : buf + d.doff;
+      const uint8_t *ma = m.pad0 == 2 ? cat + rd_cat_off(m) : buf + m.doff;
+      for (uint64_t k = 0; eq && k < d.dlen; ++k) eq = da[k] == ma[k];
       if (!eq) {
         d.st = EWAL_ERR_METADATA_CONFLICT;
         atomicMin(&ds->agg.first_fail, (unsigned long long)r);
@@ -2260,6 +2354,9 @@ __global__ __launch_bounds__(256) void k_result(const uint8_t *__restrict__ buf,
   o->gapslow = ds->gapslow;
   o->errflag = ds->errflag;
   o->nunrec = ds->nunrec;
+  o->cat_used = ds->cat_used;
+  o->cat_need = ds->cat_need;
+  o->ncatfail = ds->ncatfail;
   if (g.first_fail < n) o->fail = rd[g.first_fail];
   if (g.last_entry >= 0) o->lastent = rd[g.last_entry];
   if (n) o->last = rd[n - 1];
@@ -2395,7 +2492,7 @@ __global__ void k_ents(const RecDesc *__restrict__ rd, const uint32_t *__restric
     e.data_off = d.edoff;
     e.data_len = d.edlen;
     e.type = d.etype;
-    e.data_nil = d.enil;
+    e.data_nil = (d.pad1 & 2) ? 2 : d.enil;   // 2: a range of the side arena
     ents[k] = e;
   }
 }
@@ -2406,11 +2503,11 @@ __global__ void k_ents(const RecDesc *__restrict__ rd, const uint32_t *__restric
 // data[iNdEx:iNdEx+skippy]...)` (raft/raftpb/raft.pb.go:270, :697).
 template <int PASS>
 __global__ void k_unrec(const uint8_t *__restrict__ buf, const RecDesc *__restrict__ rd, UnrecItem *__restrict__ it,
-                        uint32_t m, uint8_t *__restrict__ arena) {
+                        uint32_t m, uint8_t *__restrict__ arena, const uint8_t *__restrict__ cat) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= m) return;
   const RecDesc d = rd[it[i].r];
-  const uint8_t *dp = buf + d.doff;
+  const uint8_t *dp = d.pad0 == 2 ? cat + rd_cat_off(d) : buf + d.doff;   // a split Data: its concatenation
   uint64_t tot = 0;
   uint8_t *dst = PASS ? arena + it[i].off : nullptr;
   auto unk = [&](int64_t a, int64_t b) {

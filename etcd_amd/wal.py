@@ -150,11 +150,34 @@ class ReadAllResult:
                           for e in self.ents])
 
 
+def split_bytes(ctx, shard=None) -> bytes:
+    """The side bytes the last ReadAll gathered on the device for split byte
+    fields (Record.Data / Entry.Data repeated with several non-empty
+    segments): data_nil == 2 ents and EWAL_FLAG_METADATA_SPLIT metadata index
+    them (ewal_copy_split_bytes; a batched shard's: ewal_batch_copy_split_bytes)."""
+    if shard is None:
+        n = lib.ewal_copy_split_bytes(ctx.handle, None, 0)
+    else:
+        n = lib.ewal_batch_copy_split_bytes(ctx.handle, shard, None, 0)
+    check(0 if n >= 0 else int(n))
+    raw = (C.c_char * max(n, 1))()
+    if n:
+        got = (lib.ewal_copy_split_bytes(ctx.handle, raw, n) if shard is None
+               else lib.ewal_batch_copy_split_bytes(ctx.handle, shard, raw, n))
+        check(0 if got >= 0 else int(got))
+    return raw.raw[:n]
+
+
 def _collect(ctx, r, buf_view, with_ents=True, shard=None):
     ok = r.status == L.OK
     md = None
+    side = None                # the split bytes, fetched when a view needs them
     if ok and r.metadata_off >= 0:
-        md = bytes(buf_view[r.metadata_off:r.metadata_off + r.metadata_len])
+        if r.flags & L.FLAG_METADATA_SPLIT:
+            side = split_bytes(ctx, shard)
+            md = side[r.metadata_off:r.metadata_off + r.metadata_len]
+        else:
+            md = bytes(buf_view[r.metadata_off:r.metadata_off + r.metadata_len])
     st = HardState(r.state_term, r.state_vote, r.state_commit) if (ok and r.has_state) else HardState()
     ents = []
     if ok and with_ents and r.n_ents:
@@ -165,7 +188,12 @@ def _collect(ctx, r, buf_view, with_ents=True, shard=None):
             n = lib.ewal_batch_copy_entries(ctx.handle, shard, arr, r.n_ents)
         check(0 if n >= 0 else int(n))
         for e in arr[:n]:
-            data = None if e.data_nil else bytes(buf_view[e.data_off:e.data_off + e.data_len])
+            if e.data_nil == 2:    # a range of the split bytes
+                if side is None:
+                    side = split_bytes(ctx, shard)
+                data = side[e.data_off:e.data_off + e.data_len]
+            else:
+                data = None if e.data_nil else bytes(buf_view[e.data_off:e.data_off + e.data_len])
             ents.append(Entry(e.type, e.term, e.index, data))
     if ok and r.n_unrec:
         for ent, b in unrecognized(ctx, r.n_unrec, shard):
@@ -266,15 +294,17 @@ def range_info(ctx: Context, stream=None, dbuf: DeviceBuffer = None):
     ri = L.RangeInfo()
     check(lib.ewal_copy_range_info(ctx.handle, C.byref(ri)))
 
-    def data(off, n):
+    def data(off, n, split):
         if off < 0:
             return None
+        if split:   # a metadata Data in several segments: its concatenation, gathered on the device
+            return split_bytes(ctx)[off:off + n]
         if stream is not None:
             return bytes(stream[off:off + n])
         return dbuf.download(n, off) if n else b""
     return dict(n_frames=ri.n_frames, first_crc=ri.first_crc, md_first_frame=ri.md_first_frame,
-                md_first=data(ri.md_first_off, ri.md_first_len) if ri.md_first_frame >= 0 else None,
-                md_value=data(ri.md_value_off, ri.md_value_len) if ri.md_value_frame >= 0 else None,
+                md_first=data(ri.md_first_off, ri.md_first_len, ri.md_split & 1) if ri.md_first_frame >= 0 else None,
+                md_value=data(ri.md_value_off, ri.md_value_len, ri.md_split & 2) if ri.md_value_frame >= 0 else None,
                 md_value_frame=ri.md_value_frame, first_entry_frame=ri.first_entry_frame,
                 first_entry_index=ri.first_entry_index, min_entry_index=ri.min_entry_index,
                 last_entry_index=ri.last_entry_index, last_op_frame=ri.last_op_frame,

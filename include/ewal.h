@@ -44,8 +44,8 @@ enum {
   EWAL_PANIC_STATE = 35,           /* mustUnmarshalState     wal/decoder.go:71-77 */
   EWAL_PANIC_INDEX_GAP = 36,       /* ents[:e.Index-ri] past len wal/wal.go:173 */
   EWAL_NONTERMINATING = 37,        /* the reference never returns */
-  EWAL_UNSUPPORTED_ENCODING = 48,  /* a record the GPU decoder does not handle yet
-                                      (non-canonical protobuf); reported, never guessed */
+  EWAL_UNSUPPORTED_ENCODING = 48,  /* protobuf groups nested deeper than the device
+                                      walker's stack; reported, never guessed */
   /* infrastructure (negative) */
   EWAL_E_HIP = -1,
   EWAL_E_INVAL = -2,
@@ -86,7 +86,13 @@ typedef struct ewal_result {
 } ewal_result;
 
 /* raftpb.Entry, raft/raftpb/raft.pb.go:100-106.  Data is a zero-copy
- * (offset,len) view of the stream; data_nil mirrors Go's nil slice. */
+ * (offset,len) view of the stream; data_nil mirrors Go's nil slice.
+ * data_nil == 2: Data is instead the range [data_off, data_off + data_len) of
+ * the split bytes (ewal_copy_split_bytes / ewal_batch_copy_split_bytes) -- the
+ * concatenation Go's append builds when the Entry's Data, or the Record.Data
+ * holding the Entry, is repeated with several non-empty segments
+ * (raft.pb.go:254, wal/walpb/record.pb.go:112; etcd's encoder never writes
+ * that, a crafted WAL can). */
 typedef struct ewal_entry {
   uint64_t term;
   uint64_t index;
@@ -156,6 +162,10 @@ int ewal_readall_device(ewal_ctx *ctx, const void *d_buf, uint64_t len, uint64_t
  * per-shard verdicts are in out[].  Replaces, per shard,
  * wal.OpenAtIndex(...).ReadAll() (wal/wal.go:108,164). */
 #define EWAL_FLAG_SHARD_FALLBACK 1
+/* ewal_result.flags: metadata_off / metadata_len index the split bytes (the
+ * metadata record's Data repeated with several non-empty segments), not the
+ * stream */
+#define EWAL_FLAG_METADATA_SPLIT 2
 int ewal_readall_batch_device(ewal_ctx *ctx, const void *d_buf, uint64_t n_shards, const uint64_t *lens,
                               const uint64_t *ri, ewal_result *out);
 /* After ewal_readall_batch_device: shard s's ents (Data offsets relative to
@@ -190,6 +200,12 @@ int64_t ewal_copy_records(ewal_ctx *ctx, ewal_record *out, int64_t cap);
  * and its bytes. */
 int64_t ewal_copy_unrec(ewal_ctx *ctx, ewal_unrec *out, int64_t cap);
 int64_t ewal_copy_unrec_bytes(ewal_ctx *ctx, uint8_t *out, int64_t cap);
+/* After a successful readall: the split bytes the data_nil == 2 ents and an
+ * EWAL_FLAG_METADATA_SPLIT metadata index (gathered on the device).  Copies
+ * min(cap, total) bytes; returns the total (0: none) or a negative error.
+ * The batched form: shard s's (a shard with split fields is replayed alone). */
+int64_t ewal_copy_split_bytes(ewal_ctx *ctx, uint8_t *out, int64_t cap);
+int64_t ewal_batch_copy_split_bytes(ewal_ctx *ctx, uint64_t shard, uint8_t *out, int64_t cap);
 
 /* What one rank's range of ONE WAL split by file contributes to the joined
  * verdict (etcd_amd/shard.py split_verdict applies ReadAll's
@@ -218,6 +234,9 @@ typedef struct ewal_range_info {
   int64_t last_op_frame;         /* the last entry frame with Index >= the ReadAll's ri (the last
                                     append to ents, wal/wal.go:171-173), -1: none */
   uint64_t last_op_index;
+  int32_t md_split;              /* bit 0: md_first_off, bit 1: md_value_off index the split bytes
+                                    (ewal_copy_split_bytes: a metadata Data in several segments) */
+  int32_t pad;
 } ewal_range_info;
 int ewal_copy_range_info(ewal_ctx *ctx, ewal_range_info *out);
 

@@ -149,8 +149,17 @@ int main(int argc, char **argv) {
   uint32_t udg = 0;
   uint64_t md_len = 0;
   const uint8_t *md = NULL;
+  uint8_t *split = NULL;   /* split byte fields' concatenations (data_nil == 2, EWAL_FLAG_METADATA_SPLIT) */
   if (rc == EWAL_OK) {
-    if (r.metadata_off >= 0) { md = buf + r.metadata_off; md_len = (uint64_t)r.metadata_len; }
+    const int64_t ns = ewal_copy_split_bytes(ctx, NULL, 0);
+    if (ns > 0) {
+      split = (uint8_t *)malloc((size_t)ns);
+      ewal_copy_split_bytes(ctx, split, ns);
+    }
+    if (r.metadata_off >= 0) {
+      md = ((r.flags & EWAL_FLAG_METADATA_SPLIT) ? split : buf) + r.metadata_off;
+      md_len = (uint64_t)r.metadata_len;
+    }
     if (r.n_ents > 0) {
       ewal_entry *ds = (ewal_entry *)malloc(sizeof(ewal_entry) * (size_t)r.n_ents);
       n = ewal_copy_entries(ctx, ds, r.n_ents);
@@ -159,7 +168,9 @@ int main(int argc, char **argv) {
         ents[i].type = ds[i].type;
         ents[i].term = ds[i].term;
         ents[i].index = ds[i].index;
-        ents[i].data = ds[i].data_nil ? NULL : buf + ds[i].data_off;   /* zero-copy view */
+        ents[i].data = ds[i].data_nil == 0 ? buf + ds[i].data_off      /* zero-copy view */
+                       : ds[i].data_nil == 2 ? split + ds[i].data_off   /* a split field's concatenation */
+                       : NULL;
         ents[i].len = ds[i].data_len;
         ents[i].unrec = NULL;
         ents[i].unrec_len = 0;
@@ -209,6 +220,7 @@ int main(int argc, char **argv) {
          t_open - t0, t2 - t0, t3 - t2, t4 - t3, t5 - t4, t5 - t0, r.device_ms);
   for (int64_t i = 0; i < n; i++) free(ents[i].unrec);
   free(state_unrec);
+  free(split);
   free(ents);
   ewal_wal_close(w);
   ewal_ctx_destroy(ctx);
