@@ -147,8 +147,8 @@ def run_shards(a, dist, rank, world, local, cpu_seconds=None):
     The verdicts cross ranks in one all-reduce (etcd_amd/shard.py).  The
     shards are generated and copied to HBM 64 at a time (host memory stays
     at ~4 GiB per rank).  `torn5`: the same batch with the last frame of 5
-    shards torn (a crash mid-write): those 5 are replayed alone, the other
-    507 keep the batch's pass (wal/decoder.go:30-36)."""
+    shards torn (a crash mid-write): the batch's own pass classifies their
+    terminal (wal/decoder.go:30-36), no shard is replayed alone."""
     nsh, smib = a.shards_per_gpu, a.shard_mib
     cpu_seconds = a.cpu_seconds if cpu_seconds is None else cpu_seconds
     first = rank * nsh
@@ -225,14 +225,14 @@ def run_shards(a, dist, rank, world, local, cpu_seconds=None):
         tstep()
     for i, x in enumerate(c_out):
         if i in torn:
-            assert x.status == L.ERR_UNEXPECTED_EOF and x.flags & L.FLAG_SHARD_FALLBACK, (i, x.status, x.flags)
+            assert x.status == L.ERR_UNEXPECTED_EOF and not x.flags & L.FLAG_SHARD_FALLBACK, (i, x.status, x.flags)
         else:
             want = (L.ERR_RECORD_CRC, 1000) if first + i == bad_shard else (L.OK, -1)
             assert (x.status, x.fail_record) == want and not x.flags & L.FLAG_SHARD_FALLBACK, (i, x.status)
     tms = timed(dist, a.steps, tstep) / a.steps * 1e3
     torn5 = {"ms_per_step": round(tms, 4), "vs_clean": round(tms / ms, 4), "torn_shards": torn,
-             "note": "the same batch with the last frame of 5 shards torn: they are replayed alone "
-                     "(EWAL_FLAG_SHARD_FALLBACK), every other shard keeps the batch's fused pass"}
+             "note": "the same batch with the last frame of 5 shards torn: the batch's fused pass gives "
+                     "their verdict (io.ErrUnexpectedEOF at the torn frame), no shard is replayed alone"}
     del tmem
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:

@@ -202,6 +202,8 @@ _SIGS = {
     "ecommit_batch_device": (C.c_int, [vp, C.c_uint64, vp, vp, vp, vp, vp, vp, vp, vp, vp, C.POINTER(C.c_double)]),
 }
 for _name, (_res, _args) in _SIGS.items():
+    if os.environ.get("EWAL_LIB_PATH") and not hasattr(lib, _name):
+        continue   # an older A/B build (tools/ab_run.py) without a newer entry point
     _f = getattr(lib, _name)
     _f.restype = _res
     _f.argtypes = _args

@@ -319,9 +319,19 @@ static int run_stream(ewal_ctx *c, DevTables *tb, const uint8_t *d_buf, uint64_t
   EW_CHECK(hipGetLastError());
   EW_CHECK(hipEventRecord(c->evs1, c->stream));
   if (find_cand && EW_SPLIT_CAND && !(EW_XS & 8))   // the exact tests on the flagged pieces -> slots, wcnt
-    hipLaunchKernelGGL(k_cand, dim3(grid_for(nunits, 64 * EW_CAND_WAVES)), dim3(64 * EW_CAND_WAVES), 0, c->stream,
-                       d_buf, B, nunits, c->hmask.as<unsigned long long>(), c->slots.as<uint16_t>(),
-                       c->wcnt.as<uint32_t>());
+  {
+    // four groups of 64 units per wave while that still gives every CU 16
+    // waves (fewer, longer waves starve the CUs on small streams)
+    const bool g4 = (uint64_t)nunits >= (uint64_t)std::max(1, c->num_cu) * 16 * 64 * 4;
+    if (g4)
+      hipLaunchKernelGGL(k_cand<4>, dim3(grid_for(nunits, 64 * EW_CAND_WAVES * 4)), dim3(64 * EW_CAND_WAVES), 0,
+                         c->stream, d_buf, B, nunits, c->hmask.as<unsigned long long>(), c->slots.as<uint16_t>(),
+                         c->wcnt.as<uint32_t>());
+    else
+      hipLaunchKernelGGL(k_cand<1>, dim3(grid_for(nunits, 64 * EW_CAND_WAVES)), dim3(64 * EW_CAND_WAVES), 0,
+                         c->stream, d_buf, B, nunits, c->hmask.as<unsigned long long>(), c->slots.as<uint16_t>(),
+                         c->wcnt.as<uint32_t>());
+  }
   ScanArgs s;
   s.nunits = nunits;
   s.ntiles = nstiles;

@@ -85,6 +85,11 @@ struct ShardAgg {
   unsigned long long ent_first;   // global op index of the shard's first entry op (~0)
   uint32_t lastop;                // 1 + the shard's last entry-op frame (0: none)
   uint32_t bad;                   // fused pass: the shard is not on the regular path (replayed alone)
+  // fused pass: the shard's frame chain ends before the shard does (a torn
+  // tail after a crash, decoder.decode's terminal, wal/decoder.go:30-36)
+  uint32_t term1;                 // 1 + the batch frame that ends the shard's frames (0: none)
+  int32_t term_st;                // the terminal's class: EWAL_OK (clean io.EOF) or its error
+  uint64_t term_off;              // where it sits in the batch
 };
 // ewal_result.flags bit of a batched shard the fused pass could not decide
 // (internal: the host replays the shard alone and clears it)

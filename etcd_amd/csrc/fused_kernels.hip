@@ -368,7 +368,12 @@ __global__ __launch_bounds__(FC_THREADS, FC_OCC) void k_fc(FcArgs a, SegArgs sg)
       ri = sg.ri[sh];
     }
     bool bad = false;   // SEG: this frame takes its shard off the regular path (the host replays it alone)
-    if (live && !ok) {
+    // SEG: the shard's last candidate runs past the shard's end -- a torn
+    // tail (a crash mid-write): decoder.decode stops at its length prefix
+    // (io.ReadFull short, wal/decoder.go:30-36), so it is no frame of the
+    // shard; the shard's verdict is its terminal's (classify below)
+    const bool torn = SEG && live && r + 1 == sg.fs[sh + 1] && s > sg.soff[sh + 1];
+    if (live && !ok && !torn) {
       if (SEG) bad = true;
       else rare |= 1u;
     }
@@ -378,8 +383,33 @@ __global__ __launch_bounds__(FC_THREADS, FC_OCC) void k_fc(FcArgs a, SegArgs sg)
       d.doff = p + 8;
     }
     if (SEG) {
-      // a shard's frames are its candidates, the last one ending at the shard's end
-      if (live && (r + 1 == sg.fs[sh + 1] ? s != sg.soff[sh + 1] : pn != s)) bad = true;
+      // a shard's frames are its candidates, the last one ending at the
+      // shard's end -- or at decoder.decode's terminal inside it (a torn tail:
+      // fewer than 8 bytes, or a length the bytes left cannot hold)
+      if (live && r + 1 == sg.fs[sh + 1] && s != sg.soff[sh + 1]) {
+        const uint64_t E = sg.soff[sh + 1];
+        const uint64_t q = torn ? p : s;   // where the terminal sits
+        int tst;
+        if (E - q < 8) {
+          tst = EWAL_ERR_UNEXPECTED_EOF;
+        } else {
+          const int64_t Lq = torn ? L : (int64_t)ld_le64_b(a.buf, a.B, q);
+          const uint64_t rem = E - q - 8;
+          if (Lq < 0) tst = EWAL_PANIC_NEG_LENGTH;
+          else if ((uint64_t)Lq > rem) tst = rem == 0 ? EWAL_OK : EWAL_ERR_UNEXPECTED_EOF;
+          else tst = -1;   // a frame that fits but is no candidate: the general walk
+        }
+        if (tst < 0) {
+          bad = true;
+        } else {
+          ShardAgg *A = sg.sagg + sh;
+          A->term1 = (torn ? r : r + 1) + 1u;
+          A->term_st = tst;
+          A->term_off = q;
+        }
+      } else if (live && r + 1 < sg.fs[sh + 1] && pn != s) {
+        bad = true;
+      }
     } else {
       if (live && r + 1 < K32 && pn != s) irr = 1;
       if (live && r + 1 == K32) {   // the chain's terminal
@@ -393,8 +423,8 @@ __global__ __launch_bounds__(FC_THREADS, FC_OCC) void k_fc(FcArgs a, SegArgs sg)
     const uint32_t cprev = (uint32_t)__shfl_up((int)d.crc, 1);
     const uint32_t pnext = (uint32_t)__shfl_down((int)Pfo, 1);
     // decoder.decode's check + ReadAll's crc-record rule (as k_check)
-    const bool dfirst = lane == 0 && r > lo;
-    const bool dlast = live && r == rl && r + 1 < K32;
+    const bool dfirst = lane == 0 && r > lo && !torn;
+    const bool dlast = live && r == rl && r + 1 < K32 && !torn;
     const uint32_t seed = r > lo ? cprev : 0u;
     int st = 0;
     uint32_t chained = seed;
@@ -445,6 +475,10 @@ __global__ __launch_bounds__(FC_THREADS, FC_OCC) void k_fc(FcArgs a, SegArgs sg)
       }
     }
     if (a.ablate & 16) st = 0;   // timing only: no failure reports (keeps the ablations' verdict path alike)
+    if (torn) {   // no frame of its shard: no verdict, no type, no op
+      st = 0;
+      d.type = 0;
+    }
     if (dfirst || dlast) st = 0;
     else if (live && r + 1 == K32) ds->fc.last_chained = chained;
     // entry ops (wal/wal.go:170-176): the op's predecessor in the tile; the
@@ -790,6 +824,9 @@ __global__ void k_shard_start_fc(const uint64_t *__restrict__ cpos, uint64_t cca
   g.ent_first = ~0ull;
   g.lastop = 0;
   g.bad = soff[s + 1] > o && (a >= n || cpos[a] != o);   // the shard does not open on a candidate
+  g.term1 = 0;
+  g.term_st = 0;
+  g.term_off = 0;
   sagg[s] = g;
 }
 
@@ -833,7 +870,7 @@ __global__ __launch_bounds__(256) void k_result_batch_fc(const uint8_t *__restri
   if (in) {
     A = sg.sagg[s];
     f0 = sg.fs[s];
-    f1 = sg.fs[s + 1];
+    f1 = A.term1 ? A.term1 - 1u : sg.fs[s + 1];   // the shard's frames end at its terminal (a torn tail)
     long long fr = -1;
     switch (k) {
     case 0: fr = A.first_fail != ~0ull ? (long long)(A.first_fail >> 8) : -1; break;
@@ -856,7 +893,7 @@ __global__ __launch_bounds__(256) void k_result_batch_fc(const uint8_t *__restri
   o.fail_offset = -1;
   o.metadata_off = -1;
   o.n_records = (int64_t)(f1 - f0);
-  o.n_candidates = (int64_t)(f1 - f0);
+  o.n_candidates = (int64_t)(sg.fs[s + 1] - f0);
   o.n_runs = 1;
   unsigned long long ef = 0;
   if (A.first_fail != ~0ull) {
@@ -867,6 +904,10 @@ __global__ __launch_bounds__(256) void k_result_batch_fc(const uint8_t *__restri
     o.n_records = o.fail_record;
     if (o.status == EWAL_ERR_UNEXPECTED_TYPE) o.detail = D[0].type;
     if (o.status == EWAL_PANIC_INDEX_GAP) o.detail = (int64_t)D[0].f1;
+  } else if (A.term1 && A.term_st != EWAL_OK) {   // ReadAll returns decoder.decode's error (wal/wal.go:197-201)
+    o.status = A.term_st;
+    o.fail_record = (int64_t)(f1 - f0);
+    o.fail_offset = (int64_t)(A.term_off - so);
   } else {
     const uint64_t enti = A.last_entry >= 0 ? D[1].f1 : 0;
     o.enti = enti;

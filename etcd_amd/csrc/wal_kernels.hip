@@ -317,7 +317,8 @@ __device__ __forceinline__ void row_transpose(uint32_t (&D)[19]) {
 #endif
 #ifndef EW_XS
 #define EW_XS 0   // timing-only k_stream ablations (tools/): 1 no CRC, 2 no candidates, 4 no v stores,
-                  // 8 the candidate filter without the exact tests / slots; results are wrong
+                  // 8 the candidate filter without the exact tests / slots, 16 v stores only for
+                  // units with a flagged piece; results are wrong
 #endif
 template <int NU, bool FIND>
 __device__ __forceinline__ void stream_units(const StreamArgs &a, const uint8_t *s_slice, const uint32_t *s_s64,
@@ -354,10 +355,13 @@ __device__ __forceinline__ void stream_units(const StreamArgs &a, const uint8_t 
     c[i] ^= tab_apply(s_s128, top ? o : 0u);
   }
   // plain stores (measured a little faster than nontemporal ones here)
+  bool vskip[NU];   // EW_XS & 16 (timing only): no v[] for units without a flagged piece
+#pragma unroll
+  for (int i = 0; i < NU; ++i) vskip[i] = (EW_XS & 16) && FIND && __ballot(fm[i] != 0) == 0ull;
   if (top) {
 #pragma unroll
     for (int i = 0; i < NU; ++i)
-      if (!(EW_XS & 4) || c[i] == 0x12345678u) a.v[(uint64_t)u[i] * EW_VPU + (lane >> 2)] = c[i];
+      if ((!(EW_XS & 4) || c[i] == 0x12345678u) && !vskip[i]) a.v[(uint64_t)u[i] * EW_VPU + (lane >> 2)] = c[i];
   }
   if (!FIND) return;
   if (EW_SPLIT_CAND && !(EW_XS & 8)) {   // the flagged pieces, for k_cand
@@ -499,7 +503,7 @@ __global__ __launch_bounds__(EW_THREADS, 1) void k_stream(StreamArgs a) {
 // ===========================================================================
 // k_cand (EW_SPLIT_CAND): the exact frame-start test on the 64-B pieces
 // k_stream's filter flagged, and every unit's slots and candidate count.
-// One wave per 64 units: lane l reads unit l's mask, the wave lists the
+// One wave per 64 G units: lane l reads unit l's masks, the wave lists the
 // flagged pieces (unit, piece) in order in LDS, then takes them 64 at a
 // time -- each lane loads its piece plus the 12 bytes after it (80 B), runs
 // the filter and the exact tests, and places its candidates after those of
@@ -523,86 +527,125 @@ __device__ __forceinline__ void load_piece80(const uint8_t *buf, uint64_t B, uin
     for (int k = 0; k < 19; ++k) D[k] = load_word_guarded(buf, B, off + 4 * k);
   }
 }
+// G groups of 64 units per wave (G = 4 when the stream has enough units to
+// fill the GPU that way): the flagged pieces of consecutive groups share one
+// list of up to 4096 entries, so a sparse WAL's wave issues the piece loads of
+// 256 units in one round trip instead of four.
+template <int G>
 __global__ __launch_bounds__(EW_CAND_WAVES * 64) void k_cand(const uint8_t *__restrict__ buf, uint64_t B,
                                                              uint32_t nunits,
                                                              const unsigned long long *__restrict__ hmask,
                                                              uint16_t *__restrict__ slots,
                                                              uint32_t *__restrict__ wcnt) {
   __shared__ uint16_t s_list[EW_CAND_WAVES][64 * 64];
-  __shared__ uint32_t s_ucnt[EW_CAND_WAVES][64];
+  __shared__ uint32_t s_ucnt[EW_CAND_WAVES][64 * G];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const uint32_t u0 = (blockIdx.x * EW_CAND_WAVES + (uint32_t)wv) * 64;
-  const bool active = u0 < nunits;   // wave-uniform
+  const uint32_t u0 = (blockIdx.x * EW_CAND_WAVES + (uint32_t)wv) * 64 * G;   // the wave's first unit
   uint16_t *list = s_list[wv];
   uint32_t *ucnt = s_ucnt[wv];
-  const uint32_t ul = u0 + (uint32_t)lane;
-  const unsigned long long hm = (active && ul < nunits) ? hmask[ul] : 0ull;
-  const uint32_t pc = (uint32_t)__popcll(hm);
-  const uint32_t incl0 = wave_incl_sum(pc);
-  const uint32_t T = (uint32_t)__shfl((int)incl0, 63);
-  ucnt[lane] = 0;
-  {
-    uint32_t k = incl0 - pc;
-    unsigned long long m = hm;
-    while (m) {
-      const int b = __ffsll((long long)m) - 1;
-      m &= m - 1;
-      list[k++] = (uint16_t)((lane << 6) | b);
-    }
+  unsigned long long hm[G];
+  uint32_t pc[G], ex[G], Tg[G];
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    const uint32_t ul = u0 + 64 * g + (uint32_t)lane;
+    hm[g] = ul < nunits ? hmask[ul] : 0ull;
   }
-  __syncthreads();
-  // up to EW_CAND_PF rounds of pieces in flight at once, then processed in order
-  for (uint32_t rb = 0; rb < T; rb += 64 * EW_CAND_PF) {
-    uint32_t D[EW_CAND_PF][19], E[EW_CAND_PF];
 #pragma unroll
-    for (int k = 0; k < EW_CAND_PF; ++k) {
-      const uint32_t i = rb + 64 * k + (uint32_t)lane;
-      E[k] = i < T ? list[i] : 0xffffu;
-      if (i < T) {
-        load_piece80(buf, B, (uint64_t)(u0 + (E[k] >> 6)) * EW_WAVE_BYTES + (uint64_t)(E[k] & 63) * EW_PIECE, D[k]);
-      } else {
+  for (int g = 0; g < G; ++g) {
+    pc[g] = (uint32_t)__popcll(hm[g]);
+    const uint32_t incl = wave_incl_sum(pc[g]);
+    ex[g] = incl - pc[g];
+    Tg[g] = (uint32_t)__shfl((int)incl, 63);
+    ucnt[64 * g + lane] = 0;
+  }
+  // chunks of consecutive groups whose flagged pieces fit the list (a group
+  // alone always does: 64 units x 64 pieces); Tg are wave-uniform
+  uint32_t gb = 0;
+  while (gb < (uint32_t)G) {
+    uint32_t T = 0, ge = gb;
 #pragma unroll
-        for (int q = 0; q < 19; ++q) D[k][q] = 0u;
+    for (int g = 0; g < G; ++g)
+      if ((uint32_t)g == ge && ge < (uint32_t)G && T + Tg[g] <= 64 * 64) { T += Tg[g]; ++ge; }
+    if (T) {
+      uint32_t base = 0;
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+        if ((uint32_t)g < gb || (uint32_t)g >= ge) continue;
+        uint32_t k = base + ex[g];
+        unsigned long long m = hm[g];
+        while (m) {
+          const int b = __ffsll((long long)m) - 1;
+          m &= m - 1;
+          list[k++] = (uint16_t)(((64 * g + lane) << 6) | b);   // (unit in the wave, piece)
+        }
+        base += Tg[g];
       }
-    }
+      // the list and the counts are this wave's alone: a wave-level fence
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      // up to EW_CAND_PF rounds of pieces in flight at once, then processed in order
+      for (uint32_t rb = 0; rb < T; rb += 64 * EW_CAND_PF) {
+        uint32_t D[EW_CAND_PF][19], E[EW_CAND_PF];
 #pragma unroll
-    for (int k = 0; k < EW_CAND_PF; ++k) {
-      const uint32_t r0 = rb + 64 * k;
-      if (r0 >= T) break;   // wave-uniform
-      const uint32_t i = r0 + (uint32_t)lane;
-      const bool live = i < T;
-      const uint32_t e = E[k];
-      const uint32_t ulo = e >> 6, pcs = e & 63;
-      const uint64_t off = (uint64_t)(u0 + ulo) * EW_WAVE_BYTES + (uint64_t)pcs * EW_PIECE;
-      uint32_t pa = 0, pb = 0, cnt = 0;
-      if (live) {
-        const uint32_t fm = cand_filter(D[k]);
-        if (fm) cnt = find_cands(D[k], fm, off, B, pcs * EW_PIECE, pa, pb);
-      }
-      // segmented exclusive scan of cnt over the round (a unit's pieces are contiguous)
-      const uint32_t incl = wave_incl_sum(cnt);
-      const uint32_t prev = (uint32_t)__shfl_up((int)e, 1);
-      const bool head = lane == 0 || (prev >> 6) != ulo;
-      const unsigned long long H = __ballot(head);
-      const int hl = 63 - __clzll((long long)(H & (lane == 63 ? ~0ull : ((2ull << lane) - 1ull))));
-      const uint32_t before = (uint32_t)__shfl((int)incl, hl > 0 ? hl - 1 : 0);
-      const uint32_t base = (live ? ucnt[ulo] : 0u) + (incl - cnt - (hl > 0 ? before : 0u));
-      const uint32_t nxt = (uint32_t)__shfl_down((int)e, 1);
-      const bool last = live && (lane == 63 || i + 1 >= T || (nxt >> 6) != ulo);
-      if (last) ucnt[ulo] = base + cnt;
-      if (cnt) {
-        uint16_t *sl = slots + (size_t)(u0 + ulo) * EW_SLOTS;
-        if (cnt > 2) {
-          slot_cands(D[k], off, B, base, sl, pcs * EW_PIECE);
-        } else {
-          if (base < EW_SLOTS) sl[base] = (uint16_t)pa;
-          if (cnt >= 2 && base + 1 < EW_SLOTS) sl[base + 1] = (uint16_t)pb;
+        for (int k = 0; k < EW_CAND_PF; ++k) {
+          const uint32_t i = rb + 64 * k + (uint32_t)lane;
+          E[k] = i < T ? list[i] : 0xffffu;
+          if (i < T) {
+            load_piece80(buf, B, (uint64_t)(u0 + (E[k] >> 6)) * EW_WAVE_BYTES + (uint64_t)(E[k] & 63) * EW_PIECE,
+                         D[k]);
+          } else {
+#pragma unroll
+            for (int q = 0; q < 19; ++q) D[k][q] = 0u;
+          }
+        }
+#pragma unroll
+        for (int k = 0; k < EW_CAND_PF; ++k) {
+          const uint32_t r0 = rb + 64 * k;
+          if (r0 >= T) break;   // wave-uniform
+          const uint32_t i = r0 + (uint32_t)lane;
+          const bool live = i < T;
+          const uint32_t e = E[k];
+          const uint32_t ulo = e >> 6, pcs = e & 63;
+          const uint64_t off = (uint64_t)(u0 + ulo) * EW_WAVE_BYTES + (uint64_t)pcs * EW_PIECE;
+          uint32_t pa = 0, pb = 0, cnt = 0;
+          if (live) {
+            const uint32_t fm = cand_filter(D[k]);
+            if (fm) cnt = find_cands(D[k], fm, off, B, pcs * EW_PIECE, pa, pb);
+          }
+          // segmented exclusive scan of cnt over the round (a unit's pieces are contiguous)
+          const uint32_t incl = wave_incl_sum(cnt);
+          const uint32_t prev = (uint32_t)__shfl_up((int)e, 1);
+          const bool head = lane == 0 || (prev >> 6) != ulo;
+          const unsigned long long H = __ballot(head);
+          const int hl = 63 - __clzll((long long)(H & (lane == 63 ? ~0ull : ((2ull << lane) - 1ull))));
+          const uint32_t before = (uint32_t)__shfl((int)incl, hl > 0 ? hl - 1 : 0);
+          const uint32_t sbase = (live ? ucnt[ulo] : 0u) + (incl - cnt - (hl > 0 ? before : 0u));
+          const uint32_t nxt = (uint32_t)__shfl_down((int)e, 1);
+          const bool last = live && (lane == 63 || i + 1 >= T || (nxt >> 6) != ulo);
+          if (last) ucnt[ulo] = sbase + cnt;
+          if (cnt) {
+            uint16_t *sl = slots + (size_t)(u0 + ulo) * EW_SLOTS;
+            if (cnt > 2) {
+              slot_cands(D[k], off, B, sbase, sl, pcs * EW_PIECE);
+            } else {
+              if (sbase < EW_SLOTS) sl[sbase] = (uint16_t)pa;
+              if (cnt >= 2 && sbase + 1 < EW_SLOTS) sl[sbase + 1] = (uint16_t)pb;
+            }
+          }
+          __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+          __builtin_amdgcn_wave_barrier();
         }
       }
     }
+    gb = ge > gb ? ge : gb + 1;
   }
-  __syncthreads();
-  if (active && ul < nunits) wcnt[ul] = ucnt[lane];
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    const uint32_t ul = u0 + 64 * g + (uint32_t)lane;
+    if (ul < nunits) wcnt[ul] = ucnt[64 * g + lane];
+  }
 }
 
 // ===========================================================================
@@ -1836,11 +1879,13 @@ __device__ __forceinline__ bool decode_canon(const uint8_t *__restrict__ buf, ui
       d.f0 = f0; d.f1 = f1; d.f2 = f2;
     }
   }
-  if (!ok) return false;
+  // P at the frame start even when the frame is not canonical: the frame
+  // before it takes it as its P(data end) (a batched shard's torn last frame)
   if constexpr (NEAR)
     Pfo = noprefix ? pin.pw
                    : (pin.slow ? prefix_at(p, pwave, v, buf, s_t4, s_svp) : prefix_finish_near(pin, s_t4, s_svp, s_inv));
   else Pfo = noprefix ? pin.pw : prefix_finish16(pin, s_t4, s_svp);
+  if (!ok) return false;
   if (d.type != 4 && d.dlen > 0) {    // P(data start): the header bytes after P(frame start)
     uint32_t c = Pfo;
     const int nh = ho - base;
@@ -2397,6 +2442,9 @@ __global__ void k_shard_start(const RecDesc *__restrict__ rd, uint32_t n, const 
   g.ent_first = ~0ull;
   g.lastop = 0;
   g.bad = 0;
+  g.term1 = 0;
+  g.term_st = 0;
+  g.term_off = 0;
   sagg[s] = g;
 }
 

@@ -5,7 +5,7 @@ Every shard's batched result must equal the oracle's ReadAll of that shard
 alone (status, failing frame and offset, lastCRC, enti, metadata, HardState,
 ents, XXX_unrecognized), whichever path each shard took: the batch's fused
 pass (one stream pass and one frame + check pass for the whole batch) or,
-for a shard that pass cannot decide (torn or corrupt framing, an index
+for a shard that pass cannot decide (corrupt framing, an index
 rewind, unknown fields), its replay alone -- which must not take any other
 shard off the batch's path."""
 import random
@@ -121,15 +121,21 @@ def test_batch_random(ctx, seed):
 def test_batch_fallback_torn_and_rewind(ctx):
     rng = random.Random(11)
     base = [build_wal(rng, 30, 500, big_terms=False) for _ in range(6)]
-    # a torn shard in the middle: its chain runs into the next shard
+    # a torn shard in the middle: its last candidate runs into the next shard;
+    # the batch's pass classifies decoder.decode's terminal itself (no replay)
     torn = list(base)
     torn[2] = torn[2][:-5]
-    check_batch(ctx, torn, [0] * 6, fallback={2})
-    # a trailing bare length prefix (io.EOF) and a negative length
+    check_batch(ctx, torn, [0] * 6, fallback=set())
+    # a trailing bare length prefix (io.EOF), a negative length, 1-7 stray bytes
     t2 = list(base)
     t2[1] = t2[1] + struct.pack("<q", 77)
     t2[4] = t2[4] + struct.pack("<q", -5) + b"zz"
-    check_batch(ctx, t2, [0] * 6, fallback={1, 4})
+    t2[5] = t2[5] + b"\x01\x02\x03"
+    check_batch(ctx, t2, [0] * 6, fallback=set())
+    # a length that fits but no canonical head after it: the general walk (replayed alone)
+    t3 = list(base)
+    t3[0] = t3[0] + struct.pack("<q", 3) + b"\x00\x01\x02"
+    check_batch(ctx, t3, [0] * 6, fallback={0})
     # an index rewind (leader overwrite) needs the op-list path
     e = O.WalEncoder(0)
     e.save_crc(0)
@@ -147,13 +153,14 @@ def test_batch_fallback_torn_and_rewind(ctx):
     u.save_entry(0, 1, 1, b"plain")
     u.encode(3, O.hardstate_marshal(1, 2, 3) + bytes([0x20, 0x07]))
     mix = [base[0], torn[2], base[1], rw[3], t2[4], u.getvalue(), base[5]]
-    res = check_batch(ctx, mix, [0, 0, 0, 2, 0, 0, 0], fallback={1, 3, 4, 5})
+    res = check_batch(ctx, mix, [0, 0, 0, 2, 0, 0, 0], fallback={3, 5})
     assert res[5].ents[0].XXX_unrecognized == bytes([0x38, 0x05]) and res[5].state.XXX_unrecognized == bytes([0x20, 7])
 
 
 def test_batch_torn_shards_stay_local(ctx):
     """C3-shaped shards with torn tails in a few of them (a crash mid-write):
-    only those shards are replayed alone; the others keep the batch's pass."""
+    the batch's own pass gives their verdict (decoder.decode's terminal,
+    wal/decoder.go:30-36) -- no shard is replayed alone."""
     shards, want = [], []
     for s in range(24):
         buf, n = W.synth_wal(1 << 20, 128, 4096, seed=40 + s)
@@ -162,7 +169,7 @@ def test_batch_torn_shards_stay_local(ctx):
             b = b[:-(100 + s)]          # the last frame torn
         shards.append(b)
         want.append(n)
-    res = check_batch(ctx, shards, [1] * 24, fallback={3, 11, 17})
+    res = check_batch(ctx, shards, [1] * 24, fallback=set())
     for s in (3, 11, 17):
         assert res[s].status == L.ERR_UNEXPECTED_EOF and res[s].fail_record == want[s] - 1
 
