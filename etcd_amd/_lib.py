@@ -55,6 +55,7 @@ E_HIP, E_INVAL, E_NOMEM, E_NODEVICE, E_TIMEOUT, E_IO = -1, -2, -3, -4, -5, -6
 
 FLAG_SHARD_FALLBACK = 1   # ewal_readall_batch_device verified this shard on its own
 FLAG_METADATA_SPLIT = 2   # metadata_off / _len index the split bytes (ewal_copy_split_bytes)
+RANGE_DEFER_FIRST = 1     # ewal_readall_range_device: frame 0's CRC check is the caller's
 
 CASTAGNOLI, IEEE, KOOPMAN = 0x82F63B78, 0xEDB88320, 0xEB31D82E
 
@@ -114,7 +115,9 @@ class RangeInfo(C.Structure):   # ewal_range_info
                 ("md_value_off", C.c_int64), ("md_value_len", C.c_int64), ("first_entry_frame", C.c_int64),
                 ("last_entry_frame", C.c_int64), ("first_entry_index", C.c_uint64),
                 ("min_entry_index", C.c_uint64), ("last_entry_index", C.c_uint64), ("last_op_frame", C.c_int64),
-                ("last_op_index", C.c_uint64), ("md_split", C.c_int32), ("pad", C.c_int32)]
+                ("last_op_index", C.c_uint64), ("md_split", C.c_int32), ("pad", C.c_int32),
+                ("first_type", C.c_int64), ("first_dlen", C.c_uint64), ("first_stored_crc", C.c_uint32),
+                ("first_u0", C.c_uint32)]
 
 
 class SnapshotDesc(C.Structure):
@@ -158,6 +161,9 @@ _SIGS = {
     "ewal_copy_unrec": (C.c_int64, [vp, C.POINTER(UnrecDesc), C.c_int64]),
     "ewal_copy_unrec_bytes": (C.c_int64, [vp, vp, C.c_int64]),
     "ewal_copy_split_bytes": (C.c_int64, [vp, vp, C.c_int64]),
+    "ewal_readall_range_device": (C.c_int, [vp, vp, C.c_uint64, C.c_uint64, C.c_uint32, C.POINTER(Result)]),
+    "ewal_range_probe": (C.c_int, [vp, vp, C.c_uint64, C.c_uint64, C.c_uint64, C.POINTER(C.c_int64),
+                                   C.POINTER(C.c_int64)]),
     "ewal_batch_copy_split_bytes": (C.c_int64, [vp, C.c_uint64, vp, C.c_int64]),
     "ewal_open_at_index": (C.c_int, [C.c_char_p, C.c_uint64, C.POINTER(vp)]),
     "ewal_wal_readall": (C.c_int, [vp, vp, C.POINTER(Result)]),

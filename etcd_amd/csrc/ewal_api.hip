@@ -138,6 +138,8 @@ struct ewal_ctx {
   DevBuf cat;
   uint64_t cat_bytes = 0;
   bool cat_retry = false;
+  bool defer_first = false;   // ewal_readall_range_device: frame 0's CRC check is the caller's
+  bool last_deferred = false;
   std::vector<std::vector<uint8_t>> bsplit_bytes;   // per shard replayed alone: its split bytes
   // batched ReadAll (ewal_readall_batch_device): shard tables, results, ents
   DevBuf bfs, bsoff, bri, bsagg, bres, bef, bents, bshard, hmask;
@@ -695,6 +697,7 @@ static int readall_impl(ewal_ctx *c, const uint8_t *d_buf, uint64_t B, uint64_t 
   c->unrec_bytes = 0;
   c->cat_bytes = 0;
   c->rd_valid = false;
+  c->last_deferred = c->defer_first;
   c->last_buf = d_buf;
   c->last_B = B;
   c->last_ri = ri;
@@ -714,6 +717,7 @@ static int readall_impl(ewal_ctx *c, const uint8_t *d_buf, uint64_t B, uint64_t 
   bool regular = false;
   bool decoded = false;    // k_frame's speculative decode holds
   bool spec_checked = false;   // ... and k_check / k_result already ran behind it
+  bool fused_done_final = false;   // the fused pass decided the call (its result carries the stored CRCs)
   if (B > 0) {
     uint64_t ccap = cand_cap(B);
     EW_CHECK(c->cpos.ensure(ccap * 8));
@@ -723,6 +727,7 @@ static int readall_impl(ewal_ctx *c, const uint8_t *d_buf, uint64_t B, uint64_t 
                                                                  B / 4096 + 1024));
     rc = run_stream(c, tb, d_buf, B, 1, ccap);
     if (rc) return rc;
+    if (c->defer_first) EW_CHECK(hipMemsetAsync(&ds->defer_first, 1, 1, c->stream));   // (Small is zeroed by k_stream)
 #if EW_XS
     // timing-only ablation builds: the stream pass alone
     EW_CHECK(hipEventRecord(c->ev1, c->stream));
@@ -812,6 +817,7 @@ static int readall_impl(ewal_ctx *c, const uint8_t *d_buf, uint64_t B, uint64_t 
     }
     K = c->h_small->total;
     c->last_k = K;
+    fused_done_final = fused_done;
     if (fused_done) {   // frames decoded and checked by k_fc; the result is in h_res
       decoded = true;
       spec_checked = true;
@@ -1007,10 +1013,19 @@ static int readall_impl(ewal_ctx *c, const uint8_t *d_buf, uint64_t B, uint64_t 
     out->enti = enti;
     if (enti < ri) {
       out->status = EWAL_ERR_INDEX_NOT_FOUND;
+      // (Go returns no lastCRC with this error; a range of a split WAL still
+      // hands its running CRC to the next range, shard.split_verdict)
+      if (n) out->last_crc = (c->defer_first && n == 1 && !fused_done_final && res.last.type != 4)
+                                 ? res.last.crc : res.last.chained;
     } else {
       out->status = EWAL_OK;
       if (n) {
         out->last_crc = res.last.chained;
+        // a deferred frame 0 that is the range's only frame: the running CRC
+        // after it is its stored CRC once the caller's check holds (the
+        // general path's descriptor keeps crc32.Update(0, Data) for the range
+        // info; the fused pass reports the stored CRC itself)
+        if (c->defer_first && n == 1 && !fused_done_final && res.last.type != 4) out->last_crc = res.last.crc;
         if (hagg.first_meta != ~0ull) {
           out->metadata_off = (int64_t)(res.md.pad0 == 2 ? rd_cat_off(res.md) : res.md.doff);
           out->metadata_len = (int64_t)res.md.dlen;
@@ -1604,6 +1619,41 @@ int ewal_readall_device(ewal_ctx *c, const void *d_buf, uint64_t len, uint64_t r
   return readall_impl(c, (const uint8_t *)d_buf, len, ri, out);
 }
 
+int ewal_readall_range_device(ewal_ctx *c, const void *d_buf, uint64_t len, uint64_t ri, uint32_t flags,
+                              ewal_result *out) {
+  if (!c || !out || (!d_buf && len) || (flags & ~(uint32_t)EWAL_RANGE_DEFER_FIRST)) return EWAL_E_INVAL;
+  EW_CHECK(hipSetDevice(c->device));
+  c->defer_first = (flags & EWAL_RANGE_DEFER_FIRST) != 0;
+  const int rc = readall_impl(c, (const uint8_t *)d_buf, len, ri, out);
+  c->defer_first = false;
+  return rc;
+}
+
+int ewal_range_probe(ewal_ctx *c, const void *d_buf, uint64_t len, uint64_t from, uint64_t window, int64_t *pos,
+                     int64_t *first_entry_index) {
+  if (!c || !pos || !first_entry_index || (!d_buf && len)) return EWAL_E_INVAL;
+  EW_CHECK(hipSetDevice(c->device));
+  *pos = -1;
+  *first_entry_index = -1;
+  if (from >= len) return EWAL_OK;
+  const uint64_t end = std::min<uint64_t>(len, from + std::max<uint64_t>(window, 1));
+  EW_CHECK(c->sdesc.ensure(32));
+  unsigned long long *dpos = c->sdesc.as<unsigned long long>();
+  long long *dout = (long long *)(dpos + 1);
+  EW_CHECK(hipMemsetAsync(dpos, 0xff, 8, c->stream));
+  const unsigned grid = (unsigned)std::min<uint64_t>(grid_for(end - from, 256), (uint64_t)std::max(1, c->num_cu) * 8);
+  hipLaunchKernelGGL(k_probe_cand, dim3(grid), dim3(256), 0, c->stream, (const uint8_t *)d_buf, len, from, end, dpos);
+  hipLaunchKernelGGL(k_probe_walk, dim3(1), dim3(64), 0, c->stream, (const uint8_t *)d_buf, len,
+                     (const unsigned long long *)dpos, 64u, dout);
+  EW_CHECK(hipGetLastError());
+  long long h[2];
+  EW_CHECK(hipMemcpyAsync(h, dout, 16, hipMemcpyDeviceToHost, c->stream));
+  EW_CHECK(hipStreamSynchronize(c->stream));
+  *pos = h[0];
+  *first_entry_index = h[1];
+  return EWAL_OK;
+}
+
 int ewal_readall_batch_device(ewal_ctx *c, const void *d_buf, uint64_t n_shards, const uint64_t *lens,
                               const uint64_t *ri, ewal_result *out) {
   if (!c || (n_shards && (!lens || !ri || !out)) || n_shards >= 0x7fffffffull) return EWAL_E_INVAL;
@@ -1788,6 +1838,7 @@ int ewal_copy_range_info(ewal_ctx *c, ewal_range_info *out) {
   o.first_crc = o.md_first_frame = o.md_value_frame = o.first_entry_frame = o.last_entry_frame = -1;
   o.last_op_frame = -1;
   o.md_first_off = o.md_value_off = -1;
+  o.first_type = -1;
   if (int rc = need_records(c)) return rc;
   const uint64_t n = c->last_n;
   o.n_frames = (int64_t)n;
@@ -1807,6 +1858,10 @@ int ewal_copy_range_info(ewal_ctx *c, ewal_range_info *out) {
     RecDesc d;
     EW_CHECK(frame(0, &d));
     if (d.type == 4) o.first_crc = d.crc;
+    o.first_type = d.type;
+    o.first_dlen = d.dlen;
+    o.first_stored_crc = d.crc;
+    o.first_u0 = d.chained;   // k_check ran frame 0 from seed 0: crc32.Update(0, Data) (crcType: the stored CRC)
     if (h.md_first != ~0ull) {
       EW_CHECK(frame(h.md_first, &d));
       o.md_first_frame = (int64_t)h.md_first;

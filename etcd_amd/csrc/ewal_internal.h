@@ -155,7 +155,8 @@ struct Small {
   unsigned long long cat_used;    // bytes handed out
   unsigned long long cat_need;    // bytes a frame wanted past the arena's capacity
   uint32_t ncatfail;              // frames left undecoded for want of room (the host grows the arena, reruns)
-  uint32_t pad_cat;
+  uint32_t defer_first;           // a range of a WAL split inside a file (ewal_readall_range_device): frame
+                                  // 0's CRC check is the caller's (the running CRC before it is not known here)
 };
 
 // A returned Entry (ent = its index in ents) or the HardState (ent = -1)

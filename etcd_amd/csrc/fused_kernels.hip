@@ -449,8 +449,12 @@ __global__ __launch_bounds__(FC_THREADS, FC_OCC) void k_fc(FcArgs a, SegArgs sg)
         computed = x ^ Pe ^ 0xffffffffu;
       }
       chained = computed;
-      if (computed != d.crc) st = EWAL_ERR_RECORD_CRC;
+      // a range split inside a file (ewal_readall_range_device): frame 0's
+      // Validate is the caller's -- the running CRC before it is not known here
+      const bool defer0 = !SEG && r == 0 && ds->defer_first;
+      if (computed != d.crc && !defer0) st = EWAL_ERR_RECORD_CRC;
       else if (d.type != 1 && d.type != 2 && d.type != 3) st = EWAL_ERR_UNEXPECTED_TYPE;
+      if (defer0) chained = d.crc;   // the running CRC after it, once the caller's check holds
     }
     TileRec *tr = a.trec + t;
     if (live && (lane == 0 || r == rl)) {

@@ -2141,7 +2141,10 @@ __global__ __launch_bounds__(1024) void k_check(const uint32_t *__restrict__ g_s
         computed = x ^ Pe ^ 0xffffffffu;
       }
       chained = computed;
-      if (computed != d.crc) {
+      // a range split inside a file: frame 0's Validate is the caller's (its
+      // chained value stays crc32.Update(0, Data) for ewal_copy_range_info)
+      const bool defer0 = !SEG && r == 0 && ds->defer_first;
+      if (computed != d.crc && !defer0) {
         st = EWAL_ERR_RECORD_CRC;
       } else if (d.type == 2) {
         if (d.sub_st == 48) st = EWAL_UNSUPPORTED_ENCODING;
@@ -2626,6 +2629,54 @@ __global__ void k_reverse_u64(const uint64_t *__restrict__ in, uint64_t *__restr
 }
 
 // P(x) for one x (pkg/crc digest over a whole device buffer).
+// ---- ONE WAL split inside a file (ewal_range_probe) -------------------------
+// The first frame-start candidate at or after `from` (the exact test of
+// k_stream / k_cand: int64 length L in [4, B-p-8], the canonical Record head
+// 08 <type<0x80> 10, record.pb.go:175-196), one position per thread -> the
+// minimum in *pos (~0: none in the window).
+__global__ void k_probe_cand(const uint8_t *__restrict__ buf, uint64_t B, uint64_t from, uint64_t end,
+                             unsigned long long *pos) {
+  for (uint64_t p = from + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; p < end;
+       p += (uint64_t)gridDim.x * blockDim.x) {
+    if (p + 11 > B || buf[p + 8] != 0x08 || buf[p + 9] >= 0x80 || buf[p + 10] != 0x10) continue;
+    const int64_t L = (int64_t)ld_le64_b(buf, B, p);
+    if (L >= 4 && (uint64_t)L <= B - p - 8) atomicMin(pos, (unsigned long long)p);
+  }
+}
+// From that candidate along the frame links (decoder.decode's framing,
+// walpb.Record.Unmarshal, wal/decoder.go:28-47): the Index of the first entry
+// record within `maxf` frames (mustUnmarshalEntry, raft.pb.go:170-277), for
+// the range's w.ri.  out[0] = the candidate (or -1), out[1] = the Index (-1:
+// none found).
+__global__ void k_probe_walk(const uint8_t *__restrict__ buf, uint64_t B, const unsigned long long *pos,
+                             uint32_t maxf, long long *out) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  const unsigned long long p0 = *pos;
+  out[0] = p0 == ~0ull ? -1ll : (long long)p0;
+  out[1] = -1;
+  uint64_t p = p0;
+  for (uint32_t f = 0; p0 != ~0ull && f < maxf; ++f) {
+    if (p + 8 > B) break;
+    const int64_t L = (int64_t)ld_le64_b(buf, B, p);
+    if (L < 0 || (uint64_t)L > B - p - 8) break;
+    PbField a1, a2, a3, a4, a5;
+    pbf_init(a1); pbf_init(a2); pbf_init(a3); pbf_init(a4); pbf_init(a5);
+    int ur = 0;
+    if (pb_walk<PB_VAR64, PB_VAR32, PB_BYTES, PB_NONE, PB_NONE>(buf + p + 8, L, a1, a2, a3, a4, a5, ur, nullptr,
+                                                                nullptr, 0) != 0 || a3.split)
+      break;
+    if (a1.v == 2 && a3.blen > 0) {
+      PbField e1, e2, e3, e4, e5;
+      pbf_init(e1); pbf_init(e2); pbf_init(e3); pbf_init(e4); pbf_init(e5);
+      if (pb_walk<PB_VAR32, PB_VAR64, PB_VAR64, PB_BYTES, PB_NONE>(buf + p + 8 + a3.boff, a3.blen, e1, e2, e3, e4,
+                                                                   e5, ur, nullptr, nullptr, 0) == 0)
+        out[1] = (long long)e3.v;
+      break;
+    }
+    p += 8 + (uint64_t)L;
+  }
+}
+
 __global__ void k_prefix_one(const uint8_t *__restrict__ buf, const uint32_t *__restrict__ pwave,
                              const uint32_t *__restrict__ v, const uint32_t *__restrict__ g_slice,
                              const uint32_t *__restrict__ g_shift, uint64_t x, uint32_t *out) {

@@ -8,9 +8,14 @@ independently.  What crosses ranks is small:
 * `combine`   -- one all-reduce of {MIN first-corrupt key, SUM frames, SUM
   failing shards}; key = shard << 40 | frame, so the minimum names the first
   corrupt record of the lowest failing shard.
-* `split_verdict` -- ONE WAL split across ranks by file: ReadAll's verdict
-  (first failure, its global frame ordinal) from the per-range results,
-  with the crc seam and metadata rules across ranges (one all-gather).
+* `split_verdict` -- ONE WAL split across ranks by file or inside a file:
+  ReadAll's verdict (first failure, its global frame ordinal) from the
+  per-range results, with the crc seam, the deferred frame-0 CRC check of a
+  range that starts inside a file, the metadata and the ents index rules
+  across ranges (one all-gather).
+* `range_bounds` -- where each rank's range of ONE WAL split inside a file
+  starts: the first frame-start candidate after its share of the bytes
+  (ewal_range_probe), one all-gather.
 * `seam_check` -- for ONE WAL whose files were verified on different ranks:
   the only cross-file rule of ReadAll (wal/wal.go:184-192): file k+1's leading
   crcType record must carry file k's final running CRC whenever that CRC is
@@ -105,8 +110,50 @@ def seam_check(dist, world: int, rank: int, first_crc_record: int, last_crc: int
 # ---- one WAL split across ranks by file -------------------------------------
 # Status numbers of the verdict (include/ewal.h)
 _OK, _UNEXPECTED_EOF, _WAL_CRC, _META_CONFLICT, _INDEX_NOT_FOUND, _INDEX_GAP = 0, 2, 4, 5, 6, 36
+_RECORD_CRC = 3
+# failures decoder.decode reports before its CRC check (wal/decoder.go:30-41:
+# framing, Record.Unmarshal) -- they win over a frame-0 CRC mismatch
+_PRE_CRC = (2, 7, 32, 33, 37, 48)
 _U64 = (1 << 64) - 1
-_ROW = 16
+_ROW = 21
+_CASTAGNOLI = 0x82F63B78
+
+
+def range_bounds(dist, world: int, rank: int, probe, n_bytes: int, ri_global: int, device="cpu"):
+    """ONE WAL of n_bytes split inside a file: rank r's range
+    starts at c_r, the first frame-start candidate at or after r * n / world
+    (c_0 = 0; probe(start) -> (candidate, Index of the first entry from it),
+    ewal_range_probe on the rank's GPU).  One all-gather.  Returns [(start,
+    end, w.ri)] of every range: end = the next range's start; w.ri = max(the
+    global ri, the first entry Index) so the range's first op is its ents[0]
+    (split_verdict carries the ents rules across ranges).  A rank whose share
+    holds no candidate gets an empty range."""
+    if rank == 0:
+        pos, idx = 0, -1
+    else:
+        pos, idx = probe(rank * n_bytes // world)
+        if pos < 0:
+            pos = n_bytes
+    mine = torch.tensor([pos, idx], dtype=torch.int64, device=device)
+    allv = [torch.zeros(2, dtype=torch.int64, device=device) for _ in range(world)]
+    dist.all_gather(allv, mine)
+    starts = [int(v[0].item()) for v in allv]
+    for k in range(1, world):           # monotone (an empty range where a share held none)
+        starts[k] = max(starts[k], starts[k - 1])
+    out = []
+    for k in range(world):
+        end = starts[k + 1] if k + 1 < world else n_bytes
+        idx = int(allv[k][1].item())
+        ri = ri_global if k == 0 or idx < 0 else max(ri_global, idx)
+        out.append((starts[k], end, ri))
+    return out
+
+
+def _crc_combine(crc_a: int, crc_b: int, len_b: int) -> int:
+    """crc32.Update(crc_a, Castagnoli, B) from crc_b = Update(0, B) and len(B)
+    (the product's host helper, ewal_crc32_combine)."""
+    from . import _lib
+    return int(_lib.lib.ewal_crc32_combine(_CASTAGNOLI, crc_a & 0xffffffff, crc_b & 0xffffffff, len_b))
 
 
 def _s64(x):
@@ -115,7 +162,8 @@ def _s64(x):
     return x - (1 << 64) if x >> 63 else x
 
 
-def split_verdict(dist, world: int, rank: int, result, info, ri_range: int, ri_global: int, device="cpu"):
+def split_verdict(dist, world: int, rank: int, result, info, ri_range: int, ri_global: int, device="cpu",
+                  deferred: bool = False):
     """ReadAll's verdict (wal/wal.go:164-216) for ONE WAL whose files were
     split into contiguous ranges, range r verified by rank r.  Every range
     but the first starts at a file boundary, so at a crcType record carrying
@@ -146,7 +194,15 @@ def split_verdict(dist, world: int, rank: int, result, info, ri_range: int, ri_g
     joined into one range (a torn frame at the end of range k reads on into
     the next file through MultiReadCloser; k = 0 for the rewind / gap cases
     and a range that does not open with a crc record) -- the caller verifies
-    them joined and calls again; status is not final then."""
+    them joined and calls again; status is not final then.
+
+    A range that starts inside a file (deferred=True: read with
+    ewal_readall_range_device, EWAL_RANGE_DEFER_FIRST) has no crcType record
+    to re-seed from: its frame 0's check is made here with the running CRC of
+    the ranges before it -- crc32.Update(running, Data) from info's first_u0
+    and first_dlen against the stored CRC (walpb.ErrCRCMismatch), or the
+    crcType rule when frame 0 is one -- before the range's own failures at
+    frame 0 except those decoder.decode reports first (framing, Unmarshal)."""
     st, fr, n, lc = result
     mdf, mdv = info.get("md_first"), info.get("md_value")
     has_md = info["md_first_frame"] >= 0
@@ -155,7 +211,8 @@ def split_verdict(dist, world: int, rank: int, result, info, ri_range: int, ri_g
            len(mdv) if (info["md_value_frame"] >= 0 and mdv is not None) else -1,
            info["first_entry_frame"], _s64(info["first_entry_index"]), _s64(info["min_entry_index"]),
            _s64(info["last_entry_index"]), _s64(ri_range), info["n_frames"], info["last_op_frame"],
-           _s64(info["last_op_index"])]
+           _s64(info["last_op_index"]), 1 if deferred else 0, info.get("first_type", -1),
+           _s64(info.get("first_dlen", 0)), info.get("first_stored_crc", 0), info.get("first_u0", 0)]
     assert len(row) == _ROW
     mine = torch.tensor(row, dtype=torch.int64, device=device)
     allv = [torch.zeros(_ROW, dtype=torch.int64, device=device) for _ in range(world)]
@@ -174,18 +231,23 @@ def split_verdict(dist, world: int, rank: int, result, info, ri_range: int, ri_g
     before, running, md, last_op, enti = 0, 0, None, None, 0
     rig = ri_global & _U64
     for k, r in enumerate(rows):
-        st, fr, n, lc, fc, mff, mfl, mvl, fef, fei, mei, lei, rir, nfr, lof, loi = r
+        st, fr, n, lc, fc, mff, mfl, mvl, fef, fei, mei, lei, rir, nfr, lof, loi, dfr, fty, fdl, fsc, fu0 = r
         fei, mei, lei, rir, loi = fei & _U64, mei & _U64, lei & _U64, rir & _U64, loi & _U64
-        if nfr == 0 and n == 0 and st == _OK:
+        if nfr == 0 and n == 0 and st in (_OK, _INDEX_NOT_FOUND):
             continue                        # an empty range (joined into an earlier one)
         first_md = None if mfl < 0 else raw[k][:mfl]
         value_md = None if mvl < 0 else raw[k][max(mfl, 0):max(mfl, 0) + mvl]
         own = fr if st not in (_OK, _INDEX_NOT_FOUND) else None
         cross = []
         if k > 0:
-            if fc < 0:
+            if dfr and nfr > 0 and fty != 4:
+                # frame 0's Validate with the running CRC (wal/decoder.go:42-46)
+                computed = _crc_combine(running, fu0, fdl & _U64) if fdl else running
+                if computed != (fsc & 0xffffffff) and not (own == 0 and st in _PRE_CRC):
+                    return _RECORD_CRC, before, before, -1
+            elif fc < 0:
                 return st, -1, before, 0    # its CRCs depend on the range before: verify joined
-            if running != 0 and fc != running:
+            if fc >= 0 and running != 0 and fc != running:   # a crcType frame 0 (wal/wal.go:184-192)
                 cross.append((0, _WAL_CRC))
             if md is not None and mff >= 0 and first_md != md:
                 cross.append((mff, _META_CONFLICT))
@@ -200,7 +262,11 @@ def split_verdict(dist, world: int, rank: int, result, info, ri_range: int, ri_g
                     return st, -1, before, 0
         first = min(cross) if cross else None
         if own is not None and (first is None or own <= first[0]):
-            if st == _UNEXPECTED_EOF and k < world - 1 and fr == n:
+            # a frame cut short at the range's end reads on into the next
+            # range's bytes (MultiReadCloser / one file split): verify joined,
+            # unless every range after it is empty (the stream's own end)
+            later = any(not (x[13] == 0 and x[2] == 0 and x[0] in (_OK, _INDEX_NOT_FOUND)) for x in rows[k + 1:])
+            if st == _UNEXPECTED_EOF and later and fr == n:
                 return st, before + own, before + own, k
             return st, before + own, before + own, -1
         if first is not None:

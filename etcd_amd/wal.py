@@ -246,6 +246,28 @@ def readall_device(dbuf: DeviceBuffer, n: int, ri: int = 0, host_view=None, with
     return _collect(dbuf.ctx, r, host_view if host_view is not None else b"", with_ents and host_view is not None)
 
 
+def readall_range_device(dbuf: DeviceBuffer, n: int, ri: int = 0, defer_first=True, host_view=None,
+                         with_ents=False) -> ReadAllResult:
+    """ReadAll over one range of a WAL split inside a file (ewal_readall_range_device):
+    with defer_first, frame 0's CRC check is left to the caller (range_info's
+    first_* operands; shard.split_verdict makes it)."""
+    r = L.Result()
+    rc = lib.ewal_readall_range_device(dbuf.ctx.handle, dbuf.ptr, n, ri, L.RANGE_DEFER_FIRST if defer_first else 0,
+                                       C.byref(r))
+    if rc < 0:
+        check(rc)
+    return _collect(dbuf.ctx, r, host_view if host_view is not None else b"", with_ents and host_view is not None)
+
+
+def range_probe(dbuf: DeviceBuffer, n: int, start: int, window: int = 1 << 20):
+    """(first frame-start candidate at or after start, Index of the first entry
+    on the chain from it) of the n stream bytes in dbuf (ewal_range_probe);
+    -1 for none."""
+    pos, idx = C.c_int64(-1), C.c_int64(-1)
+    check(lib.ewal_range_probe(dbuf.ctx.handle, dbuf.ptr, n, start, window, C.byref(pos), C.byref(idx)))
+    return pos.value, idx.value
+
+
 def readall_batch_device(dbuf: DeviceBuffer, lens, ris, host_views=None, with_ents=False) -> List[ReadAllResult]:
     """ReadAll of every shard of a batch resident in HBM: shard s is the
     lens[s] bytes after shards 0..s-1 (ewal_readall_batch_device); one
@@ -308,7 +330,8 @@ def range_info(ctx: Context, stream=None, dbuf: DeviceBuffer = None):
                 md_value_frame=ri.md_value_frame, first_entry_frame=ri.first_entry_frame,
                 first_entry_index=ri.first_entry_index, min_entry_index=ri.min_entry_index,
                 last_entry_index=ri.last_entry_index, last_op_frame=ri.last_op_frame,
-                last_op_index=ri.last_op_index)
+                last_op_index=ri.last_op_index, first_type=ri.first_type, first_dlen=ri.first_dlen,
+                first_stored_crc=ri.first_stored_crc, first_u0=ri.first_u0)
 
 
 class WAL:

@@ -70,7 +70,8 @@ typedef struct ewal_result {
   int64_t fail_record;     /* ordinal of the frame that failed, -1 if none */
   int64_t fail_offset;     /* byte offset of that frame in the stream, -1 */
   int64_t n_records;       /* frames decoded before the end / failure */
-  uint32_t last_crc;       /* decoder.lastCRC() -> seeds the encoder, wal/wal.go:213 */
+  uint32_t last_crc;       /* decoder.lastCRC() -> seeds the encoder, wal/wal.go:213 (set with
+                              ErrIndexNotFound too: a split WAL's next range starts from it) */
   uint32_t n_unrec;        /* ents / HardState carrying XXX_unrecognized: ewal_copy_unrec */
   uint64_t enti;           /* w.enti: Index of the last entry record */
   int64_t metadata_off;    /* metadata []byte as (offset,len) into the stream; -1 == nil */
@@ -237,8 +238,33 @@ typedef struct ewal_range_info {
   int32_t md_split;              /* bit 0: md_first_off, bit 1: md_value_off index the split bytes
                                     (ewal_copy_split_bytes: a metadata Data in several segments) */
   int32_t pad;
+  /* frame 0 (EWAL_RANGE_DEFER_FIRST: the caller's CRC check) */
+  int64_t first_type;            /* Record.Type, -1: no frame */
+  uint64_t first_dlen;           /* len(Data) */
+  uint32_t first_stored_crc;     /* Record.Crc */
+  uint32_t first_u0;             /* crc32.Update(0, Castagnoli, Data) (the stored CRC for a crcType frame) */
 } ewal_range_info;
 int ewal_copy_range_info(ewal_ctx *ctx, ewal_range_info *out);
+
+/* ONE WAL split across ranks INSIDE a file: rank r takes the
+ * bytes [c_r, c_{r+1}) of the stream, where c_r is the first frame-start
+ * candidate at or after r * len / ranks (ewal_range_probe; c_0 = 0).  The
+ * running CRC before a range's frame 0 is the previous range's, so with
+ * EWAL_RANGE_DEFER_FIRST frame 0's CRC check (decoder.decode's Validate,
+ * wal/decoder.go:42-46, or the crcType rule, wal/wal.go:184-192) is left to
+ * the caller, who makes it with ewal_copy_range_info's first_* operands
+ * (first_u0 = crc32.Update(0, Data), combined with the running CRC by
+ * ewal_crc32_combine); every other rule is ReadAll's over the range with
+ * w.ri = ri.  etcd_amd/shard.py split_verdict joins the ranges. */
+#define EWAL_RANGE_DEFER_FIRST 1u
+int ewal_readall_range_device(ewal_ctx *ctx, const void *d_buf, uint64_t len, uint64_t ri, uint32_t flags,
+                              ewal_result *out);
+/* The first frame-start candidate at or after `from` within `window` bytes of
+ * a device stream of len bytes (*pos, -1: none), and the Index of the first
+ * entry record on the frame chain from it within 64 frames (*first_entry_index,
+ * -1: none) -- the range's w.ri candidate. */
+int ewal_range_probe(ewal_ctx *ctx, const void *d_buf, uint64_t len, uint64_t from, uint64_t window, int64_t *pos,
+                     int64_t *first_entry_index);
 
 /* ---- directory-level API: wal.OpenAtIndex + ReadAll + writer ----------- */
 typedef struct ewal_wal ewal_wal;
