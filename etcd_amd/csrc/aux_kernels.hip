@@ -206,7 +206,9 @@ __device__ __noinline__ uint64_t quorum_select_any(const uint64_t *__restrict__ 
 // window bounds) are issued for every group of the lane before the first
 // match load, so a wave keeps 4x the independent requests in flight (the
 // kernel is a chain nvoters -> match -> select -> term gather -> store).
+#ifndef EW_COMMIT_ILP
 #define EW_COMMIT_ILP 4
+#endif
 __global__ __launch_bounds__(256) void k_commit(uint64_t G, const uint64_t *__restrict__ match,
                                                 const uint8_t *__restrict__ nvoters, const uint64_t *__restrict__ term,
                                                 uint64_t *__restrict__ committed,

@@ -201,7 +201,9 @@ def _collect(ctx, r, buf_view, with_ents=True, shard=None):
                 st.XXX_unrecognized = b
             elif ent < len(ents):
                 ents[ent].XXX_unrecognized = b
-    return ReadAllResult(r.status, r.detail, r.fail_record, r.fail_offset, r.n_records, r.last_crc if ok else 0,
+    # last_crc: Go's lastCRC on success; kept with ErrIndexNotFound too (a split WAL's next range starts from it)
+    keep_crc = ok or r.status == L.ERR_INDEX_NOT_FOUND
+    return ReadAllResult(r.status, r.detail, r.fail_record, r.fail_offset, r.n_records, r.last_crc if keep_crc else 0,
                          r.enti, md, st, ents, r.n_candidates, r.n_runs, r.device_ms, r.stream_ms, r.n_slow,
                          r.flags)
 

@@ -66,7 +66,12 @@ def oracle_range_info(buf, ri):
             break
         recs.append(r)
         p += 8 + L
+    first = recs[0] if recs else None
     info = dict(n_frames=len(recs), first_crc=recs[0]["crc"] if recs and recs[0]["type"] == 4 else -1,
+                first_type=first["type"] if first else -1, first_dlen=len(first["data"] or b"") if first else 0,
+                first_stored_crc=first["crc"] if first else 0,
+                first_u0=(first["crc"] if first["type"] == 4 else O.crc32_update(0, first["data"] or b"")) if first
+                else 0,
                 md_first_frame=-1, md_first=None, md_value_frame=-1, md_value=None, first_entry_frame=-1,
                 first_entry_index=0, min_entry_index=0, last_entry_index=0, last_op_frame=-1, last_op_index=0)
     idx = []
