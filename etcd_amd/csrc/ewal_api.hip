@@ -273,7 +273,7 @@ static int stream_ensure(ewal_ctx *c, uint64_t B, int find_cand) {
   if (find_cand) {
     EW_CHECK(c->slots.ensure((size_t)nunits * EW_SLOTS * 2));
     EW_CHECK(c->ovf.ensure((size_t)nunits * 4));
-    if (EW_SPLIT_CAND) EW_CHECK(c->hmask.ensure((size_t)nunits * 8));
+    if (EW_SPLIT_CAND) EW_CHECK(c->hmask.ensure((size_t)nunits * 16));   // {flagged pieces, of them: group 3}
   }
   EW_CHECK(c->ux.ensure((size_t)nunits * 4));
   EW_CHECK(c->tagg.ensure((size_t)nstiles * 16));

@@ -315,6 +315,9 @@ __device__ __forceinline__ void row_transpose(uint32_t (&D)[19]) {
 #ifndef EW_SPLIT_CAND
 #define EW_SPLIT_CAND 1
 #endif
+#ifndef EW_CAND_TAILMASK
+#define EW_CAND_TAILMASK 1   // hmask also says which flagged pieces need the 16 B after them (k_cand)
+#endif
 #ifndef EW_XS
 #define EW_XS 0   // timing-only k_stream ablations (tools/): 1 no CRC, 2 no candidates, 4 no v stores,
                   // 8 the candidate filter without the exact tests / slots, 16 v stores only for
@@ -369,7 +372,14 @@ __device__ __forceinline__ void stream_units(const StreamArgs &a, const uint8_t 
     for (int i = 0; i < NU; ++i) {
       const uint64_t off = (uint64_t)u[i] * EW_WAVE_BYTES + (uint64_t)lane * EW_PIECE;
       const unsigned long long hm = __ballot(fm[i] != 0 && off < B);
-      if (lane == 0) a.hmask[u[i]] = hm;
+      if (EW_CAND_TAILMASK) {
+        // the pieces flagged in their last dword group (bit 4 of each byte
+        // of fm): only their candidates can need the 12 bytes after the piece
+        const unsigned long long h3 = __ballot((fm[i] & 0x10101010u) != 0 && off < B);
+        if (lane == 0) *(ulonglong2 *)(a.hmask + 2 * (uint64_t)u[i]) = make_ulonglong2(hm, h3);
+      } else if (lane == 0) {
+        a.hmask[u[i]] = hm;
+      }
     }
     return;
   }
@@ -512,6 +522,23 @@ __global__ __launch_bounds__(EW_THREADS, 1) void k_stream(StreamArgs a) {
 // ===========================================================================
 #define EW_CAND_WAVES 4
 #define EW_CAND_PF 4      // rounds of 64 flagged pieces whose loads are in flight together
+// the piece alone (its last dword group held no flag: every candidate's head
+// bytes lie inside it); the 12 bytes after it read as zeros, which no filter
+// or exact test matches
+__device__ __forceinline__ void load_piece64(const uint8_t *buf, uint64_t B, uint64_t off, uint32_t (&D)[19]) {
+  if (off + 64 <= B) {
+    const uint4 *q = (const uint4 *)(buf + off);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint4 x = q[k];
+      D[4 * k] = x.x; D[4 * k + 1] = x.y; D[4 * k + 2] = x.z; D[4 * k + 3] = x.w;
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < 16; ++k) D[k] = load_word_guarded(buf, B, off + 4 * k);
+  }
+  D[16] = D[17] = D[18] = 0u;
+}
 __device__ __forceinline__ void load_piece80(const uint8_t *buf, uint64_t B, uint64_t off, uint32_t (&D)[19]) {
   if (off + 80 <= B) {
     const uint4 *q = (const uint4 *)(buf + off);
@@ -543,12 +570,19 @@ __global__ __launch_bounds__(EW_CAND_WAVES * 64) void k_cand(const uint8_t *__re
   const uint32_t u0 = (blockIdx.x * EW_CAND_WAVES + (uint32_t)wv) * 64 * G;   // the wave's first unit
   uint16_t *list = s_list[wv];
   uint32_t *ucnt = s_ucnt[wv];
-  unsigned long long hm[G];
+  unsigned long long hm[G], h3[G];   // flagged pieces; those of them that need the 16 B after the piece
   uint32_t pc[G], ex[G], Tg[G];
 #pragma unroll
   for (int g = 0; g < G; ++g) {
     const uint32_t ul = u0 + 64 * g + (uint32_t)lane;
-    hm[g] = ul < nunits ? hmask[ul] : 0ull;
+    if (EW_CAND_TAILMASK) {
+      const ulonglong2 hh = ul < nunits ? *(const ulonglong2 *)(hmask + 2 * (uint64_t)ul) : make_ulonglong2(0ull, 0ull);
+      hm[g] = hh.x;
+      h3[g] = hh.y;
+    } else {
+      hm[g] = ul < nunits ? hmask[ul] : 0ull;
+      h3[g] = hm[g];
+    }
   }
 #pragma unroll
   for (int g = 0; g < G; ++g) {
@@ -576,7 +610,8 @@ __global__ __launch_bounds__(EW_CAND_WAVES * 64) void k_cand(const uint8_t *__re
         while (m) {
           const int b = __ffsll((long long)m) - 1;
           m &= m - 1;
-          list[k++] = (uint16_t)(((64 * g + lane) << 6) | b);   // (unit in the wave, piece)
+          // (unit in the wave, piece, bit 15: the 16 B after it are needed)
+          list[k++] = (uint16_t)(((64 * g + lane) << 6) | b | (((h3[g] >> b) & 1ull) << 15));
         }
         base += Tg[g];
       }
@@ -591,8 +626,10 @@ __global__ __launch_bounds__(EW_CAND_WAVES * 64) void k_cand(const uint8_t *__re
           const uint32_t i = rb + 64 * k + (uint32_t)lane;
           E[k] = i < T ? list[i] : 0xffffu;
           if (i < T) {
-            load_piece80(buf, B, (uint64_t)(u0 + (E[k] >> 6)) * EW_WAVE_BYTES + (uint64_t)(E[k] & 63) * EW_PIECE,
-                         D[k]);
+            const uint64_t po = (uint64_t)(u0 + ((E[k] & 0x7fffu) >> 6)) * EW_WAVE_BYTES + (uint64_t)(E[k] & 63) * EW_PIECE;
+            if (E[k] & 0x8000u) load_piece80(buf, B, po, D[k]);
+            else load_piece64(buf, B, po, D[k]);   // no candidate can reach past the piece
+            E[k] &= 0x7fffu;
           } else {
 #pragma unroll
             for (int q = 0; q < 19; ++q) D[k][q] = 0u;
