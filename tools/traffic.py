@@ -1,26 +1,29 @@
-"""profiles/k_stream_pmc.json from tools/traffic.sh's two PMC passes:
-per-launch HBM bytes of k_stream = FETCH_SIZE (KiB) x 1024 x 2 (gfx950:
-FETCH_SIZE counts half the bytes of a wide streaming read) + WRITE_SIZE (KiB)
-x 1024.  Usage: python3 tools/traffic.py gpurun_out/traffic"""
+"""profiles/<kernel>_pmc.json from tools/traffic.sh's two PMC passes:
+per-launch HBM bytes = FETCH_SIZE (KiB) x 1024 x 2 (gfx950: FETCH_SIZE counts
+half the bytes of a wide streaming read) + WRITE_SIZE (KiB) x 1024.
+Usage: python3 tools/traffic.py ROOT [KERNEL [CONFIG]]
+  default: k_stream, configs[1] (bench.py default, 8 GiB)"""
 import csv, glob, json, os, sys
 from collections import defaultdict
 root = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/traffic"
+kern = sys.argv[2] if len(sys.argv) > 2 else "k_stream"
+config = sys.argv[3] if len(sys.argv) > 3 else "configs[1] (bench.py default, 8 GiB)"
 vals = {}
 for c in ("FETCH_SIZE", "WRITE_SIZE"):
     per = defaultdict(float)
     for f in glob.glob(os.path.join(root, c, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
-            if "k_stream" in r["Kernel_Name"] and r["Counter_Name"] == c:
+            if kern in r["Kernel_Name"] and r["Counter_Name"] == c:
                 per[r["Dispatch_Id"]] += float(r["Counter_Value"])
     v = sorted(per.values())
     vals[c] = v[len(v) // 2] if v else None
 fetch = vals["FETCH_SIZE"] * 1024 * 2
 write = vals["WRITE_SIZE"] * 1024
-out = {"kernel": "k_stream", "config": "configs[1] (bench.py default, 8 GiB)",
+out = {"kernel": kern, "config": config,
        "fetch_size_kib_median": vals["FETCH_SIZE"], "write_size_kib_median": vals["WRITE_SIZE"],
        "hbm_read_bytes_per_launch": fetch, "hbm_write_bytes_per_launch": write,
        "hbm_bytes_per_launch": fetch + write,
        "note": "FETCH_SIZE doubled per MI355X_MICROARCH.md (gfx950 counts half of a wide streaming read)"}
-json.dump(out, open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "profiles", "k_stream_pmc.json"), "w"),
+json.dump(out, open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "profiles", kern + "_pmc.json"), "w"),
           indent=1)
 print(json.dumps(out))
