@@ -68,9 +68,10 @@ def parse():
     return ap.parse_args()
 
 
-def load_traffic():
-    """Per-launch HBM bytes of k_stream from the committed PMC pass, if any."""
-    p = os.path.join(ROOT, "profiles", "k_stream_pmc.json")
+def load_traffic(kernel="k_stream"):
+    """Per-launch HBM bytes of a kernel from its committed PMC pass, if any
+    (profiles/<kernel>_pmc.json, tools/traffic.sh + tools/traffic.py)."""
+    p = os.path.join(ROOT, "profiles", kernel + "_pmc.json")
     try:
         d = json.load(open(p))
         return d.get("hbm_bytes_per_launch")
@@ -713,8 +714,12 @@ def run_commit(a, dist, rank, world, local, cpu_seconds=None):
                        "groups_per_gpu": G, "parallelism": "dp%d (group ranges)" % world},
             "roofline": {"bound": "hbm", "achieved": round(abytes / (k_avg / 1e3) / 1e9, 2), "peak": HBM_PEAK_GBPS,
                          "unit": "GB/s", "frac": round(abytes / (k_avg / 1e3) / 1e9 / HBM_PEAK_GBPS, 4),
-                         "traffic": None, "kernel": "k_commit", "kernel_ms": round(k_avg, 4),
-                         "algorithmic_bytes_per_launch": abytes},
+                         "traffic": load_traffic("k_commit"), "kernel": "k_commit", "kernel_ms": round(k_avg, 4),
+                         "algorithmic_bytes_per_launch": abytes,
+                         "traffic_source": "profiles/k_commit_pmc.json: the committed rocprofv3 PMC pass of this "
+                                           "config (FETCH_SIZE x2 + WRITE_SIZE per launch), not measured in this run; "
+                                           "the 8-B term gather costs a whole 128-B line per group "
+                                           "(profiles/r03/ab_commit_gather.txt)"},
             "cpu_baseline": cpu}
     ctx.close()
     return out
