@@ -1849,34 +1849,46 @@ __device__ __forceinline__ int pb_field_fast(const uint32_t *w, int o, uint32_t 
 struct NoOp {
   __device__ void operator()() const {}
 };
-template <int WS, bool NEAR = false, class AfterIssue = NoOp>
-__device__ __forceinline__ bool decode_canon(const uint8_t *__restrict__ buf, uint64_t B, uint64_t p,
-                                             const uint32_t *__restrict__ pwave, const uint32_t *__restrict__ v,
-                                             const uint32_t *s_t4, const uint32_t *s_svp, uint32_t *w, RecDesc &d,
-                                             int64_t &L, uint32_t &Pfo, uint32_t &Pfd, bool noprefix = false,
-                                             AfterIssue after_issue = AfterIssue(), const uint32_t *s_inv = nullptr) {
-  const uint64_t p16 = p & ~15ull;
+// The frame's loads (head + prefix operands) and the decode from them are
+// split so a caller can keep the next frame's loads in flight while it
+// decodes this one (canon_issue / canon_finish); decode_canon runs both.
+template <bool NEAR>
+struct CanonLoad {
   uint4 hq[5];
+  typename std::conditional<NEAR, PrefixNear, PrefixIn>::type pin;
+};
+template <bool NEAR>
+__device__ __forceinline__ void canon_issue(const uint8_t *__restrict__ buf, uint64_t B, uint64_t p,
+                                            const uint32_t *__restrict__ pwave, const uint32_t *__restrict__ v,
+                                            CanonLoad<NEAR> &ld) {
+  const uint64_t p16 = p & ~15ull;
 #pragma unroll
   for (int k = 0; k < 5; ++k) {
     const uint64_t o = p16 + 16 * k;
     if (o + 16 <= B) {
-      hq[k] = *(const uint4 *)(buf + o);
+      ld.hq[k] = *(const uint4 *)(buf + o);
     } else {
       uint32_t x[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) x[j] = load_word_guarded(buf, B, o + 4 * j);
-      hq[k] = make_uint4(x[0], x[1], x[2], x[3]);
+      ld.hq[k] = make_uint4(x[0], x[1], x[2], x[3]);
     }
   }
-  typename std::conditional<NEAR, PrefixNear, PrefixIn>::type pin;
-  if constexpr (NEAR) prefix_load_near(p, B, pwave, v, buf, pin);
-  else prefix_load(p, pwave, v, buf, pin);
-  after_issue();   // the caller's stores: issued behind this frame's loads, so waiting for them never waits for those
+  if constexpr (NEAR) prefix_load_near(p, B, pwave, v, buf, ld.pin);
+  else prefix_load(p, pwave, v, buf, ld.pin);
+}
+template <int WS, bool NEAR>
+__device__ __forceinline__ bool canon_finish(const uint8_t *__restrict__ buf, uint64_t B, uint64_t p,
+                                             const uint32_t *__restrict__ pwave, const uint32_t *__restrict__ v,
+                                             const uint32_t *s_t4, const uint32_t *s_svp, uint32_t *w, RecDesc &d,
+                                             int64_t &L, uint32_t &Pfo, uint32_t &Pfd, bool noprefix,
+                                             const uint32_t *s_inv, const CanonLoad<NEAR> &ld) {
+  const uint64_t p16 = p & ~15ull;
+  const auto &pin = ld.pin;
 #pragma unroll
   for (int k = 0; k < 5; ++k) {
-    w[(4 * k) * WS] = hq[k].x; w[(4 * k + 1) * WS] = hq[k].y;
-    w[(4 * k + 2) * WS] = hq[k].z; w[(4 * k + 3) * WS] = hq[k].w;
+    w[(4 * k) * WS] = ld.hq[k].x; w[(4 * k + 1) * WS] = ld.hq[k].y;
+    w[(4 * k + 2) * WS] = ld.hq[k].z; w[(4 * k + 3) * WS] = ld.hq[k].w;
   }
   const int base = (int)(p - p16);
   L = (int64_t)win8<WS>(w, base);
@@ -1933,6 +1945,17 @@ __device__ __forceinline__ bool decode_canon(const uint8_t *__restrict__ buf, ui
     Pfd = c;
   }
   return true;
+}
+template <int WS, bool NEAR = false, class AfterIssue = NoOp>
+__device__ __forceinline__ bool decode_canon(const uint8_t *__restrict__ buf, uint64_t B, uint64_t p,
+                                             const uint32_t *__restrict__ pwave, const uint32_t *__restrict__ v,
+                                             const uint32_t *s_t4, const uint32_t *s_svp, uint32_t *w, RecDesc &d,
+                                             int64_t &L, uint32_t &Pfo, uint32_t &Pfd, bool noprefix = false,
+                                             AfterIssue after_issue = AfterIssue(), const uint32_t *s_inv = nullptr) {
+  CanonLoad<NEAR> ld;
+  canon_issue<NEAR>(buf, B, p, pwave, v, ld);
+  after_issue();   // the caller's stores: issued behind this frame's loads, so waiting for them never waits for those
+  return canon_finish<WS, NEAR>(buf, B, p, pwave, v, s_t4, s_svp, w, d, L, Pfo, Pfd, noprefix, s_inv, ld);
 }
 
 // decode_canon for frame r of the general path: the descriptor and prefixes
