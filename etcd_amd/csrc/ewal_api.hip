@@ -568,6 +568,15 @@ static int walk_chain(ewal_ctx *c, DevTables *tb, const uint8_t *d_buf, uint64_t
 // reset and the caller runs the general path over the same stream pass.
 // ents / mlist are sized for every candidate being an op (*ecap), grown when
 // the candidate count exceeds them (k_fc declines before doing any work).
+#ifndef EW_SEAM_WGS
+#define EW_SEAM_WGS 2
+#endif
+// k_fc_seam's grid: grid-strided over the tiles, at most a few workgroups
+// per CU (ntiles is the capacity's tile count; the frame count is known only
+// on the device)
+static unsigned seam_grid(const ewal_ctx *c, uint64_t ntiles) {
+  return (unsigned)std::min<uint64_t>(grid_for(ntiles, 256), (uint64_t)std::max(1, c->num_cu) * EW_SEAM_WGS);
+}
 static int fused_pass(ewal_ctx *c, DevTables *tb, const uint8_t *d_buf, uint64_t B, uint64_t ri, uint64_t ccap,
                       uint64_t ecap, bool *done) {
   Small *ds = c->small.as<Small>();
@@ -597,7 +606,7 @@ static int fused_pass(ewal_ctx *c, DevTables *tb, const uint8_t *d_buf, uint64_t
     hipLaunchKernelGGL(k_fc<false>, dim3((unsigned)std::max(1, c->num_cu) * FC_WGS), dim3(FC_THREADS), 0, c->stream,
                        a, SegArgs{});
     // the seam pass; its last workgroup gathers the result (fc_result)
-    hipLaunchKernelGGL(k_fc_seam<false>, dim3(grid_for(ntiles, 256)), dim3(256), 0, c->stream, d_buf, B, a.cpos,
+    hipLaunchKernelGGL(k_fc_seam<false>, dim3(seam_grid(c, ntiles)), dim3(256), 0, c->stream, d_buf, B, a.cpos,
                        tb->shift, a.trec, a.ents, ri, ccap, ecap, ds, SegArgs{}, (const uint32_t *)a.mlist,
                        c->h_res_dev, c->h_small_dev);
     EW_CHECK(hipGetLastError());
@@ -1154,7 +1163,7 @@ static int fused_batch(ewal_ctx *c, DevTables *tb, const uint8_t *d_buf, uint64_
                        c->bsoff.as<uint64_t>(), ns, c->bfs.as<uint32_t>(), sg.sagg, ds);
     hipLaunchKernelGGL(k_fc<true>, dim3((unsigned)std::max(1, c->num_cu) * FC_WGS), dim3(FC_THREADS), 0, c->stream, a,
                        sg);
-    hipLaunchKernelGGL(k_fc_seam<true>, dim3(grid_for(ntiles, 256)), dim3(256), 0, c->stream, d_buf, B, a.cpos,
+    hipLaunchKernelGGL(k_fc_seam<true>, dim3(seam_grid(c, ntiles)), dim3(256), 0, c->stream, d_buf, B, a.cpos,
                        tb->shift, a.trec, a.ents, 0ull, ccap, ecap, ds, sg, (const uint32_t *)nullptr,
                        (ResultDev *)nullptr, (Small *)nullptr);
     hipLaunchKernelGGL(k_meta_batch_fc, dim3(64), dim3(256), 0, c->stream, d_buf, B, a.cpos, ccap, ecap, a.mlist, ds,

@@ -692,9 +692,10 @@ __global__ __launch_bounds__(256) void k_fc_seam(const uint8_t *__restrict__ buf
   }
   const uint64_t K = ds->total;
   const uint32_t ntiles = (uint32_t)((K + FC_TILE - 1) / FC_TILE);
-  const uint32_t nblocks = (ntiles + blockDim.x - 1) / blockDim.x;   // the grid is sized for the capacity
-  if (blockIdx.x >= nblocks) return;
-  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  // a grid-strided pass over the tiles: the grid (a few workgroups per CU) is
+  // sized before the candidate count is known, so every workgroup takes part
+  // in the fold below instead of a capacity-sized grid of empty workgroups
+  const uint32_t nblocks = gridDim.x;
   if (!SEG) {
     if (threadIdx.x == 0) {
       s_fail = ~0ull;
@@ -704,7 +705,7 @@ __global__ __launch_bounds__(256) void k_fc_seam(const uint8_t *__restrict__ buf
     __syncthreads();
   }
   unsigned long long fail = ~0ull;
-  if (t < ntiles) {
+  for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < ntiles; t += gridDim.x * blockDim.x) {
     const TileRec tr = trec[t];
     const uint32_t r0 = t * FC_TILE;
     const uint32_t rl = min(r0 + FC_TILE, (uint32_t)K) - 1;   // the tile's last frame
