@@ -101,3 +101,17 @@ def test_mutated_batches(ctx, block):
                        [(x["index"], x["term"], x["data"]) for x in o["ents"]]
             elif o["status"] != O.ERR_INDEX_NOT_FOUND:
                 assert (r.fail_record, r.fail_offset) == (o["fail_record"], o["fail_offset"])
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_mutated_large_wals(ctx, seed):
+    # multi-MiB WALs (thousands of 64-frame tiles, rewinds for some seeds): the
+    # damage lands far from byte 0, across tile seams, in the fused pass and in
+    # the general path's pointer jumping
+    rng = random.Random(11000 + seed)
+    size = rng.choice([1, 3, 8]) << 20
+    buf, _ = W.synth_wal(size, rng.choice([16, 64]), rng.choice([512, 4096]), seed=seed,
+                         rewind_per_mille=rng.choice([0, 0, 10]))
+    m = _mutate(rng, bytes(buf))
+    o, g = assert_parity(ctx, m, rng.choice([1, 1, 100]), check_chain=seed % 3 == 0)   # its entries start at Index 1
+    assert g["status"] != L.UNSUPPORTED_ENCODING
