@@ -286,3 +286,16 @@ def test_within_file_split_oracle_ranges(world):
 def test_within_file_split_gpu_ranges(world):
     rng = random.Random(41 + world)
     _run(world, True, _cases(rng) + _frame0_cases(rng, world))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 3])
+def test_within_file_split_gpu_mutated(world):
+    # damaged WALs (test_gpu_fuzz's mutations: flips, torn tails, inserted /
+    # deleted bytes, frames duplicated / dropped / swapped) split over the ranks:
+    # the joined verdict must still be ReadAll's over the whole WAL
+    from test_gpu_fuzz import _mutate
+    rng = random.Random(77 + world)
+    cases = [("mutated_%d" % i, _mutate(rng, _wal(rng, n=rng.randrange(60, 300), cuts=rng.randrange(0, 3))), 1, True)
+             for i in range(16)]
+    _run(world, True, cases)
