@@ -175,9 +175,29 @@ def _cases(rng, world):
     return out
 
 
-def _run(world, use_gpu):
+def _mutated_cases(rng, world, n=12):
+    """WALs of world * 2 files with one file damaged by test_gpu_fuzz's
+    mutations (flips, torn tails, inserted / deleted bytes, frames
+    duplicated / dropped / swapped), split by file over the ranks."""
+    from test_gpu_fuzz import _mutate
+    out = []
+    for _ in range(n):
+        nf = world * 2
+        per = nf // world
+        files = build_files(rng, nf, ents=(3, 30))
+        blobs = [bytes(b) for b, _ in files]
+        k = rng.randrange(nf)
+        blobs[k] = _mutate(rng, blobs[k])
+        ranges = [(b"".join(blobs[r * per:(r + 1) * per]), 0 if r == 0 else files[r * per][1]) for r in range(world)]
+        out.append((b"".join(blobs), 0, ranges))
+    return out
+
+
+def _run(world, use_gpu, cases=None):
     rng = random.Random(17 + world)
-    cases = _cases(rng, world)
+    labels = KINDS if cases is None else tuple("mutated_%d" % i for i in range(len(cases)))
+    plain = cases is None
+    cases = _cases(rng, world) if plain else cases
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -191,12 +211,13 @@ def _run(world, use_gpu):
     for r in range(world):
         got = [x for x in res[r] if x[0] != "resplit"]
         assert len(got) == len(cases)
-        assert any(x[0] == "resplit" for x in res[r])       # the torn-file case went through a resplit
+        if plain:
+            assert any(x[0] == "resplit" for x in res[r])   # the torn-file case went through a resplit
         for i, (allb, rig, _) in enumerate(cases):
             o = O.readall(allb, rig)
             want = (o["status"], o["fail_record"] if o["status"] not in (O.OK, O.ERR_INDEX_NOT_FOUND) else -1,
                     o["n_records"])
-            assert got[i] == want, (KINDS[i], r, got[i], want)
+            assert got[i] == want, (labels[i], r, got[i], want)
     return cases
 
 
@@ -211,6 +232,17 @@ def test_split_verdict_oracle_ranges(world):
 @pytest.mark.gpu
 def test_split_verdict_gpu_ranges():
     _run(2, use_gpu=True)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_split_verdict_mutated_oracle_ranges(world):
+    _run(world, False, _mutated_cases(random.Random(300 + world), world))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 3])
+def test_split_verdict_mutated_gpu_ranges(world):
+    _run(world, True, _mutated_cases(random.Random(400 + world), world))
 
 
 @pytest.mark.gpu
