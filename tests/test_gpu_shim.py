@@ -136,3 +136,28 @@ def test_shim_unknown_fields(tmp_path):
     assert o["status"] == O.OK and g["sentinel"] == "nil"
     assert (g["unrec_digest"], g["n_unrec"]) == unrec_digest(o)
     assert g["n_unrec"] > 10
+
+
+@pytest.mark.gpu
+def test_shim_damaged_directories(tmp_path):
+    # a WAL directory the engine's writer produced, one file damaged by
+    # test_gpu_fuzz's mutations: the shim's sentinel, failing frame and
+    # materialised ents must be the oracle's ReadAll over the selected files
+    from test_gpu_fuzz import _mutate
+    rng = random.Random(23)
+    for case in range(8):
+        d = tmp_path / ("wal%d" % case)
+        w = W.Create(str(d), b"metadata")
+        idx = 0
+        for f in range(rng.randrange(2, 5)):
+            cnt = rng.randrange(5, 120)
+            w.Save(W.HardState(1, 1, idx), [W.Entry(0, 1, idx + k, rng.randbytes(rng.randrange(0, 1500)))
+                                             for k in range(cnt)])
+            idx += cnt
+            w.Cut()
+        w.Close()
+        names = sorted(os.listdir(d))
+        victim = d / names[rng.randrange(len(names))]
+        victim.write_bytes(_mutate(rng, victim.read_bytes()))
+        for index in (0, rng.randrange(1, idx + 1)):
+            check(d, index)
