@@ -55,6 +55,8 @@ E_HIP, E_INVAL, E_NOMEM, E_NODEVICE, E_TIMEOUT, E_IO = -1, -2, -3, -4, -5, -6
 
 FLAG_SHARD_FALLBACK = 1   # ewal_readall_batch_device verified this shard on its own
 FLAG_METADATA_SPLIT = 2   # metadata_off / _len index the split bytes (ewal_copy_split_bytes)
+FLAG_FAST_PATH = 4        # the fused frame pass decided this result (diagnostics)
+OPT_GENERAL_PATH = 1      # ewal_ctx_set_options: every ReadAll on the general path
 RANGE_DEFER_FIRST = 1     # ewal_readall_range_device: frame 0's CRC check is the caller's
 
 CASTAGNOLI, IEEE, KOOPMAN = 0x82F63B78, 0xEDB88320, 0xEB31D82E
@@ -133,6 +135,7 @@ _SIGS = {
     "ewal_ctx_destroy": (None, [vp]),
     "ewal_ctx_set_stream": (C.c_int, [vp, vp]),
     "ewal_ctx_reserve": (C.c_int, [vp, C.c_uint64, C.c_uint32]),
+    "ewal_ctx_set_options": (C.c_int, [vp, C.c_uint32]),
     "ewal_wal_size": (C.c_uint64, [vp]),
     "ewal_status_string": (C.c_char_p, [C.c_int]),
     "ewal_last_device_ms": (C.c_float, [vp]),

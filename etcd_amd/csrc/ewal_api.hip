@@ -199,6 +199,16 @@ static int get_tables(ewal_ctx *c, uint32_t poly, DevTables **out) {
   return 0;
 }
 
+// diagnostics of the batch path's decisions (tools/ builds only: the product
+// build reads no environment variable)
+static inline bool ew_debug() {
+#ifdef EW_ABLATION_HOOKS
+  return std::getenv("EWAL_DEBUG") != nullptr;
+#else
+  return false;
+#endif
+}
+
 static inline unsigned grid_for(uint64_t n, unsigned bs) { return (unsigned)((n + bs - 1) / bs); }
 
 // hipcub DeviceSelect::Flagged(counting 0.., flags) -> out, count in *d_count
@@ -1080,6 +1090,7 @@ static int readall_impl(ewal_ctx *c, const uint8_t *d_buf, uint64_t B, uint64_t 
       c->last_ok = true;
     }
   }
+  if (fused_done_final) out->flags |= EWAL_FLAG_FAST_PATH;
   c->last_n = n;
   c->rec_rebuild = n && !c->rd_valid;   // the fused pass decided: descriptors are rebuilt on demand
   c->rec_valid = true;
@@ -1326,7 +1337,7 @@ static int readall_batch_impl(ewal_ctx *c, const uint8_t *d_buf, uint32_t ns, co
       bool done = false;
       rc = fused_batch(c, tb, d_buf, B, ns, soff, ris, ccap, rdcap, out, &done);
       if (rc) return rc;
-      if (std::getenv("EWAL_DEBUG")) {
+      if (ew_debug()) {
         uint32_t nb = 0;
         for (uint32_t i = 0; i < ns && done; ++i) nb += (out[i].flags & EW_SHARD_BAD) != 0;
         std::fprintf(stderr, "ewal batch: fused done %d bad %u (K %llu ccap %llu ecap %llu novf %u rare %u err %u)\n",
@@ -1384,7 +1395,7 @@ static int readall_batch_impl(ewal_ctx *c, const uint8_t *d_buf, uint32_t ns, co
     c->last_k = K;
     fast = K && K <= ccap && K <= rdcap && !c->h_small->novf && c->h_small->pos0 == 0 && !c->h_small->irregular &&
            c->h_small->q == B;
-    if (!fast && std::getenv("EWAL_DEBUG"))
+    if (!fast && ew_debug())
       std::fprintf(stderr, "ewal batch: one by one (K %llu ccap %llu rdcap %llu novf %u pos0 %llu irr %u q %llu B %llu)\n",
                    (unsigned long long)K, (unsigned long long)ccap, (unsigned long long)rdcap, c->h_small->novf,
                    (unsigned long long)c->h_small->pos0, c->h_small->irregular, (unsigned long long)c->h_small->q,
@@ -1442,7 +1453,7 @@ static int readall_batch_impl(ewal_ctx *c, const uint8_t *d_buf, uint32_t ns, co
       // split byte fields (no side arena in the batch) go one by one too
       fast = !c->h_small->segbad && !c->h_small->gapslow && !c->h_small->nonmono && !c->h_small->nunrec &&
              !c->h_small->ncatfail;
-      if (!fast && std::getenv("EWAL_DEBUG"))
+      if (!fast && ew_debug())
         std::fprintf(stderr, "ewal batch: one by one (segbad %u gapslow %u nonmono %u nunrec %u)\n",
                      c->h_small->segbad, c->h_small->gapslow, c->h_small->nonmono, c->h_small->nunrec);
       if (fast) {
@@ -1539,12 +1550,12 @@ int ewal_ctx_create(int device, ewal_ctx **out) {
     c->num_cu = prop.multiProcessorCount;
   EW_CHECK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
   c->own_stream = true;
-#ifdef EW_ABLATION_HOOKS   // timing experiments only (tools/fc_ablate.py): results are wrong under ablation
+#ifdef EW_ABLATION_HOOKS   // timing experiments only (tools/): results are wrong under ablation.  The product
+                           // build reads no environment variable: its path is set by ewal_ctx_set_options only.
   if (const char *e = std::getenv("EWAL_STREAM_ABLATE")) c->ablate = std::atoi(e);
   if (const char *e = std::getenv("EWAL_FC_ABLATE")) c->fc_ablate = (uint32_t)std::atoi(e);
-#endif
   if (const char *e = std::getenv("EWAL_FRAME_WG")) c->frame_wg = std::max(1, std::min(16, std::atoi(e)));
-  if (const char *e = std::getenv("EWAL_FUSED")) c->fused = std::atoi(e) != 0;
+#endif
   EW_CHECK(hipEventCreate(&c->ev0));
   EW_CHECK(hipEventCreate(&c->ev1));
   EW_CHECK(hipEventCreate(&c->evs0));
@@ -1587,6 +1598,12 @@ int ewal_ctx_set_stream(ewal_ctx *c, void *s) {
     EW_CHECK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     c->own_stream = true;
   }
+  return EWAL_OK;
+}
+
+int ewal_ctx_set_options(ewal_ctx *c, uint32_t opts) {
+  if (!c || (opts & ~EWAL_OPT_GENERAL_PATH)) return EWAL_E_INVAL;
+  c->fused = (opts & EWAL_OPT_GENERAL_PATH) ? 0 : 1;
   return EWAL_OK;
 }
 

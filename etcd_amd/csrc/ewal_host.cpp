@@ -593,7 +593,9 @@ int ewal_writer_cut(ewal_writer *w) {
   // newEncoder(w.f, prevCrc): a fresh buffer (bytes a failed sync left
   // behind belong to the old file and are dropped), the running CRC kept
   w->enc.buf.clear();
-  ewal_encoder_encode(&w->enc, EWAL_CRC, nullptr, 0, 1);          // saveCrc(prevCrc)
+  // saveCrc(prevCrc): Cut returns its error before the metadata record
+  // (wal/wal.go:234-236)
+  if (int rc = ewal_encoder_encode(&w->enc, EWAL_CRC, nullptr, 0, 1)) return rc;
   return ewal_encoder_encode(&w->enc, EWAL_METADATA, w->md.data(), w->md.size(), w->md_nil);
 }
 void ewal_writer_close(ewal_writer *w) {

@@ -74,6 +74,11 @@ class Context:
         except Exception:
             pass
 
+    def set_options(self, general_path=False):
+        """ewal_ctx_set_options: general_path=True makes every ReadAll take the
+        general path (for cross-checking it against the fused pass)."""
+        check(lib.ewal_ctx_set_options(self._p, L.OPT_GENERAL_PATH if general_path else 0))
+
     def set_stream(self, hip_stream):
         """Run this ctx's work on a caller-owned hipStream_t (e.g. torch's)."""
         check(lib.ewal_ctx_set_stream(self._p, C.c_void_p(hip_stream)))

@@ -135,6 +135,13 @@ int ewal_ctx_set_stream(ewal_ctx *ctx, void *hip_stream);
  * workspace itself. */
 #define EWAL_RESERVE_HOST_STAGING 1u   /* also the HBM staging buffer of ewal_readall_host / ewal_wal_readall */
 int ewal_ctx_reserve(ewal_ctx *ctx, uint64_t wal_bytes, uint32_t flags);
+/* Path options of ctx (default 0: the fused frame pass first, the general
+ * path when it cannot decide a WAL).  EWAL_OPT_GENERAL_PATH: every ReadAll
+ * takes the general path (framing by candidate links, per-frame descriptors)
+ * -- the same results, slower; for cross-checking the two paths.  No
+ * environment variable changes the path. */
+#define EWAL_OPT_GENERAL_PATH 1u
+int ewal_ctx_set_options(ewal_ctx *ctx, uint32_t opts);
 const char *ewal_status_string(int status);
 /* Device time (ms) of the last pipeline call on this ctx (HIP events). */
 float ewal_last_device_ms(ewal_ctx *ctx);
@@ -167,6 +174,9 @@ int ewal_readall_device(ewal_ctx *ctx, const void *d_buf, uint64_t len, uint64_t
  * metadata record's Data repeated with several non-empty segments), not the
  * stream */
 #define EWAL_FLAG_METADATA_SPLIT 2
+/* ewal_result.flags (diagnostics): the fused frame pass decided this result
+ * (no per-frame descriptors were built); absent: the general path did */
+#define EWAL_FLAG_FAST_PATH 4
 int ewal_readall_batch_device(ewal_ctx *ctx, const void *d_buf, uint64_t n_shards, const uint64_t *lens,
                               const uint64_t *ri, ewal_result *out);
 /* After ewal_readall_batch_device: shard s's ents (Data offsets relative to

@@ -60,3 +60,33 @@ def test_records_match_oracle_then_invalidate(ctx):
         assert [x["chained_crc"] for x in W.records(ctx, n)] == want[:n]
     finally:
         d.free()
+
+
+@pytest.mark.gpu
+def test_path_is_set_by_options_not_environment(monkeypatch):
+    """the product build reads no environment variable that
+    switches the ReadAll path.  A fresh ctx created with the old switches set
+    still takes the fused pass (EWAL_FLAG_FAST_PATH); only
+    ewal_ctx_set_options(EWAL_OPT_GENERAL_PATH) moves it to the general path,
+    with the same verdict and chained CRC."""
+    monkeypatch.setenv("EWAL_FUSED", "0")
+    monkeypatch.setenv("EWAL_FRAME_WG", "1")
+    buf, n = W.synth_wal(2 << 20, 64, 4096, seed=11)
+    buf = bytes(buf)
+    o = O.readall(buf, 1)
+    c = W.Context(0)
+    try:
+        d = c.alloc(len(buf) + 64)
+        d.upload(buf)
+        r = W.readall_device(d, len(buf), 1)
+        assert r.flags & L.FLAG_FAST_PATH
+        assert (r.status, r.n_records, r.last_crc) == (O.OK, o["n_records"], o["last_crc"])
+        c.set_options(general_path=True)
+        g = W.readall_device(d, len(buf), 1)
+        assert not (g.flags & L.FLAG_FAST_PATH)
+        assert (g.status, g.n_records, g.last_crc, g.enti) == (r.status, r.n_records, r.last_crc, r.enti)
+        c.set_options(general_path=False)
+        assert W.readall_device(d, len(buf), 1).flags & L.FLAG_FAST_PATH
+        d.free()
+    finally:
+        c.close()
