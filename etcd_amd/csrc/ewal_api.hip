@@ -23,6 +23,7 @@
 #include "aux_kernels.hip"
 #include "msg_kernels.hip"
 #include "fused_kernels.hip"
+#include "frame_kernels.hip"
 #include "ewal_stage.h"
 
 #define EW_CHECK(x)                                                          \
@@ -121,7 +122,8 @@ struct ewal_ctx {
   std::map<uint32_t, DevTables> tables;
   std::map<uint32_t, std::unique_ptr<ewal::CrcTables>> host_tables;
   DevBuf encw, encs, lbstat, gagg, slow, mlist, pf, v, pwave, ux, tagg, tpx, wcnt, slots, cbase, ovf, cpos, clen, nxt, exc, E, rs, jl, vis, entry, on, rec_cand, rd, opf, ops, kk, kkrev, suf,
-      ents, recs, tmp, small, sdesc, snaps, hbuf_dev, xpos, walk, fpos, ulist, uitems, uarena, ftrec;
+      ents, recs, tmp, small, sdesc, snaps, hbuf_dev, xpos, walk, fpos, ulist, uitems, uarena, ftrec, fpl, fucb,
+      fnfp, frbase, fsp, ftcb;
   HostBuf hsdesc;                  // esnap_verify_packed's per-file table (host-mapped)
   // esnap_verify_packed's residual decode (esnap_copy_field): the batch's
   // buffer, per file its residual slot (-1: none), per slot its segments
@@ -168,6 +170,7 @@ struct ewal_ctx {
   uint64_t last_B = 0, last_ri = 0;
   uint64_t pfcap = 0;      // pf = [P at data starts | P at frame starts], pfcap each
   bool last_ok = false;
+  bool scan_valid = false;   // cpos / pwave / cbase hold the current stream pass's candidates and prefixes
 };
 
 // The HBM staging buffer of host bytes (ewal_readall_host, ewal_stage_*):
@@ -301,12 +304,21 @@ static void forget_records(ewal_ctx *c) {
   c->last_n = 0;
 }
 
-static int run_stream(ewal_ctx *c, DevTables *tb, const uint8_t *d_buf, uint64_t B, int find_cand, uint64_t ccap) {
+static int run_cand_scan(ewal_ctx *c, DevTables *tb, const uint8_t *d_buf, uint64_t B, int find_cand, uint64_t ccap);
+
+// The HBM pass (k_stream) over d_buf[0..B): v[] and, with find_cand, the
+// flagged pieces (hmask).  With scan also the candidate tests and the unit
+// scan (run_cand_scan): P at every unit start (pwave) and, with find_cand,
+// the dense, position-sorted candidate list cpos[] (units with more than
+// EW_SLOTS candidates are counted in Small.novf and filled in by k_rescan
+// later), its size in Small.total.  Asynchronous: nothing waits here.
+static int run_stream(ewal_ctx *c, DevTables *tb, const uint8_t *d_buf, uint64_t B, int find_cand, uint64_t ccap,
+                      bool scan = true) {
   forget_records(c);   // cpos / pwave / v are about to change (readall_impl sets them again after)
+  c->scan_valid = false;
   const uint64_t nunits64 = B / EW_WAVE_BYTES + 1;
   if (nunits64 >= 0xffff0000ull) return EWAL_E_INVAL;
   const uint32_t nunits = (uint32_t)nunits64;
-  const uint32_t nstiles = (nunits + EW_TILE_UNITS - 1) / EW_TILE_UNITS;
   if (int rc = stream_ensure(c, B, find_cand)) return rc;
   Small *ds = c->small.as<Small>();   // zeroed by k_stream (workgroup 0), the first kernel of every call
   StreamArgs a;
@@ -330,8 +342,21 @@ static int run_stream(ewal_ctx *c, DevTables *tb, const uint8_t *d_buf, uint64_t
     hipLaunchKernelGGL(k_stream<false>, dim3(grid), dim3(EW_THREADS), 0, c->stream, a);
   EW_CHECK(hipGetLastError());
   EW_CHECK(hipEventRecord(c->evs1, c->stream));
+  if (!scan) return 0;
+  return run_cand_scan(c, tb, d_buf, B, find_cand, ccap);
+}
+
+// The general path's inputs from the stream pass's v[] / hmask: the exact
+// candidate tests (k_cand -> slots, wcnt), the unit scan (pwave, cbase) and
+// the dense candidate list (cpos).  The fused frame pass needs none of them;
+// they run when the general path or the descriptors (ewal_copy_records) do.
+static int run_cand_scan(ewal_ctx *c, DevTables *tb, const uint8_t *d_buf, uint64_t B, int find_cand, uint64_t ccap) {
+  const uint32_t nunits = (uint32_t)(B / EW_WAVE_BYTES + 1);
+  const uint32_t nstiles = (nunits + EW_TILE_UNITS - 1) / EW_TILE_UNITS;
+  Small *ds = c->small.as<Small>();
   if (find_cand && EW_SPLIT_CAND && !(EW_XS & 8))   // the exact tests on the flagged pieces -> slots, wcnt
   {
+    EW_CHECK(c->cpos.ensure(ccap * 8));
     // four groups of 64 units per wave while that still gives every CU 16
     // waves (fewer, longer waves starve the CUs on small streams)
     const bool g4 = (uint64_t)nunits >= (uint64_t)std::max(1, c->num_cu) * 16 * 64 * 4;
@@ -347,8 +372,8 @@ static int run_stream(ewal_ctx *c, DevTables *tb, const uint8_t *d_buf, uint64_t
   ScanArgs s;
   s.nunits = nunits;
   s.ntiles = nstiles;
-  s.v = a.v;
-  s.wcnt = a.wcnt;
+  s.v = c->v.as<uint32_t>();
+  s.wcnt = c->wcnt.as<uint32_t>();
   s.g_shift = tb->shift;
   s.pwave = c->pwave.as<uint32_t>();
   s.cbase = c->cbase.as<unsigned long long>();
@@ -376,6 +401,7 @@ static int run_stream(ewal_ctx *c, DevTables *tb, const uint8_t *d_buf, uint64_t
   hipLaunchKernelGGL(k_tfix, dim3(ngroups), dim3(1024), 0, c->stream, s, ngroups);
   hipLaunchKernelGGL(k_uapply, dim3(sgrid), dim3(1024), 0, c->stream, s);
   EW_CHECK(hipGetLastError());
+  c->scan_valid = find_cand != 0;
   // units with more than EW_SLOTS candidates (ds->novf) are left out of cpos
   // here: k_frame then declines to speculate and the host runs k_rescan
   return 0;
@@ -572,78 +598,103 @@ static int walk_chain(ewal_ctx *c, DevTables *tb, const uint8_t *d_buf, uint64_t
   return 0;
 }
 
-// The fused frame + check pass (k_fc + k_fc_seam / fc_result, fused_kernels.hip) over
-// the stream pass's candidates: ONE host sync.  *done when the regular case
-// held (ResultDev in c->h_res, ents in c->ents); otherwise the reductions are
-// reset and the caller runs the general path over the same stream pass.
-// ents / mlist are sized for every candidate being an op (*ecap), grown when
-// the candidate count exceeds them (k_fc declines before doing any work).
+// The frame pass (k_frames + k_frames_seam, frame_kernels.hip) over the
+// stream pass's v[] / hmask: ONE host sync.  *done when the regular case held
+// (ResultDev in c->h_res, ents in c->ents); otherwise the caller runs the
+// general path over the same stream pass.  ents and the metadata list grow
+// and the pass reruns (once) when it reported them too small.
 #ifndef EW_SEAM_WGS
 #define EW_SEAM_WGS 2
 #endif
-// k_fc_seam's grid: grid-strided over the tiles, at most a few workgroups
-// per CU (ntiles is the capacity's tile count; the frame count is known only
-// on the device)
-static unsigned seam_grid(const ewal_ctx *c, uint64_t ntiles) {
-  return (unsigned)std::min<uint64_t>(grid_for(ntiles, 256), (uint64_t)std::max(1, c->num_cu) * EW_SEAM_WGS);
+// units per tile / 64: 4 (1 MiB tiles) once the stream gives every wave of
+// the grid at least two of them, else 1 (256 KiB tiles: more waves at work)
+static int fr_upl(const ewal_ctx *c, uint32_t nunits) {
+  return (uint64_t)nunits >= (uint64_t)256 * FR_WAVES * std::max(1, c->num_cu) * 2 ? 4 : 1;
 }
-static int fused_pass(ewal_ctx *c, DevTables *tb, const uint8_t *d_buf, uint64_t B, uint64_t ri, uint64_t ccap,
-                      uint64_t ecap, bool *done) {
+static int fr_ensure(ewal_ctx *c, uint32_t nunits, uint32_t ntiles) {
+  EW_CHECK(c->ftrec.ensure((size_t)ntiles * sizeof(FrTile)));
+  EW_CHECK(c->fpl.ensure((size_t)nunits * 4));
+  EW_CHECK(c->fucb.ensure((size_t)nunits * 4));
+  return 0;
+}
+static FrArgs fr_args(ewal_ctx *c, DevTables *tb, const uint8_t *d_buf, uint64_t B, uint32_t nunits, uint32_t ntiles,
+                      uint64_t ri, ewal_entry *ents, uint64_t ecap, uint32_t mcap) {
+  FrArgs a;
+  a.buf = d_buf;
+  a.B = B;
+  a.nunits = nunits;
+  a.ntiles = ntiles;
+  a.hmask = (const ulonglong2 *)c->hmask.p;
+  a.v = c->v.as<uint32_t>();
+  a.g_slice = tb->slice;
+  a.g_shift = tb->shift;
+  a.pl = c->fpl.as<uint32_t>();
+  a.ucb = c->fucb.as<uint32_t>();
+  a.trec = c->ftrec.as<FrTile>();
+  a.ents = ents;
+  a.ecap = ecap;
+  a.mlist = c->mlist.as<uint64_t>();
+  a.mcap = mcap;
+  a.ri = ri;
+  a.ds = c->small.as<Small>();
+  return a;
+}
+// the call's scratch as k_stream leaves it (a rerun of the frame pass, or the
+// general path after it)
+static int reset_small(ewal_ctx *c) {
   Small *ds = c->small.as<Small>();
+  EW_CHECK(hipMemsetAsync(ds, 0, sizeof(Small), c->stream));
+  if (c->defer_first) EW_CHECK(hipMemsetAsync(&ds->defer_first, 1, 1, c->stream));
+  return 0;
+}
+static int frames_pass(ewal_ctx *c, DevTables *tb, const uint8_t *d_buf, uint64_t B, uint64_t ri, uint64_t ecap,
+                       bool *done) {
   *done = false;
-  const uint64_t ntiles = ccap / FC_TILE + 2;
-  EW_CHECK(c->ftrec.ensure((size_t)ntiles * sizeof(TileRec)));
-  bool rescanned = false;
+  const uint32_t nunits = (uint32_t)(B / EW_WAVE_BYTES + 1);
+  const int upl = fr_upl(c, nunits);
+  const uint32_t tu = 64u * (uint32_t)upl, ntiles = (nunits + tu - 1) / tu;
+  if (int rc = fr_ensure(c, nunits, ntiles)) return rc;
+  uint32_t mcap = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(c->mlist.cap / 8, 4096), 0xffffffffull);
   for (int pass = 0; pass < 3; ++pass) {
     EW_CHECK(c->ents.ensure((size_t)ecap * sizeof(ewal_entry)));
-    EW_CHECK(c->mlist.ensure((size_t)ecap * 4));
-    FcArgs a;
-    a.buf = d_buf;
-    a.B = B;
-    a.cpos = c->cpos.as<uint64_t>();
-    a.ccap = ccap;
-    a.ecap = ecap;
-    a.pwave = c->pwave.as<uint32_t>();
-    a.v = c->v.as<uint32_t>();
-    a.g_slice = tb->slice;
-    a.g_shift = tb->shift;
-    a.ri = ri;
-    a.trec = c->ftrec.as<TileRec>();
-    a.ents = c->ents.as<ewal_entry>();
-    a.mlist = c->mlist.as<uint32_t>();
-    a.ds = ds;
-    a.ablate = c->fc_ablate;
-    hipLaunchKernelGGL(k_fc<false>, dim3((unsigned)std::max(1, c->num_cu) * FC_WGS), dim3(FC_THREADS), 0, c->stream,
-                       a, SegArgs{});
-    // the seam pass; its last workgroup gathers the result (fc_result)
-    hipLaunchKernelGGL(k_fc_seam<false>, dim3(seam_grid(c, ntiles)), dim3(256), 0, c->stream, d_buf, B, a.cpos,
-                       tb->shift, a.trec, a.ents, ri, ccap, ecap, ds, SegArgs{}, (const uint32_t *)a.mlist,
-                       c->h_res_dev, c->h_small_dev);
+    EW_CHECK(c->mlist.ensure((size_t)mcap * 8));
+    if (pass) if (int rc = reset_small(c)) return rc;
+    FrArgs a = fr_args(c, tb, d_buf, B, nunits, ntiles, ri, c->ents.as<ewal_entry>(), ecap, mcap);
+    const unsigned grid = (unsigned)std::min<uint64_t>(grid_for(ntiles, FR_WAVES), (uint64_t)std::max(1, c->num_cu));
+    const unsigned sgrid = (unsigned)std::min<uint64_t>(grid_for(ntiles, 256), (uint64_t)std::max(1, c->num_cu) * EW_SEAM_WGS);
+    if (upl == 4) {
+      hipLaunchKernelGGL((k_frames<false, 4>), dim3(grid), dim3(FR_THREADS), 0, c->stream, a, FrSeg{});
+      hipLaunchKernelGGL((k_frames_seam<false, 4>), dim3(sgrid), dim3(256), 0, c->stream, a, FrSeg{}, c->h_res_dev,
+                         c->h_small_dev);
+    } else {
+      hipLaunchKernelGGL((k_frames<false, 1>), dim3(grid), dim3(FR_THREADS), 0, c->stream, a, FrSeg{});
+      hipLaunchKernelGGL((k_frames_seam<false, 1>), dim3(sgrid), dim3(256), 0, c->stream, a, FrSeg{}, c->h_res_dev,
+                         c->h_small_dev);
+    }
     EW_CHECK(hipGetLastError());
     // the call's end event rides behind the last kernel: when the regular
     // case held, the sync below is the call's only wait for the device
     EW_CHECK(hipEventRecord(c->ev1, c->stream));
     EW_CHECK(hipStreamSynchronize(c->stream));
-    if (c->h_small->errflag) return EWAL_E_TIMEOUT;
-    if (c->h_small->spec_n) {
+    const Small *hs = c->h_small;
+    if (hs->errflag) return EWAL_E_TIMEOUT;
+    if (hs->spec_n) {
       *done = true;
       return 0;
     }
-    hipLaunchKernelGGL(k_reset_check, dim3(1), dim3(64), 0, c->stream, ds);
-    EW_CHECK(hipGetLastError());
-    const uint64_t K = c->h_small->total;
-    if (c->h_small->novf && K <= ccap && !rescanned) {   // units with more than EW_SLOTS candidates
-      if (int rc = rescan_overflow(c, d_buf, B, ccap)) return rc;
-      rescanned = true;
-      if (K > ecap) ecap = K + K / 8 + 1024;
-      continue;
+    // declined for capacity only: room for what it asked, once more
+    const uint32_t rare = hs->fc.rare;
+    if (hs->irregular || (rare & ~(4u | 8u))) break;
+    bool again = false;
+    if ((rare & 4u) && hs->fr_need > ecap && hs->fr_need < 0xffffff00ull) {
+      ecap = hs->fr_need + hs->fr_need / 8 + 1024;
+      again = true;
     }
-    // k_fc declined for capacity only: room for every candidate, once more
-    if (c->h_small->fc.rare == 4u && K > ecap && K <= ccap && !c->h_small->novf) {
-      ecap = K + K / 8 + 1024;
-      continue;
+    if ((rare & 8u) && hs->nmeta > mcap) {
+      mcap = hs->nmeta + hs->nmeta / 8 + 1024;
+      again = true;
     }
-    break;
+    if (!again) break;
   }
   return 0;
 }
@@ -744,7 +795,7 @@ static int readall_impl(ewal_ctx *c, const uint8_t *d_buf, uint64_t B, uint64_t 
     // frame count with headroom, at least one frame per 4 KiB
     uint64_t rdcap = std::min<uint64_t>(ccap, std::max<uint64_t>(c->last_k + c->last_k / 8 + 1024,
                                                                  B / 4096 + 1024));
-    rc = run_stream(c, tb, d_buf, B, 1, ccap);
+    rc = run_stream(c, tb, d_buf, B, 1, ccap, !c->fused);
     if (rc) return rc;
     if (c->defer_first) EW_CHECK(hipMemsetAsync(&ds->defer_first, 1, 1, c->stream));   // (Small is zeroed by k_stream)
 #if EW_XS
@@ -760,9 +811,14 @@ static int readall_impl(ewal_ctx *c, const uint8_t *d_buf, uint64_t B, uint64_t 
 #endif
     bool fused_done = false;
     if (c->fused) {
-      rc = fused_pass(c, tb, d_buf, B, ri, ccap, rdcap, &fused_done);
+      const uint64_t ecap = std::max<uint64_t>(rdcap, c->ents.cap / sizeof(ewal_entry));
+      rc = frames_pass(c, tb, d_buf, B, ri, ecap, &fused_done);
       if (rc) return rc;
       ev1_final = fused_done;   // ev1 is behind the last kernel unless more work is queued below
+      if (!fused_done) {   // the general path over the same stream pass: its candidates and prefixes first
+        if ((rc = reset_small(c))) return rc;
+        if ((rc = run_cand_scan(c, tb, d_buf, B, 1, ccap))) return rc;
+      }
     }
     uint32_t *pf = nullptr;
     bool rescanned = false;
@@ -837,7 +893,7 @@ static int readall_impl(ewal_ctx *c, const uint8_t *d_buf, uint64_t B, uint64_t 
     K = c->h_small->total;
     c->last_k = K;
     fused_done_final = fused_done;
-    if (fused_done) {   // frames decoded and checked by k_fc; the result is in h_res
+    if (fused_done) {   // frames decoded and checked by k_frames; the result is in h_res
       decoded = true;
       spec_checked = true;
     } else if (K && K <= ccap && K <= rdcap && !c->h_small->novf && c->h_small->pos0 == 0 &&
@@ -1124,73 +1180,83 @@ static hipError_t grow_keep(DevBuf &b, size_t need, size_t keep, hipStream_t st)
   return hipSuccess;
 }
 
-// The batch on the fused pass (k_shard_start_fc, k_fc<true>, per-shard
-// metadata rule and results): ONE host sync.  *done when every shard took
-// the regular case (out[] and the ents / ent_first tables filled); otherwise
-// the reductions are reset and the caller runs the general batch path.
-static int fused_batch(ewal_ctx *c, DevTables *tb, const uint8_t *d_buf, uint64_t B, uint32_t ns,
-                       const std::vector<uint64_t> &soff, const uint64_t *ris, uint64_t ccap, uint64_t ecap,
-                       ewal_result *out, bool *done) {
+// The batch on the frame pass (k_shard_nfp / k_shard_rbase: every shard's
+// ents region; k_frames<true>, k_frames_seam<true>; per-shard metadata rule
+// and results): ONE host sync.  *done when the pass decided the batch (out[]
+// and the ents / ent_first tables filled; shards it could not decide carry
+// EW_SHARD_BAD); otherwise the caller runs the general batch path.  Shard s's
+// entry op k is bents[rbase[s] + k], rbase[s] = 4 x the flagged pieces of the
+// shards before s (an entry frame is >= 20 bytes: at most 4 start in a 64-B
+// piece); *have = the regions' total (shards replayed alone append after it).
+static int frames_batch(ewal_ctx *c, DevTables *tb, const uint8_t *d_buf, uint64_t B, uint32_t ns,
+                        const std::vector<uint64_t> &soff, const uint64_t *ris, ewal_result *out, bool *done,
+                        uint64_t *have) {
   Small *ds = c->small.as<Small>();
   *done = false;
-  const uint64_t ntiles = ccap / FC_TILE + 2;
-  EW_CHECK(c->ftrec.ensure((size_t)ntiles * sizeof(TileRec)));
+  const uint32_t nunits = (uint32_t)(B / EW_WAVE_BYTES + 1);
+  const int upl = fr_upl(c, nunits);
+  const uint32_t tu = 64u * (uint32_t)upl, ntiles = (nunits + tu - 1) / tu;
+  if (int rc = fr_ensure(c, nunits, ntiles)) return rc;
   EW_CHECK(c->bsoff.ensure((size_t)(ns + 1) * 8));
   EW_CHECK(c->bri.ensure((size_t)ns * 8));
-  EW_CHECK(c->bfs.ensure((size_t)(ns + 1) * 4));
-  EW_CHECK(c->bsagg.ensure((size_t)ns * sizeof(ShardAgg)));
   EW_CHECK(c->bres.ensure((size_t)ns * sizeof(ewal_result)));
   EW_CHECK(c->bef.ensure((size_t)ns * 8));
+  EW_CHECK(c->fnfp.ensure((size_t)ns * 8));
+  EW_CHECK(c->frbase.ensure((size_t)(ns + 1) * 8));
+  EW_CHECK(c->fsp.ensure((size_t)ns * sizeof(ShardPos)));
+  EW_CHECK(c->ftcb.ensure((size_t)ntiles * 4));
   EW_CHECK(hipMemcpyAsync(c->bsoff.p, soff.data(), (size_t)(ns + 1) * 8, hipMemcpyHostToDevice, c->stream));
   EW_CHECK(hipMemcpyAsync(c->bri.p, ris, (size_t)ns * 8, hipMemcpyHostToDevice, c->stream));
-  SegArgs sg;
-  sg.ulist = nullptr;
-  sg.fs = c->bfs.as<uint32_t>();
+  FrSeg sg;
   sg.ns = ns;
-  sg.ri = c->bri.as<uint64_t>();
   sg.soff = c->bsoff.as<uint64_t>();
-  sg.sagg = c->bsagg.as<ShardAgg>();
-  bool rescanned = false;
+  sg.ri = c->bri.as<uint64_t>();
+  sg.rbase = c->frbase.as<uint64_t>();
+  sg.sp = c->fsp.as<ShardPos>();
+  sg.tcb = c->ftcb.as<uint32_t>();
+  uint64_t ecap = std::max<uint64_t>(c->bents.cap / sizeof(ewal_entry), B / 256 + 1024);
+  uint32_t mcap = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(c->mlist.cap / 8, (uint64_t)ns + 4096), 0xffffffffull);
   for (int pass = 0; pass < 3; ++pass) {
     EW_CHECK(grow_keep(c->bents, (size_t)ecap * sizeof(ewal_entry), 0, c->stream));
-    EW_CHECK(c->mlist.ensure((size_t)ecap * 4));
-    FcArgs a;
-    a.buf = d_buf;
-    a.B = B;
-    a.cpos = c->cpos.as<uint64_t>();
-    a.ccap = ccap;
-    a.ecap = ecap;
-    a.pwave = c->pwave.as<uint32_t>();
-    a.v = c->v.as<uint32_t>();
-    a.g_slice = tb->slice;
-    a.g_shift = tb->shift;
-    a.ri = 0;
-    a.trec = c->ftrec.as<TileRec>();
-    a.ents = c->bents.as<ewal_entry>();
-    a.mlist = c->mlist.as<uint32_t>();
-    a.ds = ds;
-    a.ablate = c->fc_ablate;
-    hipLaunchKernelGGL(k_shard_start_fc, dim3(grid_for(ns + 1, 256)), dim3(256), 0, c->stream, a.cpos, ccap,
-                       c->bsoff.as<uint64_t>(), ns, c->bfs.as<uint32_t>(), sg.sagg, ds);
-    hipLaunchKernelGGL(k_fc<true>, dim3((unsigned)std::max(1, c->num_cu) * FC_WGS), dim3(FC_THREADS), 0, c->stream, a,
-                       sg);
-    hipLaunchKernelGGL(k_fc_seam<true>, dim3(seam_grid(c, ntiles)), dim3(256), 0, c->stream, d_buf, B, a.cpos,
-                       tb->shift, a.trec, a.ents, 0ull, ccap, ecap, ds, sg, (const uint32_t *)nullptr,
-                       (ResultDev *)nullptr, (Small *)nullptr);
-    hipLaunchKernelGGL(k_meta_batch_fc, dim3(64), dim3(256), 0, c->stream, d_buf, B, a.cpos, ccap, ecap, a.mlist, ds,
-                       sg);
-    hipLaunchKernelGGL(k_result_batch_fc, dim3(grid_for((uint64_t)ns * 8, 256)), dim3(256), 0, c->stream, d_buf, B, a.cpos, ccap,
-                       ecap, ds, sg, c->bres.as<ewal_result>(), c->bef.as<unsigned long long>());
-    hipLaunchKernelGGL(k_batch_gate_fc, dim3(1), dim3(64), 0, c->stream, ds, ccap, ecap, B, c->h_small_dev);
+    EW_CHECK(c->mlist.ensure((size_t)mcap * 8));
+    if (pass) if (int rc = reset_small(c)) return rc;
+    FrArgs a = fr_args(c, tb, d_buf, B, nunits, ntiles, 0, c->bents.as<ewal_entry>(), ecap, mcap);
+    EW_CHECK(hipMemsetAsync(c->fnfp.p, 0, (size_t)ns * 8, c->stream));
+    const unsigned ngrid = (unsigned)std::min<uint64_t>(grid_for(nunits, 256), (uint64_t)std::max(1, c->num_cu) * 8);
+    hipLaunchKernelGGL(k_shard_nfp, dim3(ngrid), dim3(256), 0, c->stream, a.hmask, nunits, sg.soff, ns,
+                       c->fnfp.as<unsigned long long>());
+    hipLaunchKernelGGL(k_shard_rbase, dim3(1), dim3(1024), 0, c->stream, (const unsigned long long *)c->fnfp.p, ns,
+                       ecap, sg.rbase, sg.sp, ds);
+    const unsigned grid = (unsigned)std::min<uint64_t>(grid_for(ntiles, FR_WAVES), (uint64_t)std::max(1, c->num_cu));
+    const unsigned sgrid = (unsigned)std::min<uint64_t>(grid_for(ntiles, 256), (uint64_t)std::max(1, c->num_cu) * EW_SEAM_WGS);
+    if (upl == 4) {
+      hipLaunchKernelGGL((k_frames<true, 4>), dim3(grid), dim3(FR_THREADS), 0, c->stream, a, sg);
+      hipLaunchKernelGGL((k_frames_seam<true, 4>), dim3(sgrid), dim3(256), 0, c->stream, a, sg, (ResultDev *)nullptr,
+                         (Small *)nullptr);
+    } else {
+      hipLaunchKernelGGL((k_frames<true, 1>), dim3(grid), dim3(FR_THREADS), 0, c->stream, a, sg);
+      hipLaunchKernelGGL((k_frames_seam<true, 1>), dim3(sgrid), dim3(256), 0, c->stream, a, sg, (ResultDev *)nullptr,
+                         (Small *)nullptr);
+    }
+    hipLaunchKernelGGL(k_tile_scan, dim3(1), dim3(1024), 0, c->stream, (const FrTile *)a.trec, ntiles, sg.tcb,
+                       (const Small *)ds);
+    hipLaunchKernelGGL(k_meta_batch_fr, dim3(64), dim3(256), 0, c->stream, a, sg);
+    if (upl == 4)
+      hipLaunchKernelGGL(k_result_batch_fr<4>, dim3(grid_for((uint64_t)ns * 64, 256)), dim3(256), 0, c->stream, a, sg,
+                         c->bres.as<ewal_result>(), c->bef.as<unsigned long long>());
+    else
+      hipLaunchKernelGGL(k_result_batch_fr<1>, dim3(grid_for((uint64_t)ns * 64, 256)), dim3(256), 0, c->stream, a, sg,
+                         c->bres.as<ewal_result>(), c->bef.as<unsigned long long>());
+    hipLaunchKernelGGL(k_batch_gate_fr, dim3(1), dim3(64), 0, c->stream, ds, c->h_small_dev);
     EW_CHECK(hipGetLastError());
     EW_CHECK(hipMemcpyAsync(out, c->bres.p, (size_t)ns * sizeof(ewal_result), hipMemcpyDeviceToHost, c->stream));
     EW_CHECK(hipMemcpyAsync(c->bent_first.data(), c->bef.p, (size_t)ns * 8, hipMemcpyDeviceToHost, c->stream));
     EW_CHECK(hipEventRecord(c->ev1, c->stream));
     EW_CHECK(hipStreamSynchronize(c->stream));
-    if (c->h_small->errflag) return EWAL_E_TIMEOUT;
-    const uint64_t K = c->h_small->total;
-    c->last_k = K;
-    if (c->h_small->spec_n) {
+    const Small *hs = c->h_small;
+    if (hs->errflag) return EWAL_E_TIMEOUT;
+    c->last_k = hs->total;
+    if (hs->spec_n) {
       float dev_ms = 0, str_ms = 0;
       EW_CHECK(hipEventElapsedTime(&dev_ms, c->ev0, c->ev1));
       EW_CHECK(hipEventElapsedTime(&str_ms, c->evs0, c->evs1));
@@ -1200,22 +1266,20 @@ static int fused_batch(ewal_ctx *c, DevTables *tb, const uint8_t *d_buf, uint64_
         c->bnents[i] = (uint64_t)out[i].n_ents;
         if (!out[i].n_ents) c->bent_first[i] = 0;
       }
+      *have = hs->fr_need;
       *done = true;
       return 0;
     }
-    hipLaunchKernelGGL(k_reset_check, dim3(1), dim3(64), 0, c->stream, ds);
-    EW_CHECK(hipGetLastError());
-    if (c->h_small->novf && K <= ccap && !rescanned) {   // units with more than EW_SLOTS candidates
-      if (int rc = rescan_overflow(c, d_buf, B, ccap)) return rc;
-      rescanned = true;
-      if (K > ecap) ecap = K + K / 8 + 1024;
-      continue;
+    bool again = false;
+    if (hs->fr_capfail && hs->fr_need > ecap) {
+      ecap = hs->fr_need + hs->fr_need / 8 + 1024;
+      again = true;
     }
-    if (c->h_small->fc.rare == 4u && K > ecap && K <= ccap && !c->h_small->novf) {
-      ecap = K + K / 8 + 1024;
-      continue;
+    if ((hs->fc.rare & 8u) && hs->nmeta > mcap) {
+      mcap = hs->nmeta + hs->nmeta / 8 + 1024;
+      again = true;
     }
-    break;
+    if (!again || (hs->fc.rare & ~8u)) break;
   }
   return 0;
 }
@@ -1318,7 +1382,7 @@ static int readall_batch_impl(ewal_ctx *c, const uint8_t *d_buf, uint32_t ns, co
     EW_CHECK(c->cpos.ensure(ccap * 8));
     uint64_t rdcap = std::min<uint64_t>(ccap, std::max<uint64_t>(c->last_k + c->last_k / 8 + 1024,
                                                                  B / 1024 + 1024));
-    rc = run_stream(c, tb, d_buf, B, 1, ccap);
+    rc = run_stream(c, tb, d_buf, B, 1, ccap, !c->fused);
     if (rc) return rc;
 #if EW_XS
     // timing-only ablation builds (tools/build_ab.sh -DEW_XS=...): the stream pass alone
@@ -1335,14 +1399,15 @@ static int readall_batch_impl(ewal_ctx *c, const uint8_t *d_buf, uint32_t ns, co
 #endif
     if (c->fused) {
       bool done = false;
-      rc = fused_batch(c, tb, d_buf, B, ns, soff, ris, ccap, rdcap, out, &done);
+      uint64_t have = 0;
+      rc = frames_batch(c, tb, d_buf, B, ns, soff, ris, out, &done, &have);
       if (rc) return rc;
       if (ew_debug()) {
         uint32_t nb = 0;
         for (uint32_t i = 0; i < ns && done; ++i) nb += (out[i].flags & EW_SHARD_BAD) != 0;
-        std::fprintf(stderr, "ewal batch: fused done %d bad %u (K %llu ccap %llu ecap %llu novf %u rare %u err %u)\n",
-                     (int)done, nb, (unsigned long long)c->h_small->total, (unsigned long long)ccap,
-                     (unsigned long long)rdcap, c->h_small->novf, c->h_small->fc.rare, c->h_small->errflag);
+        std::fprintf(stderr, "ewal batch: frame pass done %d bad %u (K %llu need %llu rare %u irr %u capfail %u err %u)\n",
+                     (int)done, nb, (unsigned long long)c->h_small->total, (unsigned long long)c->h_small->fr_need,
+                     c->h_small->fc.rare, c->h_small->irregular, c->h_small->fr_capfail, c->h_small->errflag);
       }
       if (done) {   // every shard decided but those the fused pass flagged: they are replayed alone
         std::vector<uint32_t> bad;
@@ -1354,11 +1419,14 @@ static int readall_batch_impl(ewal_ctx *c, const uint8_t *d_buf, uint32_t ns, co
           c->bsplit_bytes.assign(ns, {});
           return 0;
         }
-        rc = replay_shards(c, d_buf, soff, lens, ris, out, bad, c->h_small->total);
+        rc = replay_shards(c, d_buf, soff, lens, ris, out, bad, have);
         if (rc) return rc;
         forget_records(c);
         return 0;
       }
+      // the general batch path over the same stream pass: its candidates and prefixes first
+      if ((rc = reset_small(c))) return rc;
+      if ((rc = run_cand_scan(c, tb, d_buf, B, 1, ccap))) return rc;
     }
     uint32_t *pf = nullptr;
     bool rescanned = false;
@@ -1500,6 +1568,13 @@ static int materialise_records(ewal_ctx *c) {
   EW_CHECK(c->slow.ensure((size_t)n * 4));
   c->pfcap = n;
   uint32_t *pf = c->pf.as<uint32_t>();
+  if (!c->scan_valid) {   // the frame pass decided the call: the candidate list and prefixes first
+    EW_CHECK(hipMemsetAsync(ds, 0, sizeof(Small), c->stream));
+    if (c->last_deferred) EW_CHECK(hipMemsetAsync(&ds->defer_first, 1, 1, c->stream));
+    if ((rc = run_cand_scan(c, tb, c->last_buf, c->last_B, 1, ccap))) return rc;
+    if ((rc = sync_small(c))) return rc;
+    if (c->h_small->novf && (rc = rescan_overflow(c, c->last_buf, c->last_B, ccap))) return rc;
+  }
   hipLaunchKernelGGL(k_reset_check, dim3(1), dim3(64), 0, c->stream, ds);
   const unsigned fgrid = (unsigned)std::max(1, c->num_cu) * c->frame_wg;
   hipLaunchKernelGGL(k_frame, dim3(fgrid), dim3(256), 0, c->stream, c->last_buf, c->last_B, c->cpos.as<uint64_t>(),
@@ -1623,11 +1698,14 @@ int ewal_ctx_reserve(ewal_ctx *c, uint64_t wal_bytes, uint32_t flags) {
   EW_CHECK(c->cpos.ensure(ccap * 8));
   // the fused pass: look-back words, tile records, ents / mlist for the
   // first call's descriptor capacity (readall_impl's rdcap)
-  const uint64_t ntiles = ccap / FC_TILE + 2;
-  EW_CHECK(c->ftrec.ensure((size_t)ntiles * sizeof(TileRec)));
+  {
+    const uint32_t nunits = (uint32_t)(B / EW_WAVE_BYTES + 1);
+    const uint32_t tu = 64u * (uint32_t)fr_upl(c, nunits);
+    if ((rc = fr_ensure(c, nunits, (nunits + tu - 1) / tu))) return rc;
+  }
   const uint64_t ecap = std::min<uint64_t>(ccap, B / 4096 + 1024);
   EW_CHECK(c->ents.ensure((size_t)ecap * sizeof(ewal_entry)));
-  EW_CHECK(c->mlist.ensure((size_t)ecap * 4));
+  EW_CHECK(c->mlist.ensure((size_t)4096 * 8));
   // load the device code: a ReadAll over a one-frame WAL (a crcType record)
   static const uint8_t tiny[16] = {4, 0, 0, 0, 0, 0, 0, 0, 0x08, 0x04, 0x10, 0x00};
   EW_CHECK(stage_ensure(c, 64));

@@ -125,6 +125,13 @@ struct FcAgg {
   uint32_t last_chained;          // the running CRC after the last frame
 };
 
+// The frame pass's reductions (k_frames_seam, single WAL): stream positions.
+struct FrAgg {
+  unsigned long long le, ls;      // 1 + the last entry / state frame's position (max), 0: none
+  unsigned long long lo;          // 1 + the last entry op's position (max), 0: none
+  unsigned long long nops;        // entry ops
+};
+
 // Per-call device scratch (zeroed / initialised each call).
 struct Small {
   uint32_t ticket;
@@ -157,6 +164,9 @@ struct Small {
   uint32_t ncatfail;              // frames left undecoded for want of room (the host grows the arena, reruns)
   uint32_t defer_first;           // a range of a WAL split inside a file (ewal_readall_range_device): frame
                                   // 0's CRC check is the caller's (the running CRC before it is not known here)
+  uint32_t fr_capfail;            // batch: the shards' ents regions exceed the capacity (k_shard_rbase)
+  FrAgg fr;
+  unsigned long long fr_need;     // single WAL: ents the frame pass needed; batch: the regions' total
 };
 
 // A returned Entry (ent = its index in ents) or the HardState (ent = -1)
