@@ -117,9 +117,21 @@ class RangeInfo(C.Structure):   # ewal_range_info
                 ("md_value_off", C.c_int64), ("md_value_len", C.c_int64), ("first_entry_frame", C.c_int64),
                 ("last_entry_frame", C.c_int64), ("first_entry_index", C.c_uint64),
                 ("min_entry_index", C.c_uint64), ("last_entry_index", C.c_uint64), ("last_op_frame", C.c_int64),
-                ("last_op_index", C.c_uint64), ("md_split", C.c_int32), ("pad", C.c_int32),
+                ("last_op_index", C.c_uint64), ("md_split", C.c_int32), ("first_pre_crc", C.c_int32),
                 ("first_type", C.c_int64), ("first_dlen", C.c_uint64), ("first_stored_crc", C.c_uint32),
-                ("first_u0", C.c_uint32)]
+                ("first_u0", C.c_uint32), ("end_off", C.c_uint64), ("n_bytes", C.c_uint64)]
+
+
+class RangeRow(C.Structure):    # ewal_range_row
+    _fields_ = [("status", C.c_int32), ("deferred", C.c_int32), ("fail_record", C.c_int64),
+                ("n_records", C.c_int64), ("ri", C.c_uint64), ("last_crc", C.c_uint32), ("pad", C.c_uint32),
+                ("detail", C.c_int64), ("info", RangeInfo)]
+
+
+class SplitResult(C.Structure):  # ewal_split_result
+    _fields_ = [("status", C.c_int32), ("resplit", C.c_int32), ("fail_record", C.c_int64),
+                ("n_records", C.c_int64), ("detail", C.c_int64), ("last_crc", C.c_uint32), ("pad", C.c_uint32),
+                ("enti", C.c_uint64)]
 
 
 class SnapshotDesc(C.Structure):
@@ -161,6 +173,11 @@ _SIGS = {
     "ewal_batch_copy_unrec": (C.c_int64, [vp, C.c_uint64, C.POINTER(UnrecDesc), C.c_int64]),
     "ewal_batch_copy_unrec_bytes": (C.c_int64, [vp, C.c_uint64, vp, C.c_int64]),
     "ewal_copy_range_info": (C.c_int, [vp, C.POINTER(RangeInfo)]),
+    "ewal_split_verdict": (C.c_int, [C.POINTER(RangeRow), C.c_uint64, C.c_uint64, vp, C.c_uint64,
+                                     C.POINTER(SplitResult)]),
+    "ewal_readall_multi": (C.c_int, [C.POINTER(vp), C.c_uint32, vp, C.c_uint64, C.POINTER(C.c_uint64),
+                                     C.POINTER(C.c_uint64), C.c_uint32, C.c_uint64, C.POINTER(SplitResult),
+                                     C.POINTER(C.c_uint32)]),
     "ewal_copy_unrec": (C.c_int64, [vp, C.POINTER(UnrecDesc), C.c_int64]),
     "ewal_copy_unrec_bytes": (C.c_int64, [vp, vp, C.c_int64]),
     "ewal_copy_split_bytes": (C.c_int64, [vp, vp, C.c_int64]),

@@ -171,6 +171,7 @@ struct ewal_ctx {
   uint64_t pfcap = 0;      // pf = [P at data starts | P at frame starts], pfcap each
   bool last_ok = false;
   bool scan_valid = false;   // cpos / pwave / cbase hold the current stream pass's candidates and prefixes
+  uint64_t last_q = 0;       // where the last ReadAll's frame chain ended (decoder.decode's terminal)
 };
 
 // The HBM staging buffer of host bytes (ewal_readall_host, ewal_stage_*):
@@ -954,6 +955,7 @@ static int readall_impl(ewal_ctx *c, const uint8_t *d_buf, uint64_t B, uint64_t 
     if (rc) return rc;
   }
   int tst = classify_terminal(B, q, qlen);
+  c->last_q = q;
   // walked frames (not candidates) on the chain: decoded and checked with the
   // chain's candidates from one frame-position list (fpos)
   std::vector<uint64_t> xs;
@@ -984,6 +986,7 @@ static int readall_impl(ewal_ctx *c, const uint8_t *d_buf, uint64_t B, uint64_t 
     }
   }
 
+  c->last_q = q;   // (walk_chain may have moved it)
   ResultDev res;
   std::memset(&res, 0, sizeof(res));
   res.agg.first_fail = ~0ull;
@@ -1946,6 +1949,8 @@ int ewal_copy_range_info(ewal_ctx *c, ewal_range_info *out) {
   if (int rc = need_records(c)) return rc;
   const uint64_t n = c->last_n;
   o.n_frames = (int64_t)n;
+  o.end_off = c->last_q;
+  o.n_bytes = c->last_B;
   if (n) {
     EW_CHECK(c->sdesc.ensure(sizeof(RangeDev)));
     RangeDev h0{~0ull, ~0ull, ~0ull, ~0ull, 0ull, 0ull}, h;
@@ -1966,6 +1971,7 @@ int ewal_copy_range_info(ewal_ctx *c, ewal_range_info *out) {
     o.first_dlen = d.dlen;
     o.first_stored_crc = d.crc;
     o.first_u0 = d.chained;   // k_check ran frame 0 from seed 0: crc32.Update(0, Data) (crcType: the stored CRC)
+    o.first_pre_crc = d.st != 0;   // framing / Record.Unmarshal (d.st) fail before Validate; Entry / HardState (sub_st) after
     if (h.md_first != ~0ull) {
       EW_CHECK(frame(h.md_first, &d));
       o.md_first_frame = (int64_t)h.md_first;

@@ -107,16 +107,8 @@ def seam_check(dist, world: int, rank: int, first_crc_record: int, last_crc: int
     return -1
 
 
-# ---- one WAL split across ranks by file -------------------------------------
-# Status numbers of the verdict (include/ewal.h)
-_OK, _UNEXPECTED_EOF, _WAL_CRC, _META_CONFLICT, _INDEX_NOT_FOUND, _INDEX_GAP = 0, 2, 4, 5, 6, 36
-_RECORD_CRC = 3
-# failures decoder.decode reports before its CRC check (wal/decoder.go:30-41:
-# framing, Record.Unmarshal) -- they win over a frame-0 CRC mismatch
-_PRE_CRC = (2, 7, 32, 33, 37, 48)
+# ---- one WAL split across ranks ------------------------------------------------
 _U64 = (1 << 64) - 1
-_ROW = 21
-_CASTAGNOLI = 0x82F63B78
 
 
 def range_bounds(dist, world: int, rank: int, probe, n_bytes: int, ri_global: int, device="cpu"):
@@ -127,158 +119,111 @@ def range_bounds(dist, world: int, rank: int, probe, n_bytes: int, ri_global: in
     end, w.ri)] of every range: end = the next range's start; w.ri = max(the
     global ri, the first entry Index) so the range's first op is its ents[0]
     (split_verdict carries the ents rules across ranges).  A rank whose share
-    holds no candidate gets an empty range."""
+    holds no candidate gets an empty range and the range before it reaches to
+    the next share's candidate (ewal_readall_multi does the same)."""
     if rank == 0:
         pos, idx = 0, -1
     else:
         pos, idx = probe(rank * n_bytes // world)
-        if pos < 0:
-            pos = n_bytes
     mine = torch.tensor([pos, idx], dtype=torch.int64, device=device)
     allv = [torch.zeros(2, dtype=torch.int64, device=device) for _ in range(world)]
     dist.all_gather(allv, mine)
-    starts = [int(v[0].item()) for v in allv]
-    for k in range(1, world):           # monotone (an empty range where a share held none)
+    starts = [int(v[0].item()) for v in allv] + [n_bytes]
+    for k in range(world - 1, 0, -1):   # a miss: empty, at the next share's candidate
+        if starts[k] < 0:
+            starts[k] = starts[k + 1]
+    for k in range(1, world):           # monotone
         starts[k] = max(starts[k], starts[k - 1])
     out = []
     for k in range(world):
-        end = starts[k + 1] if k + 1 < world else n_bytes
         idx = int(allv[k][1].item())
         ri = ri_global if k == 0 or idx < 0 else max(ri_global, idx)
-        out.append((starts[k], end, ri))
+        out.append((starts[k], starts[k + 1], ri))
     return out
 
 
-def _crc_combine(crc_a: int, crc_b: int, len_b: int) -> int:
-    """crc32.Update(crc_a, Castagnoli, B) from crc_b = Update(0, B) and len(B)
-    (the product's host helper, ewal_crc32_combine)."""
+def range_row(result, info, ri_range: int, deferred: bool = False):
+    """ewal_range_row of one range (include/ewal.h) and its metadata bytes:
+    result = (status, fail_record, n_records, last_crc[, detail]) of ReadAll
+    over the range, info = wal.range_info() of it (or the oracle's stand-in)."""
     from . import _lib
-    return int(_lib.lib.ewal_crc32_combine(_CASTAGNOLI, crc_a & 0xffffffff, crc_b & 0xffffffff, len_b))
+    r = _lib.RangeRow()
+    st, fr, n, lc = result[:4]
+    r.status, r.fail_record, r.n_records, r.last_crc = st, fr, n, lc & 0xffffffff
+    r.detail = result[4] if len(result) > 4 else 0
+    r.ri = ri_range & _U64
+    r.deferred = 1 if deferred else 0
+    i = r.info
+    mdf, mdv = info.get("md_first"), info.get("md_value")
+    for key in ("n_frames", "first_crc", "md_first_frame", "md_value_frame", "first_entry_frame",
+                "last_entry_frame", "last_op_frame", "first_type"):
+        setattr(i, key, info.get(key, -1))
+    for key in ("first_entry_index", "min_entry_index", "last_entry_index", "last_op_index", "first_dlen"):
+        setattr(i, key, info.get(key, 0) & _U64)
+    i.first_stored_crc = info.get("first_stored_crc", 0) & 0xffffffff
+    i.first_u0 = info.get("first_u0", 0) & 0xffffffff
+    i.first_pre_crc = 1 if info.get("first_pre_crc") else 0
+    i.n_bytes = info["n_bytes"]
+    i.end_off = info.get("end_off", info["n_bytes"])
+    blob = b""
+    i.md_first_off, i.md_first_len = -1, 0
+    if info["md_first_frame"] >= 0 and mdf is not None:
+        i.md_first_off, i.md_first_len = 0, len(mdf)
+        blob += mdf
+    i.md_value_off, i.md_value_len = -1, 0
+    if info["md_value_frame"] >= 0:
+        i.md_value_off, i.md_value_len = 0, len(mdv)
+        blob += mdv
+    return r, blob
 
 
-def _s64(x):
-    """a uint64 in an int64 tensor slot (two's complement)"""
-    x &= _U64
-    return x - (1 << 64) if x >> 63 else x
+def join_rows(rows, blobs, ri_global: int):
+    """ewal_split_verdict over the rows of every range in order: (status,
+    global frame ordinal of the failure or -1, frames verified, resplit)."""
+    from . import _lib
+    import ctypes as C
+    arr = (_lib.RangeRow * len(rows))(*rows)
+    md = b"".join(blobs)
+    out = _lib.SplitResult()
+    rc = _lib.lib.ewal_split_verdict(arr, len(rows), ri_global & _U64, md, len(md), C.byref(out))
+    if rc != 0:
+        raise RuntimeError("ewal_split_verdict: %d" % rc)
+    return out.status, out.fail_record, out.n_records, out.resplit
 
 
 def split_verdict(dist, world: int, rank: int, result, info, ri_range: int, ri_global: int, device="cpu",
                   deferred: bool = False):
-    """ReadAll's verdict (wal/wal.go:164-216) for ONE WAL whose files were
-    split into contiguous ranges, range r verified by rank r.  Every range
-    but the first starts at a file boundary, so at a crcType record carrying
-    the running CRC (wal/wal.go:93,232-234); rank r ran ReadAll over its
-    range with w.ri = ri_range (its first file's index from the name) and
-    passes result = (status, fail_record, n_records, last_crc) plus info =
-    wal.range_info() of that ReadAll (ewal_range_info: first crc record,
-    first metadata frame and Data, the metadata value kept, first / last /
-    least entry Index, last entry op).
+    """ReadAll's verdict (wal/wal.go:164-216) for ONE WAL split into
+    contiguous ranges, range r read by rank r: by file (every range but the
+    first opens with a crcType record carrying the running CRC,
+    wal/wal.go:93,232-234) or inside a file (deferred=True: read with
+    ewal_readall_range_device, EWAL_RANGE_DEFER_FIRST -- its frame 0's check
+    made with the running CRC of the ranges before).  result / info as
+    range_row; ri_range: the range's w.ri.
 
-    One all-gather of a 16-word row per rank and one of the metadata bytes;
-    every rank then walks the ranges in file order and applies ReadAll's
-    cross-file rules before each range's own first failure, frame by frame:
-    * crc seam (wal/wal.go:184-192): running != 0 and stored != running ->
-      wal.ErrCRCMismatch at the range's frame 0;
-    * metadata (wal/wal.go:178-183): metadata != nil and not DeepEqual ->
-      ErrMetadataConflict at the range's first metadata frame (exact bytes);
-    * ents (wal/wal.go:170-173): the range's first entry op against len(ents)
-      carried from the ranges before (the index-gap panic); entries of a
-      later range below its own w.ri (a leader change rewriting indexes
-      after a Cut) are ops of the global ReadAll that the range's read
-      skipped -- and a gap its read reports at its first op that the global
-      one does not have hides the rest of the range -- so both resplit;
-    * w.enti < w.ri (wal/wal.go:203-206): the global ErrIndexNotFound, from
-      the last entry Index over all ranges.
-    Returns (status, global frame ordinal of the first failure or -1, frames
-    verified, resplit).  resplit = k >= 0: the verdict needs ranges k..
-    joined into one range (a torn frame at the end of range k reads on into
-    the next file through MultiReadCloser; k = 0 for the rewind / gap cases
-    and a range that does not open with a crc record) -- the caller verifies
-    them joined and calls again; status is not final then.
-
-    A range that starts inside a file (deferred=True: read with
-    ewal_readall_range_device, EWAL_RANGE_DEFER_FIRST) has no crcType record
-    to re-seed from: its frame 0's check is made here with the running CRC of
-    the ranges before it -- crc32.Update(running, Data) from info's first_u0
-    and first_dlen against the stored CRC (walpb.ErrCRCMismatch), or the
-    crcType rule when frame 0 is one -- before the range's own failures at
-    frame 0 except those decoder.decode reports first (framing, Unmarshal)."""
-    st, fr, n, lc = result
-    mdf, mdv = info.get("md_first"), info.get("md_value")
-    has_md = info["md_first_frame"] >= 0
-    row = [st, fr, n, lc, info["first_crc"], info["md_first_frame"],
-           (len(mdf) if mdf is not None else -1) if has_md else -2,
-           len(mdv) if (info["md_value_frame"] >= 0 and mdv is not None) else -1,
-           info["first_entry_frame"], _s64(info["first_entry_index"]), _s64(info["min_entry_index"]),
-           _s64(info["last_entry_index"]), _s64(ri_range), info["n_frames"], info["last_op_frame"],
-           _s64(info["last_op_index"]), 1 if deferred else 0, info.get("first_type", -1),
-           _s64(info.get("first_dlen", 0)), info.get("first_stored_crc", 0), info.get("first_u0", 0)]
-    assert len(row) == _ROW
-    mine = torch.tensor(row, dtype=torch.int64, device=device)
-    allv = [torch.zeros(_ROW, dtype=torch.int64, device=device) for _ in range(world)]
-    dist.all_gather(allv, mine)
-    rows = [[int(x) for x in v.tolist()] for v in allv]
-    # the metadata bytes: first metadata Data + the value kept, padded to the longest
-    blob = (mdf or b"") + (mdv or b"")
-    width = max(1, max(max(r[6], 0) + max(r[7], 0) for r in rows))
+    The exchange is torch.distributed's: one all-gather of the rank's
+    ewal_range_row and one of its metadata bytes; the rules are the C ABI's
+    ewal_split_verdict (etcd_amd/csrc/ewal_join.cpp), the same join
+    ewal_readall_multi runs for several GPUs in one process.  Returns (status,
+    global frame ordinal of the first failure or -1, frames verified,
+    resplit); resplit = k >= 0: ranges k.. must be read joined and the call
+    repeated (a frame cut short at range k's end, bytes it left unconsumed, a
+    rewind below a range's w.ri) -- status is not final then."""
+    import ctypes as C
+    row, blob = range_row(result, info, ri_range, deferred)
+    raw = bytes(C.string_at(C.addressof(row), C.sizeof(row)))
+    mine = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(device)
+    allr = [torch.zeros(len(raw), dtype=torch.uint8, device=device) for _ in range(world)]
+    dist.all_gather(allr, mine)
+    from . import _lib
+    rows = [_lib.RangeRow.from_buffer_copy(bytes(x.cpu().numpy().tobytes())) for x in allr]
+    lens = [max(r.info.md_first_len, 0) * (r.info.md_first_off >= 0 and r.info.md_first_frame >= 0) +
+            max(r.info.md_value_len, 0) * (r.info.md_value_frame >= 0) for r in rows]
+    width = max(1, max(lens))
     t = torch.zeros(width, dtype=torch.uint8, device=device)
     if blob:
         t[:len(blob)] = torch.frombuffer(bytearray(blob), dtype=torch.uint8).to(device)
     allb = [torch.zeros(width, dtype=torch.uint8, device=device) for _ in range(world)]
     dist.all_gather(allb, t)
-    raw = [bytes(x.cpu().numpy().tobytes()) for x in allb]
-
-    before, running, md, last_op, enti = 0, 0, None, None, 0
-    rig = ri_global & _U64
-    for k, r in enumerate(rows):
-        st, fr, n, lc, fc, mff, mfl, mvl, fef, fei, mei, lei, rir, nfr, lof, loi, dfr, fty, fdl, fsc, fu0 = r
-        fei, mei, lei, rir, loi = fei & _U64, mei & _U64, lei & _U64, rir & _U64, loi & _U64
-        if nfr == 0 and n == 0 and st in (_OK, _INDEX_NOT_FOUND):
-            continue                        # an empty range (joined into an earlier one)
-        first_md = None if mfl < 0 else raw[k][:mfl]
-        value_md = None if mvl < 0 else raw[k][max(mfl, 0):max(mfl, 0) + mvl]
-        own = fr if st not in (_OK, _INDEX_NOT_FOUND) else None
-        cross = []
-        if k > 0:
-            if dfr and nfr > 0 and fty != 4:
-                # frame 0's Validate with the running CRC (wal/decoder.go:42-46)
-                computed = _crc_combine(running, fu0, fdl & _U64) if fdl else running
-                if computed != (fsc & 0xffffffff) and not (own == 0 and st in _PRE_CRC):
-                    return _RECORD_CRC, before, before, -1
-            elif fc < 0:
-                return st, -1, before, 0    # its CRCs depend on the range before: verify joined
-            if fc >= 0 and running != 0 and fc != running:   # a crcType frame 0 (wal/wal.go:184-192)
-                cross.append((0, _WAL_CRC))
-            if md is not None and mff >= 0 and first_md != md:
-                cross.append((mff, _META_CONFLICT))
-            if fef >= 0:
-                if mei < rir:
-                    return st, -1, before, 0
-                gap_g = fei > last_op + 1 if last_op is not None else fei > rig
-                gap_l = fei > rir
-                if gap_g and not gap_l:
-                    cross.append((fef, _INDEX_GAP))
-                if gap_l and not gap_g and (own is None or own >= fef):
-                    return st, -1, before, 0
-        first = min(cross) if cross else None
-        if own is not None and (first is None or own <= first[0]):
-            # a frame cut short at the range's end reads on into the next
-            # range's bytes (MultiReadCloser / one file split): verify joined,
-            # unless every range after it is empty (the stream's own end)
-            later = any(not (x[13] == 0 and x[2] == 0 and x[0] in (_OK, _INDEX_NOT_FOUND)) for x in rows[k + 1:])
-            if st == _UNEXPECTED_EOF and later and fr == n:
-                return st, before + own, before + own, k
-            return st, before + own, before + own, -1
-        if first is not None:
-            return first[1], before + first[0], before + first[0], -1
-        before += n
-        running = lc
-        if value_md is not None:
-            md = value_md
-        if lof >= 0:
-            last_op = loi
-        if fef >= 0:
-            enti = lei
-    if enti < rig:
-        return _INDEX_NOT_FOUND, -1, before, -1
-    return _OK, -1, before, -1
+    blobs = [bytes(x.cpu().numpy().tobytes())[:lens[k]] for k, x in enumerate(allb)]
+    return join_rows(rows, blobs, ri_global)

@@ -315,6 +315,32 @@ def records(ctx: Context, n: int):
                  chained_crc=x.chained_crc) for x in arr[:k]]
 
 
+def readall_multi(ctxs, buf, ri=0, files=None):
+    """ewal_readall_multi: ReadAll over ONE WAL (host bytes `buf`) split
+    across the contexts `ctxs` in this process, one host thread per ctx.
+    files = [(length, name index)] splits it by file (every range a run of
+    whole files), None inside the stream (ranges opening at frame-start
+    candidates, frame 0's check deferred).  Returns (status, fail_record or
+    -1, n_records, last_crc, enti, resplits)."""
+    arr = (C.c_void_p * len(ctxs))(*[c.handle.value for c in ctxs])
+    offs = idx = None
+    nf = 0
+    if files is not None:
+        nf = len(files)
+        o = [0]
+        for n, _ in files:
+            o.append(o[-1] + n)
+        offs = (C.c_uint64 * (nf + 1))(*o)
+        idx = (C.c_uint64 * nf)(*[i & ((1 << 64) - 1) for _, i in files])
+    out = L.SplitResult()
+    nr = C.c_uint32(0)
+    b = bytes(buf)
+    rc = lib.ewal_readall_multi(arr, len(ctxs), b, len(b), offs, idx, nf, ri, C.byref(out), C.byref(nr))
+    if rc < 0:
+        check(rc)
+    return out.status, out.fail_record, out.n_records, out.last_crc, out.enti, nr.value
+
+
 def range_info(ctx: Context, stream=None, dbuf: DeviceBuffer = None):
     """ewal_copy_range_info of the last ReadAll on ctx: what its range of ONE WAL
     split by file contributes to shard.split_verdict.  The metadata Data
@@ -338,7 +364,8 @@ def range_info(ctx: Context, stream=None, dbuf: DeviceBuffer = None):
                 first_entry_index=ri.first_entry_index, min_entry_index=ri.min_entry_index,
                 last_entry_index=ri.last_entry_index, last_op_frame=ri.last_op_frame,
                 last_op_index=ri.last_op_index, first_type=ri.first_type, first_dlen=ri.first_dlen,
-                first_stored_crc=ri.first_stored_crc, first_u0=ri.first_u0)
+                first_stored_crc=ri.first_stored_crc, first_u0=ri.first_u0, last_entry_frame=ri.last_entry_frame,
+                first_pre_crc=ri.first_pre_crc, end_off=ri.end_off, n_bytes=ri.n_bytes)
 
 
 class WAL:

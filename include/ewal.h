@@ -247,12 +247,18 @@ typedef struct ewal_range_info {
   uint64_t last_op_index;
   int32_t md_split;              /* bit 0: md_first_off, bit 1: md_value_off index the split bytes
                                     (ewal_copy_split_bytes: a metadata Data in several segments) */
-  int32_t pad;
+  int32_t first_pre_crc;         /* 1: frame 0 failed inside decoder.decode before its CRC check
+                                    (framing, walpb.Record.Unmarshal, wal/decoder.go:30-41) -- that
+                                    failure wins over the caller's deferred check; 0: it did not fail
+                                    there (an Entry / HardState decode failure comes after the check) */
   /* frame 0 (EWAL_RANGE_DEFER_FIRST: the caller's CRC check) */
   int64_t first_type;            /* Record.Type, -1: no frame */
   uint64_t first_dlen;           /* len(Data) */
   uint32_t first_stored_crc;     /* Record.Crc */
   uint32_t first_u0;             /* crc32.Update(0, Castagnoli, Data) (the stored CRC for a crcType frame) */
+  uint64_t end_off;              /* where the frame chain ended (decoder.decode's terminal): n_bytes when
+                                    the range ended on a frame boundary */
+  uint64_t n_bytes;              /* the range's length */
 } ewal_range_info;
 int ewal_copy_range_info(ewal_ctx *ctx, ewal_range_info *out);
 
@@ -275,6 +281,64 @@ int ewal_readall_range_device(ewal_ctx *ctx, const void *d_buf, uint64_t len, ui
  * -1: none) -- the range's w.ri candidate. */
 int ewal_range_probe(ewal_ctx *ctx, const void *d_buf, uint64_t len, uint64_t from, uint64_t window, int64_t *pos,
                      int64_t *first_entry_index);
+
+/* ---- ONE WAL over several ranges: ReadAll's verdict joined (host C++) ------
+ * Range k of a WAL split into contiguous ranges (by file, or inside a file)
+ * was read by ReadAll on its own (ewal_readall_device / _range_device with
+ * w.ri = ri); its row carries that ReadAll's result and ewal_copy_range_info.
+ * ewal_split_verdict applies ReadAll's cross-range rules in order, before
+ * each range's own first failure (wal/wal.go:164-216):
+ *   crc seam        a crcType frame 0 against the running CRC (wal/wal.go:184-192)
+ *   deferred frame 0 (a range starting inside a file) Validate with the running
+ *                   CRC, crc32.Update(running, Data) = ewal_crc32_combine(running,
+ *                   first_u0, first_dlen) (wal/decoder.go:42-46)
+ *   metadata        metadata != nil && !DeepEqual (wal/wal.go:178-183)
+ *   ents            the range's first entry op against len(ents) carried over
+ *                   (the index-gap panic, wal/wal.go:170-173); ErrIndexNotFound
+ *                   over all ranges (wal/wal.go:203-206)
+ * resplit = k >= 0: the verdict needs ranges k.. read as ONE range (a frame
+ * cut short at range k's end, bytes range k left unconsumed, a rewind below a
+ * range's w.ri): the caller reads them joined, marks the later rows empty
+ * (n_bytes 0) and calls again.  md: the metadata bytes of every range in
+ * order -- its first metadata frame's Data (when md_first_frame >= 0 and
+ * md_first_off >= 0) then the value kept (md_value_frame >= 0). */
+typedef struct ewal_range_row {
+  int32_t status;                /* ReadAll's status over the range */
+  int32_t deferred;              /* 1: read with EWAL_RANGE_DEFER_FIRST */
+  int64_t fail_record;           /* the range's ordinal, -1 */
+  int64_t n_records;
+  uint64_t ri;                   /* the range's w.ri */
+  uint32_t last_crc;             /* ReadAll's running CRC after the range */
+  uint32_t pad;
+  int64_t detail;                /* ReadAll's detail (block type, gap index) */
+  ewal_range_info info;          /* ewal_copy_range_info of that ReadAll */
+} ewal_range_row;
+typedef struct ewal_split_result {
+  int32_t status;
+  int32_t resplit;               /* -1: final; k: read ranges k.. joined and call again */
+  int64_t fail_record;           /* the global frame ordinal of the failure, -1 */
+  int64_t n_records;             /* frames verified */
+  int64_t detail;
+  uint32_t last_crc;             /* decoder.lastCRC() after the WAL (EWAL_OK) */
+  uint32_t pad;
+  uint64_t enti;                 /* w.enti: the last entry's Index (EWAL_OK) */
+} ewal_split_result;
+int ewal_split_verdict(const ewal_range_row *rows, uint64_t n, uint64_t ri_global, const uint8_t *md, uint64_t md_len,
+                       ewal_split_result *out);
+/* ReadAll over ONE WAL (the bytes of names[nameIndex:], h_buf, len) split
+ * across n_ctx contexts in one process -- one host thread per context, each
+ * on its own device or sharing one: by file when file_off (n_files + 1
+ * offsets, file_off[0] = 0, file_off[n_files] = len) and file_index (the
+ * index in each file's name) are given, each range a run of whole files
+ * with w.ri = max(ri, its first file's index); else inside the stream, range
+ * r starting at the first frame-start candidate after r * len / n_ctx
+ * (ewal_range_probe) with frame 0's check deferred.  The ranges' verdicts
+ * are joined by ewal_split_verdict (re-reading ranges joined when it asks).
+ * out->status etc. are exactly (*WAL).ReadAll's over the whole stream with
+ * w.ri = ri; *n_resplit (nullable) counts the joined re-reads. */
+int ewal_readall_multi(ewal_ctx *const *ctxs, uint32_t n_ctx, const void *h_buf, uint64_t len, const uint64_t *file_off,
+                       const uint64_t *file_index, uint32_t n_files, uint64_t ri, ewal_split_result *out,
+                       uint32_t *n_resplit);
 
 /* ---- directory-level API: wal.OpenAtIndex + ReadAll + writer ----------- */
 typedef struct ewal_wal ewal_wal;

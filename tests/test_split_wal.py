@@ -67,13 +67,18 @@ def oracle_range_info(buf, ri):
         recs.append(r)
         p += 8 + L
     first = recs[0] if recs else None
+    # where decoder.decode stops (8 bytes with no payload read as io.EOF); frame 0
+    # failing in framing / Record.Unmarshal (before decoder.decode's CRC check)
+    end_off = p
+    pre = bool(buf) and not recs
     info = dict(n_frames=len(recs), first_crc=recs[0]["crc"] if recs and recs[0]["type"] == 4 else -1,
                 first_type=first["type"] if first else -1, first_dlen=len(first["data"] or b"") if first else 0,
                 first_stored_crc=first["crc"] if first else 0,
                 first_u0=(first["crc"] if first["type"] == 4 else O.crc32_update(0, first["data"] or b"")) if first
                 else 0,
                 md_first_frame=-1, md_first=None, md_value_frame=-1, md_value=None, first_entry_frame=-1,
-                first_entry_index=0, min_entry_index=0, last_entry_index=0, last_op_frame=-1, last_op_index=0)
+                first_entry_index=0, min_entry_index=0, last_entry_index=0, last_op_frame=-1, last_op_index=0,
+                last_entry_frame=-1, first_pre_crc=1 if pre else 0, end_off=end_off, n_bytes=len(buf))
     idx = []
     for i, r in enumerate(recs):
         if r["type"] == 1:
@@ -86,7 +91,7 @@ def oracle_range_info(buf, ri):
             idx.append((i, e["index"]))
     if idx:
         info.update(first_entry_frame=idx[0][0], first_entry_index=idx[0][1],
-                    min_entry_index=min(x for _, x in idx), last_entry_index=idx[-1][1])
+                    min_entry_index=min(x for _, x in idx), last_entry_index=idx[-1][1], last_entry_frame=idx[-1][0])
         ops = [(i, x) for i, x in idx if x >= ri]
         if ops:
             info.update(last_op_frame=ops[-1][0], last_op_index=ops[-1][1])
@@ -131,8 +136,8 @@ def _worker(rank, world, port, cases, use_gpu, q):
         dist.destroy_process_group()
 
 
-KINDS = ("clean", "corrupt_late", "corrupt_both", "seam", "meta", "meta_nil", "torn", "rewind", "gap_cross",
-         "gap_name", "name_low", "index_not_found", "ri_mid")
+KINDS = ("clean", "corrupt_late", "corrupt_both", "seam", "meta", "meta_nil", "torn", "dangling", "rewind",
+         "gap_cross", "gap_name", "name_low", "index_not_found", "ri_mid")
 
 
 def _cases(rng, world):
@@ -162,6 +167,8 @@ def _cases(rng, world):
             blobs[k] = bytearray(b2.getvalue() + body)
         if kind == "torn":          # the last file of range 0 torn: its frame reads on into range 1
             blobs[per - 1] = blobs[per - 1][:-5]
+        if kind == "dangling":      # range 0 ends with a bare length prefix (io.EOF alone; whole,
+            blobs[per - 1] += struct.pack("<q", 40)   # the frame reads its payload from the next file)
         rig = 0
         if kind == "index_not_found":    # OpenAtIndex past the last entry: the global ErrIndexNotFound
             rig = files[-1][1] + 1000

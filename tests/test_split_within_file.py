@@ -181,7 +181,9 @@ def _oracle_range(allb, start, end, ri):
         o = O.readall(buf, ri)
         return (o["status"], o["fail_record"], o["n_records"], running_after(o)), oracle_range_info(buf, ri)
     if start not in offs:   # a false candidate: the range before it is cut short and resplits first
-        return (O.ERR_UNEXPECTED_EOF, 0, 0, 0), oracle_range_info(b"", ri)
+        info = oracle_range_info(b"", ri)
+        info["n_bytes"] = end - start
+        return (O.ERR_UNEXPECTED_EOF, 0, 0, 0), info
     k = offs.index(start)
     pre = O.WalEncoder(crcs[k - 1])
     pre.save_crc(crcs[k - 1])
@@ -191,7 +193,8 @@ def _oracle_range(allb, start, end, ri):
     L = struct.unpack_from("<q", buf, 0)[0]
     st, r = O.record_unmarshal(buf[8:8 + L])
     info.update(first_type=r["type"], first_dlen=len(r["data"] or b""), first_stored_crc=r["crc"],
-                first_u0=r["crc"] if r["type"] == 4 else O.crc32_update(0, r["data"] or b""))
+                first_u0=r["crc"] if r["type"] == 4 else O.crc32_update(0, r["data"] or b""),
+                first_pre_crc=1 if st != O.OK else 0)
     return res, info
 
 
