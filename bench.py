@@ -13,6 +13,8 @@ own ms_per_step, roofline and (N=1) cpu_baseline --
   shards  configs[2]: 512 per-raft-group WALs x 64 MiB per GPU (4096 over
           8 GPUs), one batched ReadAll per step, one RCCL all-reduce
   snap    configs[3]: a resident batch of snapshot files, loadSnap's CRC
+  snapstream configs[3] at its full size: the 10k-file set (~450 GiB, 1-256
+          MiB) streamed from pinned host memory through two HBM batches
   commit  configs[4]: maybeCommit over 1M raft groups x 5/7 voters
   rewind  the configs[1]-shaped WAL after leader changes (1 % of the entries
           rewrite the last 1-8 indexes): ReadAll's rewind path timed
@@ -61,7 +63,7 @@ def parse():
                          "restart = OpenAtIndex + ReadAll + materialise through the C ABI (the cgo shim's calls)")
     ap.add_argument("--shards-per-gpu", type=int, default=512)
     ap.add_argument("--shard-mib", type=int, default=64)
-    ap.add_argument("--configs", default="c1,shards,snap,commit,rewind",
+    ap.add_argument("--configs", default="c1,shards,snap,snapstream,commit,rewind",
                     help="default line: the other BASELINE configs timed in the same run ('none' to skip)")
     ap.add_argument("--sub-cpu-seconds", type=float, default=6.0,
                     help="CPU-baseline time per leg of each `configs` sub-result")
@@ -389,7 +391,7 @@ def run_snap(a, dist, rank, world, local, cpu_seconds=None):
     return out
 
 
-def run_snapstream(a, dist, rank, world, local):
+def run_snapstream(a, dist, rank, world, local, cpu_seconds=None):
     """configs[3] at its full size on one GPU: the 10k-file snapshot set
     (~450 GiB, sizes log-uniform 1-256 MiB) streamed from pinned host
     memory through two HBM batch buffers: the H2D copies of batch b+1 (a
@@ -513,9 +515,10 @@ def run_snapstream(a, dist, rank, world, local):
         def one_pass():
             for v in views:
                 O.loadsnap(v)
-        it, cs = timed_cpu(a.cpu_seconds, one_pass)
+        csec = a.cpu_seconds if cpu_seconds is None else cpu_seconds
+        it, cs = timed_cpu(csec, one_pass)
         nth = cpu_threads()
-        it2, cs2 = timed_cpu(a.cpu_seconds / 2, lambda: O.fast_snap_verify_batch(base_addr, so, sl, nth))
+        it2, cs2 = timed_cpu(csec / 2, lambda: O.fast_snap_verify_batch(base_addr, so, sl, nth))
         cpu = dict(host_info(), **{
             "value": round(vb * it / cs / 1e9, 4), "unit": "GB/s", "cores": 1, "kind": "port",
             "sample": "oracle/ or_loadsnap (1 thread) over %d of the pool's files (<= 8 MiB each, %.2f GiB), %d "
@@ -1018,7 +1021,8 @@ def run_rewind(a, dist, rank, world, local, cpu_seconds=None):
     return out
 
 
-SUBS = {"c1": None, "shards": run_shards, "snap": run_snap, "commit": run_commit, "rewind": run_rewind}
+SUBS = {"c1": None, "shards": run_shards, "snap": run_snap, "snapstream": run_snapstream, "commit": run_commit,
+        "rewind": run_rewind}
 
 
 def main():

@@ -123,7 +123,7 @@ struct ewal_ctx {
   std::map<uint32_t, std::unique_ptr<ewal::CrcTables>> host_tables;
   DevBuf encw, encs, lbstat, gagg, slow, mlist, pf, v, pwave, ux, tagg, tpx, wcnt, slots, cbase, ovf, cpos, clen, nxt, exc, E, rs, jl, vis, entry, on, rec_cand, rd, opf, ops, kk, kkrev, suf,
       ents, recs, tmp, small, sdesc, snaps, hbuf_dev, xpos, walk, fpos, ulist, uitems, uarena, ftrec, fpl, fucb,
-      fnfp, frbase, fsp, ftcb;
+      fnfp, frbase, fsp, ftcb, fown, fcl;
   HostBuf hsdesc;                  // esnap_verify_packed's per-file table (host-mapped)
   // esnap_verify_packed's residual decode (esnap_copy_field): the batch's
   // buffer, per file its residual slot (-1: none), per slot its segments
@@ -638,6 +638,10 @@ static FrArgs fr_args(ewal_ctx *c, DevTables *tb, const uint8_t *d_buf, uint64_t
   a.mcap = mcap;
   a.ri = ri;
   a.ds = c->small.as<Small>();
+  a.rew = 0;
+  a.own = nullptr;
+  a.clist = nullptr;
+  a.ccap = 0;
   return a;
 }
 // the call's scratch as k_stream leaves it (a rerun of the frame pass, or the
@@ -656,11 +660,23 @@ static int frames_pass(ewal_ctx *c, DevTables *tb, const uint8_t *d_buf, uint64_
   const uint32_t tu = 64u * (uint32_t)upl, ntiles = (nunits + tu - 1) / tu;
   if (int rc = fr_ensure(c, nunits, ntiles)) return rc;
   uint32_t mcap = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(c->mlist.cap / 8, 4096), 0xffffffffull);
-  for (int pass = 0; pass < 3; ++pass) {
+  bool rew = false;   // rewind mode: entry indexes go back (wal/wal.go:173 truncates ents)
+  uint32_t clcap = 0;
+  for (int pass = 0; pass < 4; ++pass) {
     EW_CHECK(c->ents.ensure((size_t)ecap * sizeof(ewal_entry)));
     EW_CHECK(c->mlist.ensure((size_t)mcap * 8));
     if (pass) if (int rc = reset_small(c)) return rc;
     FrArgs a = fr_args(c, tb, d_buf, B, nunits, ntiles, ri, c->ents.as<ewal_entry>(), ecap, mcap);
+    if (rew) {
+      clcap = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(clcap, ecap), 0xffffffffull);
+      EW_CHECK(c->fown.ensure((size_t)ecap * 8));
+      EW_CHECK(c->fcl.ensure((size_t)clcap * 4));
+      EW_CHECK(hipMemsetAsync(c->fown.p, 0, (size_t)ecap * 8, c->stream));
+      a.rew = 1;
+      a.own = c->fown.as<unsigned long long>();
+      a.clist = c->fcl.as<uint32_t>();
+      a.ccap = clcap;
+    }
     const unsigned grid = (unsigned)std::min<uint64_t>(grid_for(ntiles, FR_WAVES), (uint64_t)std::max(1, c->num_cu));
     const unsigned sgrid = (unsigned)std::min<uint64_t>(grid_for(ntiles, 256), (uint64_t)std::max(1, c->num_cu) * EW_SEAM_WGS);
     if (upl == 4) {
@@ -672,6 +688,10 @@ static int frames_pass(ewal_ctx *c, DevTables *tb, const uint8_t *d_buf, uint64_
       hipLaunchKernelGGL((k_frames_seam<false, 1>), dim3(sgrid), dim3(256), 0, c->stream, a, FrSeg{}, c->h_res_dev,
                          c->h_small_dev);
     }
+    if (rew)   // the slots more than one op claimed: their last op's entry
+      hipLaunchKernelGGL(k_ents_fix, dim3((unsigned)std::max(1, c->num_cu) * 2), dim3(256), 0, c->stream, d_buf, B,
+                         (const unsigned long long *)a.own, (const uint32_t *)a.clist, a.ccap, (const Small *)a.ds,
+                         a.ents);
     EW_CHECK(hipGetLastError());
     // the call's end event rides behind the last kernel: when the regular
     // case held, the sync below is the call's only wait for the device
@@ -683,10 +703,18 @@ static int frames_pass(ewal_ctx *c, DevTables *tb, const uint8_t *d_buf, uint64_
       *done = true;
       return 0;
     }
-    // declined for capacity only: room for what it asked, once more
+    // declined for capacity or rewinds only: room for what it asked / the rewind mode, once more
     const uint32_t rare = hs->fc.rare;
-    if (hs->irregular || (rare & ~(4u | 8u))) break;
+    if (hs->irregular || (rare & ~(2u | 4u | 8u | 64u))) break;
     bool again = false;
+    if ((rare & 2u) && !rew) {
+      rew = true;
+      again = true;
+    }
+    if (rare & 64u) {
+      clcap = hs->fr_ncl + hs->fr_ncl / 8 + 1024;
+      again = true;
+    }
     if ((rare & 4u) && hs->fr_need > ecap && hs->fr_need < 0xffffff00ull) {
       ecap = hs->fr_need + hs->fr_need / 8 + 1024;
       again = true;

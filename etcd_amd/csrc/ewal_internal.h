@@ -167,6 +167,8 @@ struct Small {
   uint32_t fr_capfail;            // batch: the shards' ents regions exceed the capacity (k_shard_rbase)
   FrAgg fr;
   unsigned long long fr_need;     // single WAL: ents the frame pass needed; batch: the regions' total
+  uint32_t fr_ncl;                // rewind mode: ents slots claimed more than once (listed for k_ents_fix)
+  uint32_t fr_pad;
 };
 
 // A returned Entry (ent = its index in ents) or the HardState (ent = -1)

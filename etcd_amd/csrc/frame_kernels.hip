@@ -97,6 +97,14 @@ struct FrArgs {
   uint32_t mcap;
   uint64_t ri;                     // w.ri (single WAL)
   Small *ds;
+  // rewind mode (single WAL, ReadAll's ents = append(ents[:Index-ri], e) with
+  // indexes going back, wal/wal.go:173): every op claims its slot k with
+  // atomicMax(own[k], 1 + position); a slot claimed twice is listed (clist)
+  // and k_ents_fix stores the last op's entry there after the pass
+  int rew;
+  unsigned long long *own;
+  uint32_t *clist;
+  uint32_t ccap;
 };
 struct FrSeg {
   uint32_t ns;
@@ -684,7 +692,8 @@ __global__ __launch_bounds__(FR_THREADS, 1) void k_frames(FrArgs a, FrSeg sg) {
         if (!seam_op) {
           bool gap;
           if (has) {
-            if (k <= kq) { if (SEG) bad = true; else rare |= 2u; }   // an index rewind: the general path
+            // an index rewind: the rewind-mode pass (single WAL), the shard replayed alone (batch)
+            if (k <= kq && !a.rew) { if (SEG) bad = true; else rare |= 2u; }
             gap = k > kq && k - kq > 1;
           } else {
             gap = k > 0;
@@ -696,6 +705,10 @@ __global__ __launch_bounds__(FR_THREADS, 1) void k_frames(FrArgs a, FrSeg sg) {
           if (k < room) a.ents[rb + k] = ewal_entry{d.f0, d.f1, d.edoff - S0, d.edlen, d.etype, (int32_t)d.enil};
         } else if (k < a.ecap) {
           store_entry_nt(a.ents + k, ewal_entry{d.f0, d.f1, d.edoff, d.edlen, d.etype, (int32_t)d.enil});
+          if (a.rew && atomicMax(&a.own[k], (unsigned long long)(p + 1))) {   // a slot written twice
+            const uint32_t ci = atomicAdd(&ds->fr_ncl, 1u);
+            if (ci < a.ccap) a.clist[ci] = (uint32_t)k; else rare |= 64u;
+          }
         } else {
           rare |= 4u;
           need_ecap = max(need_ecap, (unsigned long long)(k + 1));
@@ -715,7 +728,6 @@ __global__ __launch_bounds__(FR_THREADS, 1) void k_frames(FrArgs a, FrSeg sg) {
         ophas = true;
         opk = rl64(d.f1 - ri, wl);
         opsh = rl32(sh, wl);
-        if (SEG) alo = max(alo, (long long)tr.lastop_p);
       }
       // metadata frames: ReadAll's metadata rule runs after the pass
       if (isnew && ok && !torn && d.type == 1) {
@@ -740,6 +752,7 @@ __global__ __launch_bounds__(FR_THREADS, 1) void k_frames(FrArgs a, FrSeg sg) {
           if (ms) als = max(als, (long long)rl64(p, 63 - __clzll((long long)ms)));
           if (mm) afm = min(afm, (unsigned long long)rl64(p, __ffsll((long long)mm) - 1));
           if (ma) alp = max(alp, (long long)rl64(p, 63 - __clzll((long long)ma)));
+          if (mo) alo = max(alo, (long long)rl64(p, 63 - __clzll((long long)mo)));
         } else {                                     // a shard boundary in the round: lane by lane
           ShardPos *A = sg.sp + sh;
           if (occ && st != 0) atomicMin(&A->first_fail, (p << 8) | (uint32_t)st);
@@ -1108,7 +1121,7 @@ __global__ __launch_bounds__(256) void k_frames_seam(FrArgs a, FrSeg sg, ResultD
         bool gap;
         if (has) {
           const uint64_t kq = pidx - ri;
-          if (k <= kq) {
+          if (k <= kq && !a.rew) {
             if (SEG) badsh(shf); else atomicOr(&ds->fc.rare, 2u);
           }
           gap = k > kq && k - kq > 1;
@@ -1149,6 +1162,23 @@ __global__ __launch_bounds__(256) void k_frames_seam(FrArgs a, FrSeg sg, ResultD
   if (s_last) {   // the last workgroup: every tile is in
     __threadfence();
     fr_result<UPL>(a, o, h, s_w, s_d, &s_ord);
+  }
+}
+
+// Rewind mode: every listed slot (claimed by more than one entry op) gets
+// the entry of its last op -- the one ReadAll's append leaves there (any op
+// after it with a smaller index truncated below the slot and the ops after
+// that climbed back through it, one index at a time).
+__global__ __launch_bounds__(256) void k_ents_fix(const uint8_t *__restrict__ buf, uint64_t B,
+                                                  const unsigned long long *__restrict__ own,
+                                                  const uint32_t *__restrict__ clist, uint32_t ccap, const Small *ds,
+                                                  ewal_entry *__restrict__ ents) {
+  __shared__ uint4 s_w[256][6];
+  const uint32_t n = min(ds->fr_ncl, ccap);
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const uint32_t k = clist[i];
+    const RecDesc d = fc_frame_fields(buf, B, own[k] - 1, s_w[threadIdx.x]);
+    ents[k] = ewal_entry{d.f0, d.f1, d.edoff, d.edlen, d.etype, (int32_t)d.enil};
   }
 }
 
