@@ -123,7 +123,7 @@ struct ewal_ctx {
   std::map<uint32_t, std::unique_ptr<ewal::CrcTables>> host_tables;
   DevBuf encw, encs, lbstat, gagg, slow, mlist, pf, v, pwave, ux, tagg, tpx, wcnt, slots, cbase, ovf, cpos, clen, nxt, exc, E, rs, jl, vis, entry, on, rec_cand, rd, opf, ops, kk, kkrev, suf,
       ents, recs, tmp, small, sdesc, snaps, hbuf_dev, xpos, walk, fpos, ulist, uitems, uarena, ftrec, fpl, fucb,
-      fnfp, frbase, fsp, ftcb, fown, fcl;
+      fnfp, frbase, fsp, ftcb, fown, fcl, ftl;
   HostBuf hsdesc;                  // esnap_verify_packed's per-file table (host-mapped)
   // esnap_verify_packed's residual decode (esnap_copy_field): the batch's
   // buffer, per file its residual slot (-1: none), per slot its segments
@@ -642,6 +642,8 @@ static FrArgs fr_args(ewal_ctx *c, DevTables *tb, const uint8_t *d_buf, uint64_t
   a.own = nullptr;
   a.clist = nullptr;
   a.ccap = 0;
+  a.tlist = nullptr;
+  a.ntl = 0;
   return a;
 }
 // the call's scratch as k_stream leaves it (a rerun of the frame pass, or the
@@ -691,7 +693,7 @@ static int frames_pass(ewal_ctx *c, DevTables *tb, const uint8_t *d_buf, uint64_
     if (rew)   // the slots more than one op claimed: their last op's entry
       hipLaunchKernelGGL(k_ents_fix, dim3((unsigned)std::max(1, c->num_cu) * 2), dim3(256), 0, c->stream, d_buf, B,
                          (const unsigned long long *)a.own, (const uint32_t *)a.clist, a.ccap, (const Small *)a.ds,
-                         a.ents);
+                         a.ents, (const uint64_t *)nullptr, 0u);
     EW_CHECK(hipGetLastError());
     // the call's end event rides behind the last kernel: when the regular
     // case held, the sync below is the call's only wait for the device
@@ -1315,6 +1317,111 @@ static int frames_batch(ewal_ctx *c, DevTables *tb, const uint8_t *d_buf, uint64
   return 0;
 }
 
+// The batch's shards whose entry indexes go back (leader changes: ReadAll's
+// ents = append(ents[:Index-ri], e) truncates, wal/wal.go:173): the frame
+// pass again over just their tiles, in rewind mode -- every op claims its
+// slot of the shard's region, the slots claimed twice get their last op's
+// entry (k_ents_fix) -- and the batch's results gathered again (the other
+// shards' come out the same: the reductions are minima / maxima).
+static int frames_batch_rewind(ewal_ctx *c, DevTables *tb, const uint8_t *d_buf, uint64_t B, uint32_t ns,
+                               const std::vector<uint64_t> &soff, const std::vector<uint32_t> &rews, ewal_result *out,
+                               uint64_t have) {
+  Small *ds = c->small.as<Small>();
+  const uint32_t nunits = (uint32_t)(B / EW_WAVE_BYTES + 1);
+  const int upl = fr_upl(c, nunits);
+  const uint32_t tu = 64u * (uint32_t)upl, ntiles = (nunits + tu - 1) / tu;
+  const uint64_t tb_bytes = (uint64_t)tu * EW_WAVE_BYTES;
+  std::vector<uint64_t> rbase(ns + 1);
+  EW_CHECK(hipMemcpy(rbase.data(), c->frbase.p, (size_t)(ns + 1) * 8, hipMemcpyDeviceToHost));
+  std::vector<uint32_t> tiles, shards;
+  uint64_t slots = 0;
+  for (uint32_t s : rews) {
+    if (soff[s + 1] == soff[s]) continue;
+    shards.push_back(s);
+    slots += rbase[s + 1] - rbase[s];
+    for (uint64_t t = soff[s] / tb_bytes; t <= (soff[s + 1] - 1) / tb_bytes && t < ntiles; ++t)
+      if (tiles.empty() || tiles.back() < t) tiles.push_back((uint32_t)t);
+  }
+  if (tiles.empty()) return 0;
+  std::sort(tiles.begin(), tiles.end());
+  tiles.erase(std::unique(tiles.begin(), tiles.end()), tiles.end());
+  const uint32_t nsh = (uint32_t)shards.size(), ntl = (uint32_t)tiles.size();
+  uint32_t clcap = (uint32_t)std::min<uint64_t>(slots + 1024, 0xffffffffull);
+  EW_CHECK(c->fown.ensure((size_t)std::max<uint64_t>(have, 1) * 8));
+  EW_CHECK(c->ftl.ensure((size_t)(ntl + nsh) * 4));
+  uint32_t *d_tl = c->ftl.as<uint32_t>(), *d_sl = d_tl + ntl;
+  EW_CHECK(hipMemcpyAsync(d_tl, tiles.data(), (size_t)ntl * 4, hipMemcpyHostToDevice, c->stream));
+  EW_CHECK(hipMemcpyAsync(d_sl, shards.data(), (size_t)nsh * 4, hipMemcpyHostToDevice, c->stream));
+  for (int pass = 0; pass < 2; ++pass) {
+    EW_CHECK(c->fcl.ensure((size_t)clcap * 4));
+    for (uint32_t s : shards)   // the shards' regions unclaimed
+      EW_CHECK(hipMemsetAsync(c->fown.as<unsigned long long>() + rbase[s], 0, (size_t)(rbase[s + 1] - rbase[s]) * 8,
+                              c->stream));
+    hipLaunchKernelGGL(k_shard_reset, dim3(grid_for(nsh, 256)), dim3(256), 0, c->stream, c->fsp.as<ShardPos>(),
+                       (const uint32_t *)d_sl, nsh, ds);
+    FrArgs a = fr_args(c, tb, d_buf, B, nunits, ntiles, 0, c->bents.as<ewal_entry>(), c->bents.cap / sizeof(ewal_entry),
+                       (uint32_t)std::min<uint64_t>(c->mlist.cap / 8, 0xffffffffull));
+    a.rew = 1;
+    a.own = c->fown.as<unsigned long long>();
+    a.clist = c->fcl.as<uint32_t>();
+    a.ccap = clcap;
+    a.tlist = d_tl;
+    a.ntl = ntl;
+    FrSeg sg;
+    sg.ns = ns;
+    sg.soff = c->bsoff.as<uint64_t>();
+    sg.ri = c->bri.as<uint64_t>();
+    sg.rbase = c->frbase.as<uint64_t>();
+    sg.sp = c->fsp.as<ShardPos>();
+    sg.tcb = c->ftcb.as<uint32_t>();
+    const unsigned grid = (unsigned)std::min<uint64_t>(grid_for(ntl, FR_WAVES), (uint64_t)std::max(1, c->num_cu));
+    const unsigned sgrid = (unsigned)std::min<uint64_t>(grid_for(ntl, 256), (uint64_t)std::max(1, c->num_cu) * EW_SEAM_WGS);
+    if (upl == 4) {
+      hipLaunchKernelGGL((k_frames<true, 4>), dim3(grid), dim3(FR_THREADS), 0, c->stream, a, sg);
+      hipLaunchKernelGGL((k_frames_seam<true, 4>), dim3(sgrid), dim3(256), 0, c->stream, a, sg, (ResultDev *)nullptr,
+                         (Small *)nullptr);
+    } else {
+      hipLaunchKernelGGL((k_frames<true, 1>), dim3(grid), dim3(FR_THREADS), 0, c->stream, a, sg);
+      hipLaunchKernelGGL((k_frames_seam<true, 1>), dim3(sgrid), dim3(256), 0, c->stream, a, sg, (ResultDev *)nullptr,
+                         (Small *)nullptr);
+    }
+    hipLaunchKernelGGL(k_ents_fix, dim3((unsigned)std::max(1, c->num_cu) * 2), dim3(256), 0, c->stream, d_buf, B,
+                       (const unsigned long long *)a.own, (const uint32_t *)a.clist, a.ccap, (const Small *)ds, a.ents,
+                       (const uint64_t *)sg.soff, ns);
+    hipLaunchKernelGGL(k_meta_batch_fr, dim3(64), dim3(256), 0, c->stream, a, sg);
+    if (upl == 4)
+      hipLaunchKernelGGL(k_result_batch_fr<4>, dim3(grid_for((uint64_t)ns * 64, 256)), dim3(256), 0, c->stream, a, sg,
+                         c->bres.as<ewal_result>(), c->bef.as<unsigned long long>());
+    else
+      hipLaunchKernelGGL(k_result_batch_fr<1>, dim3(grid_for((uint64_t)ns * 64, 256)), dim3(256), 0, c->stream, a, sg,
+                         c->bres.as<ewal_result>(), c->bef.as<unsigned long long>());
+    hipLaunchKernelGGL(k_batch_gate_fr, dim3(1), dim3(64), 0, c->stream, ds, c->h_small_dev);
+    EW_CHECK(hipGetLastError());
+    EW_CHECK(hipMemcpyAsync(out, c->bres.p, (size_t)ns * sizeof(ewal_result), hipMemcpyDeviceToHost, c->stream));
+    EW_CHECK(hipMemcpyAsync(c->bent_first.data(), c->bef.p, (size_t)ns * 8, hipMemcpyDeviceToHost, c->stream));
+    EW_CHECK(hipEventRecord(c->ev1, c->stream));
+    EW_CHECK(hipStreamSynchronize(c->stream));
+    const Small *hs = c->h_small;
+    if (hs->errflag) return EWAL_E_TIMEOUT;
+    if (!(hs->fc.rare & 64u)) break;
+    clcap = hs->fr_ncl + hs->fr_ncl / 8 + 1024;   // more slots claimed twice than listed: once more
+  }
+  if (c->h_small->fc.rare) {   // (not decided: every listed shard replayed alone)
+    for (uint32_t s : shards) out[s].flags = EW_SHARD_BAD;
+    return 0;
+  }
+  float dev_ms = 0, str_ms = 0;
+  EW_CHECK(hipEventElapsedTime(&dev_ms, c->ev0, c->ev1));
+  EW_CHECK(hipEventElapsedTime(&str_ms, c->evs0, c->evs1));
+  for (uint32_t i = 0; i < ns; ++i) {
+    out[i].device_ms = dev_ms;
+    out[i].stream_ms = str_ms;
+    c->bnents[i] = (uint64_t)out[i].n_ents;
+    if (!out[i].n_ents) c->bent_first[i] = 0;
+  }
+  return 0;
+}
+
 // ReadAll of the listed shards of a batch, each alone (readall_impl over an
 // aligned scratch copy: the stream pass reads 16-B aligned): shards the
 // fused pass could not decide (torn or corrupt framing, index rewinds,
@@ -1441,6 +1548,11 @@ static int readall_batch_impl(ewal_ctx *c, const uint8_t *d_buf, uint32_t ns, co
                      c->h_small->fc.rare, c->h_small->irregular, c->h_small->fr_capfail, c->h_small->errflag);
       }
       if (done) {   // every shard decided but those the fused pass flagged: they are replayed alone
+        std::vector<uint32_t> rews;
+        for (uint32_t i = 0; i < ns; ++i)
+          if ((out[i].flags & EW_SHARD_REW) && !(out[i].flags & EW_SHARD_BAD)) rews.push_back(i);
+        if (!rews.empty() && (rc = frames_batch_rewind(c, tb, d_buf, B, ns, soff, rews, out, have))) return rc;
+        for (uint32_t i = 0; i < ns; ++i) out[i].flags &= ~EW_SHARD_REW;
         std::vector<uint32_t> bad;
         for (uint32_t i = 0; i < ns; ++i)
           if (out[i].flags & EW_SHARD_BAD) bad.push_back(i);

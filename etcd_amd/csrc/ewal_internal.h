@@ -94,6 +94,9 @@ struct ShardAgg {
 // ewal_result.flags bit of a batched shard the fused pass could not decide
 // (internal: the host replays the shard alone and clears it)
 #define EW_SHARD_BAD 0x40000000
+// ... of a batched shard whose entry indexes go back (leader changes): the
+// frame pass runs again over its tiles in rewind mode
+#define EW_SHARD_REW 0x20000000
 
 struct SegArgs {
   uint2 *ulist;            // (frame, op index) of entry ops with XXX_unrecognized (both modes)

@@ -80,6 +80,7 @@ struct ShardPos {
   unsigned long long term;         // min (q << 8 | class): where the shard's frames end before it does, ~0
   long long last_entry, last_state, lastop, lastp;   // max p, -1 (lastp: any frame)
   uint32_t bad, open;              // bad: replayed alone; open: a frame starts at the shard's first byte
+  uint32_t rew, pad;               // rew: entry indexes go back (the rewind-mode pass over its tiles)
 };
 
 struct FrArgs {
@@ -105,6 +106,10 @@ struct FrArgs {
   unsigned long long *own;
   uint32_t *clist;
   uint32_t ccap;
+  // the tiles to run (nullptr: all ntiles): the rewind-mode pass over the
+  // tiles of a batch's rewinding shards
+  const uint32_t *tlist;
+  uint32_t ntl;
 };
 struct FrSeg {
   uint32_t ns;
@@ -346,7 +351,9 @@ __global__ __launch_bounds__(FR_THREADS, 1) void k_frames(FrArgs a, FrSeg sg) {
   uint32_t *w = s_win + tid;
   uint32_t rare = 0, irr = 0;
   unsigned long long need_ecap = 0;
-  for (uint32_t t = wid; t < a.ntiles; t += nwaves) {
+  const uint32_t nt_run = a.tlist ? a.ntl : a.ntiles;
+  for (uint32_t ti = wid; ti < nt_run; ti += nwaves) {
+    const uint32_t t = a.tlist ? a.tlist[ti] : ti;
     const uint32_t u0 = t * TU;
     const uint64_t ts = (uint64_t)u0 * EW_WAVE_BYTES;
     // ---- A: the tile's unit lins, P at every unit start (tile-local) ----
@@ -693,7 +700,7 @@ __global__ __launch_bounds__(FR_THREADS, 1) void k_frames(FrArgs a, FrSeg sg) {
           bool gap;
           if (has) {
             // an index rewind: the rewind-mode pass (single WAL), the shard replayed alone (batch)
-            if (k <= kq && !a.rew) { if (SEG) bad = true; else rare |= 2u; }
+            if (k <= kq && !a.rew) { if (SEG) sg.sp[sh].rew = 1u; else rare |= 2u; }
             gap = k > kq && k - kq > 1;
           } else {
             gap = k > 0;
@@ -702,7 +709,13 @@ __global__ __launch_bounds__(FR_THREADS, 1) void k_frames(FrArgs a, FrSeg sg) {
         }
         if (SEG) {   // op k of the shard: its region's entry k
           const uint64_t rb = sg.rbase[sh], room = sg.rbase[sh + 1] - rb;
-          if (k < room) a.ents[rb + k] = ewal_entry{d.f0, d.f1, d.edoff - S0, d.edlen, d.etype, (int32_t)d.enil};
+          if (k < room) {
+            a.ents[rb + k] = ewal_entry{d.f0, d.f1, d.edoff - S0, d.edlen, d.etype, (int32_t)d.enil};
+            if (a.rew && atomicMax(&a.own[rb + k], (unsigned long long)(p + 1))) {   // a slot written twice
+              const uint32_t ci = atomicAdd(&ds->fr_ncl, 1u);
+              if (ci < a.ccap) a.clist[ci] = (uint32_t)(rb + k); else rare |= 64u;
+            }
+          }
         } else if (k < a.ecap) {
           store_entry_nt(a.ents + k, ewal_entry{d.f0, d.f1, d.edoff, d.edlen, d.etype, (int32_t)d.enil});
           if (a.rew && atomicMax(&a.own[k], (unsigned long long)(p + 1))) {   // a slot written twice
@@ -998,7 +1011,9 @@ __global__ __launch_bounds__(256) void k_frames_seam(FrArgs a, FrSeg sg, ResultD
     if (SEG) atomicMin(&sg.sp[s].first_fail, k);
     else fail = min(fail, k);
   };
-  for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < a.ntiles; t += gridDim.x * blockDim.x) {
+  const uint32_t nt_run = a.tlist ? a.ntl : a.ntiles;
+  for (uint32_t ti = blockIdx.x * blockDim.x + threadIdx.x; ti < nt_run; ti += gridDim.x * blockDim.x) {
+    const uint32_t t = a.tlist ? a.tlist[ti] : ti;
     const FrTile T = a.trec[t];
     if (!T.count) continue;
     // ---- the previous frame: the last of the nearest earlier tile with frames ----
@@ -1122,7 +1137,7 @@ __global__ __launch_bounds__(256) void k_frames_seam(FrArgs a, FrSeg sg, ResultD
         if (has) {
           const uint64_t kq = pidx - ri;
           if (k <= kq && !a.rew) {
-            if (SEG) badsh(shf); else atomicOr(&ds->fc.rare, 2u);
+            if (SEG) sg.sp[shf].rew = 1u; else atomicOr(&ds->fc.rare, 2u);
           }
           gap = k > kq && k - kq > 1;
         } else {
@@ -1172,13 +1187,16 @@ __global__ __launch_bounds__(256) void k_frames_seam(FrArgs a, FrSeg sg, ResultD
 __global__ __launch_bounds__(256) void k_ents_fix(const uint8_t *__restrict__ buf, uint64_t B,
                                                   const unsigned long long *__restrict__ own,
                                                   const uint32_t *__restrict__ clist, uint32_t ccap, const Small *ds,
-                                                  ewal_entry *__restrict__ ents) {
+                                                  ewal_entry *__restrict__ ents, const uint64_t *__restrict__ soff,
+                                                  uint32_t ns) {
   __shared__ uint4 s_w[256][6];
   const uint32_t n = min(ds->fr_ncl, ccap);
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
     const uint32_t k = clist[i];
-    const RecDesc d = fc_frame_fields(buf, B, own[k] - 1, s_w[threadIdx.x]);
-    ents[k] = ewal_entry{d.f0, d.f1, d.edoff, d.edlen, d.etype, (int32_t)d.enil};
+    const uint64_t p = own[k] - 1;
+    const RecDesc d = fc_frame_fields(buf, B, p, s_w[threadIdx.x]);
+    const uint64_t base = soff ? soff[pos_shard_in(soff, 0, ns, p)] : 0ull;   // batch: Data relative to the shard
+    ents[k] = ewal_entry{d.f0, d.f1, d.edoff - base, d.edlen, d.etype, (int32_t)d.enil};
   }
 }
 
@@ -1241,6 +1259,8 @@ __global__ __launch_bounds__(1024) void k_shard_rbase(const unsigned long long *
       p.last_entry = p.last_state = p.lastop = p.lastp = -1;
       p.bad = 0;
       p.open = 0;
+      p.rew = 0;
+      p.pad = 0;
       sp[s] = p;
     }
     __syncthreads();
@@ -1252,6 +1272,27 @@ __global__ __launch_bounds__(1024) void k_shard_rbase(const unsigned long long *
     ds->fr_need = s_carry;
     if (s_carry > ecap) ds->fr_capfail = 1;
   }
+}
+
+// The listed shards' reductions initialised again (the rewind-mode pass
+// over their tiles), and the pass's scratch counters.
+__global__ void k_shard_reset(ShardPos *__restrict__ sp, const uint32_t *__restrict__ list, uint32_t n, Small *ds) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i == 0) {
+    ds->fr_ncl = 0;
+    ds->fc.rare = 0;
+  }
+  if (i >= n) return;
+  ShardPos p;
+  p.first_fail = ~0ull;
+  p.first_meta = ~0ull;
+  p.term = ~0ull;
+  p.last_entry = p.last_state = p.lastop = p.lastp = -1;
+  p.bad = 0;
+  p.open = 0;
+  p.rew = 0;
+  p.pad = 0;
+  sp[list[i]] = p;
 }
 
 // One workgroup: tcb[t] = candidates of the tiles before t.
@@ -1379,6 +1420,7 @@ __global__ __launch_bounds__(256) void k_result_batch_fr(FrArgs a, FrSeg sg, ewa
     }
   }
   o.flags = EWAL_FLAG_FAST_PATH;
+  if (A.rew) o.flags |= EW_SHARD_REW;                           // the rewind-mode pass over its tiles
   if (A.bad || (se > so && !A.open)) o.flags = EW_SHARD_BAD;   // replayed alone by the host
   out[s] = o;
   ent_first[s] = ef;
