@@ -700,6 +700,10 @@ static int frames_pass(ewal_ctx *c, DevTables *tb, const uint8_t *d_buf, uint64_
     EW_CHECK(hipEventRecord(c->ev1, c->stream));
     EW_CHECK(hipStreamSynchronize(c->stream));
     const Small *hs = c->h_small;
+    if (ew_debug())
+      std::fprintf(stderr, "ewal frames: pass %d upl %d spec %u rare %u irr %u need %llu nmeta %u K %llu\n", pass, upl,
+                   hs->spec_n, hs->fc.rare, hs->irregular, (unsigned long long)hs->fr_need, hs->nmeta,
+                   (unsigned long long)hs->total);
     if (hs->errflag) return EWAL_E_TIMEOUT;
     if (hs->spec_n) {
       *done = true;
@@ -910,6 +914,10 @@ static int readall_impl(ewal_ctx *c, const uint8_t *d_buf, uint64_t B, uint64_t 
       const uint64_t Kf = c->h_small->total;
       const bool grow = Kf > rdcap && Kf <= ccap;
       const bool resc = c->h_small->novf && Kf <= ccap && !rescanned;
+      if (ew_debug())
+        std::fprintf(stderr, "ewal readall: general pass %d K %llu novf %u pos0 %llu irr %u spec %u\n", pass,
+                     (unsigned long long)Kf, c->h_small->novf, (unsigned long long)c->h_small->pos0,
+                     c->h_small->irregular, c->h_small->spec_n);
       if (!grow && !resc) break;
       if (resc) {
         if ((rc = ensure_cand_aux(c, ccap))) return rc;
@@ -922,6 +930,10 @@ static int readall_impl(ewal_ctx *c, const uint8_t *d_buf, uint64_t B, uint64_t 
       if (grow) rdcap = Kf + Kf / 8 + 1024;
     }
     K = c->h_small->total;
+    if (ew_debug())
+      std::fprintf(stderr, "ewal readall: fused_done %d K %llu novf %u pos0 %llu irr %u q %llu\n", (int)fused_done,
+                   (unsigned long long)K, c->h_small->novf, (unsigned long long)c->h_small->pos0,
+                   c->h_small->irregular, (unsigned long long)c->h_small->q);
     c->last_k = K;
     fused_done_final = fused_done;
     if (fused_done) {   // frames decoded and checked by k_frames; the result is in h_res
@@ -986,6 +998,8 @@ static int readall_impl(ewal_ctx *c, const uint8_t *d_buf, uint64_t B, uint64_t 
   }
   int tst = classify_terminal(B, q, qlen);
   c->last_q = q;
+  // the frame pass leaves no candidate list for k_walk: it declines such a terminal itself (fc.rare 128)
+  if (fused_done_final && tst == EWAL_FRAME_FITS) return EWAL_E_INVAL;
   // walked frames (not candidates) on the chain: decoded and checked with the
   // chain's candidates from one frame-position list (fpos)
   std::vector<uint64_t> xs;
@@ -1037,6 +1051,43 @@ static int readall_impl(ewal_ctx *c, const uint8_t *d_buf, uint64_t B, uint64_t 
       const uint64_t *plist = fpos ? fpos : c->cpos.as<uint64_t>();
       EW_CHECK(hipMemsetAsync(&ds->nslow, 0, 4, c->stream));
       c->rd_valid = true;
+#ifdef EW_DEBUG_BOUNDS
+      {   // tools/ debug builds: the frame list k_decode is about to read, checked on the host
+        EW_CHECK(hipStreamSynchronize(c->stream));
+        std::vector<uint32_t> rcl(rc_list ? n : 0);
+        if (rc_list) EW_CHECK(hipMemcpy(rcl.data(), rc_list, n * 4, hipMemcpyDeviceToHost));
+        const uint64_t pcap = (fpos ? c->fpos.cap : c->cpos.cap) / 8;
+        std::vector<uint64_t> pl(pcap);
+        EW_CHECK(hipMemcpy(pl.data(), plist, pcap * 8, hipMemcpyDeviceToHost));
+        std::fprintf(stderr, "ewal dbg: n %llu K %llu regular %d fpos %d rc_list %d B %llu pcap %llu pfcap %llu "
+                     "rdcap %zu q %llu\n", (unsigned long long)n, (unsigned long long)K, (int)regular, fpos != nullptr,
+                     rc_list != nullptr, (unsigned long long)B, (unsigned long long)pcap,
+                     (unsigned long long)c->pfcap, c->rd.cap / sizeof(RecDesc), (unsigned long long)q);
+        {
+          const uint64_t cc = std::min<uint64_t>(c->cpos.cap / 8, K + 4);
+          std::vector<uint64_t> cp(cc);
+          EW_CHECK(hipMemcpy(cp.data(), c->cpos.p, cc * 8, hipMemcpyDeviceToHost));
+          std::fprintf(stderr, "ewal dbg: cpos");
+          for (uint64_t i = 0; i < cc; ++i) std::fprintf(stderr, " %llu", (unsigned long long)cp[i]);
+          std::fprintf(stderr, "\newal dbg: fpos");
+          for (uint64_t i = 0; i < pcap; ++i) std::fprintf(stderr, " %llu", (unsigned long long)pl[i]);
+          std::fprintf(stderr, "\newal dbg: xs");
+          for (uint64_t x : xs) std::fprintf(stderr, " %llu", (unsigned long long)x);
+          std::fprintf(stderr, "\n");
+        }
+        uint64_t prev = 0;
+        for (uint64_t r = 0; r < n; ++r) {
+          const uint64_t ix = rc_list ? rcl[r] : r;
+          const uint64_t p = ix < pcap ? pl[ix] : ~0ull;
+          if (ix >= pcap || p >= B || (r && p <= prev)) {
+            std::fprintf(stderr, "ewal dbg: bad frame %llu: index %llu pos %llu prev %llu\n", (unsigned long long)r,
+                         (unsigned long long)ix, (unsigned long long)p, (unsigned long long)prev);
+            return EWAL_E_INVAL;
+          }
+          prev = p;
+        }
+      }
+#endif
       hipLaunchKernelGGL(k_decode, dim3(grid_for(n, 256)), dim3(256), 0, c->stream, d_buf, B,
                          plist, rc_list, n32, c->pwave.as<uint32_t>(), c->v.as<uint32_t>(),
                          tb->slice, tb->shift, c->rd.as<RecDesc>(), pf, pf + c->pfcap, c->slow.as<uint32_t>(), ds);
@@ -1723,6 +1774,13 @@ static int materialise_records(ewal_ctx *c) {
   hipLaunchKernelGGL(k_frame, dim3(fgrid), dim3(256), 0, c->stream, c->last_buf, c->last_B, c->cpos.as<uint64_t>(),
                      ccap, n, c->pwave.as<uint32_t>(), c->v.as<uint32_t>(), tb->slice, tb->shift, c->rd.as<RecDesc>(),
                      pf, pf + n, c->slow.as<uint32_t>(), ds, 0);
+  // the frames the canonical parser declined (the frame pass decides a call
+  // whose chain ends at such a frame: its failure comes first)
+  EW_CHECK(c->cat.ensure((size_t)1 << 20));
+  hipLaunchKernelGGL(k_decode_slow, dim3(64), dim3(256), 0, c->stream, c->last_buf, c->last_B, c->cpos.as<uint64_t>(),
+                     (const uint32_t *)nullptr, c->slow.as<uint32_t>(), ds, c->pwave.as<uint32_t>(),
+                     c->v.as<uint32_t>(), tb->slice, tb->shift, c->rd.as<RecDesc>(), pf, pf + n, (uint32_t)n,
+                     c->cat.as<uint8_t>(), (uint64_t)c->cat.cap);
   const uint32_t nb = grid_for(n, 1024);
   const size_t had = c->lbstat.cap;
   EW_CHECK(c->lbstat.ensure((size_t)nb * 8));

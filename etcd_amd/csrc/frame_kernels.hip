@@ -33,7 +33,8 @@
 //
 // What the canonical pass does not decide -- a candidate chain broken by a
 // false candidate, a non-canonical encoding, an index rewind, a record
-// spanning more than FR_SCAN tiles -- sets Small.irregular / Small.fc.rare
+// spanning more than FR_SCAN tiles, a whole frame after the chain's end that
+// the filter did not admit -- sets Small.irregular / Small.fc.rare
 // (single WAL) or ShardPos.bad (batch), and the host runs the general path
 // over the same stream pass (ewal_api.hip); nothing is guessed.
 
@@ -80,7 +81,7 @@ struct ShardPos {
   unsigned long long term;         // min (q << 8 | class): where the shard's frames end before it does, ~0
   long long last_entry, last_state, lastop, lastp;   // max p, -1 (lastp: any frame)
   uint32_t bad, open;              // bad: replayed alone; open: a frame starts at the shard's first byte
-  uint32_t rew, pad;               // rew: entry indexes go back (the rewind-mode pass over its tiles)
+  uint32_t rew, rmode;             // rew: entry indexes go back; rmode: this shard's ops claim slots (the rewind-mode pass over its tiles)
 };
 
 struct FrArgs {
@@ -711,7 +712,7 @@ __global__ __launch_bounds__(FR_THREADS, 1) void k_frames(FrArgs a, FrSeg sg) {
           const uint64_t rb = sg.rbase[sh], room = sg.rbase[sh + 1] - rb;
           if (k < room) {
             a.ents[rb + k] = ewal_entry{d.f0, d.f1, d.edoff - S0, d.edlen, d.etype, (int32_t)d.enil};
-            if (a.rew && atomicMax(&a.own[rb + k], (unsigned long long)(p + 1))) {   // a slot written twice
+            if (a.rew && sg.sp[sh].rmode && atomicMax(&a.own[rb + k], (unsigned long long)(p + 1))) {   // a slot written twice
               const uint32_t ci = atomicAdd(&ds->fr_ncl, 1u);
               if (ci < a.ccap) a.clist[ci] = (uint32_t)(rb + k); else rare |= 64u;
             }
@@ -1102,6 +1103,8 @@ __global__ __launch_bounds__(256) void k_frames_seam(FrArgs a, FrSeg sg, ResultD
         ds->q = T.sz;
         ds->qlen = (T.sz <= a.B && a.B - T.sz >= 8) ? (int64_t)ld_le64_b(a.buf, a.B, T.sz) : 0;
         ds->fc.last_chained = T.crcz;
+        // a whole frame at q the piece filter did not admit: the general path walks it (k_walk)
+        if (!tornz && fr_terminal(a.buf, a.B, T.sz, a.B) < 0) atomicOr(&ds->fc.rare, 128u);
       } else if (!tornz && T.sz != EZ) {
         const int tst = fr_terminal(a.buf, a.B, T.sz, EZ);
         if (tst < 0) badsh(shz);
@@ -1260,7 +1263,7 @@ __global__ __launch_bounds__(1024) void k_shard_rbase(const unsigned long long *
       p.bad = 0;
       p.open = 0;
       p.rew = 0;
-      p.pad = 0;
+      p.rmode = 0;
       sp[s] = p;
     }
     __syncthreads();
@@ -1291,7 +1294,7 @@ __global__ void k_shard_reset(ShardPos *__restrict__ sp, const uint32_t *__restr
   p.bad = 0;
   p.open = 0;
   p.rew = 0;
-  p.pad = 0;
+  p.rmode = 1;
   sp[list[i]] = p;
 }
 

@@ -136,7 +136,7 @@ def test_batch_fallback_torn_and_rewind(ctx):
     t3 = list(base)
     t3[0] = t3[0] + struct.pack("<q", 3) + b"\x00\x01\x02"
     check_batch(ctx, t3, [0] * 6, fallback={0})
-    # an index rewind (leader overwrite) needs the op-list path
+    # an index rewind (leader overwrite): the batch's rewind-mode pass over the shard's tiles (no replay)
     e = O.WalEncoder(0)
     e.save_crc(0)
     e.encode(1, b"m")
@@ -144,7 +144,7 @@ def test_batch_fallback_torn_and_rewind(ctx):
         e.save_entry(0, i, i, bytes([i]) * i)
     rw = list(base)
     rw[3] = e.getvalue()
-    check_batch(ctx, rw, [0, 0, 0, 2, 0, 0], fallback={3})
+    check_batch(ctx, rw, [0, 0, 0, 2, 0, 0], fallback=set())
     # all of them in one batch, plus a shard whose entries carry unknown fields
     u = O.WalEncoder(0)
     u.save_crc(0)
@@ -153,7 +153,7 @@ def test_batch_fallback_torn_and_rewind(ctx):
     u.save_entry(0, 1, 1, b"plain")
     u.encode(3, O.hardstate_marshal(1, 2, 3) + bytes([0x20, 0x07]))
     mix = [base[0], torn[2], base[1], rw[3], t2[4], u.getvalue(), base[5]]
-    res = check_batch(ctx, mix, [0, 0, 0, 2, 0, 0, 0], fallback={3, 5})
+    res = check_batch(ctx, mix, [0, 0, 0, 2, 0, 0, 0], fallback={5})
     assert res[5].ents[0].XXX_unrecognized == bytes([0x38, 0x05]) and res[5].state.XXX_unrecognized == bytes([0x20, 7])
 
 
