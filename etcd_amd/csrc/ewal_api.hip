@@ -2169,7 +2169,12 @@ int ewal_copy_range_info(ewal_ctx *c, ewal_range_info *out) {
     o.first_dlen = d.dlen;
     o.first_stored_crc = d.crc;
     o.first_u0 = d.chained;   // k_check ran frame 0 from seed 0: crc32.Update(0, Data) (crcType: the stored CRC)
-    o.first_pre_crc = d.st != 0;   // framing / Record.Unmarshal (d.st) fail before Validate; Entry / HardState (sub_st) after
+    {   // k_check left the frame's verdict in d.st: framing / Record.Unmarshal fail before decoder.decode's
+        // Validate; the Entry / HardState decode (sub_st), ReadAll's type / metadata / gap rules after it
+      const bool post = d.st == EWAL_ERR_RECORD_CRC || d.st == EWAL_ERR_WAL_CRC || d.st == EWAL_ERR_UNEXPECTED_TYPE ||
+                        d.st == EWAL_ERR_METADATA_CONFLICT || d.st == EWAL_PANIC_INDEX_GAP || d.sub_st != 0;
+      o.first_pre_crc = d.st != 0 && !post;
+    }
     if (h.md_first != ~0ull) {
       EW_CHECK(frame(h.md_first, &d));
       o.md_first_frame = (int64_t)h.md_first;
