@@ -607,10 +607,42 @@ static int walk_chain(ewal_ctx *c, DevTables *tb, const uint8_t *d_buf, uint64_t
 #ifndef EW_SEAM_WGS
 #define EW_SEAM_WGS 2
 #endif
-// units per tile / 64: 4 (1 MiB tiles) once the stream gives every wave of
-// the grid at least two of them, else 1 (256 KiB tiles: more waves at work)
-static int fr_upl(const ewal_ctx *c, uint32_t nunits) {
-  return (uint64_t)nunits >= (uint64_t)256 * FR_WAVES * std::max(1, c->num_cu) * 2 ? 4 : 1;
+// log2 of the units per tile: the largest of 256 (1 MiB tiles), 64 and 16
+// that still gives every wave of the grid two tiles (more, smaller tiles on
+// small streams keep the waves busy; large tiles amortise the per-tile work)
+static int fr_tsh(const ewal_ctx *c, uint32_t nunits) {
+#ifdef EW_ABLATION_HOOKS
+  if (const char *e = std::getenv("EWAL_TSH")) return std::atoi(e);   // tools/ timing builds only
+#endif
+  const uint64_t w2 = (uint64_t)FR_WAVES * std::max(1, c->num_cu) * 2;
+  return (uint64_t)nunits >= 256 * w2 ? 8 : (uint64_t)nunits >= 64 * w2 ? 6 : 4;
+}
+template <bool SEG>
+static void fr_launch(ewal_ctx *c, int tsh, uint32_t nt, const FrArgs &a, const FrSeg &sg, ResultDev *o, Small *h) {
+  const unsigned grid = (unsigned)std::min<uint64_t>(grid_for(nt, FR_WAVES), (uint64_t)std::max(1, c->num_cu));
+  const unsigned sgrid = (unsigned)std::min<uint64_t>(grid_for(nt, 256), (uint64_t)std::max(1, c->num_cu) * EW_SEAM_WGS);
+  if (tsh == 8) {
+    hipLaunchKernelGGL((k_frames<SEG, 8>), dim3(grid), dim3(FR_THREADS), 0, c->stream, a, sg);
+    hipLaunchKernelGGL((k_frames_seam<SEG, 8>), dim3(sgrid), dim3(256), 0, c->stream, a, sg, o, h);
+  } else if (tsh == 6) {
+    hipLaunchKernelGGL((k_frames<SEG, 6>), dim3(grid), dim3(FR_THREADS), 0, c->stream, a, sg);
+    hipLaunchKernelGGL((k_frames_seam<SEG, 6>), dim3(sgrid), dim3(256), 0, c->stream, a, sg, o, h);
+  } else {
+    hipLaunchKernelGGL((k_frames<SEG, 4>), dim3(grid), dim3(FR_THREADS), 0, c->stream, a, sg);
+    hipLaunchKernelGGL((k_frames_seam<SEG, 4>), dim3(sgrid), dim3(256), 0, c->stream, a, sg, o, h);
+  }
+}
+static void fr_launch_result_batch(ewal_ctx *c, int tsh, const FrArgs &a, const FrSeg &sg) {
+  const dim3 g(grid_for((uint64_t)sg.ns * 64, 256));
+  if (tsh == 8)
+    hipLaunchKernelGGL(k_result_batch_fr<8>, g, dim3(256), 0, c->stream, a, sg, c->bres.as<ewal_result>(),
+                       c->bef.as<unsigned long long>());
+  else if (tsh == 6)
+    hipLaunchKernelGGL(k_result_batch_fr<6>, g, dim3(256), 0, c->stream, a, sg, c->bres.as<ewal_result>(),
+                       c->bef.as<unsigned long long>());
+  else
+    hipLaunchKernelGGL(k_result_batch_fr<4>, g, dim3(256), 0, c->stream, a, sg, c->bres.as<ewal_result>(),
+                       c->bef.as<unsigned long long>());
 }
 static int fr_ensure(ewal_ctx *c, uint32_t nunits, uint32_t ntiles) {
   EW_CHECK(c->ftrec.ensure((size_t)ntiles * sizeof(FrTile)));
@@ -658,8 +690,8 @@ static int frames_pass(ewal_ctx *c, DevTables *tb, const uint8_t *d_buf, uint64_
                        bool *done) {
   *done = false;
   const uint32_t nunits = (uint32_t)(B / EW_WAVE_BYTES + 1);
-  const int upl = fr_upl(c, nunits);
-  const uint32_t tu = 64u * (uint32_t)upl, ntiles = (nunits + tu - 1) / tu;
+  const int tsh = fr_tsh(c, nunits);
+  const uint32_t tu = 1u << tsh, ntiles = (nunits + tu - 1) / tu;
   if (int rc = fr_ensure(c, nunits, ntiles)) return rc;
   uint32_t mcap = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(c->mlist.cap / 8, 4096), 0xffffffffull);
   bool rew = false;   // rewind mode: entry indexes go back (wal/wal.go:173 truncates ents)
@@ -679,17 +711,7 @@ static int frames_pass(ewal_ctx *c, DevTables *tb, const uint8_t *d_buf, uint64_
       a.clist = c->fcl.as<uint32_t>();
       a.ccap = clcap;
     }
-    const unsigned grid = (unsigned)std::min<uint64_t>(grid_for(ntiles, FR_WAVES), (uint64_t)std::max(1, c->num_cu));
-    const unsigned sgrid = (unsigned)std::min<uint64_t>(grid_for(ntiles, 256), (uint64_t)std::max(1, c->num_cu) * EW_SEAM_WGS);
-    if (upl == 4) {
-      hipLaunchKernelGGL((k_frames<false, 4>), dim3(grid), dim3(FR_THREADS), 0, c->stream, a, FrSeg{});
-      hipLaunchKernelGGL((k_frames_seam<false, 4>), dim3(sgrid), dim3(256), 0, c->stream, a, FrSeg{}, c->h_res_dev,
-                         c->h_small_dev);
-    } else {
-      hipLaunchKernelGGL((k_frames<false, 1>), dim3(grid), dim3(FR_THREADS), 0, c->stream, a, FrSeg{});
-      hipLaunchKernelGGL((k_frames_seam<false, 1>), dim3(sgrid), dim3(256), 0, c->stream, a, FrSeg{}, c->h_res_dev,
-                         c->h_small_dev);
-    }
+    fr_launch<false>(c, tsh, ntiles, a, FrSeg{}, c->h_res_dev, c->h_small_dev);
     if (rew)   // the slots more than one op claimed: their last op's entry
       hipLaunchKernelGGL(k_ents_fix, dim3((unsigned)std::max(1, c->num_cu) * 2), dim3(256), 0, c->stream, d_buf, B,
                          (const unsigned long long *)a.own, (const uint32_t *)a.clist, a.ccap, (const Small *)a.ds,
@@ -701,7 +723,7 @@ static int frames_pass(ewal_ctx *c, DevTables *tb, const uint8_t *d_buf, uint64_
     EW_CHECK(hipStreamSynchronize(c->stream));
     const Small *hs = c->h_small;
     if (ew_debug())
-      std::fprintf(stderr, "ewal frames: pass %d upl %d spec %u rare %u irr %u need %llu nmeta %u K %llu\n", pass, upl,
+      std::fprintf(stderr, "ewal frames: pass %d tsh %d spec %u rare %u irr %u need %llu nmeta %u K %llu\n", pass, tsh,
                    hs->spec_n, hs->fc.rare, hs->irregular, (unsigned long long)hs->fr_need, hs->nmeta,
                    (unsigned long long)hs->total);
     if (hs->errflag) return EWAL_E_TIMEOUT;
@@ -1278,8 +1300,8 @@ static int frames_batch(ewal_ctx *c, DevTables *tb, const uint8_t *d_buf, uint64
   Small *ds = c->small.as<Small>();
   *done = false;
   const uint32_t nunits = (uint32_t)(B / EW_WAVE_BYTES + 1);
-  const int upl = fr_upl(c, nunits);
-  const uint32_t tu = 64u * (uint32_t)upl, ntiles = (nunits + tu - 1) / tu;
+  const int tsh = fr_tsh(c, nunits);
+  const uint32_t tu = 1u << tsh, ntiles = (nunits + tu - 1) / tu;
   if (int rc = fr_ensure(c, nunits, ntiles)) return rc;
   EW_CHECK(c->bsoff.ensure((size_t)(ns + 1) * 8));
   EW_CHECK(c->bri.ensure((size_t)ns * 8));
@@ -1311,26 +1333,11 @@ static int frames_batch(ewal_ctx *c, DevTables *tb, const uint8_t *d_buf, uint64
                        c->fnfp.as<unsigned long long>());
     hipLaunchKernelGGL(k_shard_rbase, dim3(1), dim3(1024), 0, c->stream, (const unsigned long long *)c->fnfp.p, ns,
                        ecap, sg.rbase, sg.sp, ds);
-    const unsigned grid = (unsigned)std::min<uint64_t>(grid_for(ntiles, FR_WAVES), (uint64_t)std::max(1, c->num_cu));
-    const unsigned sgrid = (unsigned)std::min<uint64_t>(grid_for(ntiles, 256), (uint64_t)std::max(1, c->num_cu) * EW_SEAM_WGS);
-    if (upl == 4) {
-      hipLaunchKernelGGL((k_frames<true, 4>), dim3(grid), dim3(FR_THREADS), 0, c->stream, a, sg);
-      hipLaunchKernelGGL((k_frames_seam<true, 4>), dim3(sgrid), dim3(256), 0, c->stream, a, sg, (ResultDev *)nullptr,
-                         (Small *)nullptr);
-    } else {
-      hipLaunchKernelGGL((k_frames<true, 1>), dim3(grid), dim3(FR_THREADS), 0, c->stream, a, sg);
-      hipLaunchKernelGGL((k_frames_seam<true, 1>), dim3(sgrid), dim3(256), 0, c->stream, a, sg, (ResultDev *)nullptr,
-                         (Small *)nullptr);
-    }
+    fr_launch<true>(c, tsh, ntiles, a, sg, nullptr, nullptr);
     hipLaunchKernelGGL(k_tile_scan, dim3(1), dim3(1024), 0, c->stream, (const FrTile *)a.trec, ntiles, sg.tcb,
                        (const Small *)ds);
     hipLaunchKernelGGL(k_meta_batch_fr, dim3(64), dim3(256), 0, c->stream, a, sg);
-    if (upl == 4)
-      hipLaunchKernelGGL(k_result_batch_fr<4>, dim3(grid_for((uint64_t)ns * 64, 256)), dim3(256), 0, c->stream, a, sg,
-                         c->bres.as<ewal_result>(), c->bef.as<unsigned long long>());
-    else
-      hipLaunchKernelGGL(k_result_batch_fr<1>, dim3(grid_for((uint64_t)ns * 64, 256)), dim3(256), 0, c->stream, a, sg,
-                         c->bres.as<ewal_result>(), c->bef.as<unsigned long long>());
+    fr_launch_result_batch(c, tsh, a, sg);
     hipLaunchKernelGGL(k_batch_gate_fr, dim3(1), dim3(64), 0, c->stream, ds, c->h_small_dev);
     EW_CHECK(hipGetLastError());
     EW_CHECK(hipMemcpyAsync(out, c->bres.p, (size_t)ns * sizeof(ewal_result), hipMemcpyDeviceToHost, c->stream));
@@ -1379,8 +1386,8 @@ static int frames_batch_rewind(ewal_ctx *c, DevTables *tb, const uint8_t *d_buf,
                                uint64_t have) {
   Small *ds = c->small.as<Small>();
   const uint32_t nunits = (uint32_t)(B / EW_WAVE_BYTES + 1);
-  const int upl = fr_upl(c, nunits);
-  const uint32_t tu = 64u * (uint32_t)upl, ntiles = (nunits + tu - 1) / tu;
+  const int tsh = fr_tsh(c, nunits);
+  const uint32_t tu = 1u << tsh, ntiles = (nunits + tu - 1) / tu;
   const uint64_t tb_bytes = (uint64_t)tu * EW_WAVE_BYTES;
   std::vector<uint64_t> rbase(ns + 1);
   EW_CHECK(hipMemcpy(rbase.data(), c->frbase.p, (size_t)(ns + 1) * 8, hipMemcpyDeviceToHost));
@@ -1425,27 +1432,12 @@ static int frames_batch_rewind(ewal_ctx *c, DevTables *tb, const uint8_t *d_buf,
     sg.rbase = c->frbase.as<uint64_t>();
     sg.sp = c->fsp.as<ShardPos>();
     sg.tcb = c->ftcb.as<uint32_t>();
-    const unsigned grid = (unsigned)std::min<uint64_t>(grid_for(ntl, FR_WAVES), (uint64_t)std::max(1, c->num_cu));
-    const unsigned sgrid = (unsigned)std::min<uint64_t>(grid_for(ntl, 256), (uint64_t)std::max(1, c->num_cu) * EW_SEAM_WGS);
-    if (upl == 4) {
-      hipLaunchKernelGGL((k_frames<true, 4>), dim3(grid), dim3(FR_THREADS), 0, c->stream, a, sg);
-      hipLaunchKernelGGL((k_frames_seam<true, 4>), dim3(sgrid), dim3(256), 0, c->stream, a, sg, (ResultDev *)nullptr,
-                         (Small *)nullptr);
-    } else {
-      hipLaunchKernelGGL((k_frames<true, 1>), dim3(grid), dim3(FR_THREADS), 0, c->stream, a, sg);
-      hipLaunchKernelGGL((k_frames_seam<true, 1>), dim3(sgrid), dim3(256), 0, c->stream, a, sg, (ResultDev *)nullptr,
-                         (Small *)nullptr);
-    }
+    fr_launch<true>(c, tsh, ntl, a, sg, nullptr, nullptr);
     hipLaunchKernelGGL(k_ents_fix, dim3((unsigned)std::max(1, c->num_cu) * 2), dim3(256), 0, c->stream, d_buf, B,
                        (const unsigned long long *)a.own, (const uint32_t *)a.clist, a.ccap, (const Small *)ds, a.ents,
                        (const uint64_t *)sg.soff, ns);
     hipLaunchKernelGGL(k_meta_batch_fr, dim3(64), dim3(256), 0, c->stream, a, sg);
-    if (upl == 4)
-      hipLaunchKernelGGL(k_result_batch_fr<4>, dim3(grid_for((uint64_t)ns * 64, 256)), dim3(256), 0, c->stream, a, sg,
-                         c->bres.as<ewal_result>(), c->bef.as<unsigned long long>());
-    else
-      hipLaunchKernelGGL(k_result_batch_fr<1>, dim3(grid_for((uint64_t)ns * 64, 256)), dim3(256), 0, c->stream, a, sg,
-                         c->bres.as<ewal_result>(), c->bef.as<unsigned long long>());
+    fr_launch_result_batch(c, tsh, a, sg);
     hipLaunchKernelGGL(k_batch_gate_fr, dim3(1), dim3(64), 0, c->stream, ds, c->h_small_dev);
     EW_CHECK(hipGetLastError());
     EW_CHECK(hipMemcpyAsync(out, c->bres.p, (size_t)ns * sizeof(ewal_result), hipMemcpyDeviceToHost, c->stream));
@@ -1901,7 +1893,7 @@ int ewal_ctx_reserve(ewal_ctx *c, uint64_t wal_bytes, uint32_t flags) {
   // first call's descriptor capacity (readall_impl's rdcap)
   {
     const uint32_t nunits = (uint32_t)(B / EW_WAVE_BYTES + 1);
-    const uint32_t tu = 64u * (uint32_t)fr_upl(c, nunits);
+    const uint32_t tu = 1u << fr_tsh(c, nunits);
     if ((rc = fr_ensure(c, nunits, (nunits + tu - 1) / tu))) return rc;
   }
   const uint64_t ecap = std::min<uint64_t>(ccap, B / 4096 + 1024);
@@ -2627,3 +2619,11 @@ int ecommit_batch_device(ewal_ctx *c, uint64_t G, const uint64_t *match, const u
 }
 
 }  // extern "C"
+
+#ifdef FR_TIMING
+// tools/ timing builds only: the last k_frames launch's per-wave phase cycles
+extern "C" int ewal_dbg_fr_timing(unsigned long long *out, int n) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(fr_tdbg), (size_t)n * 8) != hipSuccess) return EWAL_E_HIP;
+  return 0;
+}
+#endif

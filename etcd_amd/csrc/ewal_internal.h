@@ -171,7 +171,7 @@ struct Small {
   FrAgg fr;
   unsigned long long fr_need;     // single WAL: ents the frame pass needed; batch: the regions' total
   uint32_t fr_ncl;                // rewind mode: ents slots claimed more than once (listed for k_ents_fix)
-  uint32_t fr_pad;
+  uint32_t fr_tick;               // k_frames: tiles handed out past the first round (dynamic schedule)
 };
 
 // A returned Entry (ent = its index in ents) or the HardState (ent = -1)

@@ -7,7 +7,7 @@
 //
 // k_stream leaves, per 4 KiB unit, the lins of its 16 super-pieces (v[]) and
 // the 64-B pieces its branch-free filter flagged (hmask).  k_frames takes the
-// stream in TILES of TU = 64 * UPL units, one wave per tile:
+// stream in TILES of TU = 2^TSH units (16, 64 or 256), one wave per tile:
 //   A. the tile's unit lins (Horner over v[]) and their wave scan give P at
 //      every unit start RELATIVE TO THE TILE START (Pl) -- no global prefix
 //      scan: a record's check needs lin(Data) = S_n(P(s)) ^ P(e), the same for
@@ -327,10 +327,23 @@ struct FrCarry {
   uint32_t flags;   // 1 valid, 2 decoded, 4 torn, 8 tile-first (its seed is the seam pass's), 16 has its seed
 };
 
-template <bool SEG, int UPL>
+#ifdef FR_TIMING
+// tools/ timing builds only: per wave, the cycles of each phase of k_frames
+__device__ unsigned long long fr_tdbg[8192 * 8];
+#define FR_T(i) do { const unsigned long long t_ = clock64(); tacc[i] += t_ - tlast; tlast = t_; } while (0)
+#else
+#define FR_T(i) do {} while (0)
+#endif
+
+template <bool SEG, int TSH>
 __global__ __launch_bounds__(FR_THREADS, 1) void k_frames(FrArgs a, FrSeg sg) {
-  constexpr int TU = 64 * UPL;                       // units per tile
-  constexpr int LB = 12 + (UPL == 4 ? 2 : 0);        // log2 of a lane's span in bytes
+#ifdef FR_TIMING
+  unsigned long long tacc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tlast = clock64();
+#endif
+  constexpr int TU = 1 << TSH;                       // units per tile
+  constexpr int UPL = TSH >= 6 ? 1 << (TSH - 6) : 1; // units per lane
+  constexpr int NL = TU / UPL;                       // lanes holding units (64, or TU < 64)
+  constexpr int LB = 12 + (TSH >= 6 ? TSH - 6 : 0);  // log2 of a lane's span in bytes
   __shared__ uint32_t s_t16[16 * 256];               // slicing-by-16
   __shared__ uint32_t s_svp[1024];                   // S_256 byte tables
   __shared__ uint32_t s_nib[FR_NIB * 128];           // S_{2^0} .. S_{2^19}, nibble tables
@@ -347,13 +360,21 @@ __global__ __launch_bounds__(FR_THREADS, 1) void k_frames(FrArgs a, FrSeg sg) {
   stage_lds<FR_THREADS>(s_nib, FR_NIB * 128, [&](int i) { return nib_src(a.g_shift, i); });
   stage_lds<FR_THREADS>(s_inv, 7 * 128, [&](int i) { return nib_src(a.g_shift + EW_SHIFT_LEVELS * 1024, i); });
   __syncthreads();   // the only barrier: every wave runs its own tiles from here on
+  FR_T(0);
   uint32_t *ucnt = s_ucnt[wv];
   uint32_t *spw = s_pw[wv];
   uint32_t *w = s_win + tid;
   uint32_t rare = 0, irr = 0;
   unsigned long long need_ecap = 0;
   const uint32_t nt_run = a.tlist ? a.ntl : a.ntiles;
-  for (uint32_t ti = wid; ti < nt_run; ti += nwaves) {
+  // every wave's first tile is its id; the rest are handed out by a counter
+  // (tiles differ in work: a static stride leaves the waves uneven)
+  auto next_tile = [&]() {
+    uint32_t nx = 0;
+    if (lane == 0) nx = nwaves + atomicAdd(&ds->fr_tick, 1u);
+    return rl32(nx, 0);
+  };
+  for (uint32_t ti = wid; ti < nt_run; ti = next_tile()) {
     const uint32_t t = a.tlist ? a.tlist[ti] : ti;
     const uint32_t u0 = t * TU;
     const uint64_t ts = (uint64_t)u0 * EW_WAVE_BYTES;
@@ -365,7 +386,7 @@ __global__ __launch_bounds__(FR_THREADS, 1) void k_frames(FrArgs a, FrSeg sg) {
 #pragma unroll
       for (int j = 0; j < UPL; ++j) {
         const uint32_t u = u0 + UPL * lane + j;
-        const bool in = u < a.nunits;
+        const bool in = u < a.nunits && (NL == 64 || lane < NL);
         const uint32_t c = in ? (uint32_t)__popcll(a.hmask[u].x) : 0u;
         pcs |= c << (8 * j);
         lcnt += c;
@@ -385,7 +406,8 @@ __global__ __launch_bounds__(FR_THREADS, 1) void k_frames(FrArgs a, FrSeg sg) {
         }
     }
 #pragma unroll
-    for (int j = 0; j < UPL; ++j) ucnt[UPL * lane + j] = 0;
+    for (int j = 0; j < UPL; ++j)
+      if (NL == 64 || lane < NL) ucnt[UPL * lane + j] = 0;
     uint32_t q = 0;
 #pragma unroll
     for (int j = 0; j < UPL; ++j) q = nib_apply(s_nib + 12 * 128, q) ^ x[j];
@@ -394,7 +416,7 @@ __global__ __launch_bounds__(FR_THREADS, 1) void k_frames(FrArgs a, FrSeg sg) {
       const uint32_t o = (uint32_t)__shfl_up((int)q, 1 << d);
       if (lane >= (1 << d)) q = nib_apply(s_nib + (LB + d) * 128, o) ^ q;
     }
-    const uint32_t agg = rl32(q, 63);
+    const uint32_t agg = rl32(q, NL - 1);
     {
       uint32_t pwj = (uint32_t)__shfl_up((int)q, 1);
       if (lane == 0) pwj = 0;
@@ -402,12 +424,15 @@ __global__ __launch_bounds__(FR_THREADS, 1) void k_frames(FrArgs a, FrSeg sg) {
       for (int j = 0; j < UPL; ++j) {
         if (j) pwj = nib_apply(s_nib + 12 * 128, pwj) ^ x[j - 1];
         const uint32_t u = u0 + UPL * lane + j;
-        spw[UPL * lane + j] = pwj;
-        if (u < a.nunits) a.pl[u] = pwj;
+        if (NL == 64 || lane < NL) {
+          spw[UPL * lane + j] = pwj;
+          if (u < a.nunits) a.pl[u] = pwj;
+        }
       }
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
+    FR_T(1);
     // P at a unit start of this tile by its index in the tile
     auto pw_of = [&](uint32_t ul) { return spw[ul < (uint32_t)TU ? ul : 0u]; };
     // flagged pieces: per lane the count over its units, wave prefix
@@ -504,6 +529,7 @@ __global__ __launch_bounds__(FR_THREADS, 1) void k_frames(FrArgs a, FrSeg sg) {
       TA = rl32(ciA, 63);
       gnext = 64;
     }
+    FR_T(2);
     bool first_round = true;
     for (;;) {
       while (!haveB && TA - ca < 63 && gnext < Tf) {   // keep 63 candidates ahead while pieces remain
@@ -516,6 +542,7 @@ __global__ __launch_bounds__(FR_THREADS, 1) void k_frames(FrArgs a, FrSeg sg) {
           haveB = false;
         }
       }
+      FR_T(2);
       const uint32_t avail = (TA - ca) + (haveB ? TB : 0u);
       if (avail == 0) break;
       const uint32_t nnew = min(avail, 63u);
@@ -548,6 +575,7 @@ __global__ __launch_bounds__(FR_THREADS, 1) void k_frames(FrArgs a, FrSeg sg) {
         ok = fr_decode(a.buf, a.B, p, pwu, a.v, s_t16, s_svp, s_inv, w, d, L, Pfo, Pfd);
         if (!ok) { d.type = 0; d.dlen = 0; d.doff = p + 8; }
       }
+      FR_T(3);
       uint64_t s = p + 8 + (uint64_t)L;
       uint32_t sh = 0;
       if (SEG && isnew) sh = shlo == shhi ? shlo : pos_shard_in(sg.soff, shlo, shhi + 1, p);
@@ -655,6 +683,7 @@ __global__ __launch_bounds__(FR_THREADS, 1) void k_frames(FrArgs a, FrSeg sg) {
           }
         }
       }
+      FR_T(4);
       // the tile's first frame: its operands for the seam pass, stored by the
       // lane holding it (lane 1 of the first round; its P(data end) by the
       // lane that checks it)
@@ -748,6 +777,7 @@ __global__ __launch_bounds__(FR_THREADS, 1) void k_frames(FrArgs a, FrSeg sg) {
         const uint32_t mi = atomicAdd(&ds->nmeta, 1u);
         if (mi < a.mcap) a.mlist[mi] = p; else rare |= 8u;
       }
+      FR_T(5);
       // reductions over the round (lanes are in stream order)
       const bool rlive = isnew && !torn;
       const unsigned long long mf = __ballot(occ && st != 0), me = __ballot(rlive && d.type == 2),
@@ -815,6 +845,7 @@ __global__ __launch_bounds__(FR_THREADS, 1) void k_frames(FrArgs a, FrSeg sg) {
         cmA = cmB; poA = poB; ciA = ciB; TA = TB; ca = 0;
         haveB = false;
       }
+      FR_T(6);
     }
     if (SEG) aflush();
     // per unit: the tile's candidates before it
@@ -824,7 +855,7 @@ __global__ __launch_bounds__(FR_THREADS, 1) void k_frames(FrArgs a, FrSeg sg) {
       uint32_t c[UPL], cs = 0;
 #pragma unroll
       for (int j = 0; j < UPL; ++j) {
-        c[j] = ucnt[UPL * lane + j];
+        c[j] = (NL == 64 || lane < NL) ? ucnt[UPL * lane + j] : 0u;
         cs += c[j];
       }
       const uint32_t inc = wave_incl_sum(cs);
@@ -832,7 +863,7 @@ __global__ __launch_bounds__(FR_THREADS, 1) void k_frames(FrArgs a, FrSeg sg) {
 #pragma unroll
       for (int j = 0; j < UPL; ++j) {
         const uint32_t u = u0 + UPL * lane + j;
-        if (u < a.nunits) a.ucb[u] = run;
+        if (u < a.nunits && (NL == 64 || lane < NL)) a.ucb[u] = run;
         run += c[j];
       }
     }
@@ -863,7 +894,12 @@ __global__ __launch_bounds__(FR_THREADS, 1) void k_frames(FrArgs a, FrSeg sg) {
         atomicAdd(&ds->total, (unsigned long long)nfr);
       }
     }
+    FR_T(7);
   }
+#ifdef FR_TIMING
+  if (lane == 0 && wid < 8192)
+    for (int i = 0; i < 8; ++i) fr_tdbg[wid * 8 + i] = tacc[i];
+#endif
   uint32_t rr = rare;
   for (int o = 32; o; o >>= 1) rr |= (uint32_t)__shfl_xor((int)rr, o);
   if (lane == 0 && rr) atomicOr(&ds->fc.rare, rr);
@@ -918,7 +954,7 @@ __device__ __forceinline__ int fr_terminal(const uint8_t *buf, uint64_t B, uint6
 // The single WAL's result after the seam pass (its last workgroup):
 // ReadAll's metadata rule over the listed metadata frames, the frames the
 // result names re-read from the stream, the failing frame's ordinal.
-template <int UPL>
+template <int TSH>
 __device__ void fr_result(const FrArgs &a, ResultDev *o, Small *h, uint4 (*s_w)[6], RecDesc *s_d,
                           unsigned long long *s_ord) {
   Small *ds = a.ds;
@@ -948,9 +984,20 @@ __device__ void fr_result(const FrArgs &a, ResultDev *o, Small *h, uint4 (*s_w)[
   __threadfence();
   __syncthreads();
   const unsigned long long key = ds->fc.fail_inv ? ~ds->fc.fail_inv : ~0ull;
-  if (key != ~0ull && tid < 64) {   // the failing frame's ordinal (one wave)
-    const unsigned long long ord = fr_ordinal(a, 64 * UPL, key >> 8, nullptr);
-    if (tid == 0) *s_ord = ord;
+  if (key != ~0ull) {   // the failing frame's ordinal: the tiles before it summed by the whole workgroup
+    const uint64_t x = key >> 8, u = x >> 12;
+    const uint32_t tx = u < a.nunits ? (uint32_t)(u >> TSH) : a.ntiles;
+    if (tid == 0) *s_ord = 0;
+    __syncthreads();
+    unsigned long long part = 0;
+#pragma unroll 8
+    for (uint32_t i = tid; i < tx; i += blockDim.x) part += a.trec[i].count;
+    for (int o = 32; o; o >>= 1) part += (unsigned long long)__shfl_xor((long long)part, o);
+    if ((tid & 63) == 0 && part) atomicAdd(s_ord, part);
+    if (u < a.nunits && tid < 64) {   // the tile's units before x's, and x's unit before x
+      const unsigned long long in = a.ucb[u] + fr_incount(a.buf, a.B, a.hmask, u, x);
+      if (tid == 0) atomicAdd(s_ord, in);
+    }
   }
   const uint64_t le = ds->fr.le, ls = ds->fr.ls, lo = ds->fr.lo;
   const long long want[5] = {key != ~0ull ? (long long)(key >> 8) : -1, le ? (long long)(le - 1) : -1,
@@ -986,10 +1033,10 @@ __device__ void fr_result(const FrArgs &a, ResultDev *o, Small *h, uint4 (*s_w)[
 // next), the links between them, the gap rule of the tile's first entry op;
 // single WAL: the fold of the tiles' reductions and, in the last workgroup,
 // the result.
-template <bool SEG, int UPL>
+template <bool SEG, int TSH>
 __global__ __launch_bounds__(256) void k_frames_seam(FrArgs a, FrSeg sg, ResultDev *o, Small *h) {
-  constexpr uint32_t TU = 64 * UPL;
-  constexpr int TLOG = 18 + (UPL == 4 ? 2 : 0);
+  constexpr uint32_t TU = 1u << TSH;
+  constexpr int TLOG = 12 + TSH;
   constexpr uint64_t TB = (uint64_t)TU * EW_WAVE_BYTES;
   __shared__ unsigned long long s_red[6];   // fail, meta, le, ls, lo, nops
   __shared__ uint32_t s_last;
@@ -1179,7 +1226,7 @@ __global__ __launch_bounds__(256) void k_frames_seam(FrArgs a, FrSeg sg, ResultD
   __syncthreads();
   if (s_last) {   // the last workgroup: every tile is in
     __threadfence();
-    fr_result<UPL>(a, o, h, s_w, s_d, &s_ord);
+    fr_result<TSH>(a, o, h, s_w, s_d, &s_ord);
   }
 }
 
@@ -1283,6 +1330,7 @@ __global__ void k_shard_reset(ShardPos *__restrict__ sp, const uint32_t *__restr
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i == 0) {
     ds->fr_ncl = 0;
+    ds->fr_tick = 0;
     ds->fc.rare = 0;
   }
   if (i >= n) return;
@@ -1344,7 +1392,7 @@ __global__ void k_meta_batch_fr(FrArgs a, FrSeg sg) {
 // Per shard (one wave): its ReadAll result.  Ordinals from positions
 // (fr_ordinal with the tile prefix); the frames the result names re-read by
 // lanes 0..5.
-template <int UPL>
+template <int TSH>
 __global__ __launch_bounds__(256) void k_result_batch_fr(FrArgs a, FrSeg sg, ewal_result *__restrict__ out,
                                                          unsigned long long *__restrict__ ent_first) {
   __shared__ uint4 s_w[256][6];
@@ -1356,7 +1404,7 @@ __global__ __launch_bounds__(256) void k_result_batch_fr(FrArgs a, FrSeg sg, ewa
   if (s >= sg.ns) return;   // (wave-uniform)
   const ShardPos A = sg.sp[s];
   const uint64_t so = sg.soff[s], se = sg.soff[s + 1], ri = sg.ri[s];
-  const uint32_t tu = 64 * UPL;
+  const uint32_t tu = 1u << TSH;
   const uint64_t f0 = fr_ordinal(a, tu, so, sg.tcb);
   const uint64_t fE = fr_ordinal(a, tu, se, sg.tcb);
   const uint64_t q = A.term != ~0ull ? (A.term >> 8) : se;

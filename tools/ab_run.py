@@ -32,7 +32,7 @@ for i in range(12):
     if mode == "shards":
         assert L.lib.ewal_readall_batch_device(ctx.handle, d.ptr, ns, cl, cr, co) == 0
         r = co[0]
-        ok = all(x.status == 0 and not x.flags for x in co)
+        ok = all(x.status == 0 and not (x.flags & L.FLAG_SHARD_FALLBACK) for x in co)
     else:
         r = L.Result()
         L.lib.ewal_readall_device(ctx.handle, d.ptr, lens[0], 1, C.byref(r))

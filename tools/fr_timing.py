@@ -1,0 +1,44 @@
+"""Per-phase cycles of k_frames (a -DFR_TIMING build of the library, loaded
+through EWAL_LIB_PATH): the configs[1] WAL and configs[0]'s WAL on the GPU.
+Usage: EWAL_LIB_PATH=tools/libewal_tm.so python tools/fr_timing.py"""
+import ctypes as C
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from etcd_amd import _lib as L
+from etcd_amd import wal as W
+
+NAMES = ["stage", "A", "pieces", "decode", "checks", "ops", "reduce", "tile_end"]
+lib = L.lib
+lib.ewal_dbg_fr_timing.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
+
+
+def one(label, size, lo, hi):
+    buf, n = W.synth_wal(size, lo, hi, seed=2)
+    ctx = W.Context(0)
+    nb = len(buf)
+    d = ctx.alloc(nb + 64)
+    d.upload_ptr(C.addressof((C.c_char * nb).from_buffer(buf)), nb)
+    rs = L.Result()
+    for _ in range(3):
+        rc = lib.ewal_readall_device(ctx.handle, d.ptr, nb, 1, C.byref(rs))
+        assert rc == 0 and rs.flags & L.FLAG_FAST_PATH, (rc, rs.flags)
+    t = (C.c_ulonglong * (8192 * 8))()
+    lib.ewal_dbg_fr_timing(t, 8192 * 8)
+    waves = [list(t[w * 8:(w + 1) * 8]) for w in range(8192) if any(t[w * 8:(w + 1) * 8])]
+    tot = [sum(x) for x in waves]
+    print("%s: %d frames, %.3f GiB, device %.3f ms (stream %.3f), %d waves" %
+          (label, n, nb / (1 << 30), rs.device_ms, rs.stream_ms, len(waves)))
+    print("  per-wave total cycles: avg %.0f max %.0f" % (sum(tot) / len(tot), max(tot)))
+    for i, nm in enumerate(NAMES):
+        col = [x[i] for x in waves]
+        print("  %-9s avg %10.0f  max %10.0f  share %5.1f%%" % (nm, sum(col) / len(col), max(col),
+                                                             100.0 * sum(col) / max(1, sum(tot))))
+    d.free()
+    ctx.close()
+
+
+one("configs[1]", 8 << 30, 64, 65536)
+one("configs[0]", int(285e6), 256, 256)
