@@ -22,7 +22,7 @@
 #include "wal_kernels.hip"
 #include "aux_kernels.hip"
 #include "msg_kernels.hip"
-#include "fused_kernels.hip"
+#include "frame_fields.hip"
 #include "frame_kernels.hip"
 #include "ewal_stage.h"
 
@@ -114,7 +114,6 @@ struct ewal_ctx {
   int device = 0;
   int num_cu = 256;
   int ablate = 0;      // EWAL_STREAM_ABLATE (timing experiments only; results are wrong)
-  uint32_t fc_ablate = 0;   // EWAL_FC_ABLATE (k_fc timing experiments only; results are wrong)
   int frame_wg = 3;    // k_frame resident workgroups per CU (EWAL_FRAME_WG: A/B timing)
   hipStream_t stream = nullptr;
   bool own_stream = false;
@@ -123,7 +122,7 @@ struct ewal_ctx {
   std::map<uint32_t, std::unique_ptr<ewal::CrcTables>> host_tables;
   DevBuf encw, encs, lbstat, gagg, slow, mlist, pf, v, pwave, ux, tagg, tpx, wcnt, slots, cbase, ovf, cpos, clen, nxt, exc, E, rs, jl, vis, entry, on, rec_cand, rd, opf, ops, kk, kkrev, suf,
       ents, recs, tmp, small, sdesc, snaps, hbuf_dev, xpos, walk, fpos, ulist, uitems, uarena, ftrec, fpl, fucb,
-      fnfp, frbase, fsp, ftcb, fown, fcl, ftl;
+      fnfp, frbase, fsp, ftcb, fown, fcl, ftl, ftcnt;
   HostBuf hsdesc;                  // esnap_verify_packed's per-file table (host-mapped)
   // esnap_verify_packed's residual decode (esnap_copy_field): the batch's
   // buffer, per file its residual slot (-1: none), per slot its segments
@@ -646,6 +645,7 @@ static void fr_launch_result_batch(ewal_ctx *c, int tsh, const FrArgs &a, const 
 }
 static int fr_ensure(ewal_ctx *c, uint32_t nunits, uint32_t ntiles) {
   EW_CHECK(c->ftrec.ensure((size_t)ntiles * sizeof(FrTile)));
+  EW_CHECK(c->ftcnt.ensure((size_t)ntiles * 4));
   EW_CHECK(c->fpl.ensure((size_t)nunits * 4));
   EW_CHECK(c->fucb.ensure((size_t)nunits * 4));
   return 0;
@@ -664,6 +664,7 @@ static FrArgs fr_args(ewal_ctx *c, DevTables *tb, const uint8_t *d_buf, uint64_t
   a.pl = c->fpl.as<uint32_t>();
   a.ucb = c->fucb.as<uint32_t>();
   a.trec = c->ftrec.as<FrTile>();
+  a.tcnt = c->ftcnt.as<uint32_t>();
   a.ents = ents;
   a.ecap = ecap;
   a.mlist = c->mlist.as<uint64_t>();
@@ -1327,14 +1328,13 @@ static int frames_batch(ewal_ctx *c, DevTables *tb, const uint8_t *d_buf, uint64
     EW_CHECK(c->mlist.ensure((size_t)mcap * 8));
     if (pass) if (int rc = reset_small(c)) return rc;
     FrArgs a = fr_args(c, tb, d_buf, B, nunits, ntiles, 0, c->bents.as<ewal_entry>(), ecap, mcap);
-    EW_CHECK(hipMemsetAsync(c->fnfp.p, 0, (size_t)ns * 8, c->stream));
-    const unsigned ngrid = (unsigned)std::min<uint64_t>(grid_for(nunits, 256), (uint64_t)std::max(1, c->num_cu) * 8);
+    const unsigned ngrid = (unsigned)std::min<uint64_t>(ns, (uint64_t)std::max(1, c->num_cu) * 4);
     hipLaunchKernelGGL(k_shard_nfp, dim3(ngrid), dim3(256), 0, c->stream, a.hmask, nunits, sg.soff, ns,
                        c->fnfp.as<unsigned long long>());
     hipLaunchKernelGGL(k_shard_rbase, dim3(1), dim3(1024), 0, c->stream, (const unsigned long long *)c->fnfp.p, ns,
                        ecap, sg.rbase, sg.sp, ds);
     fr_launch<true>(c, tsh, ntiles, a, sg, nullptr, nullptr);
-    hipLaunchKernelGGL(k_tile_scan, dim3(1), dim3(1024), 0, c->stream, (const FrTile *)a.trec, ntiles, sg.tcb,
+    hipLaunchKernelGGL(k_tile_scan, dim3(1), dim3(1024), 0, c->stream, (const uint32_t *)a.tcnt, ntiles, sg.tcb,
                        (const Small *)ds);
     hipLaunchKernelGGL(k_meta_batch_fr, dim3(64), dim3(256), 0, c->stream, a, sg);
     fr_launch_result_batch(c, tsh, a, sg);
@@ -1821,7 +1821,6 @@ int ewal_ctx_create(int device, ewal_ctx **out) {
 #ifdef EW_ABLATION_HOOKS   // timing experiments only (tools/): results are wrong under ablation.  The product
                            // build reads no environment variable: its path is set by ewal_ctx_set_options only.
   if (const char *e = std::getenv("EWAL_STREAM_ABLATE")) c->ablate = std::atoi(e);
-  if (const char *e = std::getenv("EWAL_FC_ABLATE")) c->fc_ablate = (uint32_t)std::atoi(e);
   if (const char *e = std::getenv("EWAL_FRAME_WG")) c->frame_wg = std::max(1, std::min(16, std::atoi(e)));
 #endif
   EW_CHECK(hipEventCreate(&c->ev0));
@@ -2624,6 +2623,10 @@ int ecommit_batch_device(ewal_ctx *c, uint64_t G, const uint64_t *match, const u
 // tools/ timing builds only: the last k_frames launch's per-wave phase cycles
 extern "C" int ewal_dbg_fr_timing(unsigned long long *out, int n) {
   if (hipMemcpyFromSymbol(out, HIP_SYMBOL(fr_tdbg), (size_t)n * 8) != hipSuccess) return EWAL_E_HIP;
+  return 0;
+}
+extern "C" int ewal_dbg_fr_seam_timing(unsigned long long *out, int n) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(fr_sdbg), (size_t)n * 8) != hipSuccess) return EWAL_E_HIP;
   return 0;
 }
 #endif

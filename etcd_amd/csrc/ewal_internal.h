@@ -116,15 +116,16 @@ struct SnapDesc {
   int32_t resid;           // 1: raftpb.Snapshot needs k_snap_resid, 2: envelope Data split (gather first)
 };
 
-// The fused frame + check pass's reductions (k_fc).  Zero means none, so
-// k_stream's zeroing of Small initialises them.
+// The frame pass's single-WAL verdict words (k_frames / k_frames_seam).  Zero
+// means none, so k_stream's zeroing of Small initialises them.
 struct FcAgg {
   unsigned long long fail_inv;    // ~((frame << 8) | status) of the first failing frame (max)
   unsigned long long meta_inv;    // ~frame of the first non-empty metadata frame (max)
   uint32_t last_entry1;           // 1 + the last entry frame (max)
   uint32_t last_state1;           // 1 + the last state frame (max)
-  uint32_t rare;                  // a frame k_fc leaves to the general path (bit 0: declined
-                                  // encoding, 1: index rewind, 2: ents capacity)
+  uint32_t rare;                  // what the frame pass leaves to the general path or a rerun (frame_kernels.hip:
+                                  // 1 declined encoding, 2 index rewind, 4 ents capacity, 8 metadata list, 16 / 32
+                                  // far records, 64 rewind slot list, 128 a whole frame after the chain's end)
   uint32_t last_chained;          // the running CRC after the last frame
 };
 
@@ -158,7 +159,7 @@ struct Small {
   uint32_t segbad;                // k_shard_start: a shard does not start on a frame of the chain
   uint32_t spec_n;                // k_spec_gate: frames when k_frame's speculation holds, else 0
   uint32_t nunrec;                // k_check: entry ops carrying XXX_unrecognized (listed in ulist)
-  uint32_t fc_done;               // k_fc_seam workgroups done (the last one gathers the result)
+  uint32_t fc_done;               // k_frames_seam workgroups done (the last one gathers the result)
   FcAgg fc;
   // the side arena of split byte fields (Go's append over repeated
   // Record.Data / Entry.Data segments, record.pb.go:112, raft.pb.go:254)

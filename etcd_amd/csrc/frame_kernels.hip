@@ -38,6 +38,9 @@
 // (single WAL) or ShardPos.bad (batch), and the host runs the general path
 // over the same stream pass (ewal_api.hip); nothing is guessed.
 
+#ifndef FR_HORNER_NIB
+#define FR_HORNER_NIB 1    // phase A's Horner steps through the S_256 nibble tables (no bank conflicts)
+#endif
 #ifndef FR_THREADS
 #define FR_THREADS 768
 #endif
@@ -93,6 +96,7 @@ struct FrArgs {
   uint32_t *pl;                    // per unit: P at its start, relative to its tile's start
   uint32_t *ucb;                   // per unit: candidates of its tile before it
   FrTile *trec;
+  uint32_t *tcnt;                  // per tile: its frames (FrTile.count, packed for the scans)
   ewal_entry *ents;
   uint64_t ecap;                   // single WAL: ents capacity
   uint64_t *mlist;                 // positions of metadata frames
@@ -296,7 +300,7 @@ __device__ uint64_t fr_ordinal(const FrArgs &a, uint32_t tu, uint64_t x, const u
   const uint64_t u = x >> 12;
   if (u >= a.nunits) {
     unsigned long long s = 0;
-    for (uint32_t t = (uint32_t)lane; t < a.ntiles; t += 64) s += a.trec[t].count;
+    for (uint32_t t = (uint32_t)lane; t < a.ntiles; t += 64) s += a.tcnt[t];
     for (int o = 32; o; o >>= 1) s += (unsigned long long)__shfl_xor((long long)s, o);
     return s;
   }
@@ -305,7 +309,7 @@ __device__ uint64_t fr_ordinal(const FrArgs &a, uint32_t tu, uint64_t x, const u
   if (tcb) {
     before = tcb[t];
   } else {
-    for (uint32_t i = (uint32_t)lane; i < t; i += 64) before += a.trec[i].count;
+    for (uint32_t i = (uint32_t)lane; i < t; i += 64) before += a.tcnt[i];
     for (int o = 32; o; o >>= 1) before += (unsigned long long)__shfl_xor((long long)before, o);
   }
   return before + a.ucb[u] + fr_incount(a.buf, a.B, a.hmask, u, x);
@@ -330,6 +334,7 @@ struct FrCarry {
 #ifdef FR_TIMING
 // tools/ timing builds only: per wave, the cycles of each phase of k_frames
 __device__ unsigned long long fr_tdbg[8192 * 8];
+__device__ unsigned long long fr_sdbg[1024 * 4];   // k_frames_seam: per block, its loop and fr_result cycles
 #define FR_T(i) do { const unsigned long long t_ = clock64(); tacc[i] += t_ - tlast; tlast = t_; } while (0)
 #else
 #define FR_T(i) do {} while (0)
@@ -402,7 +407,11 @@ __global__ __launch_bounds__(FR_THREADS, 1) void k_frames(FrArgs a, FrSeg sg) {
         for (int j = 0; j < UPL; ++j) {
           const uint4 &g = vq[j][k >> 2];
           const uint32_t d = (k & 3) == 0 ? g.x : (k & 3) == 1 ? g.y : (k & 3) == 2 ? g.z : g.w;
+#if FR_HORNER_NIB
+          x[j] = nib_apply(s_nib + EW_VLOG * 128, x[j]) ^ d;   // S_256, conflict-free nibble lookups
+#else
           x[j] = tab_apply(s_svp, x[j]) ^ d;
+#endif
         }
     }
 #pragma unroll
@@ -669,7 +678,7 @@ __global__ __launch_bounds__(FR_THREADS, 1) void k_frames(FrArgs a, FrSeg sg) {
             if (seed != 0 && d.crc != seed) st = EWAL_ERR_WAL_CRC;
           } else {
             uint32_t computed = seed;
-            if (d.dlen) {
+            if (d.dlen && !(EW_FR_ABL & 4)) {
               uint32_t xs = seed ^ 0xffffffffu ^ Pfd;
               uint64_t m = d.dlen;
               for (int lvl = 0; m; ++lvl, m >>= 1)
@@ -870,6 +879,7 @@ __global__ __launch_bounds__(FR_THREADS, 1) void k_frames(FrArgs a, FrSeg sg) {
     if (lane == 0) {
       FrTile *T = a.trec + t;
       T->count = nfr;
+      a.tcnt[t] = nfr;
       T->agg = agg;
       if (nfr) {   // the last frame: the carried one
         T->pz = cy.p;
@@ -912,32 +922,40 @@ __global__ __launch_bounds__(FR_THREADS, 1) void k_frames(FrArgs a, FrSeg sg) {
 // ---- seam pass --------------------------------------------------------------
 // decoder.decode's check + ReadAll's crc-record rule, P(data end) given;
 // defer: frame 0 of a range split inside a file (its CRC check is the caller's)
-__device__ __forceinline__ int fr_check(const uint32_t *g_shift, int32_t type, uint32_t crc, uint32_t seed, uint32_t pfd,
-                                        uint32_t pe, uint64_t dlen, bool defer) {
+// S_n from the seam pass's LDS nibble tables (S_{2^0} .. S_{2^23}), the
+// global byte tables above them
+#define SEAM_NIB 24
+__device__ __forceinline__ uint32_t seam_shift(const uint32_t *s_n, const uint32_t *g_shift, uint64_t n, uint32_t x) {
+  for (int m = 0; n; ++m, n >>= 1)
+    if (n & 1) x = m < SEAM_NIB ? nib_apply(s_n + m * 128, x) : gshift_pow2(g_shift, m, x);
+  return x;
+}
+__device__ __forceinline__ int fr_check(const uint32_t *s_n, const uint32_t *g_shift, int32_t type, uint32_t crc,
+                                        uint32_t seed, uint32_t pfd, uint32_t pe, uint64_t dlen, bool defer) {
   if (type == 4) return (seed != 0 && crc != seed) ? EWAL_ERR_WAL_CRC : 0;
   uint32_t computed = seed;
-  if (dlen) computed = gshift_n(g_shift, dlen, seed ^ 0xffffffffu ^ pfd) ^ pe ^ 0xffffffffu;
+  if (dlen) computed = seam_shift(s_n, g_shift, dlen, seed ^ 0xffffffffu ^ pfd) ^ pe ^ 0xffffffffu;
   if (computed != crc && !defer) return EWAL_ERR_RECORD_CRC;
   return (type != 1 && type != 2 && type != 3) ? EWAL_ERR_UNEXPECTED_TYPE : 0;
 }
 
 // lin[ts_a, ts_b): the aggregates of tiles a .. b-1 (Horner, S_{tile bytes})
-__device__ uint32_t fr_span_lin(const FrTile *__restrict__ trec, uint32_t a, uint32_t b, const uint32_t *g_shift,
+__device__ uint32_t fr_span_lin(const FrTile *__restrict__ trec, uint32_t a, uint32_t b, const uint32_t *s_n,
                                 int tlog) {
   uint32_t acc = 0;
-  for (uint32_t i = a; i < b; ++i) acc = gshift_pow2(g_shift, tlog, acc) ^ trec[i].agg;
+  for (uint32_t i = a; i < b; ++i) acc = nib_apply(s_n + tlog * 128, acc) ^ trec[i].agg;
   return acc;
 }
 // P(e) in tile ta's reference for a record of tile ta whose Data ends at e
 // (ts_ta <= e <= B): S_{e - ts_b}(lin[ts_ta, ts_b)) ^ Pl_b(e), b = e's tile
-__device__ uint32_t fr_pe_far(const FrArgs &a, uint32_t ta, uint64_t e, uint32_t tu, int tlog) {
+__device__ uint32_t fr_pe_far(const FrArgs &a, const uint32_t *s_n, uint32_t ta, uint64_t e, uint32_t tu, int tlog) {
   uint64_t ue = e >> 12;
   if (ue >= a.nunits) ue = a.nunits - 1;
   const uint32_t tb = (uint32_t)(ue / tu);
   const uint64_t tsb = (uint64_t)tb * tu * EW_WAVE_BYTES;
   const uint32_t ple = prefix_at_pw(e, a.pl[ue], a.v, a.buf, a.g_slice, a.g_shift + EW_VLOG * 1024);
   if (tb <= ta) return ple;
-  return gshift_n(a.g_shift, e - tsb, fr_span_lin(a.trec, ta, tb, a.g_shift, tlog)) ^ ple;
+  return seam_shift(s_n, a.g_shift, e - tsb, fr_span_lin(a.trec, ta, tb, s_n, tlog)) ^ ple;
 }
 
 // decoder.decode's terminal at q (no frame starts there) in a shard ending at
@@ -991,7 +1009,7 @@ __device__ void fr_result(const FrArgs &a, ResultDev *o, Small *h, uint4 (*s_w)[
     __syncthreads();
     unsigned long long part = 0;
 #pragma unroll 8
-    for (uint32_t i = tid; i < tx; i += blockDim.x) part += a.trec[i].count;
+    for (uint32_t i = tid; i < tx; i += blockDim.x) part += a.tcnt[i];
     for (int o = 32; o; o >>= 1) part += (unsigned long long)__shfl_xor((long long)part, o);
     if ((tid & 63) == 0 && part) atomicAdd(s_ord, part);
     if (u < a.nunits && tid < 64) {   // the tile's units before x's, and x's unit before x
@@ -1043,15 +1061,19 @@ __global__ __launch_bounds__(256) void k_frames_seam(FrArgs a, FrSeg sg, ResultD
   __shared__ uint4 s_w[SEG ? 1 : 256][6];
   __shared__ RecDesc s_d[SEG ? 1 : 6];
   __shared__ unsigned long long s_ord;
+  __shared__ uint32_t s_n[SEAM_NIB * 128];  // S_{2^m} nibble tables, m < 24
+  static_assert(TLOG < SEAM_NIB, "tile shifts from the LDS tables");
   Small *ds = a.ds;
   if (SEG && ds->fr_capfail) return;
-  if (!SEG) {
-    if (threadIdx.x == 0) {
-      s_red[0] = s_red[1] = ~0ull;
-      s_red[2] = s_red[3] = s_red[4] = s_red[5] = 0;
-    }
-    __syncthreads();
+#ifdef FR_TIMING
+  const unsigned long long t_seam0 = clock64();
+#endif
+  stage_lds<256>(s_n, SEAM_NIB * 128, [&](int i) { return nib_src(a.g_shift, i); });
+  if (!SEG && threadIdx.x == 0) {
+    s_red[0] = s_red[1] = ~0ull;
+    s_red[2] = s_red[3] = s_red[4] = s_red[5] = 0;
   }
+  __syncthreads();
   unsigned long long fail = ~0ull, meta = ~0ull, le = 0, ls = 0, lo = 0, nops = 0;
   auto badsh = [&](uint32_t s) { atomicOr(&sg.sp[s].bad, 1u); };
   auto key_at = [&](uint32_t s, uint64_t p, int st) {
@@ -1068,7 +1090,7 @@ __global__ __launch_bounds__(256) void k_frames_seam(FrArgs a, FrSeg sg, ResultD
     int64_t pv = (int64_t)t - 1;
     uint32_t sc = 0;
     bool far = false;
-    while (pv >= 0 && a.trec[pv].count == 0) {
+    while (pv >= 0 && a.tcnt[pv] == 0) {
       if (++sc > FR_SCAN) { far = true; break; }
       --pv;
     }
@@ -1099,7 +1121,7 @@ __global__ __launch_bounds__(256) void k_frames_seam(FrArgs a, FrSeg sg, ResultD
     }
     // ---- the first frame's check, its successor in the tile ----
     if ((T.flags & FRT_T0) && (T.flags & FRT_PE0) && !(T.flags & FRT_TORN0) && seeded0) {
-      const int st = fr_check(a.g_shift, T.type0, T.crc0, seed0, T.pfd0, T.pe0, T.dlen0, false);
+      const int st = fr_check(s_n, a.g_shift, T.type0, T.crc0, seed0, T.pfd0, T.pe0, T.dlen0, false);
       if (st) key_at(sh0, T.p0, st);
     }
     // ---- the last frame ----
@@ -1118,7 +1140,7 @@ __global__ __launch_bounds__(256) void k_frames_seam(FrArgs a, FrSeg sg, ResultD
     uint32_t nx = t + 1;
     sc = 0;
     bool farn = false;
-    while (nx < a.ntiles && a.trec[nx].count == 0) {
+    while (nx < a.ntiles && a.tcnt[nx] == 0) {
       if (++sc > FR_SCAN) { farn = true; break; }
       ++nx;
     }
@@ -1142,7 +1164,7 @@ __global__ __launch_bounds__(256) void k_frames_seam(FrArgs a, FrSeg sg, ResultD
       }
       if (np == e) {
         const uint64_t tsn = (uint64_t)nx * TB;
-        Pe = gshift_n(a.g_shift, e - tsn, fr_span_lin(a.trec, t, nx, a.g_shift, TLOG)) ^ a.trec[nx].pfo0;
+        Pe = seam_shift(s_n, a.g_shift, e - tsn, fr_span_lin(a.trec, t, nx, s_n, TLOG)) ^ a.trec[nx].pfo0;
         pe_ok = true;
       }
     } else {   // the stream's last frame
@@ -1158,10 +1180,10 @@ __global__ __launch_bounds__(256) void k_frames_seam(FrArgs a, FrSeg sg, ResultD
         else atomicMin(&sg.sp[shz].term, (T.sz << 8) | (uint32_t)tst);
       }
     }
-    if (!pe_ok && !farn && T.dlenz && e <= a.B) Pe = fr_pe_far(a, t, e, TU, TLOG);
+    if (!pe_ok && !farn && T.dlenz && e <= a.B) Pe = fr_pe_far(a, s_n, t, e, TU, TLOG);
     if (!tornz && !farn && seededz && (T.flags & FRT_OKZ)) {
       const bool defer = !SEG && T.pz == 0 && ds->defer_first;
-      const int st = fr_check(a.g_shift, T.typez, T.crcz, seedz, T.pfdz, Pe, T.dlenz, defer);
+      const int st = fr_check(s_n, a.g_shift, T.typez, T.crcz, seedz, T.pfdz, Pe, T.dlenz, defer);
       if (st) key_at(shz, T.pz, st);
     }
     // ---- the gap rule for the tile's first entry op (wal/wal.go:173) ----
@@ -1224,10 +1246,21 @@ __global__ __launch_bounds__(256) void k_frames_seam(FrArgs a, FrSeg sg, ResultD
     s_last = atomicAdd(&ds->fc_done, 1u) == gridDim.x - 1;
   }
   __syncthreads();
+#ifdef FR_TIMING
+  const unsigned long long t_loop = clock64();
+#endif
   if (s_last) {   // the last workgroup: every tile is in
     __threadfence();
     fr_result<TSH>(a, o, h, s_w, s_d, &s_ord);
   }
+#ifdef FR_TIMING
+  if (threadIdx.x == 0 && blockIdx.x < 1024) {
+    fr_sdbg[blockIdx.x * 4 + 0] = t_loop - t_seam0;
+    fr_sdbg[blockIdx.x * 4 + 1] = s_last ? clock64() - t_loop : 0ull;
+    fr_sdbg[blockIdx.x * 4 + 2] = t_seam0;
+    fr_sdbg[blockIdx.x * 4 + 3] = t_loop;
+  }
+#endif
 }
 
 // Rewind mode: every listed slot (claimed by more than one entry op) gets
@@ -1253,28 +1286,26 @@ __global__ __launch_bounds__(256) void k_ents_fix(const uint8_t *__restrict__ bu
 // ---- batch (ewal_readall_batch_device) ----------------------------------------
 // Per shard: the flagged pieces of the units overlapping it (an upper bound
 // of its entry ops / 4: an entry frame is >= 20 bytes, so at most 4 of them
-// start in one 64-B piece, and every frame start is a flagged piece), and its
-// reductions initialised.  Grid-strided over the units.
+// start in one 64-B piece, and every frame start is a flagged piece).
 __global__ __launch_bounds__(256) void k_shard_nfp(const ulonglong2 *__restrict__ hmask, uint32_t nunits,
                                                    const uint64_t *__restrict__ soff, uint32_t ns,
                                                    unsigned long long *__restrict__ nfp) {
-  const int lane = threadIdx.x & 63;
-  for (uint32_t u0 = (blockIdx.x * blockDim.x + threadIdx.x) & ~63u; u0 < nunits; u0 += gridDim.x * blockDim.x) {
-    const uint32_t u = u0 + (uint32_t)lane;
-    const bool in = u < nunits;
-    const uint64_t b = (uint64_t)u * EW_WAVE_BYTES;
-    const uint32_t c = in ? (uint32_t)__popcll(hmask[u].x) : 0u;
-    const uint32_t s0 = in ? pos_shard_in(soff, 0, ns, b) : 0u;
-    const uint32_t s1 = in ? pos_shard_in(soff, s0, ns, b + EW_WAVE_BYTES - 1) : 0u;
-    const uint32_t w0 = (uint32_t)__shfl((int)s0, 0);
-    const bool one = __ballot(in && (s0 != w0 || s1 != w0)) == 0ull;
-    if (one) {
-      uint32_t sum = c;
-      for (int o = 32; o; o >>= 1) sum += (uint32_t)__shfl_xor((int)sum, o);
-      if (lane == 0 && sum) atomicAdd(&nfp[w0], (unsigned long long)sum);
-    } else if (in && c) {
-      for (uint32_t s = s0; s <= s1; ++s) atomicAdd(&nfp[s], (unsigned long long)c);
+  // one workgroup per shard (grid-strided): its units' flagged pieces summed, no atomics
+  __shared__ unsigned long long s_sum[4];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  for (uint32_t s = blockIdx.x; s < ns; s += gridDim.x) {
+    const uint64_t b0 = soff[s], b1 = soff[s + 1];
+    unsigned long long c = 0;
+    if (b1 > b0) {
+      const uint32_t ua = (uint32_t)(b0 >> 12), ub = (uint32_t)min<uint64_t>((b1 - 1) >> 12, (uint64_t)nunits - 1);
+#pragma unroll 4
+      for (uint32_t u = ua + (uint32_t)tid; u <= ub; u += blockDim.x) c += (unsigned long long)__popcll(hmask[u].x);
     }
+    for (int o = 32; o; o >>= 1) c += (unsigned long long)__shfl_xor((long long)c, o);
+    if (lane == 0) s_sum[wv] = c;
+    __syncthreads();
+    if (tid == 0) nfp[s] = s_sum[0] + s_sum[1] + s_sum[2] + s_sum[3];
+    __syncthreads();
   }
 }
 // One workgroup: rbase[s] = 4 * (flagged pieces of the shards before s) --
@@ -1347,7 +1378,7 @@ __global__ void k_shard_reset(ShardPos *__restrict__ sp, const uint32_t *__restr
 }
 
 // One workgroup: tcb[t] = candidates of the tiles before t.
-__global__ __launch_bounds__(1024) void k_tile_scan(const FrTile *__restrict__ trec, uint32_t nt, uint32_t *__restrict__ tcb,
+__global__ __launch_bounds__(1024) void k_tile_scan(const uint32_t *__restrict__ tcnt, uint32_t nt, uint32_t *__restrict__ tcb,
                                                     const Small *ds) {
   __shared__ uint32_t s_w[16];
   __shared__ uint32_t s_carry;
@@ -1357,7 +1388,7 @@ __global__ __launch_bounds__(1024) void k_tile_scan(const FrTile *__restrict__ t
   __syncthreads();
   for (uint32_t c0 = 0; c0 < nt; c0 += 1024) {
     const uint32_t t = c0 + (uint32_t)tid;
-    const uint32_t x = t < nt ? trec[t].count : 0u;
+    const uint32_t x = t < nt ? tcnt[t] : 0u;
     const uint32_t inc = wave_incl_sum(x);
     if (lane == 63) s_w[wv] = inc;
     __syncthreads();

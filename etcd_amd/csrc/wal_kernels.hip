@@ -1326,11 +1326,16 @@ __device__ __forceinline__ void prefix_load_near(uint64_t x, uint64_t B, const u
   for (int q = 0; q < 9; ++q) in.dd[q] = (16u * q < in.n) ? dq[q] : make_uint4(0, 0, 0, 0);
   in.pw = pwave[w];
 }
+#ifndef EW_FR_ABL
+#define EW_FR_ABL 0   // timing-only ablations of the frame pass (tools/): 1 no Horner over v, 2 no prefix tail,
+                      // 4 no S_dlen in the checks; results are wrong
+#endif
 __device__ __forceinline__ uint32_t prefix_finish_near(const PrefixNear &in, const uint32_t *t16, const uint32_t *svp,
                                                        const uint32_t *inv) {
   uint32_t acc = in.pw;
+  if (EW_FR_ABL & 2) return acc ^ in.vv[0].x ^ in.dd[0].y;
 #pragma unroll
-  for (int q = 0; q < EW_VPU / 4; ++q) {
+  for (int q = 0; q < EW_VPU / 4 && !(EW_FR_ABL & 1); ++q) {
     if (4u * q + 0 < in.nk) acc = tab_apply(svp, acc) ^ in.vv[q].x;
     if (4u * q + 1 < in.nk) acc = tab_apply(svp, acc) ^ in.vv[q].y;
     if (4u * q + 2 < in.nk) acc = tab_apply(svp, acc) ^ in.vv[q].z;

@@ -246,10 +246,10 @@ def test_pointer_jumping_64mib(ctx):
 
 
 def test_entries_beyond_the_ternary_shift_span(ctx):
-    """Entries whose Data is 170-600 KB long: k_fc applies S_n for n below
-    3^11 = 177147 by ternary digits from LDS and the rest from the global
-    binary tables; every chained CRC and a corruption inside such an entry
-    must match the oracle (record.pb.go Data, pkg/crc chaining)."""
+    """Entries whose Data is 170-600 KB long: the frame pass applies S_n
+    from LDS nibble tables for n below 2^20 and from the global byte tables
+    above; every chained CRC and a corruption inside such an entry must
+    match the oracle (record.pb.go Data, pkg/crc chaining)."""
     rng = random.Random(11)
     e = O.WalEncoder(0)
     e.save_crc(0)

@@ -13,6 +13,7 @@ from etcd_amd import wal as W
 NAMES = ["stage", "A", "pieces", "decode", "checks", "ops", "reduce", "tile_end"]
 lib = L.lib
 lib.ewal_dbg_fr_timing.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
+lib.ewal_dbg_fr_seam_timing.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
 
 
 def one(label, size, lo, hi):
@@ -27,6 +28,14 @@ def one(label, size, lo, hi):
         assert rc == 0 and rs.flags & L.FLAG_FAST_PATH, (rc, rs.flags)
     t = (C.c_ulonglong * (8192 * 8))()
     lib.ewal_dbg_fr_timing(t, 8192 * 8)
+    sd = (C.c_ulonglong * (1024 * 4))()
+    lib.ewal_dbg_fr_seam_timing(sd, 1024 * 4)
+    blocks = [list(sd[b * 4:(b + 1) * 4]) for b in range(1024) if sd[b * 4 + 2]]
+    if blocks:
+        t0 = min(b[2] for b in blocks)
+        print("  seam: %d blocks, loop avg %.0f max %.0f cycles, last block ends loop at +%.0f, fr_result %.0f" %
+              (len(blocks), sum(b[0] for b in blocks) / len(blocks), max(b[0] for b in blocks),
+               max(b[3] for b in blocks) - t0, max(b[1] for b in blocks)))
     waves = [list(t[w * 8:(w + 1) * 8]) for w in range(8192) if any(t[w * 8:(w + 1) * 8])]
     tot = [sum(x) for x in waves]
     print("%s: %d frames, %.3f GiB, device %.3f ms (stream %.3f), %d waves" %
