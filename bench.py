@@ -151,7 +151,9 @@ def run_shards(a, dist, rank, world, local, cpu_seconds=None):
     shards are generated and copied to HBM 64 at a time (host memory stays
     at ~4 GiB per rank).  `torn5`: the same batch with the last frame of 5
     shards torn (a crash mid-write): the batch's own pass classifies their
-    terminal (wal/decoder.go:30-36), no shard is replayed alone."""
+    terminal (wal/decoder.go:30-36), no shard is replayed alone.  `rew1pct`:
+    1 % of the shards replaced by WALs after leader changes (index rewinds,
+    wal/wal.go:170-176), decided by the batch's rewind-mode pass."""
     nsh, smib = a.shards_per_gpu, a.shard_mib
     cpu_seconds = a.cpu_seconds if cpu_seconds is None else cpu_seconds
     first = rank * nsh
@@ -237,6 +239,48 @@ def run_shards(a, dist, rank, world, local, cpu_seconds=None):
              "note": "the same batch with the last frame of 5 shards torn: the batch's fused pass gives "
                      "their verdict (io.ErrUnexpectedEOF at the torn frame), no shard is replayed alone"}
     del tmem
+    # ---- rew1pct: 1 % of the shards after leader changes (index rewinds) ----
+    nrw = max(1, nsh // 100)
+    rws = sorted({(nsh * j) // nrw + 11 for j in range(nrw)} - {bad_shard - first})[:nrw]
+    rblobs, rli = {}, {}
+    for i in rws:
+        li = []
+        b, _ = W.synth_wal(target, 128, 4096, seed=700000 + first + i, rewind_per_mille=10, last_index=li)
+        rblobs[i], rli[i] = b, li[0]
+    rlens = [len(rblobs[i]) if i in rblobs else x for i, x in enumerate(lens)]
+    rmem = torch.empty(sum(rlens) + 64, dtype=torch.uint8, device=dev)
+    so, to = 0, 0
+    for i, (x, y) in enumerate(zip(lens, rlens)):
+        if i in rblobs:
+            rmem[to:to + y].copy_(torch.frombuffer(rblobs[i], dtype=torch.uint8))
+        else:
+            rmem[to:to + y].copy_(dmem[so:so + y])
+        so += x
+        to += y
+    del rblobs
+    rbuf = W.DeviceBuffer(ctx, C.c_void_p(rmem.data_ptr()), rmem.numel())
+    c_rlens = (C.c_uint64 * nsh)(*rlens)
+    torch.cuda.synchronize()
+
+    def rstep():
+        rc = L.lib.ewal_readall_batch_device(ctx.handle, rbuf.ptr, nsh, c_rlens, c_ris, c_out)
+        assert rc == 0, rc
+
+    for _ in range(max(a.warmup, 1)):
+        rstep()
+    for i, x in enumerate(c_out):
+        assert not x.flags & L.FLAG_SHARD_FALLBACK, (i, x.status, x.flags)
+        if i in rli:
+            assert x.status == L.OK and x.n_ents == rli[i], (i, x.status, x.n_ents, rli[i])
+        else:
+            want = (L.ERR_RECORD_CRC, 1000) if first + i == bad_shard else (L.OK, -1)
+            assert (x.status, x.fail_record) == want, (i, x.status)
+    rwms = timed(dist, a.steps, rstep) / a.steps * 1e3
+    rew1pct = {"ms_per_step": round(rwms, 4), "vs_clean": round(rwms / ms, 4), "rewinding_shards": rws,
+               "note": "the same batch with %d shards (1 %%) replaced by WALs after leader changes (1 %% of their "
+                       "entries rewrite the last 1-8 indexes, wal/wal.go:170-176): the batch's rewind-mode pass "
+                       "over those shards' tiles, no shard is replayed alone" % len(rws)}
+    del rmem
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         from oracle import oracle as O   # baseline only
@@ -280,6 +324,7 @@ def run_shards(a, dist, rank, world, local, cpu_seconds=None):
                      "step_frac": round(nb / (ms / 1e3) / 1e9 / HBM_PEAK_GBPS, 4)},
         "pipeline_device_ms": round(r0.device_ms, 4),
         "torn5": torn5,
+        "rew1pct": rew1pct,
         "cpu_baseline": cpu,
         "gen_seconds": round(gen_s, 2),
     }
@@ -628,9 +673,12 @@ def run_restart(a, dist, rank, world, local):
 def run_commit(a, dist, rank, world, local, cpu_seconds=None):
     """configs[4]: batched raft.maybeCommit (raft/raft.go:248-258 +
     raft/log.go:148-154) over 1M raft groups per GPU, 5 or 7 voters (seed 6),
-    SoA matchIndex, a 16-entry log-term window per group; one
-    ecommit_batch_device launch per step (committed reset from a copy
-    first, so every step does the same work)."""
+    a 16-entry log-term window per group.  The line times
+    ecommit_batch_rec_device over 192-B group records (the voters' Match,
+    committed, Term, log bounds and the log's last 13 terms: coalesced
+    loads, no term gather for quorum indexes in that tail); `soa` times
+    ecommit_batch_device over the SoA arrays (committed reset from a copy
+    each step, so every step does the same work)."""
     import numpy as np
     G = 1 << 20
     rng = np.random.default_rng(6 + rank)
@@ -681,6 +729,33 @@ def run_commit(a, dist, rank, world, local, cpu_seconds=None):
     # algorithmic bytes: nvoters 1 + n match words + term, committed (r+w), log_offset, 2 log_ptr, the term gather,
     # changed + status
     abytes = int(G + 8 * int(nv.astype(np.int64).sum()) + G * (8 + 16 + 8 + 16 + 8 + 2))
+    # ---- the same groups as 192-B records (ecommit_batch_rec_device) ----
+    from etcd_amd import raftcommit as RC
+    d_rec = T(RC.pack_groups(match, nv, committed0, term, log_offset, log_ptr, log_terms).reshape(-1))
+    d_co = torch.zeros(G, dtype=torch.int64, device=dev)
+    d_ch2 = torch.zeros(G, dtype=torch.uint8, device=dev)
+    d_st2 = torch.zeros(G, dtype=torch.uint8, device=dev)
+    P = lambda t: C.c_void_p(t.data_ptr())   # noqa: E731
+    rkms = []
+
+    def rstep(logs=True):
+        rc = L.lib.ecommit_batch_rec_device(ctx.handle, G, P(d_rec), P(d_ptr) if logs else None,
+                                            P(d_lt) if logs else None, P(d_co), P(d_ch2), P(d_st2), C.byref(dms))
+        assert rc == 0, rc
+        rkms.append(dms.value)
+        if dist is not None:
+            shard.combine_commit(dist, d_ch2.sum(dtype=torch.int64), d_co.min(), d_co.max(), out=summary)
+
+    rstep(logs=False)   # (untimed) the groups whose quorum term lies before the tail window: they read the log
+    n_gather = int((d_st2 == L.UNSUPPORTED_ENCODING).sum())
+    for _ in range(max(a.warmup, 1)):
+        rstep()
+    assert (d_co.cpu() == d_c.cpu()).all() and (d_ch2.cpu() == d_ch.cpu()).all() and not d_st2.cpu().any()
+    rkms.clear()
+    rms = timed(dist, a.steps, rstep) / a.steps * 1e3
+    rk_avg = sum(rkms) / len(rkms)
+    # record 192 B + committed_out 8 + changed/status 2 per group; log_ptr + the term gather for n_gather groups
+    rbytes = int(G * (192 + 8 + 2) + n_gather * 16)
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         from oracle import oracle as O   # baseline only
@@ -709,20 +784,30 @@ def run_commit(a, dist, rank, world, local, cpu_seconds=None):
                                     "(orf_maybe_commit_batch), %d passes, %.1f s" % (nth, it2, cs2)}})
     out = {
             "metric": "maybeCommit groups/s (configs[4]); WAL verify GB/s is the headline metric",
-            "value": round(world * G / (ms / 1e3), 1), "unit": "groups/s", "n_gpus": world, "steps": a.steps,
-            "warmup": a.warmup, "ms_per_step": round(ms, 4), "higher_is_better": True, "scaling": "weak",
+            "value": round(world * G / (rms / 1e3), 1), "unit": "groups/s", "n_gpus": world, "steps": a.steps,
+            "warmup": a.warmup, "ms_per_step": round(rms, 4), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "u64", "data": "synthetic",
             "config": {"workload": "configs[4]: maybeCommit over %d raft groups per GPU, 5/7 voters (50/50), 16-entry "
-                                   "log-term window; %d groups advance commit" % (G, nchanged),
+                                   "log-term window; %d groups advance commit; one ecommit_batch_rec_device per step "
+                                   "(192-B group records, the log's last 13 terms inside; %d groups read their "
+                                   "quorum term from the log arrays)" % (G, nchanged, n_gather),
                        "groups_per_gpu": G, "parallelism": "dp%d (group ranges)" % world},
-            "roofline": {"bound": "hbm", "achieved": round(abytes / (k_avg / 1e3) / 1e9, 2), "peak": HBM_PEAK_GBPS,
-                         "unit": "GB/s", "frac": round(abytes / (k_avg / 1e3) / 1e9 / HBM_PEAK_GBPS, 4),
-                         "traffic": load_traffic("k_commit"), "kernel": "k_commit", "kernel_ms": round(k_avg, 4),
-                         "algorithmic_bytes_per_launch": abytes,
-                         "traffic_source": "profiles/k_commit_pmc.json: the committed rocprofv3 PMC pass of this "
-                                           "config (FETCH_SIZE x2 + WRITE_SIZE per launch), not measured in this run; "
-                                           "the 8-B term gather costs a whole 128-B line per group "
-                                           "(profiles/r03/ab_commit_gather.txt)"},
+            "roofline": {"bound": "hbm", "achieved": round(rbytes / (rk_avg / 1e3) / 1e9, 2), "peak": HBM_PEAK_GBPS,
+                         "unit": "GB/s", "frac": round(rbytes / (rk_avg / 1e3) / 1e9 / HBM_PEAK_GBPS, 4),
+                         "traffic": load_traffic("k_commit_rec"), "kernel": "k_commit_rec",
+                         "kernel_ms": round(rk_avg, 4), "algorithmic_bytes_per_launch": rbytes,
+                         "traffic_source": "profiles/k_commit_rec_pmc.json: the committed rocprofv3 PMC pass of this "
+                                           "config (FETCH_SIZE x2 + WRITE_SIZE per launch), not measured in this run"},
+            "soa": {"note": "the same groups through ecommit_batch_device (SoA match[v*G+g], log_terms gather; "
+                            "committed reset from a copy each step)", "ms_per_step": round(ms, 4),
+                    "value": round(world * G / (ms / 1e3), 1),
+                    "roofline": {"bound": "hbm", "achieved": round(abytes / (k_avg / 1e3) / 1e9, 2),
+                                 "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                                 "frac": round(abytes / (k_avg / 1e3) / 1e9 / HBM_PEAK_GBPS, 4),
+                                 "traffic": load_traffic("k_commit"), "kernel": "k_commit",
+                                 "kernel_ms": round(k_avg, 4), "algorithmic_bytes_per_launch": abytes,
+                                 "traffic_source": "profiles/k_commit_pmc.json (the 8-B term gather costs a whole "
+                                                   "128-B line per group)"}},
             "cpu_baseline": cpu}
     ctx.close()
     return out

@@ -226,6 +226,7 @@ _SIGS = {
     "esnap_copy_snapshot": (C.c_int, [vp, C.c_uint32, C.POINTER(SnapshotDesc)]),
     "esnap_load_dir": (C.c_int, [vp, C.c_char_p, C.c_uint32, C.POINTER(SnapshotDesc), C.POINTER(C.c_char_p)]),
     "ecommit_batch_device": (C.c_int, [vp, C.c_uint64, vp, vp, vp, vp, vp, vp, vp, vp, vp, C.POINTER(C.c_double)]),
+    "ecommit_batch_rec_device": (C.c_int, [vp, C.c_uint64, vp, vp, vp, vp, vp, vp, C.POINTER(C.c_double)]),
 }
 for _name, (_res, _args) in _SIGS.items():
     if os.environ.get("EWAL_LIB_PATH") and not hasattr(lib, _name):

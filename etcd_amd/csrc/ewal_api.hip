@@ -170,6 +170,7 @@ struct ewal_ctx {
   uint64_t pfcap = 0;      // pf = [P at data starts | P at frame starts], pfcap each
   bool last_ok = false;
   bool scan_valid = false;   // cpos / pwave / cbase hold the current stream pass's candidates and prefixes
+  bool fr_rew_hint = false;  // the last single ReadAll needed the frame pass's rewind mode
   uint64_t last_q = 0;       // where the last ReadAll's frame chain ended (decoder.decode's terminal)
 };
 
@@ -695,7 +696,11 @@ static int frames_pass(ewal_ctx *c, DevTables *tb, const uint8_t *d_buf, uint64_
   const uint32_t tu = 1u << tsh, ntiles = (nunits + tu - 1) / tu;
   if (int rc = fr_ensure(c, nunits, ntiles)) return rc;
   uint32_t mcap = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(c->mlist.cap / 8, 4096), 0xffffffffull);
-  bool rew = false;   // rewind mode: entry indexes go back (wal/wal.go:173 truncates ents)
+  // rewind mode: entry indexes go back (wal/wal.go:173 truncates ents).  A
+  // ctx whose last ReadAll met rewinds starts in it (a restarted member
+  // replays the same WAL again and again); a call that then meets none
+  // clears the hint.
+  bool rew = c->fr_rew_hint;
   uint32_t clcap = 0;
   for (int pass = 0; pass < 4; ++pass) {
     EW_CHECK(c->ents.ensure((size_t)ecap * sizeof(ewal_entry)));
@@ -730,6 +735,7 @@ static int frames_pass(ewal_ctx *c, DevTables *tb, const uint8_t *d_buf, uint64_
     if (hs->errflag) return EWAL_E_TIMEOUT;
     if (hs->spec_n) {
       *done = true;
+      c->fr_rew_hint = rew && hs->fr_rews;
       return 0;
     }
     // declined for capacity or rewinds only: room for what it asked / the rewind mode, once more
@@ -2606,6 +2612,28 @@ int ecommit_batch_device(ewal_ctx *c, uint64_t G, const uint64_t *match, const u
     hipLaunchKernelGGL(k_commit, dim3((unsigned)((G + 256 * EW_COMMIT_ILP - 1) / (256 * EW_COMMIT_ILP))), dim3(256), 0,
                        c->stream, G, match, nvoters, term,
                        committed, log_offset, log_ptr, log_terms, changed, status);
+  EW_CHECK(hipGetLastError());
+  EW_CHECK(hipEventRecord(c->ev1, c->stream));
+  EW_CHECK(hipEventSynchronize(c->ev1));
+  if (device_ms) {
+    float ms = 0;
+    EW_CHECK(hipEventElapsedTime(&ms, c->ev0, c->ev1));
+    *device_ms = ms;
+  }
+  return EWAL_OK;
+}
+
+static_assert(sizeof(ecommit_group) == 192, "a group record is 12 16-B loads");
+int ecommit_batch_rec_device(ewal_ctx *c, uint64_t G, const ecommit_group *groups, const uint64_t *log_ptr,
+                             const uint64_t *log_terms, uint64_t *committed_out, uint8_t *changed, uint8_t *status,
+                             double *device_ms) {
+  if (!c || (G && (!groups || !committed_out || !changed || !status))) return EWAL_E_INVAL;
+  if (((uintptr_t)groups & 15) != 0) return EWAL_E_INVAL;
+  EW_CHECK(hipSetDevice(c->device));
+  EW_CHECK(hipEventRecord(c->ev0, c->stream));
+  if (G)
+    hipLaunchKernelGGL(k_commit_rec, dim3((unsigned)((G + 255) / 256)), dim3(256), 0, c->stream, G, groups, log_ptr,
+                       log_terms, committed_out, changed, status);
   EW_CHECK(hipGetLastError());
   EW_CHECK(hipEventRecord(c->ev1, c->stream));
   EW_CHECK(hipEventSynchronize(c->ev1));

@@ -173,6 +173,8 @@ struct Small {
   unsigned long long fr_need;     // single WAL: ents the frame pass needed; batch: the regions' total
   uint32_t fr_ncl;                // rewind mode: ents slots claimed more than once (listed for k_ents_fix)
   uint32_t fr_tick;               // k_frames: tiles handed out past the first round (dynamic schedule)
+  uint32_t fr_rews;               // single WAL in rewind mode: an index rewind was met (the next call starts so)
+  uint32_t fr_pad2;
 };
 
 // A returned Entry (ent = its index in ents) or the HardState (ent = -1)

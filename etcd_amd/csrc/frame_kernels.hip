@@ -369,7 +369,7 @@ __global__ __launch_bounds__(FR_THREADS, 1) void k_frames(FrArgs a, FrSeg sg) {
   uint32_t *ucnt = s_ucnt[wv];
   uint32_t *spw = s_pw[wv];
   uint32_t *w = s_win + tid;
-  uint32_t rare = 0, irr = 0;
+  uint32_t rare = 0, irr = 0, rews = 0;   // rews: rewind mode met an index rewind
   unsigned long long need_ecap = 0;
   const uint32_t nt_run = a.tlist ? a.ntl : a.ntiles;
   // every wave's first tile is its id; the rest are handed out by a counter
@@ -739,7 +739,10 @@ __global__ __launch_bounds__(FR_THREADS, 1) void k_frames(FrArgs a, FrSeg sg) {
           bool gap;
           if (has) {
             // an index rewind: the rewind-mode pass (single WAL), the shard replayed alone (batch)
-            if (k <= kq && !a.rew) { if (SEG) sg.sp[sh].rew = 1u; else rare |= 2u; }
+            if (k <= kq) {
+              if (!a.rew) { if (SEG) sg.sp[sh].rew = 1u; else rare |= 2u; }
+              else rews = 1u;
+            }
             gap = k > kq && k - kq > 1;
           } else {
             gap = k > 0;
@@ -914,6 +917,7 @@ __global__ __launch_bounds__(FR_THREADS, 1) void k_frames(FrArgs a, FrSeg sg) {
   for (int o = 32; o; o >>= 1) rr |= (uint32_t)__shfl_xor((int)rr, o);
   if (lane == 0 && rr) atomicOr(&ds->fc.rare, rr);
   if (__ballot(irr) && lane == 0) atomicOr(&ds->irregular, 1u);
+  if (!SEG && __ballot(rews) && lane == 0) atomicOr(&ds->fr_rews, 1u);
   for (int o = 32; o; o >>= 1)
     need_ecap = max(need_ecap, (unsigned long long)__shfl_xor((long long)need_ecap, o));
   if (lane == 0 && need_ecap) atomicMax(&ds->fr_need, need_ecap);
@@ -999,14 +1003,20 @@ __device__ void fr_result(const FrArgs &a, ResultDev *o, Small *h, uint4 (*s_w)[
       if (!eq) atomicMax(&ds->fc.fail_inv, ~((p << 8) | EWAL_ERR_METADATA_CONFLICT));
     }
   }
+  if (tid == 0) *s_ord = 0;
   __threadfence();
   __syncthreads();
   const unsigned long long key = ds->fc.fail_inv ? ~ds->fc.fail_inv : ~0ull;
+  const uint64_t le = ds->fr.le, ls = ds->fr.ls, lo = ds->fr.lo;
+  const long long want[5] = {key != ~0ull ? (long long)(key >> 8) : -1, le ? (long long)(le - 1) : -1,
+                             ls ? (long long)(ls - 1) : -1, fm != ~0ull ? (long long)fm : -1,
+                             lo ? (long long)(lo - 1) : -1};
+  // the frames the result names (wave 1) while the failing frame's ordinal is summed
+  if (tid >= 64 && tid < 69 && want[tid - 64] >= 0)
+    s_d[tid - 64] = fc_frame_fields(a.buf, a.B, (uint64_t)want[tid - 64], s_w[tid]);
   if (key != ~0ull) {   // the failing frame's ordinal: the tiles before it summed by the whole workgroup
     const uint64_t x = key >> 8, u = x >> 12;
     const uint32_t tx = u < a.nunits ? (uint32_t)(u >> TSH) : a.ntiles;
-    if (tid == 0) *s_ord = 0;
-    __syncthreads();
     unsigned long long part = 0;
 #pragma unroll 8
     for (uint32_t i = tid; i < tx; i += blockDim.x) part += a.tcnt[i];
@@ -1017,11 +1027,6 @@ __device__ void fr_result(const FrArgs &a, ResultDev *o, Small *h, uint4 (*s_w)[
       if (tid == 0) atomicAdd(s_ord, in);
     }
   }
-  const uint64_t le = ds->fr.le, ls = ds->fr.ls, lo = ds->fr.lo;
-  const long long want[5] = {key != ~0ull ? (long long)(key >> 8) : -1, le ? (long long)(le - 1) : -1,
-                             ls ? (long long)(ls - 1) : -1, fm != ~0ull ? (long long)fm : -1,
-                             lo ? (long long)(lo - 1) : -1};
-  if (tid < 5 && want[tid] >= 0) s_d[tid] = fc_frame_fields(a.buf, a.B, (uint64_t)want[tid], s_w[tid]);
   __syncthreads();
   if (tid != 0) return;
   ResultDev res;
@@ -1085,14 +1090,25 @@ __global__ __launch_bounds__(256) void k_frames_seam(FrArgs a, FrSeg sg, ResultD
   for (uint32_t ti = blockIdx.x * blockDim.x + threadIdx.x; ti < nt_run; ti += gridDim.x * blockDim.x) {
     const uint32_t t = a.tlist ? a.tlist[ti] : ti;
     const FrTile T = a.trec[t];
+    // the neighbours' fields loaded together with T: the usual case (both
+    // hold frames, the previous one ops) needs no further round trip
+    const bool hp = t > 0, hn = t + 1 < a.ntiles;
+    const uint32_t cp = hp ? a.tcnt[t - 1] : 0u, cn = hn ? a.tcnt[t + 1] : 0u;
+    const FrTile *TP = a.trec + (hp ? t - 1 : t), *TN = a.trec + (hn ? t + 1 : t);
+    const uint64_t P_pz = TP->pz, P_sz = TP->sz, P_lastop = TP->lastop_p, P_lastidx = TP->last_index;
+    const uint32_t P_crcz = TP->crcz, P_nops = TP->nops;
+    const uint64_t N_p0 = TN->p0;
+    const uint32_t N_pfo0 = TN->pfo0, T_agg = T.agg;
     if (!T.count) continue;
     // ---- the previous frame: the last of the nearest earlier tile with frames ----
     int64_t pv = (int64_t)t - 1;
     uint32_t sc = 0;
     bool far = false;
-    while (pv >= 0 && a.tcnt[pv] == 0) {
-      if (++sc > FR_SCAN) { far = true; break; }
-      --pv;
+    if (!(hp && cp)) {
+      while (pv >= 0 && a.tcnt[pv] == 0) {
+        if (++sc > FR_SCAN) { far = true; break; }
+        --pv;
+      }
     }
     const uint32_t sh0 = SEG ? pos_shard_in(sg.soff, 0, sg.ns, T.p0) : 0u;
     const bool sfirst0 = T.p0 == (SEG ? sg.soff[sh0] : 0ull);
@@ -1104,8 +1120,9 @@ __global__ __launch_bounds__(256) void k_frames_seam(FrArgs a, FrSeg sg, ResultD
       if (!SEG) ds->pos0 = T.p0;   // the stream's first candidate: ReadAll's first frame must be it (at 0)
       else if (!sfirst0) badsh(sh0);
     } else {
-      const uint64_t ppz = a.trec[pv].pz, psz = a.trec[pv].sz;
-      const uint32_t pcrc = a.trec[pv].crcz;
+      const bool near = pv == (int64_t)t - 1;
+      const uint64_t ppz = near ? P_pz : a.trec[pv].pz, psz = near ? P_sz : a.trec[pv].sz;
+      const uint32_t pcrc = near ? P_crcz : a.trec[pv].crcz;
       const uint32_t psh = SEG ? pos_shard_in(sg.soff, 0, sg.ns, ppz) : 0u;
       if (!SEG || psh == sh0) {
         if (psz != T.p0) {
@@ -1140,9 +1157,11 @@ __global__ __launch_bounds__(256) void k_frames_seam(FrArgs a, FrSeg sg, ResultD
     uint32_t nx = t + 1;
     sc = 0;
     bool farn = false;
-    while (nx < a.ntiles && a.tcnt[nx] == 0) {
-      if (++sc > FR_SCAN) { farn = true; break; }
-      ++nx;
+    if (!(hn && cn)) {
+      while (nx < a.ntiles && a.tcnt[nx] == 0) {
+        if (++sc > FR_SCAN) { farn = true; break; }
+        ++nx;
+      }
     }
     const bool hasn = !farn && nx < a.ntiles;
     const uint64_t e = T.sz;   // canonical layout: the Data ends at the frame end
@@ -1151,7 +1170,8 @@ __global__ __launch_bounds__(256) void k_frames_seam(FrArgs a, FrSeg sg, ResultD
     if (farn) {
       if (SEG) badsh(shz); else atomicOr(&ds->fc.rare, 32u);
     } else if (hasn) {
-      const uint64_t np = a.trec[nx].p0;
+      const bool nnear = nx == t + 1;
+      const uint64_t np = nnear ? N_p0 : a.trec[nx].p0;
       const uint32_t nsh = SEG ? pos_shard_in(sg.soff, 0, sg.ns, np) : 0u;
       if (!SEG || nsh == shz) {
         if (np != T.sz) {
@@ -1164,7 +1184,8 @@ __global__ __launch_bounds__(256) void k_frames_seam(FrArgs a, FrSeg sg, ResultD
       }
       if (np == e) {
         const uint64_t tsn = (uint64_t)nx * TB;
-        Pe = seam_shift(s_n, a.g_shift, e - tsn, fr_span_lin(a.trec, t, nx, s_n, TLOG)) ^ a.trec[nx].pfo0;
+        const uint32_t span = nnear ? T_agg : fr_span_lin(a.trec, t, nx, s_n, TLOG);
+        Pe = seam_shift(s_n, a.g_shift, e - tsn, span) ^ (nnear ? N_pfo0 : a.trec[nx].pfo0);
         pe_ok = true;
       }
     } else {   // the stream's last frame
@@ -1194,7 +1215,13 @@ __global__ __launch_bounds__(256) void k_frames_seam(FrArgs a, FrSeg sg, ResultD
       bool has = false, farop = false;
       uint64_t pidx = 0;
       uint32_t scanned = 0;
-      for (int64_t u = (int64_t)t - 1; u >= 0 && (uint64_t)(u + 1) * TB > lo_p; --u) {
+      int64_t u0 = (int64_t)t - 1;
+      if (hp && P_nops && (uint64_t)t * TB > lo_p) {   // the previous tile holds the predecessor op
+        has = !SEG || P_lastop >= lo_p;
+        pidx = P_lastidx;
+        u0 = -1;
+      }
+      for (int64_t u = u0; u >= 0 && (uint64_t)(u + 1) * TB > lo_p; --u) {
         if (++scanned > FR_SCAN) { farop = true; break; }
         if (!a.trec[u].nops) continue;
         has = !SEG || a.trec[u].lastop_p >= lo_p;
@@ -1208,8 +1235,12 @@ __global__ __launch_bounds__(256) void k_frames_seam(FrArgs a, FrSeg sg, ResultD
         bool gap;
         if (has) {
           const uint64_t kq = pidx - ri;
-          if (k <= kq && !a.rew) {
-            if (SEG) sg.sp[shf].rew = 1u; else atomicOr(&ds->fc.rare, 2u);
+          if (k <= kq) {
+            if (!a.rew) {
+              if (SEG) sg.sp[shf].rew = 1u; else atomicOr(&ds->fc.rare, 2u);
+            } else if (!SEG) {
+              atomicOr(&ds->fr_rews, 1u);
+            }
           }
           gap = k > kq && k - kq > 1;
         } else {

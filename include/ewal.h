@@ -505,6 +505,29 @@ int ecommit_batch_device(ewal_ctx *ctx, uint64_t G, const uint64_t *match, const
                          const uint64_t *term, uint64_t *committed, const uint64_t *log_offset,
                          const uint64_t *log_ptr, const uint64_t *log_terms, uint8_t *changed,
                          uint8_t *status, double *device_ms);
+/* The same maybeCommit over one 192-B record per group (the kernel reads
+ * each group's state with coalesced loads instead of seven strided match
+ * words plus a term gather that costs a whole line).  tail_term[k] is the
+ * term of raftLog.ents[nlog-1-k] for k < min(13, nlog); when the quorum index lies
+ * further back its term is read from log_terms[log_ptr[g] + (index -
+ * log_offset)] (both may be NULL when the caller knows it never does: such a
+ * group then gets status EWAL_UNSUPPORTED_ENCODING, as does a group with more
+ * than 7 voters -- ecommit_batch_device takes those).  Outputs are SoA:
+ * committed_out[g] (the new raftLog.committed), changed[g], status[g] as in
+ * ecommit_batch_device.  All pointers are DEVICE pointers. */
+typedef struct ecommit_group {
+  uint64_t match[7];       /* Progress.Match of voters 0 .. nvoters-1 (raft/raft.go:252) */
+  uint64_t committed;      /* raftLog.committed */
+  uint64_t term;           /* raft.Term */
+  uint64_t log_offset;     /* raftLog.offset: the index of ents[0] */
+  uint32_t nlog;           /* len(raftLog.ents) */
+  uint8_t nvoters;         /* 1..7 */
+  uint8_t pad[3];
+  uint64_t tail_term[13];  /* term of ents[nlog-1-k] */
+} ecommit_group;
+int ecommit_batch_rec_device(ewal_ctx *ctx, uint64_t G, const ecommit_group *groups, const uint64_t *log_ptr,
+                             const uint64_t *log_terms, uint64_t *committed_out, uint8_t *changed,
+                             uint8_t *status, double *device_ms);
 
 /* ---- raft ingress: raftpb.Message.Unmarshal, raft/raftpb/raft.pb.go:407-617
  * (called per POST /raft in etcdserver/etcdhttp/http.go:119-146), batched

@@ -197,6 +197,23 @@ def test_configs4_1m_groups_against_oracle(ctx):
     np.testing.assert_array_equal(ch.cpu().numpy(), chc)
     ok = stc == 0
     np.testing.assert_array_equal(got_c[ok], c[ok])
+    # the same groups as 128-B records (ecommit_batch_rec_device): the quorum
+    # index's term from the record's tail window, else the log_terms gather
+    from etcd_amd import raftcommit as RC
+    rec = T(RC.pack_groups(match, nv, committed0, term, log_offset, log_ptr, log_terms).reshape(-1))
+    co = torch.zeros(G, dtype=torch.int64, device=dev)
+    ch.zero_()
+    st.zero_()
+    assert L.lib.ecommit_batch_rec_device(ctx.handle, G, P(rec), P(d["p"]), P(d["lt"]), P(co), P(ch), P(st), None) == 0
+    np.testing.assert_array_equal(st.cpu().numpy(), stc)
+    np.testing.assert_array_equal(ch.cpu().numpy(), chc)
+    np.testing.assert_array_equal(co.cpu().numpy().view(np.uint64)[ok], c[ok])
+    # without the log arrays: only groups whose quorum term lies before the window lose their verdict
+    assert L.lib.ecommit_batch_rec_device(ctx.handle, G, P(rec), None, None, P(co), P(ch), P(st), None) == 0
+    st2 = st.cpu().numpy()
+    moved = st2 != stc
+    assert (st2[moved] == L.UNSUPPORTED_ENCODING).all() and moved.sum() < G // 10
+    np.testing.assert_array_equal(co.cpu().numpy().view(np.uint64)[ok & ~moved], c[ok & ~moved])
 
 
 @pytest.mark.gpu

@@ -223,3 +223,30 @@ def test_shim_harness_links_and_fails_loudly_without_gpu():
     out = json.loads(p.stdout.strip().splitlines()[-1])
     if L.lib.ewal_device_count() == 0:
         assert out["ok"] is False and out["rc"] == L.E_NODEVICE
+
+
+def test_commit_records_pack():
+    """raftcommit.pack_groups: the 192-B ecommit_group rows (include/ewal.h)
+    hold the voters' Match, committed, Term, the log bounds and the terms of
+    the log's last 13 entries -- checked field by field on a small batch."""
+    import numpy as np
+    from etcd_amd import raftcommit as RC
+    rng = np.random.default_rng(3)
+    G = 50
+    nv = rng.integers(1, 8, size=G).astype(np.uint8)
+    match = rng.integers(0, 1 << 40, size=(7, G), dtype=np.uint64)
+    c0 = rng.integers(0, 1 << 30, size=G, dtype=np.uint64)
+    term = rng.integers(1, 9, size=G, dtype=np.uint64)
+    off = rng.integers(0, 1 << 30, size=G, dtype=np.uint64)
+    lens = rng.integers(0, 20, size=G).astype(np.uint64)
+    ptr = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
+    lt = rng.integers(1, 1 << 20, size=int(lens.sum()), dtype=np.uint64)
+    rec = RC.pack_groups(match, nv, c0, term, off, ptr, lt)
+    assert rec.shape == (G, 24) and rec.dtype == np.uint64
+    for g in range(G):
+        assert list(rec[g, :7]) == list(match[:, g])
+        assert (rec[g, 7], rec[g, 8], rec[g, 9]) == (c0[g], term[g], off[g])
+        assert int(rec[g, 10]) == int(lens[g]) | (int(nv[g]) << 32)
+        for k in range(13):
+            want = lt[int(ptr[g + 1]) - 1 - k] if k < lens[g] else 0
+            assert rec[g, 11 + k] == want
