@@ -271,82 +271,97 @@ __global__ __launch_bounds__(256) void k_commit(uint64_t G, const uint64_t *__re
 // index's term comes from the record's tail window when it is one of the
 // last 13 entries (the usual case: the uncommitted tail of a raft log is a
 // few appends deep), else from the log_terms gather as in k_commit.
-__global__ __launch_bounds__(256) void k_commit_rec(uint64_t G, const ecommit_group *__restrict__ rec,
-                                                    const uint64_t *__restrict__ log_ptr,
-                                                    const uint64_t *__restrict__ log_terms,
-                                                    uint64_t *__restrict__ committed_out,
-                                                    uint8_t *__restrict__ changed, uint8_t *__restrict__ status) {
-  // the workgroup's 256 records (48 KiB) staged through LDS with fully
-  // coalesced 16-B loads (a lane reading its own 192-B record directly would
-  // touch 64 lines per load instruction)
+__global__ __launch_bounds__(64) void k_commit_rec(uint64_t G, const ecommit_group *__restrict__ rec,
+                                                   const uint64_t *__restrict__ log_ptr,
+                                                   const uint64_t *__restrict__ log_terms,
+                                                   uint64_t *__restrict__ committed_out,
+                                                   uint8_t *__restrict__ changed, uint8_t *__restrict__ status) {
+  // one wave per workgroup, persistent over chunks of 64 records (12 KiB):
+  // a chunk is read with fully coalesced 16-B loads (a lane reading its own
+  // 192-B record directly would touch 64 lines per load instruction) while
+  // the previous one is selected from LDS
   typedef uint32_t v4u __attribute__((ext_vector_type(4)));
-  __shared__ v4u s_rec[256 * 12];
-  const uint64_t g0 = (uint64_t)blockIdx.x * 256;
-  const uint64_t nrec = G - g0 < 256 ? G - g0 : 256;
-  const v4u *src = (const v4u *)(rec + g0);
+  __shared__ v4u s_rec[64 * 12];
+  const uint32_t lane = threadIdx.x;
+  const uint64_t nchunk = (G + 63) / 64;
+  auto load = [&](uint64_t ch, v4u (&x)[12]) {
+    const uint64_t g0 = ch * 64;
+    const uint64_t n12 = (G - g0 < 64 ? G - g0 : 64) * 12;
+    const v4u *src = (const v4u *)(rec + g0);
 #pragma unroll
-  for (int k = 0; k < 12; ++k) {
-    const uint32_t i = (uint32_t)k * 256 + threadIdx.x;
-    if (i < nrec * 12) s_rec[i] = __builtin_nontemporal_load(src + i);   // read once
-  }
-  __syncthreads();
-  const uint64_t g = g0 + threadIdx.x;
-  if (g >= G) return;
-  const uint64_t *w = (const uint64_t *)(s_rec + threadIdx.x * 12);
-  auto u64 = [&](int i) { return w[i]; };   // the record's i-th 8-byte word
-  const uint64_t c = u64(7), tm = u64(8), off = u64(9);
-  const uint64_t w10 = u64(10);
-  const uint64_t nlog = (uint32_t)w10;
-  const int nv = (int)((w10 >> 32) & 0xff);
-  uint8_t chg = 0, st = 0;
-  uint64_t cn = c;
-  if (nv <= 0) {
-    st = EWAL_PANIC_BOUNDS;   // mis[q-1] on an empty slice (raft/raft.go:255)
-  } else if (nv > 7) {
-    st = EWAL_UNSUPPORTED_ENCODING;   // more voters than a record holds: ecommit_batch_device
-  } else {
-    uint64_t m[8];
-#pragma unroll
-    for (int v = 0; v < 8; ++v) m[v] = v < 7 ? u64(v) : 0ull;
-    const int qn = nv / 2 + 1;
-    uint64_t mci = 0;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {   // rank-select: the qn-th largest (quorum_select's rule)
-      int gt = 0, ge = 0;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        gt += (j < nv && m[j] > m[i]);
-        ge += (j < nv && m[j] >= m[i]);
-      }
-      if (i < nv && gt < qn && qn <= ge) mci = m[i];
+    for (int k = 0; k < 12; ++k) {
+      const uint32_t i = (uint32_t)k * 64 + lane;
+      x[k] = (ch < nchunk && i < n12) ? __builtin_nontemporal_load(src + i) : v4u{0, 0, 0, 0};   // read once
     }
-    if (mci > c) {   // raftLog.maybeCommit: term(mci) == Term (raft/log.go:148-154)
-      const uint64_t last = nlog - 1 + off;   // lastIndex(), uint64 wrap
-      uint64_t t = 0;
-      bool panic = false;
-      if (!(mci < off || mci > last)) {       // raftLog.at / isOutOfBounds (raft/log.go:194-217)
-        const uint64_t kk = mci - off;
-        if (kk >= nlog) {
-          panic = true;
-        } else if (nlog - 1 - kk < 13) {
-          t = u64(11 + (int)(nlog - 1 - kk));
-        } else if (log_ptr && log_terms) {
-          t = log_terms[log_ptr[g] + kk];
-        } else {
-          st = EWAL_UNSUPPORTED_ENCODING;    // the term lies before the tail window and no log was given
+  };
+  v4u cur[12], nxt[12];
+  uint64_t ch = blockIdx.x;
+  load(ch, cur);
+  for (; ch < nchunk; ch += gridDim.x) {
+    load(ch + gridDim.x, nxt);
+#pragma unroll
+    for (int k = 0; k < 12; ++k) s_rec[k * 64 + lane] = cur[k];
+    __syncthreads();
+    const uint64_t g = ch * 64 + lane;
+    if (g < G) {
+      const uint64_t *w = (const uint64_t *)(s_rec + lane * 12);   // the record's 8-byte words
+      const uint64_t c = w[7], tm = w[8], off = w[9], w10 = w[10];
+      const uint64_t nlog = (uint32_t)w10;
+      const int nv = (int)((w10 >> 32) & 0xff);
+      uint8_t chg = 0, st = 0;
+      uint64_t cn = c;
+      if (nv <= 0) {
+        st = EWAL_PANIC_BOUNDS;   // mis[q-1] on an empty slice (raft/raft.go:255)
+      } else if (nv > 7) {
+        st = EWAL_UNSUPPORTED_ENCODING;   // more voters than a record holds: ecommit_batch_device
+      } else {
+        uint64_t m[8];
+#pragma unroll
+        for (int v = 0; v < 8; ++v) m[v] = v < 7 ? w[v] : 0ull;
+        const int qn = nv / 2 + 1;
+        uint64_t mci = 0;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {   // rank-select: the qn-th largest (quorum_select's rule)
+          int gt = 0, ge = 0;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            gt += (j < nv && m[j] > m[i]);
+            ge += (j < nv && m[j] >= m[i]);
+          }
+          if (i < nv && gt < qn && qn <= ge) mci = m[i];
+        }
+        if (mci > c) {   // raftLog.maybeCommit: term(mci) == Term (raft/log.go:148-154)
+          const uint64_t last = nlog - 1 + off;   // lastIndex(), uint64 wrap
+          uint64_t t = 0;
+          bool panic = false;
+          if (!(mci < off || mci > last)) {       // raftLog.at / isOutOfBounds (raft/log.go:194-217)
+            const uint64_t kk = mci - off;
+            if (kk >= nlog) {
+              panic = true;
+            } else if (nlog - 1 - kk < 13) {
+              t = w[11 + (nlog - 1 - kk)];
+            } else if (log_ptr && log_terms) {
+              t = log_terms[log_ptr[g] + kk];
+            } else {
+              st = EWAL_UNSUPPORTED_ENCODING;    // the term lies before the tail window and no log was given
+            }
+          }
+          if (panic) {
+            st = EWAL_PANIC_BOUNDS;
+          } else if (!st && t == tm) {
+            cn = mci;
+            chg = 1;
+          }
         }
       }
-      if (panic) {
-        st = EWAL_PANIC_BOUNDS;
-      } else if (!st && t == tm) {
-        cn = mci;
-        chg = 1;
-      }
+      committed_out[g] = cn;
+      changed[g] = chg;
+      status[g] = st;
     }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 12; ++k) cur[k] = nxt[k];
   }
-  committed_out[g] = cn;
-  changed[g] = chg;
-  status[g] = st;
 }
 
 // ===========================================================================

@@ -2632,7 +2632,8 @@ int ecommit_batch_rec_device(ewal_ctx *c, uint64_t G, const ecommit_group *group
   EW_CHECK(hipSetDevice(c->device));
   EW_CHECK(hipEventRecord(c->ev0, c->stream));
   if (G)
-    hipLaunchKernelGGL(k_commit_rec, dim3((unsigned)((G + 255) / 256)), dim3(256), 0, c->stream, G, groups, log_ptr,
+    hipLaunchKernelGGL(k_commit_rec, dim3((unsigned)std::min<uint64_t>((G + 63) / 64, (uint64_t)std::max(1, c->num_cu) * 12)),
+                       dim3(64), 0, c->stream, G, groups, log_ptr,
                        log_terms, committed_out, changed, status);
   EW_CHECK(hipGetLastError());
   EW_CHECK(hipEventRecord(c->ev1, c->stream));
