@@ -2658,4 +2658,8 @@ extern "C" int ewal_dbg_fr_seam_timing(unsigned long long *out, int n) {
   if (hipMemcpyFromSymbol(out, HIP_SYMBOL(fr_sdbg), (size_t)n * 8) != hipSuccess) return EWAL_E_HIP;
   return 0;
 }
+extern "C" int ewal_dbg_fr_seam_steps(unsigned long long *out, int n) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(fr_sdbg2), (size_t)n * 8) != hipSuccess) return EWAL_E_HIP;
+  return 0;
+}
 #endif

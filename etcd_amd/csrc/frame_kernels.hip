@@ -335,6 +335,7 @@ struct FrCarry {
 // tools/ timing builds only: per wave, the cycles of each phase of k_frames
 __device__ unsigned long long fr_tdbg[8192 * 8];
 __device__ unsigned long long fr_sdbg[1024 * 4];   // k_frames_seam: per block, its loop and fr_result cycles
+__device__ unsigned long long fr_sdbg2[1024 * 8];  // k_frames_seam thread 0: the loop's steps
 #define FR_T(i) do { const unsigned long long t_ = clock64(); tacc[i] += t_ - tlast; tlast = t_; } while (0)
 #else
 #define FR_T(i) do {} while (0)
@@ -1079,6 +1080,12 @@ __global__ __launch_bounds__(256) void k_frames_seam(FrArgs a, FrSeg sg, ResultD
     s_red[2] = s_red[3] = s_red[4] = s_red[5] = 0;
   }
   __syncthreads();
+#ifdef FR_TIMING
+  unsigned long long tq[8] = {(unsigned long long)clock64(), 0, 0, 0, 0, 0, 0, 0};
+#define SEAM_T(i) do { if (threadIdx.x == 0 && !tq[i]) tq[i] = clock64(); } while (0)
+#else
+#define SEAM_T(i) do {} while (0)
+#endif
   unsigned long long fail = ~0ull, meta = ~0ull, le = 0, ls = 0, lo = 0, nops = 0;
   auto badsh = [&](uint32_t s) { atomicOr(&sg.sp[s].bad, 1u); };
   auto key_at = [&](uint32_t s, uint64_t p, int st) {
@@ -1100,6 +1107,10 @@ __global__ __launch_bounds__(256) void k_frames_seam(FrArgs a, FrSeg sg, ResultD
     const uint64_t N_p0 = TN->p0;
     const uint32_t N_pfo0 = TN->pfo0, T_agg = T.agg;
     if (!T.count) continue;
+#ifdef FR_TIMING
+    if (threadIdx.x == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+    SEAM_T(1);
     // ---- the previous frame: the last of the nearest earlier tile with frames ----
     int64_t pv = (int64_t)t - 1;
     uint32_t sc = 0;
@@ -1141,6 +1152,7 @@ __global__ __launch_bounds__(256) void k_frames_seam(FrArgs a, FrSeg sg, ResultD
       const int st = fr_check(s_n, a.g_shift, T.type0, T.crc0, seed0, T.pfd0, T.pe0, T.dlen0, false);
       if (st) key_at(sh0, T.p0, st);
     }
+    SEAM_T(2);
     // ---- the last frame ----
     const uint32_t shz = SEG ? pos_shard_in(sg.soff, 0, sg.ns, T.pz) : 0u;
     const uint64_t EZ = SEG ? sg.soff[shz + 1] : a.B;
@@ -1207,6 +1219,7 @@ __global__ __launch_bounds__(256) void k_frames_seam(FrArgs a, FrSeg sg, ResultD
       const int st = fr_check(s_n, a.g_shift, T.typez, T.crcz, seedz, T.pfdz, Pe, T.dlenz, defer);
       if (st) key_at(shz, T.pz, st);
     }
+    SEAM_T(3);
     // ---- the gap rule for the tile's first entry op (wal/wal.go:173) ----
     if (T.seam && T.nops) {
       const uint32_t shf = SEG ? pos_shard_in(sg.soff, 0, sg.ns, T.firstop_p) : 0u;
@@ -1258,6 +1271,11 @@ __global__ __launch_bounds__(256) void k_frames_seam(FrArgs a, FrSeg sg, ResultD
       nops += T.nops;
     }
   }
+  SEAM_T(4);
+#ifdef FR_TIMING
+  if (threadIdx.x == 0 && blockIdx.x < 1024)
+    for (int i = 0; i < 8; ++i) fr_sdbg2[blockIdx.x * 8 + i] = tq[i] ? tq[i] - tq[0] : 0ull;
+#endif
   if (SEG) return;
   if (fail != ~0ull) atomicMin(&s_red[0], fail);
   if (meta != ~0ull) atomicMin(&s_red[1], meta);

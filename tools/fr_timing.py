@@ -14,6 +14,7 @@ NAMES = ["stage", "A", "pieces", "decode", "checks", "ops", "reduce", "tile_end"
 lib = L.lib
 lib.ewal_dbg_fr_timing.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
 lib.ewal_dbg_fr_seam_timing.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
+lib.ewal_dbg_fr_seam_steps.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
 
 
 def one(label, size, lo, hi):
@@ -36,6 +37,13 @@ def one(label, size, lo, hi):
         print("  seam: %d blocks, loop avg %.0f max %.0f cycles, last block ends loop at +%.0f, fr_result %.0f" %
               (len(blocks), sum(b[0] for b in blocks) / len(blocks), max(b[0] for b in blocks),
                max(b[3] for b in blocks) - t0, max(b[1] for b in blocks)))
+    st = (C.c_ulonglong * (1024 * 8))()
+    lib.ewal_dbg_fr_seam_steps(st, 1024 * 8)
+    rows = [list(st[b * 8:(b + 1) * 8]) for b in range(1024) if any(st[b * 8:(b + 1) * 8])]
+    if rows:
+        print("  seam thread 0 steps (cycles from the loop start, median over blocks): " +
+              " ".join("%s=%d" % (nm, sorted(r[i] for r in rows)[len(rows) // 2])
+                       for i, nm in ((1, "loads"), (2, "first"), (3, "last"), (4, "end"))))
     waves = [list(t[w * 8:(w + 1) * 8]) for w in range(8192) if any(t[w * 8:(w + 1) * 8])]
     tot = [sum(x) for x in waves]
     print("%s: %d frames, %.3f GiB, device %.3f ms (stream %.3f), %d waves" %
