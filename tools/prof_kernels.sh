@@ -6,10 +6,4 @@ OUT=$1; W=$2; shift 2
 export TMPDIR=/tmp
 timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT -o run -- python3 bench.py --workload $W --steps 5 --warmup 1 \
   --no-cpu-baseline --no-e2e "$@" > $OUT.bench.json 2> $OUT.err || exit 1
-f=$(find $OUT -name "*kernel_stats.csv" | head -1)
-python3 - "$f" <<'PY'
-import csv, sys
-rows = list(csv.DictReader(open(sys.argv[1])))
-for r in rows[:16]:
-    print("%-60s calls %4s avg_us %9.1f" % (r["Name"][:60], r["Calls"], float(r["AverageNs"]) / 1e3))
-PY
+python3 tools/prof_summary.py $OUT
