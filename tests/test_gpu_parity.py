@@ -642,3 +642,54 @@ def test_save_device_matches_reference_writer(ctx, seed):
     assert o["status"] == O.OK and len(o["ents"]) == 89 and o["state"]["commit"] == 80
     assert_parity(ctx, head + body, 1)
     assert body[offs[40] + 8:offs[40] + 10] == b"\x08\x04"      # the Cut's file starts with its crcType record
+
+
+def test_commit_records_kats_and_edges(ctx):
+    """ecommit_batch_rec_device over hand-made groups: the TestCommit shapes
+    (raft/raft_test.go commit cases via O.maybe_commit), quorum terms inside
+    and before the 13-term tail window, logs shorter than the window, an
+    empty log, no voters (Go's bounds panic) and more voters than a record
+    holds (EWAL_UNSUPPORTED_ENCODING: ecommit_batch_device takes those)."""
+    import numpy as np
+    import torch
+    from etcd_amd import raftcommit as RC
+    rng = random.Random(23)
+    groups = []
+    for _ in range(400):
+        n = rng.choice([1, 2, 3, 4, 5, 6, 7])
+        nlog = rng.choice([0, 1, 3, 12, 13, 14, 30])
+        off = rng.randrange(0, 5)
+        lt = sorted(rng.randrange(1, 4) for _ in range(nlog))
+        m = [rng.randrange(0, off + nlog + 3) for _ in range(n)]
+        groups.append((m, lt, off, rng.randrange(1, 4), rng.randrange(0, off + nlog + 1)))
+    groups.append(([], [1, 1], 0, 1, 0))                       # no voters: mis[q-1] panics
+    groups.append(([5] * 9, [1] * 8, 0, 1, 0))                  # 9 voters: not a record's shape
+    G = len(groups)
+    match = np.zeros((9, G), np.uint64)
+    nv = np.array([len(g[0]) for g in groups], np.uint8)
+    for gi, g in enumerate(groups):
+        match[:len(g[0]), gi] = g[0]
+    lens = np.array([len(g[1]) for g in groups], np.uint64)
+    ptr = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
+    lt = np.array([t for g in groups for t in g[1]] or [0], np.uint64)
+    rec = RC.pack_groups(match, nv, np.array([g[4] for g in groups], np.uint64),
+                         np.array([g[3] for g in groups], np.uint64), np.array([g[2] for g in groups], np.uint64),
+                         ptr, lt)
+    dev = torch.device("cuda", 0)
+    T = lambda x: torch.from_numpy(x.view(np.int64)).to(dev)   # noqa: E731
+    d_rec, d_ptr, d_lt = T(rec.reshape(-1)), T(ptr), T(lt)
+    co = torch.zeros(G, dtype=torch.int64, device=dev)
+    ch = torch.zeros(G, dtype=torch.uint8, device=dev)
+    st = torch.zeros(G, dtype=torch.uint8, device=dev)
+    P = lambda t: C.c_void_p(t.data_ptr())   # noqa: E731
+    assert L.lib.ecommit_batch_rec_device(ctx.handle, G, P(d_rec), P(d_ptr), P(d_lt), P(co), P(ch), P(st), None) == 0
+    co, ch, st = co.cpu().numpy().view(np.uint64), ch.cpu().numpy(), st.cpu().numpy()
+    for gi, (m, lts, off, term, c) in enumerate(groups):
+        if len(m) > 7:
+            assert st[gi] == L.UNSUPPORTED_ENCODING, gi
+            continue
+        rc, want = O.maybe_commit(m, term, c, lts, off)
+        if rc < 0 or not m:
+            assert st[gi] == L.PANIC_BOUNDS, (gi, rc, st[gi])
+            continue
+        assert (st[gi], int(co[gi]), int(ch[gi])) == (0, want, 1 if rc == 1 else 0), (gi, m, lts, off, term, c)
