@@ -103,11 +103,12 @@ __device__ RecDesc fc_frame_fields(const uint8_t *__restrict__ buf, uint64_t B, 
   d.type = 0; d.crc = 0; d.chained = 0; d.st = 0; d.sub_st = 0;
   d.doff = p + 8; d.dlen = 0; d.dnil = 1;
   d.f0 = d.f1 = d.f2 = 0; d.edoff = 0; d.edlen = 0; d.enil = 1; d.etype = 0; d.pad0 = 0; d.pad1 = 0;
-  const int64_t L = (int64_t)ld_le64_b(buf, B, p);
-  if (p + 8 > B || L < 0 || (uint64_t)L > B - p - 8) {   // not a frame (only a void pass asks)
+  if (p + 8 > B) {   // not a frame (only a void pass asks)
     d.st = EWAL_ERR_UNEXPECTED_EOF;
     return d;
   }
+  // the 96 bytes from the 16-B boundary below p in one round trip; the
+  // length prefix is read back from them (p - p16 + 8 <= 24)
   const uint64_t p16 = p & ~15ull;
 #pragma unroll
   for (int k = 0; k < 6; ++k) {
@@ -122,6 +123,18 @@ __device__ RecDesc fc_frame_fields(const uint8_t *__restrict__ buf, uint64_t B, 
       x = make_uint4(y[0], y[1], y[2], y[3]);
     }
     w[k] = x;
+  }
+  int64_t L = 0;
+  {
+    const uint8_t *hb = (const uint8_t *)w + (p - p16);
+    uint64_t v = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v |= (uint64_t)hb[i] << (8 * i);
+    L = (int64_t)v;
+  }
+  if (L < 0 || (uint64_t)L > B - p - 8) {
+    d.st = EWAL_ERR_UNEXPECTED_EOF;
+    return d;
   }
   if (fc_canon_fields((const uint8_t *)w + (p - p16), 96 - (int)(p - p16), p, L, d)) return d;
   // not the canonical layout (a frame the general path also decodes): the walkers

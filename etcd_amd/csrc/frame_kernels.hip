@@ -979,7 +979,7 @@ __device__ __forceinline__ int fr_terminal(const uint8_t *buf, uint64_t B, uint6
 // result names re-read from the stream, the failing frame's ordinal.
 template <int TSH>
 __device__ void fr_result(const FrArgs &a, ResultDev *o, Small *h, uint4 (*s_w)[6], RecDesc *s_d,
-                          unsigned long long *s_ord) {
+                          unsigned long long *s_ord, ResultDev *s_res) {
   Small *ds = a.ds;
   const uint32_t tid = threadIdx.x;
   const uint64_t K = ds->total;
@@ -1029,27 +1029,39 @@ __device__ void fr_result(const FrArgs &a, ResultDev *o, Small *h, uint4 (*s_w)[
     }
   }
   __syncthreads();
-  if (tid != 0) return;
-  ResultDev res;
-  memset(&res, 0, sizeof(res));
-  res.agg.first_fail = key != ~0ull ? *s_ord : ~0ull;
-  res.agg.last_entry = le ? 0 : -1;
-  res.agg.last_state = ls ? 0 : -1;
-  res.agg.first_meta = fm != ~0ull ? 0ull : ~0ull;
-  if (key != ~0ull) {
-    res.fail = s_d[0];
-    res.fail.st = (int32_t)(key & 0xff);
+  // the result composed in LDS by thread 0, then written to host-mapped
+  // memory by a whole wave (wide PCIe writes instead of one lane's stores)
+  ResultDev &res = *s_res;
+  if (tid == 0) {
+    memset(&res, 0, sizeof(res));
+    res.agg.first_fail = key != ~0ull ? *s_ord : ~0ull;
+    res.agg.last_entry = le ? 0 : -1;
+    res.agg.last_state = ls ? 0 : -1;
+    res.agg.first_meta = fm != ~0ull ? 0ull : ~0ull;
+    if (key != ~0ull) {
+      res.fail = s_d[0];
+      res.fail.st = (int32_t)(key & 0xff);
+    }
+    if (le) res.lastent = s_d[1];
+    if (ls) res.sd = s_d[2];
+    if (fm != ~0ull) res.md = s_d[3];
+    res.last.chained = ds->fc.last_chained;
+    res.nops = (uint32_t)ds->fr.nops;
+    res.klast = lo ? s_d[4].f1 - a.ri : 0;
+    res.errflag = ds->errflag;
+    ds->spec_n = (uint32_t)K;
   }
-  if (le) res.lastent = s_d[1];
-  if (ls) res.sd = s_d[2];
-  if (fm != ~0ull) res.md = s_d[3];
-  res.last.chained = ds->fc.last_chained;
-  res.nops = (uint32_t)ds->fr.nops;
-  res.klast = lo ? s_d[4].f1 - a.ri : 0;
-  res.errflag = ds->errflag;
-  *o = res;
-  ds->spec_n = (uint32_t)K;
-  *h = *ds;
+  __threadfence_block();
+  __syncthreads();
+  if (tid < 64) {
+    static_assert(sizeof(ResultDev) % 4 == 0 && sizeof(Small) % 4 == 0, "dword copies");
+    const uint32_t *rs = (const uint32_t *)&res;
+    uint32_t *rd = (uint32_t *)o;
+    for (uint32_t i = tid; i < sizeof(ResultDev) / 4; i += 64) rd[i] = rs[i];
+    const uint32_t *ss = (const uint32_t *)ds;
+    uint32_t *sd = (uint32_t *)h;
+    for (uint32_t i = tid; i < sizeof(Small) / 4; i += 64) sd[i] = ss[i];
+  }
 }
 
 // One thread per tile: the checks of the tile's first frame (its seed from
@@ -1067,6 +1079,7 @@ __global__ __launch_bounds__(256) void k_frames_seam(FrArgs a, FrSeg sg, ResultD
   __shared__ uint4 s_w[SEG ? 1 : 256][6];
   __shared__ RecDesc s_d[SEG ? 1 : 6];
   __shared__ unsigned long long s_ord;
+  __shared__ ResultDev s_res[SEG ? 1 : 1];
   __shared__ uint32_t s_n[SEAM_NIB * 128];  // S_{2^m} nibble tables, m < 24
   static_assert(TLOG < SEAM_NIB, "tile shifts from the LDS tables");
   Small *ds = a.ds;
@@ -1300,7 +1313,7 @@ __global__ __launch_bounds__(256) void k_frames_seam(FrArgs a, FrSeg sg, ResultD
 #endif
   if (s_last) {   // the last workgroup: every tile is in
     __threadfence();
-    fr_result<TSH>(a, o, h, s_w, s_d, &s_ord);
+    fr_result<TSH>(a, o, h, s_w, s_d, &s_ord, s_res);
   }
 #ifdef FR_TIMING
   if (threadIdx.x == 0 && blockIdx.x < 1024) {
@@ -1308,6 +1321,8 @@ __global__ __launch_bounds__(256) void k_frames_seam(FrArgs a, FrSeg sg, ResultD
     fr_sdbg[blockIdx.x * 4 + 1] = s_last ? clock64() - t_loop : 0ull;
     fr_sdbg[blockIdx.x * 4 + 2] = t_seam0;
     fr_sdbg[blockIdx.x * 4 + 3] = t_loop;
+    fr_sdbg2[blockIdx.x * 8 + 5] = tq[0] - t_seam0;            // staging + the first barrier
+    fr_sdbg2[blockIdx.x * 8 + 6] = tq[4] ? t_loop - tq[4] : 0ull;   // after thread 0's last tile: the block's wait + fold
   }
 #endif
 }

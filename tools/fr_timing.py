@@ -43,7 +43,8 @@ def one(label, size, lo, hi):
     if rows:
         print("  seam thread 0 steps (cycles from the loop start, median over blocks): " +
               " ".join("%s=%d" % (nm, sorted(r[i] for r in rows)[len(rows) // 2])
-                       for i, nm in ((1, "loads"), (2, "first"), (3, "last"), (4, "end"))))
+                       for i, nm in ((1, "loads"), (2, "first"), (3, "last"), (4, "end"), (5, "staging"),
+                                     (6, "wait+fold"))))
     waves = [list(t[w * 8:(w + 1) * 8]) for w in range(8192) if any(t[w * 8:(w + 1) * 8])]
     tot = [sum(x) for x in waves]
     print("%s: %d frames, %.3f GiB, device %.3f ms (stream %.3f), %d waves" %
