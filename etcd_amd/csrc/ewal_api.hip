@@ -1822,7 +1822,11 @@ int ewal_ctx_create(int device, ewal_ctx **out) {
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
     c->num_cu = prop.multiProcessorCount;
-  EW_CHECK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+  // a blocking stream: ordered with the legacy default stream, so device
+  // buffers a caller filled there (torch's default stream, hipMemcpy) are
+  // complete before the ctx's kernels read them, and its results before the
+  // caller's next default-stream work reads them
+  EW_CHECK(hipStreamCreateWithFlags(&c->stream, hipStreamDefault));
   c->own_stream = true;
 #ifdef EW_ABLATION_HOOKS   // timing experiments only (tools/): results are wrong under ablation.  The product
                            // build reads no environment variable: its path is set by ewal_ctx_set_options only.
@@ -1868,7 +1872,7 @@ int ewal_ctx_set_stream(ewal_ctx *c, void *s) {
     c->stream = (hipStream_t)s;
     c->own_stream = false;
   } else {
-    EW_CHECK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    EW_CHECK(hipStreamCreateWithFlags(&c->stream, hipStreamDefault));   // blocking, as in ewal_ctx_create
     c->own_stream = true;
   }
   return EWAL_OK;

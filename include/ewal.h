@@ -125,7 +125,11 @@ typedef struct ewal_record {
 /* ---- context ------------------------------------------------------------ */
 int ewal_ctx_create(int device, ewal_ctx **out);
 void ewal_ctx_destroy(ewal_ctx *ctx);
-/* Run on a caller-owned hipStream_t (NULL = the ctx's own stream). */
+/* Run on a caller-owned hipStream_t (NULL = the ctx's own stream).  The
+ * ctx's own stream is a blocking stream: it is ordered with the legacy
+ * default stream (stream 0, torch's default stream), so inputs written there
+ * are complete before the ctx reads them.  A caller-owned non-blocking
+ * stream gets no such ordering: the caller orders its own work on it. */
 int ewal_ctx_set_stream(ewal_ctx *ctx, void *hip_stream);
 /* Pre-size ctx's workspace for a ReadAll over up to wal_bytes and load the
  * device code, so that the first ReadAll (the one-shot restart,
