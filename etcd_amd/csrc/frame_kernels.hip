@@ -341,6 +341,27 @@ __device__ unsigned long long fr_sdbg2[1024 * 8];  // k_frames_seam thread 0: th
 #define FR_T(i) do {} while (0)
 #endif
 
+// The tile record's running fields (wave-uniform) and a batch's per-shard
+// reductions folded over the rounds, kept in a per-wave LDS slot instead of
+// registers: the frame loop is at the 168-VGPR / 104-SGPR limit of 12
+// waves/CU, and these long-lived uniform values spilled (A/B: configs[0]
+// post-stream -8 %, 128 shards -3 %; the carried frame and the piece rounds'
+// per-lane results in LDS too: no gain / +11 %, profiles/r04/ab_notes.txt).
+// FR_TR_LDS=0 keeps them in registers (A/B builds).
+#ifndef FR_TR_LDS
+#define FR_TR_LDS 1
+#endif
+struct FrTr {
+  unsigned long long first_index, last_index, firstop_p, lastop_p;
+  unsigned long long fail, last_entry1, last_state1, meta0;
+  uint32_t nops, seam;
+};
+struct FrAcc {
+  unsigned long long aff, afm;
+  long long ale, als, alo, alp;
+  uint32_t ash, pad;
+};
+
 template <bool SEG, int TSH>
 __global__ __launch_bounds__(FR_THREADS, 1) void k_frames(FrArgs a, FrSeg sg) {
 #ifdef FR_TIMING
@@ -357,6 +378,10 @@ __global__ __launch_bounds__(FR_THREADS, 1) void k_frames(FrArgs a, FrSeg sg) {
   __shared__ uint32_t s_win[20 * FR_THREADS];        // frame heads, transposed
   __shared__ uint32_t s_ucnt[FR_WAVES][TU];          // candidates per unit of each wave's tile
   __shared__ uint32_t s_pw[FR_WAVES][TU];            // P at every unit start of each wave's tile (tile-local)
+#if FR_TR_LDS
+  __shared__ FrTr s_tr[FR_WAVES];
+  __shared__ FrAcc s_acc[FR_WAVES];
+#endif
   Small *ds = a.ds;
   if (SEG && ds->fr_capfail) return;                 // ents regions past the capacity: the host grows them, reruns
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -501,20 +526,27 @@ __global__ __launch_bounds__(FR_THREADS, 1) void k_frames(FrArgs a, FrSeg sg) {
     uint32_t opsh = 0;
     // the tile's record (wave-uniform values; the first frame's fields are
     // stored where they are found)
-    struct {
-      uint32_t nops, seam;
-      uint64_t first_index, last_index, firstop_p, lastop_p;
-      unsigned long long fail;
-      uint64_t last_entry1, last_state1, meta0;
-    } tr;
+#if FR_TR_LDS
+    FrTr &tr = s_tr[wv];
+#else
+    FrTr tr;
+#endif
     tr.nops = 0; tr.seam = 0; tr.first_index = tr.last_index = 0;
     tr.firstop_p = tr.lastop_p = 0;
     tr.fail = ~0ull; tr.last_entry1 = tr.last_state1 = 0; tr.meta0 = ~0ull;
     uint32_t tflags = 0;
     // batch: per-shard reductions folded while the rounds stay in one shard
-    uint32_t ash = EW_NIL;
-    unsigned long long aff = ~0ull, afm = ~0ull;
-    long long ale = -1, als = -1, alo = -1, alp = -1;
+#if FR_TR_LDS
+    FrAcc &acc = s_acc[wv];
+#else
+    FrAcc acc;
+#endif
+    uint32_t &ash = acc.ash;
+    unsigned long long &aff = acc.aff, &afm = acc.afm;
+    long long &ale = acc.ale, &als = acc.als, &alo = acc.alo, &alp = acc.alp;
+    ash = EW_NIL;
+    aff = afm = ~0ull;
+    ale = als = alo = alp = -1;
     auto aflush = [&]() {
       if (SEG && ash != EW_NIL && lane == 0) {
         ShardPos *A = sg.sp + ash;
