@@ -3,7 +3,7 @@ per-launch HBM bytes = FETCH_SIZE (KiB) x 1024 x 2 (gfx950: FETCH_SIZE counts
 half the bytes of a wide streaming read) + WRITE_SIZE (KiB) x 1024.
 Usage: python3 tools/traffic.py ROOT [KERNEL [CONFIG]]
   default: k_stream, configs[1] (bench.py default, 8 GiB)"""
-import csv, glob, json, os, sys
+import csv, glob, json, os, re, sys
 from collections import defaultdict
 root = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/traffic"
 kern = sys.argv[2] if len(sys.argv) > 2 else "k_stream"
@@ -13,7 +13,8 @@ for c in ("FETCH_SIZE", "WRITE_SIZE"):
     per = defaultdict(float)
     for f in glob.glob(os.path.join(root, c, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
-            if kern in r["Kernel_Name"] and r["Counter_Name"] == c:
+            # the kernel itself, not others whose names contain it (k_frames_seam)
+            if re.match(r"(void )?%s[<(]" % re.escape(kern), r["Kernel_Name"]) and r["Counter_Name"] == c:
                 per[r["Dispatch_Id"]] += float(r["Counter_Value"])
     v = sorted(per.values())
     vals[c] = v[len(v) // 2] if v else None
