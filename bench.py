@@ -1161,6 +1161,8 @@ def main():
         out = {"shards": run_shards, "snap": run_snap, "snapstream": run_snapstream, "commit": run_commit,
                "msg": run_msg, "restart": run_restart, "rewind": run_rewind}[a.workload](a, dist, rank, world, local)
     if rank == 0:
+        import resource   # this rank's peak host memory (synthetic inputs, pinned snapshot pool): for N-rank nodes
+        out["host_peak_rss_gib"] = round(resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / (1 << 20), 2)
         print(json.dumps(out), flush=True)
     if dist is not None:
         dist.destroy_process_group()
