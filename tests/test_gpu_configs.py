@@ -8,7 +8,9 @@
   (32 GiB, ~29 M frames: more than 2^24 frames, the segmented check spans
   many 1 GiB tile groups): every clean shard OK with its exact frame count,
   the corrupt shard's walpb.ErrCRCMismatch at its exact frame, no shard on
-  the one-by-one fallback; the oracle's full result on a sample of shards.
+  the one-by-one fallback; the faithful oracle's full result (ents digest
+  included) on a sample of shards, the optimised C restatement's full result
+  (every entry descriptor) on all the others.
 * configs[3]: snapshot files of 1-256 MiB (log-uniform) in one
   esnap_verify_packed call against or_loadsnap, corrupt files included.
 
@@ -116,8 +118,47 @@ def test_configs2_512_shards_x_64mib(ctx):
             g = W._collect(ctx, out[s], memoryview(sb), with_ents=False, shard=s)
             g.n_ents = out[s].n_ents
             _assert_result(ctx, g, o, sb, shard=s)
+        # every other shard's whole result against the optimised C restatement
+        # (orf_readall, pinned to the faithful or_readall by
+        # tests/test_cpu_baseline.py): the verdict fields and every entry
+        # descriptor (Data as offset + length into the shard, so equal views
+        # mean equal bytes)
+        _all_shards_vs_fast_oracle(ctx, blob, offs, lens, out, skip=set(sample))
     finally:
         d.free()
+
+
+_ENT_DT = np.dtype([("term", "<u8"), ("index", "<u8"), ("data_off", "<u8"), ("data_len", "<u8"), ("type", "<i4"),
+                    ("data_nil", "<i4")])
+
+
+def _all_shards_vs_fast_oracle(ctx, blob, offs, lens, out, skip):
+    raw = (C.c_char * len(blob)).from_buffer(blob)
+    base = C.addressof(raw)
+    checked = 0
+    for s in range(len(lens)):
+        if s in skip:
+            continue
+        fr = O.FastResult()
+        st = O.lib.orf_readall(C.c_void_p(base + int(offs[s])), int(lens[s]), 1, 8, C.byref(fr))
+        try:
+            assert st != O.IRREGULAR, s
+            r = out[s]
+            assert (r.status, r.fail_record, r.n_records, r.last_crc, r.enti, r.n_ents) == \
+                (fr.status, fr.fail_record, fr.n_records, fr.last_crc, fr.enti, fr.n_ents), s
+            assert (r.metadata_off, r.metadata_len) == (fr.metadata_off, fr.metadata_len), s
+            assert (r.has_state, r.state_term, r.state_vote, r.state_commit) == \
+                (fr.has_state, fr.state_term, fr.state_vote, fr.state_commit), s
+            n = int(fr.n_ents)
+            got = (L.EntryDesc * max(n, 1))()
+            assert L.lib.ewal_batch_copy_entries(ctx.handle, s, got, n) == n
+            want = np.frombuffer(C.string_at(fr.ents, n * _ENT_DT.itemsize) if n else b"", dtype=_ENT_DT)
+            assert np.array_equal(np.frombuffer(got, dtype=_ENT_DT)[:n], want), s
+            checked += 1
+        finally:
+            O.lib.orf_result_free(C.byref(fr))
+    del raw
+    assert checked == len(lens) - len(skip)
 
 
 def test_configs3_snapshots_1_to_256mib(ctx):
@@ -153,6 +194,52 @@ def test_configs3_snapshots_1_to_256mib(ctx):
                 assert (s.index, s.term, list(s.nodes[:s.n_nodes])) == (i + 1, 1, [1, 2, 3])
                 assert packed[s.data_off:s.data_off + s.data_len] == o["snap"]["data"]
         assert [i for i in range(len(files)) if st[i] != L.OK] == bad
+    finally:
+        d.free()
+
+
+def test_configs3_ten_k_distribution_sample(ctx):
+    """192 files drawn from configs[3]'s 10k-file size distribution
+    (log-uniform 1-256 MiB, ~9 GiB, ~2 % corrupt: a flipped byte in the body,
+    the stored CRC or the envelope) in one esnap_verify_packed call: every
+    file's verdict and computed CRC against the optimised C restatement
+    (orf_snap_verify_batch, pinned to or_loadsnap by
+    tests/test_cpu_baseline.py), the faithful or_loadsnap on 12 of them."""
+    rng, crng = random.Random(14), random.Random(15)
+    pool = np.random.default_rng(14).integers(0, 256, size=(256 << 20) + 4096, dtype=np.uint8).tobytes()
+    sizes = [int(math.exp(rng.uniform(math.log(1 << 20), math.log(256 << 20)))) for _ in range(192)]
+    offs, lens, pos = [], [], 0
+    for n in sizes:
+        offs.append(pos)
+        lens.append(n + 64)           # upper bound of the envelope; trimmed below
+        pos += (n + 64 + 15) & ~15
+    packed = bytearray(pos)
+    bad = []
+    for i, n in enumerate(sizes):
+        st = rng.randrange(0, len(pool) - n)
+        f = bytearray(S.snap_file(S.snapshot_marshal(pool[st:st + n], (1, 2, 3), i + 1, 1)))
+        if i in (5, 77, 150) or crng.random() < 0.02:
+            f[crng.choice([1, 3, len(f) // 2, len(f) - 1])] ^= 0x10   # stored CRC, envelope length, body
+            bad.append(i)
+        lens[i] = len(f)
+        packed[offs[i]:offs[i] + len(f)] = f
+    del pool
+    d = ctx.alloc(len(packed) + 64)
+    try:
+        raw = (C.c_char * len(packed)).from_buffer(packed)
+        d.upload_ptr(C.addressof(raw), len(packed))
+        st, sc, cc = S.verify_packed(d, len(packed), offs, lens)
+        fst, fcc = O.fast_snap_verify_batch(C.addressof(raw), offs, lens, 8)
+        assert st == fst
+        assert [cc[i] for i in range(len(sizes)) if st[i] == L.OK] == [fcc[i] for i in range(len(sizes)) if fst[i] == O.OK]
+        assert all(st[i] != L.OK for i in bad)
+        assert sum(1 for x in st if x != L.OK) == len(bad)
+        for i in sorted(set(bad[:6]) | set(random.Random(16).sample(range(len(sizes)), 6))):
+            o = O.loadsnap(bytes(packed[offs[i]:offs[i] + lens[i]]))
+            assert st[i] == o["status"], (i, st[i], o["status"])
+            if o["status"] in (O.OK, O.ERR_SNAP_CRC):
+                assert (sc[i], cc[i]) == (o["stored_crc"], o["computed_crc"]), i
+        del raw
     finally:
         d.free()
 
