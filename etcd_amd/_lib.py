@@ -119,7 +119,9 @@ class RangeInfo(C.Structure):   # ewal_range_info
                 ("min_entry_index", C.c_uint64), ("last_entry_index", C.c_uint64), ("last_op_frame", C.c_int64),
                 ("last_op_index", C.c_uint64), ("md_split", C.c_int32), ("first_pre_crc", C.c_int32),
                 ("first_type", C.c_int64), ("first_dlen", C.c_uint64), ("first_stored_crc", C.c_uint32),
-                ("first_u0", C.c_uint32), ("end_off", C.c_uint64), ("n_bytes", C.c_uint64)]
+                ("first_u0", C.c_uint32), ("end_off", C.c_uint64), ("n_bytes", C.c_uint64),
+                ("state_frame", C.c_int64), ("state_term", C.c_uint64), ("state_vote", C.c_uint64),
+                ("state_commit", C.c_uint64), ("state_unrec", C.c_int32), ("pad2", C.c_int32)]
 
 
 class RangeRow(C.Structure):    # ewal_range_row
@@ -131,7 +133,10 @@ class RangeRow(C.Structure):    # ewal_range_row
 class SplitResult(C.Structure):  # ewal_split_result
     _fields_ = [("status", C.c_int32), ("resplit", C.c_int32), ("fail_record", C.c_int64),
                 ("n_records", C.c_int64), ("detail", C.c_int64), ("last_crc", C.c_uint32), ("pad", C.c_uint32),
-                ("enti", C.c_uint64)]
+                ("enti", C.c_uint64), ("md_range", C.c_int32), ("md_split", C.c_int32), ("md_off", C.c_int64),
+                ("md_len", C.c_int64), ("md_blob_off", C.c_int64), ("state_range", C.c_int32), ("pad2", C.c_int32),
+                ("state_term", C.c_uint64), ("state_vote", C.c_uint64), ("state_commit", C.c_uint64),
+                ("n_ents", C.c_int64)]
 
 
 class SnapshotDesc(C.Structure):
@@ -178,6 +183,25 @@ _SIGS = {
     "ewal_readall_multi": (C.c_int, [C.POINTER(vp), C.c_uint32, vp, C.c_uint64, C.POINTER(C.c_uint64),
                                      C.POINTER(C.c_uint64), C.c_uint32, C.c_uint64, C.POINTER(SplitResult),
                                      C.POINTER(C.c_uint32)]),
+    "ewal_split_ents_layout": (C.c_int64, [C.POINTER(RangeRow), C.c_uint64, C.c_uint64, C.POINTER(C.c_int64),
+                                           C.POINTER(C.c_int64)]),
+    "ewal_range_probe_aligned": (C.c_int, [vp, vp, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint32,
+                                           C.POINTER(C.c_int64), C.POINTER(C.c_int64)]),
+    "ewal_multi_create": (C.c_int, [C.POINTER(vp), C.c_uint32, C.POINTER(vp)]),
+    "ewal_multi_destroy": (None, [vp]),
+    "ewal_multi_readall": (C.c_int, [vp, vp, C.c_uint64, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.c_uint32,
+                                     C.c_uint64, C.POINTER(SplitResult)]),
+    "ewal_multi_readall_device": (C.c_int, [vp, C.POINTER(vp), C.POINTER(C.c_uint64), C.POINTER(C.c_uint64),
+                                            C.POINTER(C.c_uint32), C.c_uint64, C.POINTER(SplitResult)]),
+    "ewal_multi_plan_device": (C.c_int, [vp, vp, C.c_uint64, C.c_uint64, C.POINTER(C.c_uint64),
+                                         C.POINTER(C.c_uint64)]),
+    "ewal_multi_copy_entries": (C.c_int64, [vp, C.POINTER(EntryDesc), C.c_int64]),
+    "ewal_multi_copy_metadata": (C.c_int64, [vp, vp, C.c_int64]),
+    "ewal_multi_copy_split_bytes": (C.c_int64, [vp, vp, C.c_int64]),
+    "ewal_multi_copy_unrec": (C.c_int64, [vp, C.POINTER(UnrecDesc), C.c_int64]),
+    "ewal_multi_copy_unrec_bytes": (C.c_int64, [vp, vp, C.c_int64]),
+    "ewal_multi_copy_rows": (C.c_int, [vp, C.POINTER(RangeRow), C.POINTER(C.c_uint64), C.c_uint32]),
+    "ewal_multi_timing": (C.c_int, [vp, C.POINTER(C.c_double)]),
     "ewal_copy_unrec": (C.c_int64, [vp, C.POINTER(UnrecDesc), C.c_int64]),
     "ewal_copy_unrec_bytes": (C.c_int64, [vp, vp, C.c_int64]),
     "ewal_copy_split_bytes": (C.c_int64, [vp, vp, C.c_int64]),
@@ -209,10 +233,6 @@ _SIGS = {
     "ewal_encoder_bytes": (u8p, [vp, C.POINTER(C.c_uint64)]),
     "ewal_encoder_crc": (C.c_uint32, [vp]),
     "ewal_encoder_free": (None, [vp]),
-    "ewal_synth_wal": (C.c_int64, [C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint32, C.c_int64, vp, C.c_uint64,
-                                   C.POINTER(C.c_int64)]),
-    "ewal_synth_wal_ex": (C.c_int64, [C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint32, C.c_int64, C.c_uint32, vp,
-                                      C.c_uint64, C.POINTER(C.c_int64), C.POINTER(C.c_uint64)]),
     "ewal_encode_entries_device": (C.c_int, [vp, vp, C.c_uint64, vp, C.c_uint64, C.c_uint32, vp, C.c_uint64,
                                              C.POINTER(C.c_uint64), C.POINTER(C.c_uint32)]),
     "ewal_save_device": (C.c_int, [vp, vp, C.c_uint64, vp, C.c_uint64, C.c_uint32, vp, C.c_uint64,
@@ -234,6 +254,24 @@ for _name, (_res, _args) in _SIGS.items():
     _f = getattr(lib, _name)
     _f.restype = _res
     _f.argtypes = _args
+
+
+_synth = None
+
+
+def synth_lib():
+    """libewal_synth.so (include/ewal_synth.h): the synthetic-WAL generator of
+    bench.py and the tests -- plumbing, not part of the product library."""
+    global _synth
+    if _synth is None:
+        _synth = C.CDLL(os.path.join(_HERE, "libewal_synth.so"))
+        _synth.ewal_synth_wal.restype = C.c_int64
+        _synth.ewal_synth_wal.argtypes = [C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint32, C.c_int64, vp, C.c_uint64,
+                                          C.POINTER(C.c_int64)]
+        _synth.ewal_synth_wal_ex.restype = C.c_int64
+        _synth.ewal_synth_wal_ex.argtypes = [C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint32, C.c_int64, C.c_uint32,
+                                             vp, C.c_uint64, C.POINTER(C.c_int64), C.POINTER(C.c_uint64)]
+    return _synth
 
 
 def header_symbols(path=HEADER):

@@ -18,7 +18,9 @@ struct StreamArgs {
   uint32_t *wcnt;          // candidates in the unit         [nunits]
   uint16_t *slots;         // first EW_SLOTS candidate offsets per unit
   unsigned long long *hmask;   // EW_SPLIT_CAND: per unit, the lanes (64-B pieces) the candidate filter flagged
-  Small *small;            // the call's device scratch, zeroed by k_stream's workgroup 0
+  Small *small;            // the call's device scratch, zeroed by k_stream's workgroup 0 (of the launch
+                           // that starts at unit 0)
+  uint32_t u_begin, u_end; // the units this launch covers (a chunk of the stream: u_begin even; all: 0, nunits)
 };
 
 struct ScanArgs {
@@ -137,6 +139,8 @@ struct FrAgg {
 };
 
 // Per-call device scratch (zeroed / initialised each call).
+#define EW_ERR_LOOKBACK 1u   // Small.errflag: k_check's look-back gave up waiting (EWAL_E_TIMEOUT)
+#define EW_ERR_LIST 2u       // Small.errflag: k_decode met a frame-list index past its capacity (EWAL_E_INVAL)
 struct Small {
   uint32_t ticket;
   uint32_t errflag;

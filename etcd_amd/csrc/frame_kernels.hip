@@ -115,6 +115,10 @@ struct FrArgs {
   // tiles of a batch's rewinding shards
   const uint32_t *tlist;
   uint32_t ntl;
+  // without tlist: the tiles [t0, t0 + nrun) (nrun 0: all ntiles) -- a chunk
+  // of the stream whose stream pass has completed (the overlapped pipeline)
+  uint32_t t0, nrun;
+  uint32_t *tick;                  // this launch's tile counter (zeroed before it)
 };
 struct FrSeg {
   uint32_t ns;
@@ -397,16 +401,17 @@ __global__ __launch_bounds__(FR_THREADS, 1) void k_frames(FrArgs a, FrSeg sg) {
   uint32_t *w = s_win + tid;
   uint32_t rare = 0, irr = 0, rews = 0;   // rews: rewind mode met an index rewind
   unsigned long long need_ecap = 0;
-  const uint32_t nt_run = a.tlist ? a.ntl : a.ntiles;
+  const uint32_t nt_run = a.tlist ? a.ntl : (a.nrun ? a.nrun : a.ntiles);
   // every wave's first tile is its id; the rest are handed out by a counter
   // (tiles differ in work: a static stride leaves the waves uneven)
+  uint32_t *tick = a.tick ? a.tick : &ds->fr_tick;
   auto next_tile = [&]() {
     uint32_t nx = 0;
-    if (lane == 0) nx = nwaves + atomicAdd(&ds->fr_tick, 1u);
+    if (lane == 0) nx = nwaves + atomicAdd(tick, 1u);
     return rl32(nx, 0);
   };
   for (uint32_t ti = wid; ti < nt_run; ti = next_tile()) {
-    const uint32_t t = a.tlist ? a.tlist[ti] : ti;
+    const uint32_t t = a.tlist ? a.tlist[ti] : a.t0 + ti;
     const uint32_t u0 = t * TU;
     const uint64_t ts = (uint64_t)u0 * EW_WAVE_BYTES;
     // ---- A: the tile's unit lins, P at every unit start (tile-local) ----
@@ -1377,6 +1382,74 @@ __global__ __launch_bounds__(256) void k_ents_fix(const uint8_t *__restrict__ bu
     const uint64_t base = soff ? soff[pos_shard_in(soff, 0, ns, p)] : 0ull;   // batch: Data relative to the shard
     ents[k] = ewal_entry{d.f0, d.f1, d.edoff - base, d.edlen, d.etype, (int32_t)d.enil};
   }
+}
+
+// ---- batch rewinds -------------------------------------------------------------
+// A batched shard whose entry indexes go back (a leader change:
+// ents = append(ents[:Index-ri], e), wal/wal.go:170-173) comes out of the
+// batch's frame pass with every verdict field right -- the reductions are by
+// stream position and a rewind is no gap -- except the ents slots written by
+// more than one op: the waves store in no fixed order, and the slot must hold
+// the LAST op's entry.  k_rew_claim walks the rewinding shards again at
+// 64 KiB tiles (one wave per tile, many tiles per shard): the flagged pieces,
+// the exact candidate tests, each candidate's canonical fields (no CRC, no
+// prefixes -- the first pass checked them) and, per entry op, a claim of its
+// slot with atomicMax(own, position + 1); the slots claimed twice are listed
+// for k_ents_fix.  smask: the shards to claim for (1 byte each).
+#define REW_TU 16   // units per claim tile (64 KiB)
+__global__ __launch_bounds__(256) void k_rew_claim(const uint8_t *__restrict__ buf, uint64_t B, uint32_t nunits,
+                                                   const ulonglong2 *__restrict__ hmask,
+                                                   const uint32_t *__restrict__ tlist, uint32_t ntl,
+                                                   const uint64_t *__restrict__ soff, uint32_t ns,
+                                                   const uint64_t *__restrict__ ri, const uint64_t *__restrict__ rbase,
+                                                   const uint8_t *__restrict__ smask,
+                                                   unsigned long long *__restrict__ own, uint32_t *__restrict__ clist,
+                                                   uint32_t ccap, Small *ds) {
+  __shared__ uint4 s_w[256][6];
+  const int lane = threadIdx.x & 63;
+  const uint32_t wid = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, nw = (gridDim.x * blockDim.x) >> 6;
+  uint32_t over = 0;
+  for (uint32_t ti = wid; ti < ntl; ti += nw) {   // (wave-uniform)
+    const uint32_t u0 = tlist[ti] * REW_TU;
+    const uint32_t u = u0 + (uint32_t)lane;
+    const bool in = lane < REW_TU && u < nunits;
+    const ulonglong2 h = in ? hmask[u] : make_ulonglong2(0ull, 0ull);
+    const uint32_t c = (uint32_t)__popcll(h.x);
+    const uint32_t incl = wave_incl_sum(c);
+    const uint32_t Tf = rl32(incl, 63);
+    for (uint32_t g0 = 0; g0 < Tf; g0 += 64) {
+      const uint32_t g = g0 + (uint32_t)lane;
+      const uint32_t gg = g < Tf ? g : Tf - 1;
+      const int ol = owner_lane(incl, gg);
+      const uint32_t r = gg - ((uint32_t)__shfl((int)incl, ol) - (uint32_t)__shfl((int)c, ol));
+      const unsigned long long mx = shfl64(h.x, ol), m3 = shfl64(h.y, ol);
+      if (g >= Tf) continue;
+      const uint32_t pc = nth_bit(mx, r);
+      const uint64_t poff = (uint64_t)(u0 + (uint32_t)ol) * EW_WAVE_BYTES + (uint64_t)pc * EW_PIECE;
+      uint32_t D[19];
+      if ((m3 >> pc) & 1ull) load_piece80(buf, B, poff, D);
+      else load_piece64(buf, B, poff, D);
+      const uint32_t fm = cand_filter(D);
+      unsigned long long cm = fm ? cand_bits(D, fm, poff, B) : 0ull;
+      while (cm) {
+        const uint64_t p = poff + (uint64_t)__builtin_ctzll(cm);
+        cm &= cm - 1;
+        const uint32_t sh = pos_shard_in(soff, 0, ns, p);
+        if (!smask[sh]) continue;
+        const int64_t L = (int64_t)ld_le64_b(buf, B, p);
+        if (L < 0 || p + 8 + (uint64_t)L > soff[sh + 1]) continue;   // torn: decoder.decode's terminal, no op
+        const RecDesc d = fc_frame_fields(buf, B, p, s_w[threadIdx.x]);
+        if (d.st || d.sub_st || d.type != 2 || d.f1 < ri[sh]) continue;
+        const uint64_t k = d.f1 - ri[sh], rb = rbase[sh];
+        if (k >= rbase[sh + 1] - rb) continue;
+        if (atomicMax(&own[rb + k], (unsigned long long)(p + 1))) {   // a slot claimed twice
+          const uint32_t ci = atomicAdd(&ds->fr_ncl, 1u);
+          if (ci < ccap) clist[ci] = (uint32_t)(rb + k); else over = 1u;
+        }
+      }
+    }
+  }
+  if (over) atomicOr(&ds->fc.rare, 64u);
 }
 
 // ---- batch (ewal_readall_batch_device) ----------------------------------------

@@ -425,7 +425,7 @@ __global__ __launch_bounds__(EW_THREADS, 1) void k_stream(StreamArgs a) {
   __shared__ uint32_t s_s64[1024], s_s128[1024];   // S_64, S_128 byte tables (super-piece tree)
   const int tid = threadIdx.x, lane = tid & 63;
   static_assert(sizeof(Small) % 4 == 0 && sizeof(Small) / 4 <= EW_THREADS, "Small is zeroed by one workgroup");
-  if (blockIdx.x == 0 && tid < (int)(sizeof(Small) / 4)) ((uint32_t *)a.small)[tid] = 0u;   // the call's scratch
+  if (blockIdx.x == 0 && a.u_begin == 0 && tid < (int)(sizeof(Small) / 4)) ((uint32_t *)a.small)[tid] = 0u;   // the call's scratch
   uint32_t Lt[4];
   lane_regs(lane, Lt);
   const uint64_t B = a.B;
@@ -433,7 +433,9 @@ __global__ __launch_bounds__(EW_THREADS, 1) void k_stream(StreamArgs a) {
   const uint32_t wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const uint32_t p0 = blockIdx.x * EW_WAVES + wv;
   const uint32_t nsafe = B >= 16 ? (uint32_t)std::min<uint64_t>(a.nunits, (B - 16) / EW_WAVE_BYTES) : 0u;
-  const uint32_t NP = nsafe / 2;   // pairs whose units are both safe
+  // pairs whose units are both safe, inside this launch's units [u_begin, u_end)
+  const uint32_t PB = a.u_begin / 2;
+  const uint32_t NP = std::max(PB, std::min(nsafe / 2, a.u_end / 2));
   // Unit loads are fully coalesced: load r covers unit bytes [1024 r, 1024 r + 1024)
   // with lane (g, m) = (lane >> 4, lane & 15) taking chunk g of piece 16 r + m
   // (a permutation inside the 1 KiB row, measured as fast as the plain order).
@@ -472,9 +474,9 @@ __global__ __launch_bounds__(EW_THREADS, 1) void k_stream(StreamArgs a) {
     const uint32_t uu[2] = {2 * p, 2 * p + 1};
     stream_units<2, FIND>(a, s_slice, s_s64, s_s128, Lt, uu, T);
   };
-  const uint32_t npairs = p0 < NP ? (NP - 1 - p0) / W + 1 : 0u;
+  const uint32_t npairs = PB + p0 < NP ? (NP - 1 - PB - p0) / W + 1 : 0u;
   auto pair_at = [&](uint32_t k) {   // clamped: a prefetch past the end reloads the last pair
-    return __builtin_amdgcn_readfirstlane(p0 + W * (k < npairs ? k : npairs - 1));
+    return __builtin_amdgcn_readfirstlane(PB + p0 + W * (k < npairs ? k : npairs - 1));
   };
   uint32_t DA[2][19], DB[2][19], DC[2][19];
   ew_v3u nA, nB, nC;
@@ -500,7 +502,7 @@ __global__ __launch_bounds__(EW_THREADS, 1) void k_stream(StreamArgs a) {
     __builtin_amdgcn_sched_barrier(0);
     run_pair(pair_at(k + 2), DC, nC);
   }
-  for (uint32_t u = 2 * NP + p0; u < a.nunits; u += W) {
+  for (uint32_t u = std::max(2 * NP, a.u_begin) + p0; u < a.u_end; u += W) {
     const uint64_t off = (uint64_t)u * EW_WAVE_BYTES + (uint64_t)lane * EW_PIECE;
     uint32_t D1[1][19];
     load_piece(a.buf, B, off, D1[0]);
@@ -1989,9 +1991,14 @@ __device__ __forceinline__ int64_t decode_fast(const uint8_t *__restrict__ buf, 
 }
 
 // k_decode: the frames of a chain the host framed (frame r = candidate
-// rec_cand[r], or candidate r when rec_cand is null).
+// rec_cand[r], or candidate r when rec_cand is null).  Every list index is
+// checked against the list's capacity (pcap, rccap) and every position
+// against B: a frame list that breaks the host's invariant raises
+// Small.errflag bit EW_ERR_LIST (the call fails with EWAL_E_INVAL) instead of
+// reading out of bounds.
 __global__ __launch_bounds__(256) void k_decode(const uint8_t *__restrict__ buf, uint64_t B,
-                         const uint64_t *__restrict__ pos, const uint32_t *__restrict__ rec_cand, uint32_t n,
+                         const uint64_t *__restrict__ pos, uint64_t pcap, const uint32_t *__restrict__ rec_cand,
+                         uint64_t rccap, uint32_t n,
                          const uint32_t *__restrict__ pwave, const uint32_t *__restrict__ v,
                          const uint32_t *__restrict__ g_slice, const uint32_t *__restrict__ g_shift,
                          RecDesc *__restrict__ rd, uint32_t *__restrict__ pfd, uint32_t *__restrict__ pfo,
@@ -2004,8 +2011,18 @@ __global__ __launch_bounds__(256) void k_decode(const uint8_t *__restrict__ buf,
   __syncthreads();
   const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= n) return;
-  decode_fast(buf, B, pos[rec_cand ? rec_cand[r] : r], r, r == n - 1, pwave, v, s_t4, s_svp, s_win + threadIdx.x, rd, pfd, pfo,
-              slow, ds);
+  const uint64_t ix = rec_cand ? (r < rccap ? (uint64_t)rec_cand[r] : ~0ull) : (uint64_t)r;
+  const uint64_t p = ix < pcap ? pos[ix] : ~0ull;
+  if (p >= B) {
+    atomicOr(&ds->errflag, EW_ERR_LIST);
+    RecDesc d{};
+    d.off = 0;
+    d.type = 0;
+    d.st = EWAL_ERR_UNEXPECTED_EOF;
+    rd[r] = d;
+    return;
+  }
+  decode_fast(buf, B, p, r, r == n - 1, pwave, v, s_t4, s_svp, s_win + threadIdx.x, rd, pfd, pfo, slow, ds);
 }
 
 // k_frame: framing and decode in one pass, speculating that the candidates
@@ -2664,10 +2681,10 @@ __global__ void k_records_out(const RecDesc *__restrict__ rd, uint32_t n, ewal_r
 // over the chain's frames.  Maxima are folded as frame + 1 (0: none).
 struct RangeDev {
   unsigned long long md_first, md_value, ent_first, min_index;   // min (~0: none)
-  unsigned long long ent_last1, op_last1;                        // max (0: none)
+  unsigned long long ent_last1, op_last1, st_last1;              // max (0: none)
 };
 __global__ void k_range_info(const RecDesc *__restrict__ rd, uint32_t n, uint64_t ri, RangeDev *o) {
-  unsigned long long mf = ~0ull, mv = ~0ull, ef = ~0ull, mi = ~0ull, el = 0, ol = 0;
+  unsigned long long mf = ~0ull, mv = ~0ull, ef = ~0ull, mi = ~0ull, el = 0, ol = 0, sl = 0;
   for (uint32_t r = blockIdx.x * blockDim.x + threadIdx.x; r < n; r += gridDim.x * blockDim.x) {
     const RecDesc &d = rd[r];
     if (d.type == 1) {
@@ -2678,8 +2695,11 @@ __global__ void k_range_info(const RecDesc *__restrict__ rd, uint32_t n, uint64_
       el = max(el, (unsigned long long)r + 1);
       if (d.f1 >= ri) ol = max(ol, (unsigned long long)r + 1);
       mi = min(mi, (unsigned long long)d.f1);
+    } else if (d.type == 3) {
+      sl = max(sl, (unsigned long long)r + 1);
     }
   }
+  if (sl) atomicMax(&o->st_last1, sl);
   if (mf != ~0ull) atomicMin(&o->md_first, mf);
   if (mv != ~0ull) atomicMin(&o->md_value, mv);
   if (ef != ~0ull) atomicMin(&o->ent_first, ef);
@@ -2700,10 +2720,10 @@ __global__ void k_reverse_u64(const uint64_t *__restrict__ in, uint64_t *__restr
 // 08 <type<0x80> 10, record.pb.go:175-196), one position per thread -> the
 // minimum in *pos (~0: none in the window).
 __global__ void k_probe_cand(const uint8_t *__restrict__ buf, uint64_t B, uint64_t from, uint64_t end,
-                             unsigned long long *pos) {
+                             uint32_t align, unsigned long long *pos) {
   for (uint64_t p = from + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; p < end;
        p += (uint64_t)gridDim.x * blockDim.x) {
-    if (p + 11 > B || buf[p + 8] != 0x08 || buf[p + 9] >= 0x80 || buf[p + 10] != 0x10) continue;
+    if ((p & (align - 1)) || p + 11 > B || buf[p + 8] != 0x08 || buf[p + 9] >= 0x80 || buf[p + 10] != 0x10) continue;
     const int64_t L = (int64_t)ld_le64_b(buf, B, p);
     if (L >= 4 && (uint64_t)L <= B - p - 8) atomicMin(pos, (unsigned long long)p);
   }

@@ -16,6 +16,8 @@ def pack_groups(match, nvoters, committed, term, log_offset, log_ptr, log_terms)
     array whose rows are ecommit_group records."""
     match = np.asarray(match, dtype=np.uint64)
     G = match.shape[1]
+    nvoters = np.asarray(nvoters)
+    assert int(nvoters.max(initial=0)) <= min(7, match.shape[0]), "at most 7 voters, all present in match"
     rec = np.zeros((G, RECORD_WORDS), dtype=np.uint64)
     nv = min(7, match.shape[0])
     rec[:, :nv] = match[:nv].T
@@ -24,6 +26,7 @@ def pack_groups(match, nvoters, committed, term, log_offset, log_ptr, log_terms)
     rec[:, 9] = log_offset
     lp = np.asarray(log_ptr, dtype=np.uint64)
     nlog = (lp[1:] - lp[:-1]).astype(np.uint64)
+    assert int(nlog.max(initial=0)) < 1 << 32, "nlog shares word 10 with nvoters: it must fit 32 bits"
     rec[:, 10] = nlog | (np.asarray(nvoters, dtype=np.uint64) << np.uint64(32))
     lt = np.asarray(log_terms, dtype=np.uint64)
     for k in range(TAIL):

@@ -165,6 +165,9 @@ def range_row(result, info, ri_range: int, deferred: bool = False):
     i.first_pre_crc = 1 if info.get("first_pre_crc") else 0
     i.n_bytes = info["n_bytes"]
     i.end_off = info.get("end_off", info["n_bytes"])
+    i.state_frame = info.get("state_frame", -1)
+    i.state_term, i.state_vote, i.state_commit = [x & _U64 for x in info.get("state", (0, 0, 0))]
+    i.state_unrec = 1 if info.get("state_unrec") else 0
     blob = b""
     i.md_first_off, i.md_first_len = -1, 0
     if info["md_first_frame"] >= 0 and mdf is not None:
@@ -191,8 +194,36 @@ def join_rows(rows, blobs, ri_global: int):
     return out.status, out.fail_record, out.n_records, out.resplit
 
 
+def join_rows_full(rows, blobs, ri_global: int):
+    """ewal_split_verdict over the rows with the rest of ReadAll's result:
+    dict(status, fail_record, n_records, resplit, last_crc, enti, metadata
+    (bytes, None == nil), state ((term, vote, commit), None == HardState{}),
+    n_ents, layout = [(base, count)] per range: range k's ents are the joined
+    ents [base, base + count) (ewal_split_ents_layout))."""
+    from . import _lib
+    import ctypes as C
+    arr = (_lib.RangeRow * len(rows))(*rows)
+    md = b"".join(blobs)
+    out = _lib.SplitResult()
+    rc = _lib.lib.ewal_split_verdict(arr, len(rows), ri_global & _U64, md, len(md), C.byref(out))
+    if rc != 0:
+        raise RuntimeError("ewal_split_verdict: %d" % rc)
+    ok = out.status == _lib.OK and out.resplit < 0
+    base = (C.c_int64 * len(rows))()
+    cnt = (C.c_int64 * len(rows))()
+    if ok:
+        n = _lib.lib.ewal_split_ents_layout(arr, len(rows), ri_global & _U64, base, cnt)
+        if n < 0:
+            raise RuntimeError("ewal_split_ents_layout: %d" % n)
+    metadata = md[out.md_blob_off:out.md_blob_off + out.md_len] if ok and out.md_range >= 0 else None
+    state = (out.state_term, out.state_vote, out.state_commit) if ok and out.state_range >= 0 else None
+    return dict(status=out.status, fail_record=out.fail_record, n_records=out.n_records, resplit=out.resplit,
+                last_crc=out.last_crc, enti=out.enti, metadata=metadata, state=state,
+                n_ents=out.n_ents if ok else 0, layout=list(zip(base, cnt)))
+
+
 def split_verdict(dist, world: int, rank: int, result, info, ri_range: int, ri_global: int, device="cpu",
-                  deferred: bool = False):
+                  deferred: bool = False, full: bool = False):
     """ReadAll's verdict (wal/wal.go:164-216) for ONE WAL split into
     contiguous ranges, range r read by rank r: by file (every range but the
     first opens with a crcType record carrying the running CRC,
@@ -208,7 +239,9 @@ def split_verdict(dist, world: int, rank: int, result, info, ri_range: int, ri_g
     global frame ordinal of the first failure or -1, frames verified,
     resplit); resplit = k >= 0: ranges k.. must be read joined and the call
     repeated (a frame cut short at range k's end, bytes it left unconsumed, a
-    rewind below a range's w.ri) -- status is not final then."""
+    rewind below a range's w.ri) -- status is not final then.  full=True
+    returns join_rows_full's dict instead: the metadata, the HardState,
+    len(ents) and where every rank's ents land in the joined ents."""
     import ctypes as C
     row, blob = range_row(result, info, ri_range, deferred)
     raw = bytes(C.string_at(C.addressof(row), C.sizeof(row)))
@@ -226,4 +259,4 @@ def split_verdict(dist, world: int, rank: int, result, info, ri_range: int, ri_g
     allb = [torch.zeros(width, dtype=torch.uint8, device=device) for _ in range(world)]
     dist.all_gather(allb, t)
     blobs = [bytes(x.cpu().numpy().tobytes())[:lens[k]] for k, x in enumerate(allb)]
-    return join_rows(rows, blobs, ri_global)
+    return join_rows_full(rows, blobs, ri_global) if full else join_rows(rows, blobs, ri_global)

@@ -315,30 +315,150 @@ def records(ctx: Context, n: int):
                  chained_crc=x.chained_crc) for x in arr[:k]]
 
 
-def readall_multi(ctxs, buf, ri=0, files=None):
-    """ewal_readall_multi: ReadAll over ONE WAL (host bytes `buf`) split
-    across the contexts `ctxs` in this process, one host thread per ctx.
-    files = [(length, name index)] splits it by file (every range a run of
-    whole files), None inside the stream (ranges opening at frame-start
-    candidates, frame 0's check deferred).  Returns (status, fail_record or
-    -1, n_records, last_crc, enti, resplits)."""
-    arr = (C.c_void_p * len(ctxs))(*[c.handle.value for c in ctxs])
-    offs = idx = None
-    nf = 0
-    if files is not None:
-        nf = len(files)
-        o = [0]
-        for n, _ in files:
-            o.append(o[-1] + n)
-        offs = (C.c_uint64 * (nf + 1))(*o)
-        idx = (C.c_uint64 * nf)(*[i & ((1 << 64) - 1) for _, i in files])
-    out = L.SplitResult()
-    nr = C.c_uint32(0)
-    b = bytes(buf)
-    rc = lib.ewal_readall_multi(arr, len(ctxs), b, len(b), offs, idx, nf, ri, C.byref(out), C.byref(nr))
-    if rc < 0:
-        check(rc)
-    return out.status, out.fail_record, out.n_records, out.last_crc, out.enti, nr.value
+class Multi:
+    """ewal_multi: (*WAL).ReadAll over ONE WAL split across the contexts
+    `ctxs` of this process (distinct ctxs; they may share a device), one host
+    thread per ctx, returning ReadAll's whole result -- verdict, metadata,
+    HardState and the ents joined across the ranges (wal/wal.go:164-216, the
+    caller etcdserver/server.go:153-168)."""
+
+    def __init__(self, ctxs):
+        arr = (C.c_void_p * len(ctxs))(*[c.handle.value for c in ctxs])
+        h = C.c_void_p()
+        check(lib.ewal_multi_create(arr, len(ctxs), C.byref(h)))
+        self._h = h
+        self.ctxs = list(ctxs)
+        self.resplit = -1
+
+    def close(self):
+        if self._h:
+            lib.ewal_multi_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def readall(self, buf, ri=0, files=None, with_ents=True) -> ReadAllResult:
+        """From host bytes; files = [(length, name index)] splits by file,
+        None inside the stream (ranges at frame-start candidates)."""
+        offs = idx = None
+        nf = 0
+        if files is not None:
+            nf = len(files)
+            o = [0]
+            for n, _ in files:
+                o.append(o[-1] + n)
+            offs = (C.c_uint64 * (nf + 1))(*o)
+            idx = (C.c_uint64 * nf)(*[i & ((1 << 64) - 1) for _, i in files])
+        out = L.SplitResult()
+        b = bytes(buf)
+        rc = lib.ewal_multi_readall(self._h, b, len(b), offs, idx, nf, ri & ((1 << 64) - 1), C.byref(out))
+        if rc < 0:
+            check(rc)
+        return self._result(out, memoryview(b), with_ents)
+
+    def plan_device(self, dbuf: DeviceBuffer, n: int, ri=0):
+        """ewal_multi_plan_device: range starts (n_ctx + 1) and w.ri per range
+        of the device-resident stream dbuf[0, n)."""
+        k = len(self.ctxs)
+        st = (C.c_uint64 * (k + 1))()
+        ris = (C.c_uint64 * k)()
+        check(lib.ewal_multi_plan_device(self._h, dbuf.ptr, n, ri & ((1 << 64) - 1), st, ris))
+        return list(st), list(ris)
+
+    def readall_device(self, dbuf: DeviceBuffer, n: int, ri=0, plan=None, host_view=None,
+                       with_ents=False) -> ReadAllResult:
+        """Device-resident: range r = dbuf[starts[r], starts[r + 1]) read by
+        ctx r in place (ewal_multi_readall_device); plan = plan_device's
+        answer (computed here when None).  host_view: the same bytes on the
+        host, for the ents' Data (with_ents)."""
+        starts, ris = plan if plan is not None else self.plan_device(dbuf, n, ri)
+        k = len(self.ctxs)
+        base = dbuf.ptr.value if isinstance(dbuf.ptr, C.c_void_p) else int(dbuf.ptr)
+        dr = (C.c_void_p * k)(*[base + starts[r] for r in range(k)])
+        st = (C.c_uint64 * (k + 1))(*starts)
+        rs = (C.c_uint64 * k)(*ris)
+        out = L.SplitResult()
+        rc = lib.ewal_multi_readall_device(self._h, dr, st, rs, None, ri & ((1 << 64) - 1), C.byref(out))
+        if rc < 0:
+            check(rc)
+        return self._result(out, host_view, with_ents and host_view is not None)
+
+    def timing(self):
+        t = (C.c_double * 4)()
+        check(lib.ewal_multi_timing(self._h, t))
+        return dict(wall_ms=t[0], max_range_device_ms=t[1], join_ms=t[2], resplits=int(t[3]))
+
+    def rows(self):
+        k = len(self.ctxs)
+        arr = (L.RangeRow * k)()
+        st = (C.c_uint64 * k)()
+        check(min(0, lib.ewal_multi_copy_rows(self._h, arr, st, k)))
+        return list(arr), list(st)
+
+    def _result(self, out, view, with_ents) -> ReadAllResult:
+        self.resplit = out.resplit
+        ok = out.status == L.OK
+        md = None
+        if ok and out.md_range >= 0:
+            n = max(out.md_len, 0)
+            raw = (C.c_char * max(n, 1))()
+            got = lib.ewal_multi_copy_metadata(self._h, raw, n)
+            check(0 if got >= 0 else int(got))
+            md = raw.raw[:n]
+        st = HardState(out.state_term, out.state_vote, out.state_commit) if (ok and out.state_range >= 0) \
+            else HardState()
+        ents = []
+        if ok and with_ents and out.n_ents:
+            arr = (L.EntryDesc * out.n_ents)()
+            n = lib.ewal_multi_copy_entries(self._h, arr, out.n_ents)
+            check(0 if n >= 0 else int(n))
+            side = None
+            for e in arr[:n]:
+                if e.data_nil == 2:
+                    if side is None:
+                        k = lib.ewal_multi_copy_split_bytes(self._h, None, 0)
+                        raw = (C.c_char * max(k, 1))()
+                        lib.ewal_multi_copy_split_bytes(self._h, raw, k)
+                        side = raw.raw[:k]
+                    data = side[e.data_off:e.data_off + e.data_len]
+                else:
+                    data = None if e.data_nil else bytes(view[e.data_off:e.data_off + e.data_len])
+                ents.append(Entry(e.type, e.term, e.index, data))
+        if ok:
+            nu = lib.ewal_multi_copy_unrec(self._h, None, 0)
+            check(0 if nu >= 0 else int(nu))
+            if nu:
+                arr = (L.UnrecDesc * nu)()
+                lib.ewal_multi_copy_unrec(self._h, arr, nu)
+                tot = lib.ewal_multi_copy_unrec_bytes(self._h, None, 0)
+                raw = (C.c_char * max(tot, 1))()
+                lib.ewal_multi_copy_unrec_bytes(self._h, raw, tot)
+                for a in arr[:nu]:
+                    b = raw.raw[a.off:a.off + a.len]
+                    if a.ent < 0:
+                        st.XXX_unrecognized = b
+                    elif a.ent < len(ents):
+                        ents[a.ent].XXX_unrecognized = b
+        keep_crc = ok or out.status == L.ERR_INDEX_NOT_FOUND
+        r = ReadAllResult(out.status, out.detail, out.fail_record, -1, out.n_records,
+                          out.last_crc if keep_crc else 0, out.enti, md, st, ents)
+        r.n_ents = out.n_ents
+        return r
+
+
+def readall_multi(ctxs, buf, ri=0, files=None, with_ents=True):
+    """ewal_multi_readall through a one-call Multi: ReadAll over ONE WAL (host
+    bytes `buf`) split across `ctxs`.  Returns (ReadAllResult, timing)."""
+    m = Multi(ctxs)
+    try:
+        r = m.readall(buf, ri, files, with_ents)
+        return r, m.timing()
+    finally:
+        m.close()
 
 
 def range_info(ctx: Context, stream=None, dbuf: DeviceBuffer = None):
@@ -365,7 +485,9 @@ def range_info(ctx: Context, stream=None, dbuf: DeviceBuffer = None):
                 last_entry_index=ri.last_entry_index, last_op_frame=ri.last_op_frame,
                 last_op_index=ri.last_op_index, first_type=ri.first_type, first_dlen=ri.first_dlen,
                 first_stored_crc=ri.first_stored_crc, first_u0=ri.first_u0, last_entry_frame=ri.last_entry_frame,
-                first_pre_crc=ri.first_pre_crc, end_off=ri.end_off, n_bytes=ri.n_bytes)
+                first_pre_crc=ri.first_pre_crc, end_off=ri.end_off, n_bytes=ri.n_bytes,
+                state_frame=ri.state_frame, state=(ri.state_term, ri.state_vote, ri.state_commit),
+                state_unrec=ri.state_unrec)
 
 
 class WAL:
@@ -601,7 +723,7 @@ def synth_wal(target_bytes, min_data=64, max_data=65536, seed=2, corrupt_record=
     out = bytearray(cap)
     nrec = C.c_int64(0)
     li = C.c_uint64(0)
-    n = lib.ewal_synth_wal_ex(seed, target_bytes, min_data, max_data, corrupt_record, rewind_per_mille,
+    n = L.synth_lib().ewal_synth_wal_ex(seed, target_bytes, min_data, max_data, corrupt_record, rewind_per_mille,
                               (C.c_char * cap).from_buffer(out), cap, C.byref(nrec), C.byref(li))
     if n < 0:
         check(int(n))
@@ -623,7 +745,7 @@ def synth_shards(seeds, target_bytes, min_data, max_data, corrupt=None):
     lens, nrec, pos = [], [], 0
     for i, sd in enumerate(seeds):
         nr = C.c_int64(0)
-        n = lib.ewal_synth_wal(sd, target_bytes, min_data, max_data, corrupt.get(i, -1), C.c_void_p(base + pos),
+        n = L.synth_lib().ewal_synth_wal(sd, target_bytes, min_data, max_data, corrupt.get(i, -1), C.c_void_p(base + pos),
                                per, C.byref(nr))
         if n < 0:
             check(int(n))

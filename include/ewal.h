@@ -263,6 +263,13 @@ typedef struct ewal_range_info {
   uint64_t end_off;              /* where the frame chain ended (decoder.decode's terminal): n_bytes when
                                     the range ended on a frame boundary */
   uint64_t n_bytes;              /* the range's length */
+  /* the range's last stateType frame (ReadAll's `state = mustUnmarshalState`,
+     wal/wal.go:176-177): the HardState the whole WAL returns when no later
+     range holds one */
+  int64_t state_frame;           /* -1: none */
+  uint64_t state_term, state_vote, state_commit;
+  int32_t state_unrec;           /* 1: that HardState carries XXX_unrecognized */
+  int32_t pad2;
 } ewal_range_info;
 int ewal_copy_range_info(ewal_ctx *ctx, ewal_range_info *out);
 
@@ -285,6 +292,11 @@ int ewal_readall_range_device(ewal_ctx *ctx, const void *d_buf, uint64_t len, ui
  * -1: none) -- the range's w.ri candidate. */
 int ewal_range_probe(ewal_ctx *ctx, const void *d_buf, uint64_t len, uint64_t from, uint64_t window, int64_t *pos,
                      int64_t *first_entry_index);
+/* The same, taking only candidates at positions that are multiples of align
+ * (a power of two): with 16 a range of a device-resident WAL starts on an
+ * address every kernel can read without a copy (ewal_multi_plan_device). */
+int ewal_range_probe_aligned(ewal_ctx *ctx, const void *d_buf, uint64_t len, uint64_t from, uint64_t window,
+                             uint32_t align, int64_t *pos, int64_t *first_entry_index);
 
 /* ---- ONE WAL over several ranges: ReadAll's verdict joined (host C++) ------
  * Range k of a WAL split into contiguous ranges (by file, or inside a file)
@@ -326,9 +338,26 @@ typedef struct ewal_split_result {
   uint32_t last_crc;             /* decoder.lastCRC() after the WAL (EWAL_OK) */
   uint32_t pad;
   uint64_t enti;                 /* w.enti: the last entry's Index (EWAL_OK) */
+  /* the rest of ReadAll's (metadata, state, ents) on EWAL_OK (wal/wal.go:206-215) */
+  int32_t md_range;              /* the range whose metadata Data ReadAll returns, -1: nil */
+  int32_t md_split;              /* 1: md_off indexes that range's split bytes, 0: its stream */
+  int64_t md_off, md_len;        /* the Data inside that range */
+  int64_t md_blob_off;           /* the same bytes inside the md blob given to ewal_split_verdict */
+  int32_t state_range;           /* the range whose last HardState ReadAll returns, -1: HardState{} */
+  int32_t pad2;
+  uint64_t state_term, state_vote, state_commit;
+  int64_t n_ents;                /* len(ents): ranges' ents stitched as ewal_split_ents_layout says */
 } ewal_split_result;
 int ewal_split_verdict(const ewal_range_row *rows, uint64_t n, uint64_t ri_global, const uint8_t *md, uint64_t md_len,
                        ewal_split_result *out);
+/* Where each range's ents land in the joined ents of a final EWAL_OK verdict
+ * (wal/wal.go:170-173, `ents = append(ents[:e.Index-w.ri], e)` carried across
+ * the ranges): range k's ents (its own ReadAll's, with w.ri = rows[k].ri) are
+ * joined ents [base[k], base[k] + count[k]), where base[k] = rows[k].ri - ri
+ * and count[k] is cut where a later range's base overwrites them; ranges
+ * without entry ops get count 0.  Returns len(ents) or a negative error. */
+int64_t ewal_split_ents_layout(const ewal_range_row *rows, uint64_t n, uint64_t ri_global, int64_t *base,
+                               int64_t *count);
 /* ReadAll over ONE WAL (the bytes of names[nameIndex:], h_buf, len) split
  * across n_ctx contexts in one process -- one host thread per context, each
  * on its own device or sharing one: by file when file_off (n_files + 1
@@ -343,6 +372,59 @@ int ewal_split_verdict(const ewal_range_row *rows, uint64_t n, uint64_t ri_globa
 int ewal_readall_multi(ewal_ctx *const *ctxs, uint32_t n_ctx, const void *h_buf, uint64_t len, const uint64_t *file_off,
                        const uint64_t *file_index, uint32_t n_files, uint64_t ri, ewal_split_result *out,
                        uint32_t *n_resplit);
+
+/* ---- ONE WAL over several contexts: ReadAll's whole result ---------------
+ * An ewal_multi drives n_ctx DISTINCT contexts (they may share a device; one
+ * ctx is never used from two threads) and keeps, after each call, what
+ * (*WAL).ReadAll returns over the whole stream (wal/wal.go:164-216, its
+ * caller etcdserver/server.go:153-168): the verdict in ewal_split_result
+ * (status, lastCRC, enti, the metadata's range and bytes, the HardState,
+ * len(ents)) and, on EWAL_OK, the joined ents, metadata, split bytes and
+ * XXX_unrecognized side list through the ewal_multi_copy_* calls -- which
+ * read the ranges' ReadAll state left on each ctx: no other call may run on
+ * those ctxs in between.  A ctx stays ordered with the legacy default stream
+ * (ewal_ctx_set_stream); on a shared device a ctx's blocking stream also
+ * waits for the others' null-stream allocations and copies, which is why the
+ * host path stages into each ctx's reusable buffer instead of allocating. */
+typedef struct ewal_multi ewal_multi;
+int ewal_multi_create(ewal_ctx *const *ctxs, uint32_t n_ctx, ewal_multi **out);
+void ewal_multi_destroy(ewal_multi *m);
+/* From host bytes (each range staged into its ctx's staging buffer), split as
+ * ewal_readall_multi says.  out->resplit is always -1 on return. */
+int ewal_multi_readall(ewal_multi *m, const void *h_buf, uint64_t len, const uint64_t *file_off,
+                       const uint64_t *file_index, uint32_t n_files, uint64_t ri, ewal_split_result *out);
+/* Device-resident ranges: range r is the bytes [starts[r], starts[r + 1]) of
+ * the stream, already in HBM at d_ranges[r] (16-B aligned) where ctx r reads
+ * them, read with w.ri = ris[r] and flags[r] (EWAL_RANGE_DEFER_FIRST for a
+ * range starting inside a file; flags NULL: every range but the first).  No
+ * allocation, no host copy of the WAL.  A joined re-read the verdict asks for
+ * runs on ctx k when ranges k.. form one contiguous device span; otherwise
+ * out->resplit = k comes back and the caller reads ranges k.. joined itself. */
+int ewal_multi_readall_device(ewal_multi *m, const void *const *d_ranges, const uint64_t *starts, const uint64_t *ris,
+                              const uint32_t *flags, uint64_t ri, ewal_split_result *out);
+/* Ranges of ONE device-resident stream d_buf[0, len) that every ctx of m can
+ * read (the contexts on d_buf's device): starts[0..n_ctx] (range r opens at a
+ * 16-B aligned frame-start candidate after r * len / n_ctx, found by
+ * ewal_range_probe_aligned on ctx r) and each range's w.ri; then
+ * d_ranges[r] = d_buf + starts[r] for ewal_multi_readall_device. */
+int ewal_multi_plan_device(ewal_multi *m, const void *d_buf, uint64_t len, uint64_t ri, uint64_t *starts,
+                           uint64_t *ris);
+/* After a final EWAL_OK: len(ents) entries joined in order (Data offsets into
+ * the whole stream, or into ewal_multi_copy_split_bytes for data_nil == 2),
+ * the metadata Data (returns its length; 0 with md_range -1: nil), the
+ * ranges' split bytes joined, the XXX_unrecognized side list (ent into the
+ * joined ents, -1 the HardState; sorted) and its bytes.  Each returns the
+ * total (entries, bytes) and copies min(cap, total). */
+int64_t ewal_multi_copy_entries(ewal_multi *m, ewal_entry *out, int64_t cap);
+int64_t ewal_multi_copy_metadata(ewal_multi *m, uint8_t *out, int64_t cap);
+int64_t ewal_multi_copy_split_bytes(ewal_multi *m, uint8_t *out, int64_t cap);
+int64_t ewal_multi_copy_unrec(ewal_multi *m, ewal_unrec *out, int64_t cap);
+int64_t ewal_multi_copy_unrec_bytes(ewal_multi *m, uint8_t *out, int64_t cap);
+/* The last call's ranges (rows and stream starts; returns n_ctx) and timing:
+ * out4 = {wall ms of the call, the slowest range's device ms, host ms in the
+ * join, joined re-reads}. */
+int ewal_multi_copy_rows(ewal_multi *m, ewal_range_row *out, uint64_t *starts, uint32_t cap);
+int ewal_multi_timing(ewal_multi *m, double *out4);
 
 /* ---- directory-level API: wal.OpenAtIndex + ReadAll + writer ----------- */
 typedef struct ewal_wal ewal_wal;
@@ -390,21 +472,6 @@ int ewal_encoder_save_state(ewal_encoder *e, uint64_t term, uint64_t vote, uint6
 const uint8_t *ewal_encoder_bytes(ewal_encoder *e, uint64_t *len);
 uint32_t ewal_encoder_crc(ewal_encoder *e);
 void ewal_encoder_free(ewal_encoder *e);
-
-/* Synthetic WAL generator used by bench.py (BASELINE.json configs):
- * Create(metadata) + Save(HardState{1,1,0}, ents) with entry Data sizes
- * log-uniform in [min_data, max_data], payload bytes from xorshift64*(seed),
- * until at least target_bytes.  Writes into out (cap bytes).  Optionally
- * flips one payload byte of record ordinal corrupt_record (-1 = none).
- * Returns bytes written; *n_records receives the frame count. */
-int64_t ewal_synth_wal(uint64_t seed, uint64_t target_bytes, uint32_t min_data, uint32_t max_data,
-                       int64_t corrupt_record, uint8_t *out, uint64_t cap, int64_t *n_records);
-/* The same with rewind_per_mille / 1000 of the entries opening a new
- * leader's term that rewrites the last 1..8 indexes (leader changes);
- * *last_index (nullable) = the last entry's Index. */
-int64_t ewal_synth_wal_ex(uint64_t seed, uint64_t target_bytes, uint32_t min_data, uint32_t max_data,
-                          int64_t corrupt_record, uint32_t rewind_per_mille, uint8_t *out, uint64_t cap,
-                          int64_t *n_records, uint64_t *last_index);
 
 /* ---- batched write path: (*WAL).SaveEntry / encoder.encode on the GPU ---- */
 /* encoder.encode(&walpb.Record{Type: entryType, Data: pbutil.MustMarshal(e)})

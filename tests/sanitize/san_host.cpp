@@ -16,6 +16,7 @@
 #include <vector>
 
 #include "../../include/ewal.h"
+#include "../../include/ewal_synth.h"
 
 extern "C" {
 // the device side of ewal_wal_readall / esnap_load_dir: no GPU here

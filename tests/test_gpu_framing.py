@@ -264,3 +264,27 @@ def test_entries_beyond_the_ternary_shift_span(ctx):
     bad[len(bad) * 2 // 3] ^= 0x01
     o, g = assert_parity(ctx, bad, 1)
     assert o["status"] != O.OK
+
+
+@pytest.mark.parametrize("tail", [struct.pack("<q", 3) + b"\x00\x01\x02",          # round 4's r04b shape
+                                  struct.pack("<q", 4) + b"\x08\x01\x10\x00",      # a whole frame, canonical head
+                                  struct.pack("<q", 12) + b"\x10\x05\x08\x02" + bytes(8),
+                                  struct.pack("<q", 3) + b"\x00\x01",              # torn: 2 of 3 bytes
+                                  struct.pack("<q", 0)])                            # zero length, nothing after
+def test_single_wal_trailing_frame_that_fits(ctx, tail):
+    """The single-WAL form of test_gpu_batch's t3 shard: a WAL ending in a
+    length prefix whose frame fits in the bytes left (decoder.decode then
+    Unmarshals it, wal/decoder.go:30-47).  The frame pass declines such a
+    terminal (fc.rare 128) and the general path walks it; both option
+    settings must give the oracle's verdict, never an infrastructure error."""
+    rng = random.Random(len(tail) * 7 + (tail[-1] if tail[8:] else 5))
+    base = build_wal(rng, 40, 700, big_terms=False)
+    for general in (False, True):
+        ctx.set_options(general_path=general)
+        try:
+            assert_parity(ctx, base + tail, 0, check_chain=False)
+            # and behind a WAL long enough for the 64 KiB / 1 MiB tile sizes
+            big = build_wal(rng, 1500, 3000, big_terms=False)
+            assert_parity(ctx, big + tail, 0, check_chain=False)
+        finally:
+            ctx.set_options(general_path=False)

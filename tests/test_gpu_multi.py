@@ -1,5 +1,5 @@
-"""ONE WAL split over several contexts in one process (ewal_readall_multi,
-VERDICT r03 #3): one host thread per ctx -- here 2 and 3 ctxs on device 0 --
+"""ONE WAL split over several contexts in one process (ewal_multi_readall /
+ewal_multi_readall_device): one host thread per ctx -- here 2 and 3 ctxs on device 0 --
 each reading its range (whole files, or a range opening at a frame-start
 candidate inside a file with frame 0's check deferred), and ReadAll's
 cross-range rules joined in the C ABI (ewal_split_verdict, the join
@@ -8,7 +8,11 @@ joined verdict must be the oracle's ReadAll over the whole WAL, on clean and
 on damaged WALs (test_gpu_fuzz's mutations), and on the two cases ADVICE r03
 found in the Python join: a range whose frame 0 fails its Entry decode (that
 comes after decoder.decode's CRC check, so the deferred CRC check wins) and a
-file ending in a bare length prefix (io.EOF for the range alone)."""
+file ending in a bare length prefix (io.EOF for the range alone).  Since
+round 5 the join returns ReadAll's whole result -- metadata, HardState and
+the ents stitched across the ranges (ewal_split_ents_layout) -- and every
+field is compared with the oracle's; a 1 GiB configs[1]-shaped WAL split
+in HBM (no copy) must give the single-ctx ReadAll exactly."""
 import random
 import struct
 
@@ -37,6 +41,20 @@ def ctxs():
         c.close()
 
 
+def _check_full(buf, ri, g, tag):
+    """the joined ReadAll against the oracle's over the whole WAL, every field"""
+    o = O.readall(bytes(buf), ri)
+    got = (g.status, g.fail_record if g.status not in (O.OK, O.ERR_INDEX_NOT_FOUND) else -1, g.n_records)
+    assert got == _want(bytes(buf), ri), (tag, got, _want(bytes(buf), ri))
+    if o["status"] == O.OK:
+        gd = g.as_dict()
+        for k in ("last_crc", "enti", "metadata", "state"):
+            assert gd[k] == o[k], (tag, k, gd[k], o[k])
+        assert gd["ents"] == o["ents"], tag
+    elif o["status"] == O.ERR_INDEX_NOT_FOUND:
+        assert g.enti == o["enti"], tag
+
+
 @pytest.mark.parametrize("n", [2, 3])
 def test_multi_inside_file_mutated(ctxs, n):
     rng = random.Random(500 + n)
@@ -45,11 +63,9 @@ def test_multi_inside_file_mutated(ctxs, n):
         buf = _wal(rng, n=rng.randrange(60, 300), cuts=rng.randrange(0, 3))
         if i % 4:
             buf = _mutate(rng, buf)
-        g = W.readall_multi(ctxs[:n], buf, 1)
-        assert g[:3] == _want(buf, 1), (i, g, _want(buf, 1))
-        if g[0] == O.OK:
-            assert g[3] == O.readall(buf, 1)["last_crc"]
-        resplits += g[5]
+        g, t = W.readall_multi(ctxs[:n], buf, 1)
+        _check_full(buf, 1, g, i)
+        resplits += t["resplits"]
     assert resplits   # damage at a range edge made some ranges read joined
 
 
@@ -65,8 +81,85 @@ def test_multi_by_file_mutated(ctxs, n):
         if i == 1:   # a middle file ending in a bare length prefix
             blobs[1] += struct.pack("<q", 40)
         buf = b"".join(blobs)
-        g = W.readall_multi(ctxs[:n], buf, 0, files=[(len(b), idx) for b, (_, idx) in zip(blobs, files)])
-        assert g[:3] == _want(buf, 0), (i, g, _want(buf, 0))
+        g, _ = W.readall_multi(ctxs[:n], buf, 0, files=[(len(b), idx) for b, (_, idx) in zip(blobs, files)])
+        _check_full(buf, 0, g, i)
+
+
+def _rich_wal(rng, n_ents, rewinds=False):
+    """metadata in every file, HardStates between entries, entries carrying
+    unknown fields and a leader change's index rewind: what the stitched
+    result has to carry across the ranges"""
+    e = O.WalEncoder(0)
+    e.save_crc(0)
+    e.encode(1, b"node-md")
+    idx = 1
+    for i in range(n_ents):
+        if rewinds and i and i % 37 == 0:
+            idx = max(1, idx - rng.randrange(1, 4))
+        data = rng.randbytes(rng.randrange(0, 400))
+        if i % 23 == 5:
+            e.encode(2, O.entry_marshal(0, 3, idx, data) + bytes([0x38, i & 0x7F]))
+        else:
+            e.save_entry(0, 3, idx, data)
+        idx += 1
+        if i % 17 == 3:
+            e.save_state(3, 1, idx - 2)
+        if i % 61 == 60:   # a cut: the next file opens with the running CRC and the metadata again
+            e.save_crc(e.crc)
+            e.encode(1, b"node-md")
+    e.encode(3, O.hardstate_marshal(4, 2, idx - 1) + bytes([0x20, 0x05]))
+    return e.getvalue()
+
+
+@pytest.mark.parametrize("n", [2, 3])
+def test_multi_full_result_rich(ctxs, n):
+    """metadata, the last HardState (with XXX_unrecognized), ents with
+    unknown fields and index rewinds, joined from 2 / 3 ranges inside a file"""
+    rng = random.Random(700 + n)
+    for i in range(8):
+        buf = _rich_wal(rng, rng.randrange(100, 400), rewinds=i % 2 == 1)
+        for ri in (1, 7):
+            g, _ = W.readall_multi(ctxs[:n], buf, ri)
+            _check_full(buf, ri, g, (i, ri))
+
+
+@pytest.mark.parametrize("n", [2, 3])
+def test_multi_device_resident_1gib(ctxs, n):
+    """configs[1]-shaped WAL (64 B - 64 KiB entries) of 1 GiB resident in HBM,
+    split over n ctxs on device 0 at 16-B aligned frame starts (no copy):
+    the joined result equals the single-ctx ReadAll exactly -- verdict,
+    lastCRC, enti, metadata, HardState and every entry descriptor."""
+    import ctypes as C
+    from etcd_amd import _lib as L
+    buf, nrec = W.synth_wal(1 << 30, 64, 65536, seed=5)
+    d = ctxs[0].alloc(len(buf) + 64)
+    d.upload_ptr(C.addressof((C.c_char * len(buf)).from_buffer(buf)), len(buf))
+    try:
+        one = W.readall_device(d, len(buf), 1)
+        assert one.status == O.OK and one.n_records == nrec
+        ne = one.n_ents if hasattr(one, "n_ents") else None
+        a1 = (L.EntryDesc * max(1, nrec))()
+        k1 = L.lib.ewal_copy_entries(ctxs[0].handle, a1, nrec)
+        m = W.Multi(ctxs[:n])
+        try:
+            plan = m.plan_device(d, len(buf), 1)
+            assert all(s % 16 == 0 for s in plan[0]) and len(set(plan[0])) == n + 1, plan
+            g = m.readall_device(d, len(buf), 1, plan=plan)
+            assert (g.status, g.n_records, g.last_crc, g.enti) == (one.status, one.n_records, one.last_crc, one.enti)
+            assert g.metadata == one.metadata and g.state == one.state
+            assert m.timing()["resplits"] == 0
+            a2 = (L.EntryDesc * max(1, nrec))()
+            k2 = L.lib.ewal_multi_copy_entries(m._h, a2, nrec)
+            assert k1 == k2 == g.n_ents and (ne is None or ne == k1)
+            assert C.string_at(a1, k1 * C.sizeof(L.EntryDesc)) == C.string_at(a2, k2 * C.sizeof(L.EntryDesc))
+            # and from host bytes (each range staged into its ctx's buffer)
+            h = m.readall(buf, 1, with_ents=False)
+            assert (h.status, h.n_records, h.last_crc, h.enti, h.metadata) == \
+                (one.status, one.n_records, one.last_crc, one.enti, one.metadata)
+        finally:
+            m.close()
+    finally:
+        d.free()
 
 
 def _entry_panic_wal():

@@ -36,6 +36,6 @@ def test_host_cpp_under_asan_ubsan(tmp_path):
     exe = str(tmp_path / "san_host")
     _run(["g++", "-std=c++17", *SAN, "-I", os.path.join(ROOT, "include"), "-o", exe,
           os.path.join(HERE, "sanitize", "san_host.cpp"), os.path.join(ROOT, "etcd_amd", "csrc", "ewal_host.cpp"),
-          "-lpthread"])
+          os.path.join(ROOT, "etcd_amd", "csrc", "ewal_synth.cpp"), "-lpthread"])
     out = _run([exe, str(tmp_path / "wal")], env=ENV, timeout=300)
     assert "san_host ok (0 failures)" in out

@@ -78,9 +78,13 @@ def oracle_range_info(buf, ri):
                 else 0,
                 md_first_frame=-1, md_first=None, md_value_frame=-1, md_value=None, first_entry_frame=-1,
                 first_entry_index=0, min_entry_index=0, last_entry_index=0, last_op_frame=-1, last_op_index=0,
-                last_entry_frame=-1, first_pre_crc=1 if pre else 0, end_off=end_off, n_bytes=len(buf))
+                last_entry_frame=-1, first_pre_crc=1 if pre else 0, end_off=end_off, n_bytes=len(buf),
+                state_frame=-1, state=(0, 0, 0), state_unrec=0)
     idx = []
     for i, r in enumerate(recs):
+        if r["type"] == 3:   # the range's last HardState
+            _, h = O.hardstate_unmarshal(r["data"] or b"")
+            info.update(state_frame=i, state=(h["term"], h["vote"], h["commit"]), state_unrec=int(bool(h["unrec"])))
         if r["type"] == 1:
             if info["md_first_frame"] < 0:
                 info["md_first_frame"], info["md_first"] = i, r["data"] or None
@@ -113,14 +117,17 @@ def _worker(rank, world, port, cases, use_gpu, q):
             while True:
                 buf, ri = ranges[rank]
                 if use_gpu:    # the product alone: ReadAll + ewal_range_info over the range
-                    g = W.readall_bytes(buf, ri, ctx, with_ents=False)
+                    g = W.readall_bytes(buf, ri, ctx, with_ents=True)
                     res = (g.status, g.fail_record, g.n_records, g.last_crc)
+                    mine = g.as_dict()["ents"] if g.status == O.OK else []
                     info = W.range_info(ctx, stream=buf)
                 else:
                     o = O.readall(buf, ri)
                     res = (o["status"], o["fail_record"], o["n_records"], o["last_crc"])
+                    mine = o["ents"] if o["status"] == O.OK else []
                     info = oracle_range_info(buf, ri)
-                v = shard.split_verdict(dist, world, rank, res, info, ri, rig)
+                full = shard.split_verdict(dist, world, rank, res, info, ri, rig, full=True)
+                v = (full["status"], full["fail_record"], full["n_records"], full["resplit"])
                 if v[3] < 0:
                     break
                 # ranges k.. verified joined, on rank k
@@ -128,7 +135,8 @@ def _worker(rank, world, port, cases, use_gpu, q):
                 ranges = ranges[:k] + [(b"".join(b for b, _ in ranges[k:]), ranges[k][1])] + \
                     [(b"", 0)] * (world - k - 1)
                 out.append(("resplit", k))
-            out.append(v[:3])
+            full["ents"] = mine
+            out.append((v[:3], full))
         if ctx is not None:
             ctx.close()
         q.put((rank, out))
@@ -224,7 +232,22 @@ def _run(world, use_gpu, cases=None):
             o = O.readall(allb, rig)
             want = (o["status"], o["fail_record"] if o["status"] not in (O.OK, O.ERR_INDEX_NOT_FOUND) else -1,
                     o["n_records"])
-            assert got[i] == want, (labels[i], r, got[i], want)
+            assert got[i][0] == want, (labels[i], r, got[i][0], want)
+            if o["status"] != O.OK:
+                continue
+            # the rest of ReadAll's result: metadata, HardState, ents stitched from every rank's
+            f = got[i][1]
+            assert (f["last_crc"], f["enti"], f["metadata"]) == (o["last_crc"], o["enti"], o["metadata"]), labels[i]
+            st = o["state"]
+            assert (f["state"] or (0, 0, 0)) == (st["term"], st["vote"], st["commit"]), labels[i]
+            assert f["n_ents"] == len(o["ents"]), labels[i]
+            joined = []
+            for k in range(world):
+                b, c = f["layout"][k]
+                if c > 0:
+                    rk = [x for x in res[k] if x[0] != "resplit"][i][1]["ents"]
+                    joined = joined[:b] + rk[:c]
+            assert joined == o["ents"], labels[i]
     return cases
 
 
