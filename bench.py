@@ -63,7 +63,7 @@ def parse():
                          "restart = OpenAtIndex + ReadAll + materialise through the C ABI (the cgo shim's calls)")
     ap.add_argument("--shards-per-gpu", type=int, default=512)
     ap.add_argument("--shard-mib", type=int, default=64)
-    ap.add_argument("--configs", default="c1,shards,snap,snapstream,commit,rewind",
+    ap.add_argument("--configs", default="c1,shards,snap,snapstream,commit,rewind,split2",
                     help="default line: the other BASELINE configs timed in the same run ('none' to skip)")
     ap.add_argument("--sub-cpu-seconds", type=float, default=6.0,
                     help="CPU-baseline time per leg of each `configs` sub-result")
@@ -146,6 +146,27 @@ def timed(dist, steps, fn):
     return elapsed
 
 
+# k_frames' algorithmic bytes: per frame its 80-B head read and
+# its 40-B ewal_entry written (every synthetic frame but the 3 head frames is
+# an entry op), per 4 KiB unit its 64 B of v[] and 16 B of hmask read and 8 B
+# (pl, ucb) written.
+FR_FRAME_B, FR_UNIT_B = 80 + 40, 64 + 16 + 8
+
+
+def frames_roofline(frames, nbytes, kernel_ms):
+    if not kernel_ms:
+        return None
+    ab = frames * FR_FRAME_B + (nbytes // 4096 + 1) * FR_UNIT_B
+    ach = ab / (kernel_ms / 1e3) / 1e9
+    return {"bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+            "frac": round(ach / HBM_PEAK_GBPS, 4), "kernel": "k_frames", "kernel_ms": round(kernel_ms, 4),
+            "algorithmic_bytes_per_launch": int(ab),
+            "bytes_model": "per frame 80-B head + 40-B entry, per 4 KiB unit 64-B v[] + 16-B hmask + 8 B out",
+            "traffic": load_traffic("k_frames"),
+            "note": "the frame pass is issue- and latency-bound (profiles/r05/sq_counters_k_stream_k_frames.txt), "
+                    "not HBM-bound: its fraction is low by construction"}
+
+
 def run_shards(a, dist, rank, world, local, cpu_seconds=None):
     """configs[2]: 4096 per-raft-group WAL shards x 64 MiB over the node --
     each GPU replays its 512 (at N=8) in ONE batched ReadAll
@@ -207,9 +228,16 @@ def run_shards(a, dist, rank, world, local, cpu_seconds=None):
             shard.combine_batch(dist, first, [(x.fail_record if x.status != L.OK else -1, x.n_records,
                                                x.status != L.OK) for x in c_out], out=summary)
 
-    elapsed = timed(dist, a.steps, step)
+    fr_ms = []
+
+    def step_t():
+        step()
+        fr_ms.append(c_out[0].frames_ms)
+
+    elapsed = timed(dist, a.steps, step_t)
     ms = elapsed / a.steps * 1e3
     r0 = L.Result.from_buffer_copy(last["r"][0])   # (c_out is reused below)
+    frames_ms = sum(fr_ms) / len(fr_ms)
     assert all((x.status, x.fail_record) == ((L.ERR_RECORD_CRC, 1000) if first + i == bad_shard else (L.OK, -1))
                for i, x in enumerate(c_out))
     frames = sum(nrec)
@@ -327,6 +355,8 @@ def run_shards(a, dist, rank, world, local, cpu_seconds=None):
                      "pipeline_frac": round(nb / (r0.device_ms / 1e3) / 1e9 / HBM_PEAK_GBPS, 4),
                      "step_frac": round(nb / (ms / 1e3) / 1e9 / HBM_PEAK_GBPS, 4)},
         "pipeline_device_ms": round(r0.device_ms, 4),
+        "post_stream_ms": round(r0.post_ms, 4),
+        "roofline_frames": frames_roofline(frames, nb, frames_ms),
         "torn5": torn5,
         "rew1pct": rew1pct,
         "cpu_baseline": cpu,
@@ -960,13 +990,15 @@ def run_wal(a, dist, rank, world, local, size, min_data, max_data, label, cpu_se
     assert r.status == L.ERR_RECORD_CRC and r.fail_record == k, (r.status, r.fail_record, k)
 
     summary = torch.zeros(3, dtype=torch.int64, device="cuda") if dist is not None else None
-    stream_ms, dev_ms = [], []
+    stream_ms, dev_ms, post_ms, fr_ms = [], [], [], []
 
     def step():
         rc = L.lib.ewal_readall_device(ctx.handle, dbuf.ptr, nb, 1, C.byref(rs))
         assert rc == L.ERR_RECORD_CRC and rs.fail_record == k, (rc, rs.fail_record)
         stream_ms.append(rs.stream_ms)
         dev_ms.append(rs.device_ms)
+        post_ms.append(rs.post_ms)
+        fr_ms.append(rs.frames_ms)
         if dist is not None:   # one all-reduce of the shard verdicts (etcd_amd/shard.py)
             shard.combine(dist, rank, rs.fail_record, rs.n_records, rs.status != L.OK, out=summary)
 
@@ -976,6 +1008,8 @@ def run_wal(a, dist, rank, world, local, size, min_data, max_data, label, cpu_se
     recs_per_s = world * n / (ms_per_step / 1e3)
     stream_avg = sum(stream_ms) / len(stream_ms)
     dev_avg = sum(dev_ms) / len(dev_ms)
+    post_avg = sum(post_ms) / len(post_ms)
+    fr_avg = sum(fr_ms) / len(fr_ms)
     achieved = nb / (stream_avg / 1e3) / 1e9
 
     # ---- end-to-end variant (host -> device included), one pass -------------
@@ -1043,7 +1077,17 @@ def run_wal(a, dist, rank, world, local, size, min_data, max_data, label, cpu_se
                      "pipeline_frac": round(nb / (dev_avg / 1e3) / 1e9 / HBM_PEAK_GBPS, 4),
                      "step_frac": round(gbps / world / HBM_PEAK_GBPS, 4)},
         "pipeline_device_ms": round(dev_avg, 4),
+        "post_stream_ms": round(post_avg, 4),
     }
+    if fr_avg:   # the frame pass ran as one launch after the stream pass: its own roofline entry
+        out["roofline_frames"] = frames_roofline(n, nb, fr_avg)
+        if fr_avg > stream_avg:   # the dominant kernel by time names the line's roofline
+            out["roofline"], out["roofline_stream"] = out["roofline_frames"], out["roofline"]
+            del out["roofline_frames"]
+    else:
+        out["pipeline"] = ("overlapped: the stream pass in chunks on %s CUs, each chunk's frame pass on the other CUs "
+                           "as it completes; post_stream_ms = the part after the last stream chunk" %
+                           "most")
     if label == "configs[1]":
         out["roofline"]["traffic_source"] = ("profiles/k_stream_pmc.json: the committed rocprofv3 PMC pass of this "
                                              "config (FETCH_SIZE x2 + WRITE_SIZE per launch), not measured in this run")
@@ -1120,8 +1164,60 @@ def run_rewind(a, dist, rank, world, local, cpu_seconds=None):
     return out
 
 
+def run_split(a, dist, rank, world, local, cpu_seconds=None, nctx=2):
+    """configs[1]'s WAL read as ONE WAL split over `nctx` contexts on THIS
+    GPU (ewal_multi_readall_device: the ranges stay where they lie in HBM,
+    each opening at a 16-B aligned frame start; one host thread per ctx; the
+    verdict, metadata, HardState and len(ents) joined in C).  A one-GPU
+    rehearsal of the multi-GPU split of SURVEY §8(e) -- both ranges share one
+    GPU's CUs and HBM, so this is not scaling data.  Checked against the
+    single-ctx ReadAll of the same bytes before the timed steps."""
+    buf, n = W.synth_wal(int(a.size_gib * (1 << 30)), a.min_data, a.max_data, seed=2 + rank)
+    nb = len(buf)
+    ctxs = [W.Context(local) for _ in range(nctx)]
+    d = ctxs[0].alloc(nb + 64)
+    d.upload_ptr(C.addressof((C.c_char * nb).from_buffer(buf)), nb)
+    one = W.readall_device(d, nb, 1)
+    assert one.status == L.OK and one.n_records == n, (one.status, one.n_records)
+    m = W.Multi(ctxs)
+    t0 = time.perf_counter()
+    plan = m.plan_device(d, nb, 1)
+    plan_ms = (time.perf_counter() - t0) * 1e3
+    g = m.readall_device(d, nb, 1, plan=plan)
+    assert (g.status, g.n_records, g.last_crc, g.enti, g.metadata, g.state) == \
+        (one.status, one.n_records, one.last_crc, one.enti, one.metadata, one.state), (g.status, g.n_records)
+    assert m.timing()["resplits"] == 0
+    tim = []
+
+    def step():
+        r = m.readall_device(d, nb, 1, plan=plan)
+        assert r.status == L.OK and r.n_records == n, (r.status, r.n_records)
+        tim.append(m.timing())
+
+    for _ in range(max(a.warmup, 1)):
+        step()
+    tim.clear()
+    ms = timed(dist, a.steps, step) / a.steps * 1e3
+    avg = lambda k: sum(t[k] for t in tim) / len(tim)   # noqa: E731
+    out = {"metric": METRIC, "value": round(world * nb / (ms / 1e3) / 1e9, 3), "unit": "GB/s",
+           "ms_per_step": round(ms, 4), "steps": a.steps, "dtype": "u8",
+           "config": {"workload": "configs[1]'s %.2f GiB WAL as ONE WAL split over %d contexts on one GPU "
+                                  "(device-resident ranges at %s)" % (nb / (1 << 30), nctx, plan[0]),
+                      "wal_bytes": nb, "frames": n, "ranges": nctx, "parallelism": "one-GPU rehearsal"},
+           "range_device_ms_max": round(avg("max_range_device_ms"), 4),
+           "join_host_ms": round(avg("join_ms"), 4), "call_wall_ms": round(avg("wall_ms"), 4),
+           "plan_ms": round(plan_ms, 3), "resplits": int(avg("resplits")),
+           "note": "rehearsal, not scaling data: the ranges share one GPU; each range's ReadAll is followed by "
+                   "ewal_copy_range_info (its per-frame descriptors rebuilt on the device) for the join"}
+    m.close()
+    d.free()
+    for c in ctxs:
+        c.close()
+    return out
+
+
 SUBS = {"c1": None, "shards": run_shards, "snap": run_snap, "snapstream": run_snapstream, "commit": run_commit,
-        "rewind": run_rewind}
+        "rewind": run_rewind, "split2": run_split}
 
 
 def main():

@@ -86,7 +86,7 @@ class Result(C.Structure):
                 ("metadata_len", C.c_int64), ("has_state", C.c_int32), ("n_slow", C.c_int32),
                 ("state_term", C.c_uint64), ("state_vote", C.c_uint64), ("state_commit", C.c_uint64),
                 ("n_ents", C.c_int64), ("n_candidates", C.c_int64), ("n_runs", C.c_int64), ("device_ms", C.c_double),
-                ("stream_ms", C.c_double)]
+                ("stream_ms", C.c_double), ("post_ms", C.c_double), ("frames_ms", C.c_double)]
 
 
 class EntryDesc(C.Structure):

@@ -118,6 +118,8 @@ struct ewal_ctx {
   hipStream_t stream = nullptr;
   bool own_stream = false;
   hipEvent_t ev0 = nullptr, ev1 = nullptr, evs0 = nullptr, evs1 = nullptr;
+  hipEvent_t evf0 = nullptr, evf1 = nullptr;   // around k_frames (the serial pipeline)
+  bool frames_timed = false;                   // evf0 / evf1 bracket this call's frame pass
   std::map<uint32_t, DevTables> tables;
   std::map<uint32_t, std::unique_ptr<ewal::CrcTables>> host_tables;
   DevBuf encw, encs, lbstat, gagg, slow, mlist, pf, v, pwave, ux, tagg, tpx, wcnt, slots, cbase, ovf, cpos, clen, nxt, exc, E, rs, jl, vis, entry, on, rec_cand, rd, opf, ops, kk, kkrev, suf,
@@ -178,6 +180,7 @@ struct ewal_ctx {
   hipStream_t ov_s[2] = {nullptr, nullptr};
   int ov_state = 0;          // 0 not tried, 1 ready, -1 unavailable (the serial pipeline)
   int ov_chunks = 8, ov_fcus = 32, ov_cu[2] = {0, 0};
+  int ov_nofr = 0;           // tools/ hooks builds only (EWAL_OV_NOFR): every frame chunk after the stream pass
   std::vector<hipEvent_t> ov_ev;
   DevBuf fticks;             // per chunk: its frame pass's tile counter
   StreamArgs ov_sa{};        // the call's stream-pass arguments (run_stream), launched per chunk
@@ -633,23 +636,12 @@ static int fr_tsh(const ewal_ctx *c, uint32_t nunits) {
   const uint64_t w2 = (uint64_t)FR_WAVES * std::max(1, c->num_cu) * 2;
   return (uint64_t)nunits >= 256 * w2 ? 8 : (uint64_t)nunits >= 64 * w2 ? 6 : 4;
 }
-template <bool SEG>
-static void fr_launch(ewal_ctx *c, int tsh, uint32_t nt, const FrArgs &a, const FrSeg &sg, ResultDev *o, Small *h) {
-  unsigned grid = (unsigned)std::min<uint64_t>(grid_for(nt, FR_WAVES), (uint64_t)std::max(1, c->num_cu));
+// the frame pass's workgroups (one per CU; tools/ hooks builds: EWAL_FRAME_CUS)
+static int fr_cus(const ewal_ctx *c) {
 #ifdef EW_ABLATION_HOOKS
-  if (const char *e = std::getenv("EWAL_FRAME_CUS")) grid = std::min<unsigned>(grid, (unsigned)std::atoi(e));   // tools/ only
+  if (const char *e = std::getenv("EWAL_FRAME_CUS")) return std::max(1, std::atoi(e));   // tools/ only
 #endif
-  const unsigned sgrid = (unsigned)std::min<uint64_t>(grid_for(nt, 256), (uint64_t)std::max(1, c->num_cu) * EW_SEAM_WGS);
-  if (tsh == 8) {
-    hipLaunchKernelGGL((k_frames<SEG, 8>), dim3(grid), dim3(FR_THREADS), 0, c->stream, a, sg);
-    hipLaunchKernelGGL((k_frames_seam<SEG, 8>), dim3(sgrid), dim3(256), 0, c->stream, a, sg, o, h);
-  } else if (tsh == 6) {
-    hipLaunchKernelGGL((k_frames<SEG, 6>), dim3(grid), dim3(FR_THREADS), 0, c->stream, a, sg);
-    hipLaunchKernelGGL((k_frames_seam<SEG, 6>), dim3(sgrid), dim3(256), 0, c->stream, a, sg, o, h);
-  } else {
-    hipLaunchKernelGGL((k_frames<SEG, 4>), dim3(grid), dim3(FR_THREADS), 0, c->stream, a, sg);
-    hipLaunchKernelGGL((k_frames_seam<SEG, 4>), dim3(sgrid), dim3(256), 0, c->stream, a, sg, o, h);
-  }
+  return std::max(1, c->num_cu);
 }
 static void fr_launch_result_batch(ewal_ctx *c, int tsh, const FrArgs &a, const FrSeg &sg) {
   const dim3 g(grid_for((uint64_t)sg.ns * 64, 256));
@@ -710,6 +702,24 @@ static int reset_small(ewal_ctx *c) {
   if (c->defer_first) EW_CHECK(hipMemsetAsync(&ds->defer_first, 1, 1, c->stream));
   return 0;
 }
+// The call's device times from its events (ev1 already synchronised):
+// device_ms ev0 -> ev1, stream_ms evs0 -> evs1, post_ms evs1 -> ev1 and, when
+// the frame pass ran as one launch, frames_ms evf0 -> evf1.
+static int set_times(ewal_ctx *c, ewal_result *o, uint32_t n = 1) {
+  float dev = 0, str = 0, post = 0, fr = 0;
+  EW_CHECK(hipEventElapsedTime(&dev, c->ev0, c->ev1));
+  EW_CHECK(hipEventElapsedTime(&str, c->evs0, c->evs1));
+  EW_CHECK(hipEventElapsedTime(&post, c->evs1, c->ev1));
+  if (c->frames_timed) EW_CHECK(hipEventElapsedTime(&fr, c->evf0, c->evf1));
+  for (uint32_t i = 0; i < n; ++i) {
+    o[i].device_ms = dev;
+    o[i].stream_ms = str;
+    o[i].post_ms = post;
+    o[i].frames_ms = fr;
+  }
+  return 0;
+}
+
 // ---- the overlapped pipeline (round 5) ----------------------------------------
 // Both passes are issue-bound on the SIMDs rather than HBM-bound: k_stream
 // keeps 98 % of its speed on 224 of the 256 CUs (1.675 vs 1.638 ms over
@@ -800,7 +810,7 @@ static int ov_launch(ewal_ctx *c, int tsh, uint32_t nunits, uint32_t ntiles, con
     const uint32_t ub = tb * tu, ue = std::min(nunits, te * tu);
     ov_stream_chunk(c, ub, ue, c->ov_cu[0], sA);
     EW_CHECK(hipEventRecord(ev[1 + k], sA));
-    const bool last = te == ntiles;
+    const bool last = te == ntiles || c->ov_nofr;
     hipStream_t sf = last ? c->stream : sB;   // the last chunk's frames: the whole chip, on the call's stream
     EW_CHECK(hipStreamWaitEvent(sf, ev[1 + k], 0));
     if (k == 0 && c->defer_first) EW_CHECK(hipMemsetAsync(&ds->defer_first, 1, 1, sf));   // (after k_stream zeroed Small)
@@ -810,9 +820,9 @@ static int ov_launch(ewal_ctx *c, int tsh, uint32_t nunits, uint32_t ntiles, con
     a.tick = c->fticks.as<uint32_t>() + k;
     fr_launch_frames<false>(tsh, te - tb, a, FrSeg{}, last ? std::max(1, c->num_cu) : c->ov_cu[1], sf);
     if (!last) EW_CHECK(hipEventRecord(ev[1 + C + k], sB));
-    if (last) {
+    if (te == ntiles) {
       EW_CHECK(hipEventRecord(c->evs1, sA));
-      if (k) EW_CHECK(hipStreamWaitEvent(c->stream, ev[C + k], 0));   // join: the frames of the chunks before
+      if (k && !c->ov_nofr) EW_CHECK(hipStreamWaitEvent(c->stream, ev[C + k], 0));   // join: the frames before
       break;
     }
   }
@@ -853,8 +863,13 @@ static int frames_pass(ewal_ctx *c, DevTables *tb, const uint8_t *d_buf, uint64_
     }
     if (ov && pass == 0) {
       if (int rc = ov_launch(c, tsh, nunits, ntiles, a)) return rc;
+      c->frames_timed = false;
     } else {
-      fr_launch<false>(c, tsh, ntiles, a, FrSeg{}, c->h_res_dev, c->h_small_dev);
+      EW_CHECK(hipEventRecord(c->evf0, c->stream));
+      fr_launch_frames<false>(tsh, ntiles, a, FrSeg{}, fr_cus(c), c->stream);
+      EW_CHECK(hipEventRecord(c->evf1, c->stream));
+      fr_launch_seam<false>(c, tsh, ntiles, a, FrSeg{}, c->h_res_dev, c->h_small_dev);
+      c->frames_timed = true;
     }
     if (rew)   // the slots more than one op claimed: their last op's entry
       hipLaunchKernelGGL(k_ents_fix, dim3((unsigned)std::max(1, c->num_cu) * 2), dim3(256), 0, c->stream, d_buf, B,
@@ -1420,12 +1435,12 @@ static int readall_impl(ewal_ctx *c, const uint8_t *d_buf, uint64_t B, uint64_t 
   c->rec_valid = true;
   if (!ev1_final) EW_CHECK(hipEventRecord(c->ev1, c->stream));
   EW_CHECK(hipEventSynchronize(c->ev1));
-  float ms = 0;
-  EW_CHECK(hipEventElapsedTime(&ms, c->ev0, c->ev1));
-  out->device_ms = ms;
   if (B) {
-    EW_CHECK(hipEventElapsedTime(&ms, c->evs0, c->evs1));
-    out->stream_ms = ms;
+    if (int rc2 = set_times(c, out)) return rc2;
+  } else {
+    float ms = 0;
+    EW_CHECK(hipEventElapsedTime(&ms, c->ev0, c->ev1));
+    out->device_ms = ms;
   }
   return out->status;
 }
@@ -1494,7 +1509,11 @@ static int frames_batch(ewal_ctx *c, DevTables *tb, const uint8_t *d_buf, uint64
                        c->fnfp.as<unsigned long long>());
     hipLaunchKernelGGL(k_shard_rbase, dim3(1), dim3(1024), 0, c->stream, (const unsigned long long *)c->fnfp.p, ns,
                        ecap, sg.rbase, sg.sp, ds);
-    fr_launch<true>(c, tsh, ntiles, a, sg, nullptr, nullptr);
+    EW_CHECK(hipEventRecord(c->evf0, c->stream));
+    fr_launch_frames<true>(tsh, ntiles, a, sg, fr_cus(c), c->stream);
+    EW_CHECK(hipEventRecord(c->evf1, c->stream));
+    fr_launch_seam<true>(c, tsh, ntiles, a, sg, nullptr, nullptr);
+    c->frames_timed = true;
     hipLaunchKernelGGL(k_tile_scan, dim3(1), dim3(1024), 0, c->stream, (const uint32_t *)a.tcnt, ntiles, sg.tcb,
                        (const Small *)ds);
     hipLaunchKernelGGL(k_meta_batch_fr, dim3(64), dim3(256), 0, c->stream, a, sg);
@@ -1509,12 +1528,8 @@ static int frames_batch(ewal_ctx *c, DevTables *tb, const uint8_t *d_buf, uint64
     if (hs->errflag) return EWAL_E_TIMEOUT;
     c->last_k = hs->total;
     if (hs->spec_n) {
-      float dev_ms = 0, str_ms = 0;
-      EW_CHECK(hipEventElapsedTime(&dev_ms, c->ev0, c->ev1));
-      EW_CHECK(hipEventElapsedTime(&str_ms, c->evs0, c->evs1));
+      if (int rc = set_times(c, out, ns)) return rc;
       for (uint32_t i = 0; i < ns; ++i) {
-        out[i].device_ms = dev_ms;
-        out[i].stream_ms = str_ms;
         c->bnents[i] = (uint64_t)out[i].n_ents;
         if (!out[i].n_ents) c->bent_first[i] = 0;
       }
@@ -1603,14 +1618,7 @@ static int frames_batch_rewind(ewal_ctx *c, DevTables *tb, const uint8_t *d_buf,
     for (uint32_t s : rews) out[s].flags = EW_SHARD_BAD;
     return 0;
   }
-  float dev_ms = 0, str_ms = 0;
-  EW_CHECK(hipEventElapsedTime(&dev_ms, c->ev0, c->ev1));
-  EW_CHECK(hipEventElapsedTime(&str_ms, c->evs0, c->evs1));
-  for (uint32_t i = 0; i < ns; ++i) {
-    out[i].device_ms = dev_ms;
-    out[i].stream_ms = str_ms;
-  }
-  return 0;
+  return set_times(c, out, ns);
 }
 
 // ReadAll of the listed shards of a batch, each alone (readall_impl over an
@@ -1980,11 +1988,14 @@ int ewal_ctx_create(int device, ewal_ctx **out) {
     if (ch > 0) c->ov_chunks = std::min(ch, 64);
     if (fc > 0) c->ov_fcus = fc;
   }
+  if (const char *e = std::getenv("EWAL_OV_NOFR")) c->ov_nofr = std::atoi(e);
 #endif
   EW_CHECK(hipEventCreate(&c->ev0));
   EW_CHECK(hipEventCreate(&c->ev1));
   EW_CHECK(hipEventCreate(&c->evs0));
   EW_CHECK(hipEventCreate(&c->evs1));
+  EW_CHECK(hipEventCreate(&c->evf0));
+  EW_CHECK(hipEventCreate(&c->evf1));
   EW_CHECK(hipHostMalloc((void **)&c->h_small, sizeof(Small), hipHostMallocMapped));
   EW_CHECK(hipHostMalloc((void **)&c->h_res, sizeof(ResultDev), hipHostMallocMapped));
   EW_CHECK(hipHostGetDevicePointer((void **)&c->h_small_dev, c->h_small, 0));
@@ -2008,6 +2019,8 @@ void ewal_ctx_destroy(ewal_ctx *c) {
   (void)hipEventDestroy(c->ev1);
   (void)hipEventDestroy(c->evs0);
   (void)hipEventDestroy(c->evs1);
+  (void)hipEventDestroy(c->evf0);
+  (void)hipEventDestroy(c->evf1);
   for (hipEvent_t e : c->ov_ev) (void)hipEventDestroy(e);
   for (hipStream_t st : c->ov_s)
     if (st) {

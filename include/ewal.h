@@ -84,6 +84,10 @@ typedef struct ewal_result {
   int64_t n_runs;          /* diagnostics: chain runs in the framing pass */
   double device_ms;        /* device time of the pipeline (HIP events) */
   double stream_ms;        /* device time of the k_stream HBM pass alone */
+  double post_ms;          /* device time from the end of the stream pass to the end of the pipeline: the part
+                              of device_ms the stream pass does not hide (diagnostics) */
+  double frames_ms;        /* device time of the frame pass kernel k_frames, when it ran as one launch after the
+                              stream pass (0 in the overlapped pipeline, where post_ms is its exposed part) */
 } ewal_result;
 
 /* raftpb.Entry, raft/raftpb/raft.pb.go:100-106.  Data is a zero-copy

@@ -1,6 +1,6 @@
 """Timing of ONE library build under environment variants in one GPU session
 (hooks builds: EWAL_STREAM_CUS / EWAL_FRAME_CUS / EWAL_TSH ...).
-Usage: python3 tools/env_sweep.py MODE ROUNDS LIB 'K=V,K=V' ...   MODE: wal | shards | c1
+Usage: python3 tools/env_sweep.py MODE ROUNDS LIB 'K=V+K=V' ...   MODE: wal | shards | c1
 Each round runs every library in its own process (EWAL_LIB_PATH) and prints
 the median k_stream and pipeline device times of 10 calls (after 2 warmups);
 AB_NOCHECK=1 skips the verdict check (timing-only ablation builds)."""
@@ -47,7 +47,7 @@ res = {v: [] for v in variants}
 for rd in range(rounds):
     for v in variants:
         env = dict(os.environ, EWAL_LIB_PATH=os.path.abspath(lib))
-        for kv in filter(None, v.split(",")):
+        for kv in filter(None, v.split("+")):
             k, x = kv.split("=")
             env[k] = x
         out = subprocess.run([sys.executable, "-c", child, mode], env=env, capture_output=True, text=True,
