@@ -178,8 +178,9 @@ struct ewal_ctx {
   // the stream pass's chunks on ov_s[0] (ov_cu[0] CUs), the frame pass's on
   // ov_s[1] (ov_cu[1] CUs) -- and the events that order them
   hipStream_t ov_s[2] = {nullptr, nullptr};
+  bool ov_opt = false;       // EWAL_OPT_OVERLAP
   int ov_state = 0;          // 0 not tried, 1 ready, -1 unavailable (the serial pipeline)
-  int ov_chunks = 8, ov_fcus = 32, ov_cu[2] = {0, 0};
+  int ov_chunks = 4, ov_fcus = 32, ov_cu[2] = {0, 0};
   int ov_nofr = 0;           // tools/ hooks builds only (EWAL_OV_NOFR): every frame chunk after the stream pass
   std::vector<hipEvent_t> ov_ev;
   DevBuf fticks;             // per chunk: its frame pass's tile counter
@@ -1015,7 +1016,8 @@ static int readall_impl(ewal_ctx *c, const uint8_t *d_buf, uint64_t B, uint64_t 
     // the overlapped pipeline for large single WALs (ov_launch): the stream
     // pass is launched in chunks by frames_pass
     const uint32_t nunits_ov = (uint32_t)(B / EW_WAVE_BYTES + 1);
-    const bool ov = !EW_XS && c->fused && B >= (512ull << 20) && fr_tsh(c, nunits_ov) == 8 && ov_ready(c);
+    const bool ov = !EW_XS && c->ov_opt && c->fused && B >= (512ull << 20) && fr_tsh(c, nunits_ov) == 8 &&
+                    ov_ready(c);
     rc = run_stream(c, tb, d_buf, B, 1, ccap, !c->fused, !ov);
     if (rc) return rc;
     if (c->defer_first && !ov) EW_CHECK(hipMemsetAsync(&ds->defer_first, 1, 1, c->stream));   // (Small is zeroed by k_stream)
@@ -1982,9 +1984,10 @@ int ewal_ctx_create(int device, ewal_ctx **out) {
                            // build reads no environment variable: its path is set by ewal_ctx_set_options only.
   if (const char *e = std::getenv("EWAL_STREAM_ABLATE")) c->ablate = std::atoi(e);
   if (const char *e = std::getenv("EWAL_FRAME_WG")) c->frame_wg = std::max(1, std::min(16, std::atoi(e)));
-  if (const char *e = std::getenv("EWAL_OV")) {   // "0": the serial pipeline; "C,F": C chunks, F frame CUs
+  if (const char *e = std::getenv("EWAL_OV")) {   // "0": the serial pipeline; "C,F": overlapped, C chunks, F frame CUs
     int ch = 0, fc = 0;
     if (std::sscanf(e, "%d,%d", &ch, &fc) >= 1 && ch <= 0) c->ov_state = -1;
+    c->ov_opt = ch > 0;
     if (ch > 0) c->ov_chunks = std::min(ch, 64);
     if (fc > 0) c->ov_fcus = fc;
   }
@@ -2046,8 +2049,9 @@ int ewal_ctx_set_stream(ewal_ctx *c, void *s) {
 }
 
 int ewal_ctx_set_options(ewal_ctx *c, uint32_t opts) {
-  if (!c || (opts & ~EWAL_OPT_GENERAL_PATH)) return EWAL_E_INVAL;
+  if (!c || (opts & ~(EWAL_OPT_GENERAL_PATH | EWAL_OPT_OVERLAP))) return EWAL_E_INVAL;
   c->fused = (opts & EWAL_OPT_GENERAL_PATH) ? 0 : 1;
+  c->ov_opt = (opts & EWAL_OPT_OVERLAP) != 0;
   return EWAL_OK;
 }
 

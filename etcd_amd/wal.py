@@ -10,7 +10,9 @@ Errors are raised as exceptions carrying the Go sentinel they stand for
 (see ERRORS); Go panics are raised as GoPanic.  All verification runs on
 the GPU through libewal.so.
 """
+import atexit
 import ctypes as C
+import weakref
 from dataclasses import dataclass, field
 from typing import List, Optional
 
@@ -51,6 +53,20 @@ class Entry:
     XXX_unrecognized: Optional[bytes] = None
 
 
+_live = weakref.WeakSet()
+
+
+@atexit.register
+def _close_all():
+    """every ctx still open at interpreter exit is destroyed before the HIP
+    runtime's own teardown (a ctx's CU-masked streams must go first)"""
+    for c in list(_live):
+        try:
+            c.close()
+        except Exception:
+            pass
+
+
 class Context:
     """One GPU context (device workspace + stream), ewal_ctx_create."""
 
@@ -58,6 +74,7 @@ class Context:
         self._p = C.c_void_p()
         check(lib.ewal_ctx_create(device, C.byref(self._p)))
         self.device = device
+        _live.add(self)
 
     @property
     def handle(self):
@@ -74,10 +91,12 @@ class Context:
         except Exception:
             pass
 
-    def set_options(self, general_path=False):
+    def set_options(self, general_path=False, overlap=False):
         """ewal_ctx_set_options: general_path=True makes every ReadAll take the
-        general path (for cross-checking it against the fused pass)."""
-        check(lib.ewal_ctx_set_options(self._p, L.OPT_GENERAL_PATH if general_path else 0))
+        general path (for cross-checking it against the fused pass);
+        overlap=True the opt-in overlapped stream / frame pipeline."""
+        check(lib.ewal_ctx_set_options(self._p, (L.OPT_GENERAL_PATH if general_path else 0) |
+                                       (L.OPT_OVERLAP if overlap else 0)))
 
     def set_stream(self, hip_stream):
         """Run this ctx's work on a caller-owned hipStream_t (e.g. torch's)."""

@@ -149,6 +149,15 @@ int ewal_ctx_reserve(ewal_ctx *ctx, uint64_t wal_bytes, uint32_t flags);
  * -- the same results, slower; for cross-checking the two paths.  No
  * environment variable changes the path. */
 #define EWAL_OPT_GENERAL_PATH 1u
+/* EWAL_OPT_OVERLAP: a single ReadAll of >= 512 MiB streams its bytes in four
+ * chunks on 224 CUs (a CU-masked stream) while each finished chunk's frame
+ * pass runs on the other 32 (a second CU-masked stream).  Off by default:
+ * measured on MI355X it does not pay (profiles/r05/): the
+ * stream pass loses speed faster than the frame pass gains CUs, and masks
+ * of more than 32 CUs on the frame side slowed the stream side 2.4x.  A ctx
+ * with this option owns two extra streams: destroy it before the process
+ * exits. */
+#define EWAL_OPT_OVERLAP 2u
 int ewal_ctx_set_options(ewal_ctx *ctx, uint32_t opts);
 const char *ewal_status_string(int status);
 /* Device time (ms) of the last pipeline call on this ctx (HIP events). */

@@ -1,12 +1,13 @@
-"""GPU parity of the overlapped pipeline (round 5, ewal_api.hip ov_launch):
-a single WAL of >= 512 MiB is streamed in chunks on one CU-masked stream
-while each finished chunk's frame pass runs on the other CUs, the last chunk's
-frame pass and the seam pass on the call's own stream.  Every outcome must be
-the oracle's ReadAll (wal/wal.go:164-216) -- clean, a corrupt record in the
-first chunk, in the frame that straddles a chunk boundary and in the last
-chunk, a torn tail, an index rewind (the frame pass's rewind mode), a range
-of a WAL split inside a file (frame 0's check deferred) -- and the general
-path (EWAL_OPT_GENERAL_PATH, no overlap) must agree."""
+"""GPU parity of the overlapped pipeline (round 5, ewal_api.hip ov_launch,
+opt-in: EWAL_OPT_OVERLAP): a single WAL of >= 512 MiB is streamed in chunks
+on one CU-masked stream while each finished chunk's frame pass runs on the
+other CUs, the last chunk's frame pass and the seam pass on the call's own
+stream.  Every outcome must be the oracle's ReadAll (wal/wal.go:164-216) --
+clean, a corrupt record in the first chunk, in the frame that straddles a
+chunk boundary and in the last chunk, a torn tail, an index rewind (the frame
+pass's rewind mode), a range of a WAL split inside a file (frame 0's check
+deferred) -- and the default (serial) pipeline and the general path
+(EWAL_OPT_GENERAL_PATH) must agree."""
 import bisect
 
 import pytest
@@ -28,20 +29,22 @@ def big():
 
 
 def _both_paths(ctx, b, ri=1):
-    """the default (overlapped) path and the general path over the same bytes,
-    each against the oracle"""
+    """the overlapped pipeline, the serial one and the general path over the
+    same bytes, each against the oracle"""
     o = O.readall_digest(b, ri)
     d = ctx.alloc(len(b) + 64)
     try:
         d.upload(b)
-        g = _readall(ctx, d, len(b), ri, memoryview(b))
-        _assert_result(ctx, g, o, b)
-        ctx.set_options(general_path=True)
         try:
-            g2 = _readall(ctx, d, len(b), ri, memoryview(b))
-            _assert_result(ctx, g2, o, b)
+            ctx.set_options(overlap=True)
+            g = _readall(ctx, d, len(b), ri, memoryview(b))
+            _assert_result(ctx, g, o, b)
+            for general in (False, True):
+                ctx.set_options(general_path=general)
+                g2 = _readall(ctx, d, len(b), ri, memoryview(b))
+                _assert_result(ctx, g2, o, b)
         finally:
-            ctx.set_options(general_path=False)
+            ctx.set_options()
     finally:
         d.free()
     return g, o
@@ -93,9 +96,12 @@ def test_overlap_rewind_mode(ctx):
     d = ctx.alloc(len(buf) + 64)
     try:
         d.upload(bytes(buf))
-        g2 = _readall(ctx, d, len(buf), 1, memoryview(bytes(buf)))
-        _assert_result(ctx, g2, o, bytes(buf))
+        ctx.set_options(overlap=True)
+        for _ in range(2):
+            g2 = _readall(ctx, d, len(buf), 1, memoryview(bytes(buf)))
+            _assert_result(ctx, g2, o, bytes(buf))
     finally:
+        ctx.set_options()
         d.free()
 
 
@@ -117,14 +123,14 @@ def test_overlap_deferred_range(ctx, big):
     try:
         d.upload(part)
         infos = []
-        for general in (False, True):
-            ctx.set_options(general_path=general)
+        for general, overlap in ((False, True), (False, False), (True, False)):
+            ctx.set_options(general_path=general, overlap=overlap)
             try:
                 g = W.readall_range_device(d, len(part), 1, defer_first=True)
                 infos.append(((g.status, g.n_records, g.last_crc, g.enti), W.range_info(ctx, stream=part)))
             finally:
-                ctx.set_options(general_path=False)
-        assert infos[0] == infos[1]
+                ctx.set_options()
+        assert infos[0] == infos[1] == infos[2]
         assert infos[0][0][0] == O.OK
     finally:
         d.free()
