@@ -1332,13 +1332,6 @@ __device__ __forceinline__ void prefix_load_near(uint64_t x, uint64_t B, const u
 #define EW_FR_ABL 0   // timing-only ablations of the frame pass (tools/): 1 no Horner over v, 2 no prefix tail,
                       // 4 no S_dlen in the checks; results are wrong
 #endif
-// Both directions in ONE pass over the loaded window (round 5): the lanes of
-// a wave hold frames in either half of their super-piece, and the former
-// two-branch form ran both branches' chunk loops for every wave.  Down: the
-// register runs from P(x0) over window bytes [0, n); up: from 0 over [lead, n),
-// then P(x) = S_{x1-x}^-1(P(x1) ^ c).  Chunk 0 goes dword by dword (a partial
-// start for up lanes, a partial end for short down windows), chunks 1.. by
-// slicing-by-16, a down window's partial last chunk dword by dword.
 __device__ __forceinline__ uint32_t prefix_finish_near(const PrefixNear &in, const uint32_t *t16, const uint32_t *svp,
                                                        const uint32_t *inv) {
   uint32_t acc = in.pw;
@@ -1350,45 +1343,41 @@ __device__ __forceinline__ uint32_t prefix_finish_near(const PrefixNear &in, con
     if (4u * q + 2 < in.nk) acc = tab_apply(svp, acc) ^ in.vv[q].z;
     if (4u * q + 3 < in.nk) acc = tab_apply(svp, acc) ^ in.vv[q].w;
   }
-  const bool up = in.up != 0;
-  const uint32_t n = in.n, s0 = up ? in.lead : 0u;   // window bytes [s0, n)
-  const uint32_t e0 = n < 16 ? n : 16u;              // chunk 0's end
-  uint32_t c = up ? 0u : acc;
-  // chunk 0, dword by dword over [s0, e0)
+  if (!in.up) {   // forward over the n <= 128 bytes after x0
+    const uint32_t nq = in.n >> 4;
+    uint4 pc = in.dd[0];
+#pragma unroll
+    for (int q = 0; q < 9; ++q) {
+      if ((uint32_t)q < nq) acc = step16(t16, acc, in.dd[q]);
+      if (q && (uint32_t)q == nq) pc = in.dd[q];
+    }
+    const uint32_t nd = (in.n & 15) >> 2;
+    if (nd > 0) acc = step4_flat(t16, acc ^ pc.x);
+    if (nd > 1) acc = step4_flat(t16, acc ^ pc.y);
+    if (nd > 2) acc = step4_flat(t16, acc ^ pc.z);
+    uint32_t wd = nd == 0 ? pc.x : nd == 1 ? pc.y : nd == 2 ? pc.z : pc.w;
+    for (uint32_t b = 0; b < (in.n & 3); ++b, wd >>= 8) acc = t16[(acc ^ wd) & 0xff] ^ (acc >> 8);
+    return acc;
+  }
+  // lin(stream[x, x1)) from register 0: chunk 0 from byte `lead` on, then whole chunks
+  uint32_t c = 0;
+  const uint32_t lead = in.lead;
   const uint32_t w0[4] = {in.dd[0].x, in.dd[0].y, in.dd[0].z, in.dd[0].w};
 #pragma unroll
   for (uint32_t j = 0; j < 4; ++j) {
-    const uint32_t lo = 4 * j, hi = 4 * j + 4;
-    if (lo >= s0 && hi <= e0) {
+    if (4 * j >= lead) {
       c = step4_flat(t16, c ^ w0[j]);
-    } else {
-      const uint32_t b0 = s0 > lo ? s0 : lo, b1 = e0 < hi ? e0 : hi;
-      uint32_t t = w0[j] >> (8 * (b0 & 3));
-      for (uint32_t b = b0; b < b1; ++b, t >>= 8) c = t16[(c ^ t) & 0xff] ^ (c >> 8);
+    } else if (4 * j + 4 > lead) {
+      uint32_t t = w0[j] >> (8 * (lead & 3));
+      for (uint32_t b = lead & 3; b < 4; ++b, t >>= 8) c = t16[(c ^ t) & 0xff] ^ (c >> 8);
     }
   }
-  // whole chunks 1 .. n/16 - 1
-  const uint32_t nq = n >> 4;
+  const uint32_t nq = in.n >> 4;   // in.n is a multiple of 16 here
 #pragma unroll
   for (int q = 1; q < 9; ++q)
     if ((uint32_t)q < nq) c = step16(t16, c, in.dd[q]);
-  // a down window's partial last chunk (n > 16, n % 16 != 0): chunk nq over [16 nq, n)
-  const uint32_t rem = n > 16 ? (n & 15) : 0u;
-  if (rem) {
-    uint4 pc = in.dd[1];
-#pragma unroll
-    for (int q = 2; q < 9; ++q)
-      if ((uint32_t)q == nq) pc = in.dd[q];
-    const uint32_t nd = rem >> 2;
-    if (nd > 0) c = step4_flat(t16, c ^ pc.x);
-    if (nd > 1) c = step4_flat(t16, c ^ pc.y);
-    if (nd > 2) c = step4_flat(t16, c ^ pc.z);
-    uint32_t wd = nd == 0 ? pc.x : nd == 1 ? pc.y : nd == 2 ? pc.z : pc.w;
-    for (uint32_t b = 0; b < (rem & 3); ++b, wd >>= 8) c = t16[(c ^ wd) & 0xff] ^ (c >> 8);
-  }
-  if (!up) return c;
   uint32_t x = acc ^ c;
-  const uint32_t m = n - s0;   // x1 - x, 1..127
+  const uint32_t m = in.n - lead;   // x1 - x, 1..127
 #pragma unroll
   for (int l = 0; l < 7; ++l)
     if ((m >> l) & 1) x = nib_apply(inv + l * 128, x);

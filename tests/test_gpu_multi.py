@@ -135,7 +135,7 @@ def test_multi_device_resident_1gib(ctxs, n):
     d = ctxs[0].alloc(len(buf) + 64)
     d.upload_ptr(C.addressof((C.c_char * len(buf)).from_buffer(buf)), len(buf))
     try:
-        one = W.readall_device(d, len(buf), 1)
+        one = W.readall_device(d, len(buf), 1, host_view=memoryview(buf))
         assert one.status == O.OK and one.n_records == nrec
         ne = one.n_ents if hasattr(one, "n_ents") else None
         a1 = (L.EntryDesc * max(1, nrec))()
