@@ -167,6 +167,13 @@ struct ewal_ctx {
   bool rec_rebuild = false;   // the last ReadAll was decided by the fused pass and the stream pass's
                               // state (cpos, pwave, v) is still its own: ewal_copy_records can rebuild
                               // the descriptors from it and the caller's stream bytes
+  // the last ReadAll's frame pass when it decided the call (rec_rebuild):
+  // ewal_copy_range_info reads its reductions instead of rebuilding descriptors
+  bool fi_valid = false;
+  int fi_tsh = 0;
+  FrArgs fi_a{};
+  Small fi_small{};
+  DevBuf rfr;                // RangeFr
   const uint8_t *last_buf = nullptr;   // the last ReadAll's stream (materialise_records)
   uint64_t last_B = 0, last_ri = 0;
   uint64_t pfcap = 0;      // pf = [P at data starts | P at frame starts], pfcap each
@@ -890,6 +897,10 @@ static int frames_pass(ewal_ctx *c, DevTables *tb, const uint8_t *d_buf, uint64_
     if (hs->spec_n) {
       *done = true;
       c->fr_rew_hint = rew && hs->fr_rews;
+      c->fi_valid = true;
+      c->fi_tsh = tsh;
+      c->fi_a = a;
+      c->fi_small = *hs;
       return 0;
     }
     // declined for capacity or rewinds only: room for what it asked / the rewind mode, once more
@@ -985,6 +996,7 @@ static int readall_impl(ewal_ctx *c, const uint8_t *d_buf, uint64_t B, uint64_t 
   c->unrec_bytes = 0;
   c->cat_bytes = 0;
   c->rd_valid = false;
+  c->fi_valid = false;
   c->last_deferred = c->defer_first;
   c->last_buf = d_buf;
   c->last_B = B;
@@ -2314,6 +2326,66 @@ int64_t ewal_copy_records(ewal_ctx *c, ewal_record *out, int64_t cap) {
   return n;
 }
 
+// The range info of a ReadAll the frame pass decided, from its reductions
+// (k_range_info_fr): the fields k_range_info derives from the descriptors.
+// 1: an entry below ri or an index rewind was met (the descriptors decide).
+static int range_info_fused(ewal_ctx *c, ewal_range_info &o) {
+  const Small &hs = c->fi_small;
+  if (hs.fr_below || (c->fi_a.rew && hs.fr_rews)) return 1;
+  EW_CHECK(hipSetDevice(c->device));
+  EW_CHECK(c->rfr.ensure(sizeof(RangeFr)));
+  RangeFr *d = c->rfr.as<RangeFr>();
+  const FrArgs &a = c->fi_a;
+  const uint64_t K = c->last_n;
+#define RFR_LAUNCH(T) hipLaunchKernelGGL(k_range_info_fr<T>, dim3(1), dim3(512), 0, c->stream, a, hs.nmeta, \
+                                         hs.fc.meta_inv, hs.fr.le, hs.fr.lo, hs.fr.ls, (unsigned long long)K, d)
+  if (c->fi_tsh == 8) RFR_LAUNCH(8);
+  else if (c->fi_tsh == 6) RFR_LAUNCH(6);
+  else RFR_LAUNCH(4);
+#undef RFR_LAUNCH
+  EW_CHECK(hipGetLastError());
+  RangeFr h;
+  EW_CHECK(hipMemcpyAsync(&h, d, sizeof(h), hipMemcpyDeviceToHost, c->stream));
+  EW_CHECK(hipStreamSynchronize(c->stream));
+  const RecDesc &f = h.d[6];   // frame 0 (fused: its canonical fields; no failure before the CRC check)
+  o.first_type = f.type;
+  if (f.type == 4) o.first_crc = f.crc;
+  o.first_dlen = f.dlen;
+  o.first_stored_crc = f.crc;
+  o.first_u0 = f.type == 4 ? f.crc : h.u0;
+  o.first_pre_crc = 0;
+  if (h.pos[0] != ~0ull) {
+    o.md_first_frame = (int64_t)h.ord[0];
+    if (!h.d[0].dnil && h.d[0].dlen) {
+      o.md_first_off = (int64_t)h.d[0].doff;
+      o.md_first_len = (int64_t)h.d[0].dlen;
+    }
+  }
+  if (h.pos[1] != ~0ull) {
+    o.md_value_frame = (int64_t)h.ord[1];
+    o.md_value_off = (int64_t)h.d[1].doff;
+    o.md_value_len = (int64_t)h.d[1].dlen;
+  }
+  if (h.pos[2] != ~0ull && h.pos[3] != ~0ull) {
+    o.first_entry_frame = (int64_t)h.ord[2];
+    o.first_entry_index = h.d[2].f1;
+    o.min_entry_index = h.d[2].f1;   // no entry below ri, ops in order: the first op's
+    o.last_entry_frame = (int64_t)h.ord[3];
+    o.last_entry_index = h.d[3].f1;
+    if (h.pos[4] != ~0ull) {
+      o.last_op_frame = (int64_t)h.ord[4];
+      o.last_op_index = h.d[4].f1;
+    }
+  }
+  if (h.pos[5] != ~0ull) {
+    o.state_frame = (int64_t)h.ord[5];
+    o.state_term = h.d[5].f0;
+    o.state_vote = h.d[5].f1;
+    o.state_commit = h.d[5].f2;
+  }
+  return 0;
+}
+
 int ewal_copy_range_info(ewal_ctx *c, ewal_range_info *out) {
   if (!c || !out) return EWAL_E_INVAL;
   ewal_range_info o;
@@ -2323,11 +2395,20 @@ int ewal_copy_range_info(ewal_ctx *c, ewal_range_info *out) {
   o.md_first_off = o.md_value_off = -1;
   o.first_type = -1;
   o.state_frame = -1;
-  if (int rc = need_records(c)) return rc;
+  if (!c->rec_valid) return EWAL_E_INVAL;
   const uint64_t n = c->last_n;
   o.n_frames = (int64_t)n;
   o.end_off = c->last_q;
   o.n_bytes = c->last_B;
+  if (n && !c->rd_valid && c->rec_rebuild && c->fi_valid) {
+    const int rc = range_info_fused(c, o);
+    if (rc < 0) return rc;
+    if (rc == 0) {
+      *out = o;
+      return EWAL_OK;
+    }
+  }
+  if (int rc = need_records(c)) return rc;
   if (n) {
     EW_CHECK(c->sdesc.ensure(sizeof(RangeDev)));
     RangeDev h0{~0ull, ~0ull, ~0ull, ~0ull, 0ull, 0ull, 0ull}, h;
@@ -2850,6 +2931,10 @@ extern "C" int ewal_dbg_fr_seam_timing(unsigned long long *out, int n) {
 }
 extern "C" int ewal_dbg_fr_seam_steps(unsigned long long *out, int n) {
   if (hipMemcpyFromSymbol(out, HIP_SYMBOL(fr_sdbg2), (size_t)n * 8) != hipSuccess) return EWAL_E_HIP;
+  return 0;
+}
+extern "C" int ewal_dbg_fr_wave_times(unsigned long long *out, int n) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(fr_wt), (size_t)n * 8) != hipSuccess) return EWAL_E_HIP;
   return 0;
 }
 #endif

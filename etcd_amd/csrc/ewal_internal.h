@@ -178,7 +178,7 @@ struct Small {
   uint32_t fr_ncl;                // rewind mode: ents slots claimed more than once (listed for k_ents_fix)
   uint32_t fr_tick;               // k_frames: tiles handed out past the first round (dynamic schedule)
   uint32_t fr_rews;               // single WAL in rewind mode: an index rewind was met (the next call starts so)
-  uint32_t fr_pad2;
+  uint32_t fr_below;              // single WAL: an entry with Index < ri was met (not an op)
 };
 
 // A returned Entry (ent = its index in ents) or the HardState (ent = -1)

@@ -340,6 +340,7 @@ struct FrCarry {
 __device__ unsigned long long fr_tdbg[8192 * 8];
 __device__ unsigned long long fr_sdbg[1024 * 4];   // k_frames_seam: per block, its loop and fr_result cycles
 __device__ unsigned long long fr_sdbg2[1024 * 8];  // k_frames_seam thread 0: the loop's steps
+__device__ unsigned long long fr_wt[8192 * 4];     // k_frames per wave: realtime at start, end; tiles run
 #define FR_T(i) do { const unsigned long long t_ = clock64(); tacc[i] += t_ - tlast; tlast = t_; } while (0)
 #else
 #define FR_T(i) do {} while (0)
@@ -396,10 +397,14 @@ __global__ __launch_bounds__(FR_THREADS, 1) void k_frames(FrArgs a, FrSeg sg) {
   stage_lds<FR_THREADS>(s_inv, 7 * 128, [&](int i) { return nib_src(a.g_shift + EW_SHIFT_LEVELS * 1024, i); });
   __syncthreads();   // the only barrier: every wave runs its own tiles from here on
   FR_T(0);
+#ifdef FR_TIMING
+  const unsigned long long rt0 = __builtin_amdgcn_s_memrealtime();
+  uint32_t ntl_run = 0;
+#endif
   uint32_t *ucnt = s_ucnt[wv];
   uint32_t *spw = s_pw[wv];
   uint32_t *w = s_win + tid;
-  uint32_t rare = 0, irr = 0, rews = 0;   // rews: rewind mode met an index rewind
+  uint32_t rare = 0, irr = 0, rews = 0;   // rews: 1 rewind mode met an index rewind, 2 an entry below ri (no op)
   unsigned long long need_ecap = 0;
   const uint32_t nt_run = a.tlist ? a.ntl : (a.nrun ? a.nrun : a.ntiles);
   // every wave's first tile is its id; the rest are handed out by a counter
@@ -413,6 +418,9 @@ __global__ __launch_bounds__(FR_THREADS, 1) void k_frames(FrArgs a, FrSeg sg) {
   for (uint32_t ti = wid; ti < nt_run; ti = next_tile()) {
     const uint32_t t = a.tlist ? a.tlist[ti] : a.t0 + ti;
     const uint32_t u0 = t * TU;
+#ifdef FR_TIMING
+    ++ntl_run;
+#endif
     const uint64_t ts = (uint64_t)u0 * EW_WAVE_BYTES;
     // ---- A: the tile's unit lins, P at every unit start (tile-local) ----
     uint32_t x[UPL];
@@ -754,7 +762,9 @@ __global__ __launch_bounds__(FR_THREADS, 1) void k_frames(FrArgs a, FrSeg sg) {
       // ---- per new frame: ReadAll's rules, entry ops ----
       uint64_t ri = a.ri;
       if (SEG) ri = sg.ri[sh];
-      const bool op = isnew && ok && !torn && d.type == 2 && d.f1 >= ri;
+      const bool ent = isnew && ok && !torn && d.type == 2;
+      const bool op = ent && d.f1 >= ri;
+      if (!SEG && ent && !op) rews |= 2u;   // an entry below ri: the range info's descriptors decide (ewal_copy_range_info)
       const unsigned long long mo = __ballot(op);
       const unsigned long long below = mo & ((1ull << lane) - 1ull);
       const int pol = below ? 63 - __clzll((long long)below) : lane;
@@ -779,7 +789,7 @@ __global__ __launch_bounds__(FR_THREADS, 1) void k_frames(FrArgs a, FrSeg sg) {
             // an index rewind: the rewind-mode pass (single WAL), the shard replayed alone (batch)
             if (k <= kq) {
               if (!a.rew) { if (SEG) sg.sp[sh].rew = 1u; else rare |= 2u; }
-              else rews = 1u;
+              else rews |= 1u;
             }
             gap = k > kq && k - kq > 1;
           } else {
@@ -948,14 +958,23 @@ __global__ __launch_bounds__(FR_THREADS, 1) void k_frames(FrArgs a, FrSeg sg) {
     FR_T(7);
   }
 #ifdef FR_TIMING
-  if (lane == 0 && wid < 8192)
+  if (lane == 0 && wid < 8192) {
     for (int i = 0; i < 8; ++i) fr_tdbg[wid * 8 + i] = tacc[i];
+    fr_wt[wid * 4] = rt0;
+    fr_wt[wid * 4 + 1] = __builtin_amdgcn_s_memrealtime();
+    fr_wt[wid * 4 + 2] = ntl_run;
+  }
 #endif
   uint32_t rr = rare;
   for (int o = 32; o; o >>= 1) rr |= (uint32_t)__shfl_xor((int)rr, o);
   if (lane == 0 && rr) atomicOr(&ds->fc.rare, rr);
   if (__ballot(irr) && lane == 0) atomicOr(&ds->irregular, 1u);
-  if (!SEG && __ballot(rews) && lane == 0) atomicOr(&ds->fr_rews, 1u);
+  if (!SEG) {
+    uint32_t rw = rews;
+    for (int o = 32; o; o >>= 1) rw |= (uint32_t)__shfl_xor((int)rw, o);
+    if (lane == 0 && (rw & 1u)) atomicOr(&ds->fr_rews, 1u);
+    if (lane == 0 && (rw & 2u)) atomicOr(&ds->fr_below, 1u);
+  }
   for (int o = 32; o; o >>= 1)
     need_ecap = max(need_ecap, (unsigned long long)__shfl_xor((long long)need_ecap, o));
   if (lane == 0 && need_ecap) atomicMax(&ds->fr_need, need_ecap);
@@ -1362,6 +1381,79 @@ __global__ __launch_bounds__(256) void k_frames_seam(FrArgs a, FrSeg sg, ResultD
     fr_sdbg2[blockIdx.x * 8 + 6] = tq[4] ? t_loop - tq[4] : 0ull;   // after thread 0's last tile: the block's wait + fold
   }
 #endif
+}
+
+// ewal_copy_range_info after a ReadAll the frame pass decided (no per-frame
+// descriptors to run k_range_info over): the frames k_range_info names, from
+// the pass's reductions -- the first metadata frame (the metadata list), the
+// first non-empty one, the first entry op (the first tile with ops; no entry
+// below ri met, so it is the first entry frame), the last entry / op / state
+// frame -- and frame 0, each re-read (fc_frame_fields) with its ordinal
+// (fr_ordinal).  One workgroup of 8 waves; hs = the pass's Small.
+#define RFR_N 7   // md_first, md_value, ent_first, ent_last, op_last, st_last, frame 0
+struct RangeFr {
+  unsigned long long pos[RFR_N];   // stream position (~0: none)
+  unsigned long long ord[RFR_N];
+  RecDesc d[RFR_N];
+  uint32_t u0, pad;                // frame 0: crc32.Update(0, Data) (the caller's check of a deferred frame 0)
+};
+template <int TSH>
+__global__ __launch_bounds__(512) void k_range_info_fr(FrArgs a, uint32_t nmeta, unsigned long long meta_inv,
+                                                       unsigned long long le, unsigned long long lo,
+                                                       unsigned long long ls, unsigned long long K, RangeFr *o) {
+  constexpr uint32_t TU = 1u << TSH;
+  __shared__ unsigned long long s_pos[RFR_N];
+  __shared__ uint4 s_w[RFR_N][6];
+  __shared__ uint32_t s_n[SEAM_NIB * 128];
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  stage_lds<512>(s_n, SEAM_NIB * 128, [&](int i) { return nib_src(a.g_shift, i); });
+  if (tid == 0) {
+    s_pos[0] = ~0ull;
+    s_pos[1] = meta_inv ? ~meta_inv : ~0ull;
+    s_pos[3] = le ? le - 1 : ~0ull;
+    s_pos[4] = lo ? lo - 1 : ~0ull;
+    s_pos[5] = ls ? ls - 1 : ~0ull;
+    s_pos[6] = K ? 0ull : ~0ull;
+  }
+  __syncthreads();
+  unsigned long long mf = ~0ull;
+  for (uint32_t i = tid; i < min(nmeta, a.mcap); i += blockDim.x) mf = min(mf, (unsigned long long)a.mlist[i]);
+  for (int s = 32; s; s >>= 1) mf = min(mf, (unsigned long long)__shfl_xor((long long)mf, s));
+  if (lane == 0 && mf != ~0ull) atomicMin(&s_pos[0], mf);
+  if (wid == 7) {   // the first tile holding ops (count written for every tile, nops for tiles with frames)
+    unsigned long long fp = ~0ull;
+    for (uint32_t t0 = 0; t0 < a.ntiles; t0 += 64) {
+      const uint32_t t = t0 + lane;
+      const bool has = t < a.ntiles && a.tcnt[t] && a.trec[t].nops;
+      const unsigned long long m = __ballot(has);
+      if (m) {
+        fp = a.trec[t0 + __ffsll((long long)m) - 1].firstop_p;
+        break;
+      }
+    }
+    if (lane == 0) s_pos[2] = fp;
+  }
+  __syncthreads();
+  if (wid < RFR_N) {
+    const unsigned long long x = s_pos[wid];
+    unsigned long long ord = 0;
+    if (x != ~0ull && wid != 6) ord = fr_ordinal(a, TU, x, nullptr);
+    if (lane == 0) {
+      o->pos[wid] = x;
+      o->ord[wid] = ord;
+      if (x != ~0ull) {
+        const RecDesc f = fc_frame_fields(a.buf, a.B, x, s_w[wid]);
+        o->d[wid] = f;
+        if (wid == 6) {   // S_n(~0 ^ P(data start)) ^ P(data end) ^ ~0 (tile 0's prefixes are global)
+          uint32_t u = 0;
+          if (f.dlen)
+            u = seam_shift(s_n, a.g_shift, f.dlen, 0xffffffffu ^ a.trec[0].pfd0) ^
+                fr_pe_far(a, s_n, 0, f.doff + f.dlen, TU, 12 + TSH) ^ 0xffffffffu;
+          o->u0 = u;
+        }
+      }
+    }
+  }
 }
 
 // Rewind mode: every listed slot (claimed by more than one entry op) gets

@@ -17,7 +17,9 @@ def pack_groups(match, nvoters, committed, term, log_offset, log_ptr, log_terms)
     match = np.asarray(match, dtype=np.uint64)
     G = match.shape[1]
     nvoters = np.asarray(nvoters)
-    assert int(nvoters.max(initial=0)) <= min(7, match.shape[0]), "at most 7 voters, all present in match"
+    # every voter's Match present; a group of more than 7 voters keeps its count in the
+    # record (the device reports EWAL_UNSUPPORTED_ENCODING for it: ecommit_batch_device takes those)
+    assert int(nvoters.max(initial=0)) <= match.shape[0], "every voter's Match must be present in match"
     rec = np.zeros((G, RECORD_WORDS), dtype=np.uint64)
     nv = min(7, match.shape[0])
     rec[:, :nv] = match[:nv].T

@@ -110,14 +110,13 @@ def test_overlap_deferred_range(ctx, big):
     caller's (EWAL_RANGE_DEFER_FIRST); its range info must match the general
     path's"""
     b, _ = big
-    start = None
     d = ctx.alloc(len(b) + 64)
     try:
         d.upload(b)
-        p, _ = W.range_probe(d, len(b), 300 << 20, 1 << 20)
-        start = p
+        start, ri = W.range_probe(d, len(b), 300 << 20, 1 << 20)
     finally:
         d.free()
+    assert start > 0 and ri > 1
     part = b[start:]
     d = ctx.alloc(len(part) + 64)
     try:
@@ -126,7 +125,7 @@ def test_overlap_deferred_range(ctx, big):
         for general, overlap in ((False, True), (False, False), (True, False)):
             ctx.set_options(general_path=general, overlap=overlap)
             try:
-                g = W.readall_range_device(d, len(part), 1, defer_first=True)
+                g = W.readall_range_device(d, len(part), ri, defer_first=True)
                 infos.append(((g.status, g.n_records, g.last_crc, g.enti), W.range_info(ctx, stream=part)))
             finally:
                 ctx.set_options()

@@ -15,6 +15,7 @@ lib = L.lib
 lib.ewal_dbg_fr_timing.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
 lib.ewal_dbg_fr_seam_timing.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
 lib.ewal_dbg_fr_seam_steps.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
+lib.ewal_dbg_fr_wave_times.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
 
 
 def one(label, size, lo, hi):
@@ -45,6 +46,19 @@ def one(label, size, lo, hi):
               " ".join("%s=%d" % (nm, sorted(r[i] for r in rows)[len(rows) // 2])
                        for i, nm in ((1, "loads"), (2, "first"), (3, "last"), (4, "end"), (5, "staging"),
                                      (6, "wait+fold"))))
+    wt = (C.c_ulonglong * (8192 * 4))()
+    lib.ewal_dbg_fr_wave_times(wt, 8192 * 4)
+    ws = [(wt[w * 4], wt[w * 4 + 1], wt[w * 4 + 2]) for w in range(8192) if wt[w * 4 + 1]]
+    if ws:   # s_memrealtime ticks at 100 MHz: 10 ns
+        t0 = min(x[0] for x in ws)
+        ends = sorted((x[1] - t0) / 100.0 for x in ws)
+        starts = sorted((x[0] - t0) / 100.0 for x in ws)
+        q = lambda v, f: v[min(len(v) - 1, int(f * len(v)))]   # noqa: E731
+        tl = sorted(x[2] for x in ws)
+        print("  wave start us: p50 %.1f p99 %.1f max %.1f | end us: p10 %.1f p50 %.1f p90 %.1f p99 %.1f max %.1f"
+              " | tiles per wave p10 %d p50 %d p90 %d max %d" %
+              (q(starts, .5), q(starts, .99), starts[-1], q(ends, .1), q(ends, .5), q(ends, .9), q(ends, .99),
+               ends[-1], q(tl, .1), q(tl, .5), q(tl, .9), tl[-1]))
     waves = [list(t[w * 8:(w + 1) * 8]) for w in range(8192) if any(t[w * 8:(w + 1) * 8])]
     tot = [sum(x) for x in waves]
     print("%s: %d frames, %.3f GiB, device %.3f ms (stream %.3f), %d waves" %
