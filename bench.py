@@ -74,10 +74,11 @@ def parse():
     return ap.parse_args()
 
 
-def load_traffic(kernel="k_stream"):
-    """Per-launch HBM bytes of a kernel from its committed PMC pass, if any
-    (profiles/<kernel>_pmc.json, tools/traffic.sh + tools/traffic.py)."""
-    p = os.path.join(ROOT, "profiles", kernel + "_pmc.json")
+def load_traffic(kernel="k_stream", workload=None):
+    """Per-launch HBM bytes of a kernel from its committed PMC pass at this
+    workload, if any (profiles/<kernel>_pmc[_<workload>].json, tools/traffic.sh
+    + tools/traffic.py)."""
+    p = os.path.join(ROOT, "profiles", kernel + "_pmc" + ("_" + workload if workload else "") + ".json")
     try:
         d = json.load(open(p))
         return d.get("hbm_bytes_per_launch")
@@ -153,7 +154,7 @@ def timed(dist, steps, fn):
 FR_FRAME_B, FR_UNIT_B = 80 + 40, 64 + 16 + 8
 
 
-def frames_roofline(frames, nbytes, kernel_ms):
+def frames_roofline(frames, nbytes, kernel_ms, workload):
     if not kernel_ms:
         return None
     ab = frames * FR_FRAME_B + (nbytes // 4096 + 1) * FR_UNIT_B
@@ -162,7 +163,8 @@ def frames_roofline(frames, nbytes, kernel_ms):
             "frac": round(ach / HBM_PEAK_GBPS, 4), "kernel": "k_frames", "kernel_ms": round(kernel_ms, 4),
             "algorithmic_bytes_per_launch": int(ab),
             "bytes_model": "per frame 80-B head + 40-B entry, per 4 KiB unit 64-B v[] + 16-B hmask + 8 B out",
-            "traffic": load_traffic("k_frames"),
+            "traffic": load_traffic("k_frames", workload),
+            "traffic_source": "profiles/k_frames_pmc_%s.json (a committed PMC pass of this workload; null: none)" % workload,
             "note": "the frame pass is issue- and latency-bound (profiles/r05/sq_counters_k_stream_k_frames.txt), "
                     "not HBM-bound: its fraction is low by construction"}
 
@@ -356,7 +358,7 @@ def run_shards(a, dist, rank, world, local, cpu_seconds=None):
                      "step_frac": round(nb / (ms / 1e3) / 1e9 / HBM_PEAK_GBPS, 4)},
         "pipeline_device_ms": round(r0.device_ms, 4),
         "post_stream_ms": round(r0.post_ms, 4),
-        "roofline_frames": frames_roofline(frames, nb, frames_ms),
+        "roofline_frames": frames_roofline(frames, nb, frames_ms, "shards"),
         "torn5": torn5,
         "rew1pct": rew1pct,
         "cpu_baseline": cpu,
@@ -1080,7 +1082,8 @@ def run_wal(a, dist, rank, world, local, size, min_data, max_data, label, cpu_se
         "post_stream_ms": round(post_avg, 4),
     }
     if fr_avg:   # the frame pass ran as one launch after the stream pass: its own roofline entry
-        out["roofline_frames"] = frames_roofline(n, nb, fr_avg)
+        wk = "wal" if label == "configs[1]" else ("c1" if label.startswith("configs[0]") else "none")
+        out["roofline_frames"] = frames_roofline(n, nb, fr_avg, wk)
         if fr_avg > stream_avg:   # the dominant kernel by time names the line's roofline
             out["roofline"], out["roofline_stream"] = out["roofline_frames"], out["roofline"]
             del out["roofline_frames"]
@@ -1177,7 +1180,7 @@ def run_split(a, dist, rank, world, local, cpu_seconds=None, nctx=2):
     ctxs = [W.Context(local) for _ in range(nctx)]
     d = ctxs[0].alloc(nb + 64)
     d.upload_ptr(C.addressof((C.c_char * nb).from_buffer(buf)), nb)
-    one = W.readall_device(d, nb, 1)
+    one = W.readall_device(d, nb, 1, host_view=memoryview(buf))   # (the metadata bytes from the host copy)
     assert one.status == L.OK and one.n_records == n, (one.status, one.n_records)
     m = W.Multi(ctxs)
     t0 = time.perf_counter()
@@ -1208,7 +1211,7 @@ def run_split(a, dist, rank, world, local, cpu_seconds=None, nctx=2):
            "join_host_ms": round(avg("join_ms"), 4), "call_wall_ms": round(avg("wall_ms"), 4),
            "plan_ms": round(plan_ms, 3), "resplits": int(avg("resplits")),
            "note": "rehearsal, not scaling data: the ranges share one GPU; each range's ReadAll is followed by "
-                   "ewal_copy_range_info (its per-frame descriptors rebuilt on the device) for the join"}
+                   "ewal_copy_range_info (read from the frame pass's reductions, k_range_info_fr) for the join"}
     m.close()
     d.free()
     for c in ctxs:

@@ -639,7 +639,10 @@ static int walk_chain(ewal_ctx *c, DevTables *tb, const uint8_t *d_buf, uint64_t
 // small streams keep the waves busy; large tiles amortise the per-tile work)
 static int fr_tsh(const ewal_ctx *c, uint32_t nunits) {
 #ifdef EW_ABLATION_HOOKS
-  if (const char *e = std::getenv("EWAL_TSH")) return std::atoi(e);   // tools/ timing builds only
+  if (const char *e = std::getenv("EWAL_TSH")) {   // tools/ timing builds only: an instantiated tile size
+    const int t = std::atoi(e);
+    return t >= 8 ? 8 : t >= 6 ? 6 : 4;
+  }
 #endif
   const uint64_t w2 = (uint64_t)FR_WAVES * std::max(1, c->num_cu) * 2;
   return (uint64_t)nunits >= 256 * w2 ? 8 : (uint64_t)nunits >= 64 * w2 ? 6 : 4;
