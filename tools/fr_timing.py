@@ -16,6 +16,8 @@ lib.ewal_dbg_fr_timing.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
 lib.ewal_dbg_fr_seam_timing.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
 lib.ewal_dbg_fr_seam_steps.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
 lib.ewal_dbg_fr_wave_times.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
+lib.ewal_dbg_fr_seam_maxsteps.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
+lib.ewal_dbg_fr_result_steps.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
 
 
 def one(label, size, lo, hi):
@@ -25,7 +27,10 @@ def one(label, size, lo, hi):
     d = ctx.alloc(nb + 64)
     d.upload_ptr(C.addressof((C.c_char * nb).from_buffer(buf)), nb)
     rs = L.Result()
-    for _ in range(3):
+    mx = (C.c_ulonglong * (1024 * 8))()
+    for i in range(3):
+        if i == 2:   # the per-block maxima accumulate: zeroed before the measured call
+            lib.ewal_dbg_fr_seam_maxsteps(mx, 1024 * 8)
         rc = lib.ewal_readall_device(ctx.handle, d.ptr, nb, 1, C.byref(rs))
         assert rc == 0 and rs.flags & L.FLAG_FAST_PATH, (rc, rs.flags)
     t = (C.c_ulonglong * (8192 * 8))()
@@ -46,6 +51,16 @@ def one(label, size, lo, hi):
               " ".join("%s=%d" % (nm, sorted(r[i] for r in rows)[len(rows) // 2])
                        for i, nm in ((1, "loads"), (2, "first"), (3, "last"), (4, "end"), (5, "staging"),
                                      (6, "wait+fold"))))
+    lib.ewal_dbg_fr_seam_maxsteps(mx, 1024 * 8)
+    rows = [list(mx[b * 8:(b + 1) * 8]) for b in range(1024) if any(mx[b * 8:(b + 1) * 8])]
+    if rows:
+        print("  seam slowest thread per block (cycles from the loop start; median / max over blocks): " +
+              " ".join("%s=%d/%d" % (nm, sorted(r[i] for r in rows)[len(rows) // 2], max(r[i] for r in rows))
+                       for i, nm in ((1, "loads"), (2, "first"), (3, "last"), (4, "end"))))
+    rt = (C.c_ulonglong * 8)()
+    lib.ewal_dbg_fr_result_steps(rt, 8)
+    print("  fr_result thread 0 (cycles from its start): metadata %d, fence+sync %d, frames+ordinal %d, "
+          "compose %d, host writes %d" % tuple(rt[i] - rt[0] for i in range(1, 6)))
     wt = (C.c_ulonglong * (8192 * 4))()
     lib.ewal_dbg_fr_wave_times(wt, 8192 * 4)
     ws = [(wt[w * 4], wt[w * 4 + 1], wt[w * 4 + 2]) for w in range(8192) if wt[w * 4 + 1]]
