@@ -2932,6 +2932,16 @@ extern "C" int ewal_dbg_fr_seam_timing(unsigned long long *out, int n) {
   if (hipMemcpyFromSymbol(out, HIP_SYMBOL(fr_sdbg), (size_t)n * 8) != hipSuccess) return EWAL_E_HIP;
   return 0;
 }
+extern "C" int ewal_dbg_fr_seam_maxsteps(unsigned long long *out, int n) {   // and zeroes them
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(fr_sdbg3), (size_t)n * 8) != hipSuccess) return EWAL_E_HIP;
+  std::vector<unsigned long long> z((size_t)n, 0ull);
+  if (hipMemcpyToSymbol(HIP_SYMBOL(fr_sdbg3), z.data(), (size_t)n * 8) != hipSuccess) return EWAL_E_HIP;
+  return 0;
+}
+extern "C" int ewal_dbg_fr_result_steps(unsigned long long *out, int n) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(fr_rdbg), (size_t)std::min(n, 8) * 8) != hipSuccess) return EWAL_E_HIP;
+  return 0;
+}
 extern "C" int ewal_dbg_fr_seam_steps(unsigned long long *out, int n) {
   if (hipMemcpyFromSymbol(out, HIP_SYMBOL(fr_sdbg2), (size_t)n * 8) != hipSuccess) return EWAL_E_HIP;
   return 0;

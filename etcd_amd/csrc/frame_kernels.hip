@@ -340,10 +340,14 @@ struct FrCarry {
 __device__ unsigned long long fr_tdbg[8192 * 8];
 __device__ unsigned long long fr_sdbg[1024 * 4];   // k_frames_seam: per block, its loop and fr_result cycles
 __device__ unsigned long long fr_sdbg2[1024 * 8];  // k_frames_seam thread 0: the loop's steps
+__device__ unsigned long long fr_sdbg3[1024 * 8];  // k_frames_seam: per block, the max over its threads of each step
+__device__ unsigned long long fr_rdbg[8];          // fr_result thread 0: clock at its steps
+#define FR_RT(i) do { if (threadIdx.x == 0) fr_rdbg[i] = clock64(); } while (0)
 __device__ unsigned long long fr_wt[8192 * 4];     // k_frames per wave: realtime at start, end; tiles run
 #define FR_T(i) do { const unsigned long long t_ = clock64(); tacc[i] += t_ - tlast; tlast = t_; } while (0)
 #else
 #define FR_T(i) do {} while (0)
+#define FR_RT(i) do {} while (0)
 #endif
 
 // The tile record's running fields (wave-uniform) and a batch's per-shard
@@ -1048,6 +1052,7 @@ __device__ void fr_result(const FrArgs &a, ResultDev *o, Small *h, uint4 (*s_w)[
     }
     return;
   }
+  FR_RT(0);
   const uint64_t fm = ds->fc.meta_inv ? ~ds->fc.meta_inv : ~0ull;
   if (fm != ~0ull && ds->nmeta > 1) {
     const RecDesc m = fc_frame_fields(a.buf, a.B, fm, s_w[tid]);
@@ -1060,9 +1065,11 @@ __device__ void fr_result(const FrArgs &a, ResultDev *o, Small *h, uint4 (*s_w)[
       if (!eq) atomicMax(&ds->fc.fail_inv, ~((p << 8) | EWAL_ERR_METADATA_CONFLICT));
     }
   }
+  FR_RT(1);
   if (tid == 0) *s_ord = 0;
   __threadfence();
   __syncthreads();
+  FR_RT(2);
   const unsigned long long key = ds->fc.fail_inv ? ~ds->fc.fail_inv : ~0ull;
   const uint64_t le = ds->fr.le, ls = ds->fr.ls, lo = ds->fr.lo;
   const long long want[5] = {key != ~0ull ? (long long)(key >> 8) : -1, le ? (long long)(le - 1) : -1,
@@ -1085,6 +1092,7 @@ __device__ void fr_result(const FrArgs &a, ResultDev *o, Small *h, uint4 (*s_w)[
     }
   }
   __syncthreads();
+  FR_RT(3);
   // the result composed in LDS by thread 0, then written to host-mapped
   // memory by a whole wave (wide PCIe writes instead of one lane's stores)
   ResultDev &res = *s_res;
@@ -1109,6 +1117,7 @@ __device__ void fr_result(const FrArgs &a, ResultDev *o, Small *h, uint4 (*s_w)[
   }
   __threadfence_block();
   __syncthreads();
+  FR_RT(4);
   if (tid < 64) {
     static_assert(sizeof(ResultDev) % 4 == 0 && sizeof(Small) % 4 == 0, "dword copies");
     const uint32_t *rs = (const uint32_t *)&res;
@@ -1118,6 +1127,7 @@ __device__ void fr_result(const FrArgs &a, ResultDev *o, Small *h, uint4 (*s_w)[
     uint32_t *sd = (uint32_t *)h;
     for (uint32_t i = tid; i < sizeof(Small) / 4; i += 64) sd[i] = ss[i];
   }
+  FR_RT(5);
 }
 
 // One thread per tile: the checks of the tile's first frame (its seed from
@@ -1151,7 +1161,7 @@ __global__ __launch_bounds__(256) void k_frames_seam(FrArgs a, FrSeg sg, ResultD
   __syncthreads();
 #ifdef FR_TIMING
   unsigned long long tq[8] = {(unsigned long long)clock64(), 0, 0, 0, 0, 0, 0, 0};
-#define SEAM_T(i) do { if (threadIdx.x == 0 && !tq[i]) tq[i] = clock64(); } while (0)
+#define SEAM_T(i) do { if (!tq[i]) tq[i] = clock64(); } while (0)
 #else
 #define SEAM_T(i) do {} while (0)
 #endif
@@ -1344,14 +1354,28 @@ __global__ __launch_bounds__(256) void k_frames_seam(FrArgs a, FrSeg sg, ResultD
 #ifdef FR_TIMING
   if (threadIdx.x == 0 && blockIdx.x < 1024)
     for (int i = 0; i < 8; ++i) fr_sdbg2[blockIdx.x * 8 + i] = tq[i] ? tq[i] - tq[0] : 0ull;
+  if (blockIdx.x < 1024)
+    for (int i = 1; i < 5; ++i)
+      if (tq[i]) atomicMax(&fr_sdbg3[blockIdx.x * 8 + i], tq[i] - tq[0]);   // cycles from the loop start
 #endif
   if (SEG) return;
-  if (fail != ~0ull) atomicMin(&s_red[0], fail);
-  if (meta != ~0ull) atomicMin(&s_red[1], meta);
-  if (le) atomicMax(&s_red[2], le);
-  if (ls) atomicMax(&s_red[3], ls);
-  if (lo) atomicMax(&s_red[4], lo);
-  if (nops) atomicAdd(&s_red[5], nops);
+  // the block's fold: a wave reduction first, then one LDS atomic per wave
+  for (int o = 32; o; o >>= 1) {
+    fail = min(fail, (unsigned long long)__shfl_xor((long long)fail, o));
+    meta = min(meta, (unsigned long long)__shfl_xor((long long)meta, o));
+    le = max(le, (unsigned long long)__shfl_xor((long long)le, o));
+    ls = max(ls, (unsigned long long)__shfl_xor((long long)ls, o));
+    lo = max(lo, (unsigned long long)__shfl_xor((long long)lo, o));
+    nops += (unsigned long long)__shfl_xor((long long)nops, o);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    if (fail != ~0ull) atomicMin(&s_red[0], fail);
+    if (meta != ~0ull) atomicMin(&s_red[1], meta);
+    if (le) atomicMax(&s_red[2], le);
+    if (ls) atomicMax(&s_red[3], ls);
+    if (lo) atomicMax(&s_red[4], lo);
+    if (nops) atomicAdd(&s_red[5], nops);
+  }
   __syncthreads();
   if (threadIdx.x == 0) {
     if (s_red[0] != ~0ull) atomicMax(&ds->fc.fail_inv, ~s_red[0]);

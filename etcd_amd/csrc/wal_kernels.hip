@@ -117,8 +117,8 @@ __device__ __forceinline__ uint32_t load_word_guarded(const uint8_t *buf, uint64
 // for the accumulated zero-byte test.
 // The pattern is CAND_TEST's pre-test, "length MSB 00 + tag 08" at p+7 / p+8:
 // byte k of z = (stream byte b ^ 08) | (byte b-1), zero iff the pair
-// matches.  Per dword pair: 2 alignbyte + 2 bitop3 (z) + ONE 64-bit add for
-// both borrow tests + 2 bitop3 (accumulate) = 3.5 VALU per dword.
+// matches.  Per dword pair: 2 alignbyte + 2 bitop3 (z) + 2 adds (the
+// borrow tests) + 2 bitop3 (accumulate) = 4 VALU per dword.
 __device__ __forceinline__ uint32_t cand_filter(const uint32_t (&D)[19]) {
   //   z   = (x ^ 08..) | y             bitop3 0xDE ((a ^ c) | b)
   //   acc = ((z - 01..) & ~z) | acc    bitop3 0xBA ((a & ~b) | c)
@@ -132,9 +132,12 @@ __device__ __forceinline__ uint32_t cand_filter(const uint32_t (&D)[19]) {
     const uint32_t y1 = __builtin_amdgcn_alignbyte(D[J + 3], D[J + 2], 3);
     const uint32_t z0 = __builtin_amdgcn_bitop3_b32(D[J + 2], y0, 0x08080808u, 0xDE);
     const uint32_t z1 = __builtin_amdgcn_bitop3_b32(D[J + 3], y1, 0x08080808u, 0xDE);
-    const uint64_t s = (((uint64_t)z1 << 32) | z0) + 0xFEFEFEFEFEFEFEFFull;
-    const uint32_t a0 = __builtin_amdgcn_bitop3_b32((uint32_t)s, z0, (J & 2) ? acc : 0u, 0xBA);
-    acc = __builtin_amdgcn_bitop3_b32((uint32_t)(s >> 32), z1, a0, 0xBA);
+    // z - 01.. per dword (a borrow only adds false hits, never hides a zero
+    // byte; two 32-bit adds: the 64-bit form cost the compiler a register
+    // pair copy and a carry add, round 5)
+    const uint32_t s0 = z0 + 0xFEFEFEFFu, s1 = z1 + 0xFEFEFEFFu;
+    const uint32_t a0 = __builtin_amdgcn_bitop3_b32(s0, z0, (J & 2) ? acc : 0u, 0xBA);
+    acc = __builtin_amdgcn_bitop3_b32(s1, z1, a0, 0xBA);
     if (J & 2) {   // group g = J >> 2 complete: into bit 7 - g, (a & b) | c
       const int g = J >> 2;
       r = g == 0 ? (acc & 0x80808080u) : __builtin_amdgcn_bitop3_b32(acc >> g, 0x80808080u >> g, r, 0xEA);
@@ -301,6 +304,22 @@ __device__ __forceinline__ void row_transpose(uint32_t (&D)[19]) {
   }
 }
 
+// EW_LOAD_HALF layout: register group r (D[4r..4r+3]) of lane (h, j) =
+// (lane >> 5, lane & 31) holds chunk 2 (r >> 1) + h of piece j + 32 (r & 1).
+// Swapping the upper half of group 2c with the lower half of group 2c + 1
+// (one v_permlane32_swap per register) leaves chunk c of piece `lane` in
+// group c, for every c.
+__device__ __forceinline__ void half_transpose(uint32_t (&D)[19]) {
+#pragma unroll
+  for (int c = 0; c < 4; c += 2)
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      auto s = __builtin_amdgcn_permlane32_swap(D[4 * c + d], D[4 * (c + 1) + d], false, false);
+      D[4 * c + d] = s[0];
+      D[4 * (c + 1) + d] = s[1];
+    }
+}
+
 // NU units (4 KiB each, 64 B per lane) once D[i][0..18] is in registers:
 // lin of every 256-B super-piece -> v[] (1/64 of the stream bytes) and
 // frame-start candidates -> slots[] / wcnt[] (the unit's candidate count,
@@ -318,12 +337,18 @@ __device__ __forceinline__ void row_transpose(uint32_t (&D)[19]) {
 #ifndef EW_CAND_TAILMASK
 #define EW_CAND_TAILMASK 1   // hmask also says which flagged pieces need the 16 B after them (k_cand)
 #endif
+#ifndef EW_LOAD_HALF
+#define EW_LOAD_HALF 0   // A/B: half-used-line loads + one permlane32 stage (see k_stream)
+#endif
+#ifndef EW_TREE4
+#define EW_TREE4 1   // the super-piece lins in one table step per lane + two DPP xors (round 5)
+#endif
 #ifndef EW_XS
 #define EW_XS 0   // timing-only k_stream ablations (tools/): 1 no CRC, 2 no candidates, 4 no v stores,
                   // 8 the candidate filter without the exact tests / slots, 16 v stores only for
                   // units with a flagged piece; results are wrong
 #endif
-template <int NU, bool FIND>
+template <int NU, bool FIND, bool SAFE = false>   // SAFE: every piece lies inside the stream (the pair loop)
 __device__ __forceinline__ void stream_units(const StreamArgs &a, const uint8_t *s_slice, const uint32_t *s_s64,
                                              const uint32_t *s_s128, const uint32_t (&Lt)[4],
                                              const uint32_t (&u)[NU], const uint32_t (&D)[NU][19]) {
@@ -341,12 +366,36 @@ __device__ __forceinline__ void stream_units(const StreamArgs &a, const uint8_t 
   } else {
     crc_pieces<NU>(s_slice, Lt, D, c);
   }
+  const bool top = (lane & 3) == 3;
+#if EW_TREE4
+  // lin of every 256-B super-piece (lanes 4m .. 4m+3):
+  //   S_192(c[4m]) ^ S_128(c[4m+1]) ^ S_64(c[4m+2]) ^ c[4m+3]
+  // lane 4m+k moves its own piece's lin by the 64 (3 - k) bytes after it --
+  // ONE byte-table step through its own table (s_s64 = the four tables,
+  // k = 3 the identity) -- and two DPP xors gather the quad in lane 4m+3
+  // (row_shr 1 then 2: lane 4m+1 holds c'0 ^ c'1 when lane 4m+3 reads it).
+  const uint32_t tb = (uint32_t)(lane & 3) * 4096u;
+  const uint8_t *st = (const uint8_t *)s_s64;
+#pragma unroll
+  for (int i = 0; i < NU; ++i) {
+    const uint32_t x = c[i];
+    const uint32_t l0 = lds_lookup(st, tb | ((x << 2) & 0x3fcu));
+    const uint32_t l1 = lds_lookup(st, tb | 1024u | ((x >> 6) & 0x3fcu));
+    const uint32_t l2 = lds_lookup(st, tb | 2048u | ((x >> 14) & 0x3fcu));
+    const uint32_t l3 = lds_lookup(st, tb | 3072u | ((x >> 22) & 0x3fcu));
+    uint32_t d = __builtin_amdgcn_bitop3_b32(__builtin_amdgcn_bitop3_b32(l0, l1, l2, 0x96), l3, 0u, 0x96);
+    d ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)d, EW_DPP_ROW_SHR(1), 0xf, 0xf, false);
+    d ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)d, EW_DPP_ROW_SHR(2), 0xf, 0xf, false);
+    c[i] = d;
+  }
+  (void)s_s128;
+#else
   // lin of every 256-B super-piece (lanes 4m .. 4m+3) by a two-level tree,
   // branch-free: the lanes that do not combine look up entry 0 (one address,
   // a broadcast, no extra bank cycles).  Lane 4m+3 ends with the value.
   //   level 0 (odd lanes):      y = S_64(c[L-1]) ^ c[L]
   //   level 1 (lanes 3 mod 4):  z = S_128(y[L-2]) ^ y[L]
-  const bool odd = lane & 1, top = (lane & 3) == 3;
+  const bool odd = lane & 1;
 #pragma unroll
   for (int i = 0; i < NU; ++i) {
     const uint32_t o = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c[i], EW_DPP_ROW_SHR(1), 0xf, 0xf, false);
@@ -357,6 +406,7 @@ __device__ __forceinline__ void stream_units(const StreamArgs &a, const uint8_t 
     const uint32_t o = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c[i], EW_DPP_ROW_SHR(2), 0xf, 0xf, false);
     c[i] ^= tab_apply(s_s128, top ? o : 0u);
   }
+#endif
   // plain stores (measured a little faster than nontemporal ones here)
   bool vskip[NU];   // EW_XS & 16 (timing only): no v[] for units without a flagged piece
 #pragma unroll
@@ -371,11 +421,12 @@ __device__ __forceinline__ void stream_units(const StreamArgs &a, const uint8_t 
 #pragma unroll
     for (int i = 0; i < NU; ++i) {
       const uint64_t off = (uint64_t)u[i] * EW_WAVE_BYTES + (uint64_t)lane * EW_PIECE;
-      const unsigned long long hm = __ballot(fm[i] != 0 && off < B);
+      const bool in = SAFE || off < B;
+      const unsigned long long hm = __ballot(fm[i] != 0 && in);
       if (EW_CAND_TAILMASK) {
         // the pieces flagged in their last dword group (bit 4 of each byte
         // of fm): only their candidates can need the 12 bytes after the piece
-        const unsigned long long h3 = __ballot((fm[i] & 0x10101010u) != 0 && off < B);
+        const unsigned long long h3 = __ballot((fm[i] & 0x10101010u) != 0 && in);
         if (lane == 0) *(ulonglong2 *)(a.hmask + 2 * (uint64_t)u[i]) = make_ulonglong2(hm, h3);
       } else if (lane == 0) {
         a.hmask[u[i]] = hm;
@@ -422,7 +473,12 @@ __device__ __forceinline__ void stream_units(const StreamArgs &a, const uint8_t 
 template <bool FIND>
 __global__ __launch_bounds__(EW_THREADS, 1) void k_stream(StreamArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t s_slice[EW_SLICE_DWORDS * 4];
+#if EW_TREE4
+  __shared__ uint32_t s_s64[4096];   // the super-piece step: S_192, S_128, S_64, identity byte tables
+  uint32_t *const s_s128 = nullptr;
+#else
   __shared__ uint32_t s_s64[1024], s_s128[1024];   // S_64, S_128 byte tables (super-piece tree)
+#endif
   const int tid = threadIdx.x, lane = tid & 63;
   static_assert(sizeof(Small) % 4 == 0 && sizeof(Small) / 4 <= EW_THREADS, "Small is zeroed by one workgroup");
   if (blockIdx.x == 0 && a.u_begin == 0 && tid < (int)(sizeof(Small) / 4)) ((uint32_t *)a.small)[tid] = 0u;   // the call's scratch
@@ -440,7 +496,15 @@ __global__ __launch_bounds__(EW_THREADS, 1) void k_stream(StreamArgs a) {
   // with lane (g, m) = (lane >> 4, lane & 15) taking chunk g of piece 16 r + m
   // (a permutation inside the 1 KiB row, measured as fast as the plain order).
   // row_transpose() then gives every lane the 64 contiguous bytes of piece `lane`.
+#if EW_LOAD_HALF
+  // A/B variant: lane (h, j) = (lane >> 5, lane & 31) loads chunk c + h of
+  // piece j (and of piece 32 + j, 2 KiB on) -- 16 half-used lines per load
+  // instead of 8 whole ones -- so ONE permlane32 stage puts piece `lane` in
+  // every lane (half_transpose: 8 swaps per unit instead of 16)
+  const uint32_t lo = (uint32_t)(64 * (lane & 31) + 16 * (lane >> 5));
+#else
   const uint32_t lo = (uint32_t)(64 * (lane & 15) + 16 * (lane >> 4));
+#endif
   // Raw buffer loads: the pair base lives in the (scalar) buffer resource,
   // the per-lane offset is a loop-invariant VGPR, so no address VGPR is ever
   // rewritten while loads are in flight.  Lane 63 also fetches the 12 bytes
@@ -455,15 +519,25 @@ __global__ __launch_bounds__(EW_THREADS, 1) void k_stream(StreamArgs a) {
     for (int i = 0; i < 2; ++i) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const ew_v4u w = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)lo + EW_WAVE_BYTES * i + 1024 * r, 0, 2 /* nt */);
+#if EW_LOAD_HALF   // register group r: chunk c = 2 (r >> 1) (+ h) of piece j + 32 (r & 1)
+        const int off = EW_WAVE_BYTES * i + 2048 * (r & 1) + 32 * (r >> 1);
+#else
+        const int off = EW_WAVE_BYTES * i + 1024 * r;
+#endif
+        const ew_v4u w = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)lo + off, 0, 2 /* nt */);
         T[i][4 * r] = w.x; T[i][4 * r + 1] = w.y; T[i][4 * r + 2] = w.z; T[i][4 * r + 3] = w.w;
       }
     }
     t3 = __builtin_amdgcn_raw_buffer_load_b96(rs, o3, 0, 2);
   };
   auto run_pair = [&](uint32_t p, uint32_t (&T)[2][19], const ew_v3u &t3) {
+#if EW_LOAD_HALF
+    half_transpose(T[0]);
+    half_transpose(T[1]);
+#else
     row_transpose(T[0]);
     row_transpose(T[1]);
+#endif
     // unit 0's lane 63 continues into unit 1's piece 0 (lane 0): wave_rol:1
     ew_v3u f3;
     f3.x = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)T[1][0], EW_DPP_WAVE_ROL1, 0xf, 0xf, false);
@@ -472,7 +546,7 @@ __global__ __launch_bounds__(EW_THREADS, 1) void k_stream(StreamArgs a) {
     next3_fast(f3, T[0]);
     next3_fast(t3, T[1]);
     const uint32_t uu[2] = {2 * p, 2 * p + 1};
-    stream_units<2, FIND>(a, s_slice, s_s64, s_s128, Lt, uu, T);
+    stream_units<2, FIND, true>(a, s_slice, s_s64, s_s128, Lt, uu, T);
   };
   const uint32_t npairs = PB + p0 < NP ? (NP - 1 - PB - p0) / W + 1 : 0u;
   auto pair_at = [&](uint32_t k) {   // clamped: a prefetch past the end reloads the last pair
@@ -485,8 +559,18 @@ __global__ __launch_bounds__(EW_THREADS, 1) void k_stream(StreamArgs a) {
     load_pair(pair_at(1), DB, nB);
   }
   stage_lds<EW_THREADS>((uint32_t *)s_slice, EW_SLICE_DWORDS, [&](int i) { return a.g_slice[slice_src(i)]; });
+#if EW_TREE4
+  stage_lds<EW_THREADS>(s_s64, 4096, [&](int i) {
+    const int k = i >> 10, j = i & 1023;   // table k of lane class k; j = t * 256 + b: S(b << 8t)
+    if (k == 3) return (uint32_t)(j & 255) << (8 * (j >> 8));
+    if (k == 2) return a.g_shift[6 * 1024 + j];
+    if (k == 1) return a.g_shift[7 * 1024 + j];
+    return tab_apply(a.g_shift + 7 * 1024, a.g_shift[6 * 1024 + j]);   // S_192 = S_128 . S_64
+  });
+#else
   stage_lds<EW_THREADS>(s_s64, 1024, [&](int i) { return a.g_shift[6 * 1024 + i]; });
   stage_lds<EW_THREADS>(s_s128, 1024, [&](int i) { return a.g_shift[7 * 1024 + i]; });
+#endif
   __syncthreads();
   // sched_barrier: each batch of loads stays ahead of the previous pair's arithmetic
   for (uint32_t k = 0; k < npairs; k += 3) {   // A is processed while B and C load, and so on
