@@ -119,6 +119,7 @@ struct ewal_ctx {
   bool own_stream = false;
   hipEvent_t ev0 = nullptr, ev1 = nullptr, evs0 = nullptr, evs1 = nullptr;
   hipEvent_t evf0 = nullptr, evf1 = nullptr;   // around k_frames (the serial pipeline)
+  hipEvent_t evf_start = nullptr;              // the frame pass's start: evf0, or evs1 when nothing ran between
   bool frames_timed = false;                   // evf0 / evf1 bracket this call's frame pass
   std::map<uint32_t, DevTables> tables;
   std::map<uint32_t, std::unique_ptr<ewal::CrcTables>> host_tables;
@@ -369,7 +370,10 @@ static int run_stream(ewal_ctx *c, DevTables *tb, const uint8_t *d_buf, uint64_t
   else
     hipLaunchKernelGGL(k_stream<false>, dim3(grid), dim3(EW_THREADS), 0, c->stream, a);
   EW_CHECK(hipGetLastError());
-  EW_CHECK(hipEventRecord(c->evs1, c->stream));
+#ifdef EW_ABLATION_HOOKS
+  if (!std::getenv("EWAL_NO_MID_EVENTS"))   // tools/ only
+#endif
+    EW_CHECK(hipEventRecord(c->evs1, c->stream));
   if (!scan) return 0;
   return run_cand_scan(c, tb, d_buf, B, find_cand, ccap);
 }
@@ -716,12 +720,21 @@ static int reset_small(ewal_ctx *c) {
 // The call's device times from its events (ev1 already synchronised):
 // device_ms ev0 -> ev1, stream_ms evs0 -> evs1, post_ms evs1 -> ev1 and, when
 // the frame pass ran as one launch, frames_ms evf0 -> evf1.
+#ifndef EW_FR_EVF0
+#define EW_FR_EVF0 0
+#endif
 static int set_times(ewal_ctx *c, ewal_result *o, uint32_t n = 1) {
   float dev = 0, str = 0, post = 0, fr = 0;
   EW_CHECK(hipEventElapsedTime(&dev, c->ev0, c->ev1));
+#ifdef EW_ABLATION_HOOKS
+  if (std::getenv("EWAL_NO_MID_EVENTS")) {   // tools/ only: the whole call's time alone
+    for (uint32_t i = 0; i < n; ++i) o[i].device_ms = dev;
+    return 0;
+  }
+#endif
   EW_CHECK(hipEventElapsedTime(&str, c->evs0, c->evs1));
   EW_CHECK(hipEventElapsedTime(&post, c->evs1, c->ev1));
-  if (c->frames_timed) EW_CHECK(hipEventElapsedTime(&fr, c->evf0, c->evf1));
+  if (c->frames_timed) EW_CHECK(hipEventElapsedTime(&fr, c->evf_start ? c->evf_start : c->evf0, c->evf1));
   for (uint32_t i = 0; i < n; ++i) {
     o[i].device_ms = dev;
     o[i].stream_ms = str;
@@ -876,9 +889,22 @@ static int frames_pass(ewal_ctx *c, DevTables *tb, const uint8_t *d_buf, uint64_
       if (int rc = ov_launch(c, tsh, nunits, ntiles, a)) return rc;
       c->frames_timed = false;
     } else {
-      EW_CHECK(hipEventRecord(c->evf0, c->stream));
+      // the stream pass's end event doubles as the frame pass's start on the
+      // first pass (no work between them): one marker fewer between the two
+      // kernels (EW_FR_EVF0=1: its own event, A/B)
+      if (EW_FR_EVF0 || pass) {
+        EW_CHECK(hipEventRecord(c->evf0, c->stream));
+        c->evf_start = c->evf0;
+      } else {
+        c->evf_start = c->evs1;
+      }
+#ifdef EW_ABLATION_HOOKS
+      const bool mid = !std::getenv("EWAL_NO_MID_EVENTS");   // tools/ only: the markers' own cost
+#else
+      const bool mid = true;
+#endif
       fr_launch_frames<false>(tsh, ntiles, a, FrSeg{}, fr_cus(c), c->stream);
-      EW_CHECK(hipEventRecord(c->evf1, c->stream));
+      if (mid) EW_CHECK(hipEventRecord(c->evf1, c->stream));
       fr_launch_seam<false>(c, tsh, ntiles, a, FrSeg{}, c->h_res_dev, c->h_small_dev);
       c->frames_timed = true;
     }
@@ -1527,6 +1553,7 @@ static int frames_batch(ewal_ctx *c, DevTables *tb, const uint8_t *d_buf, uint64
     hipLaunchKernelGGL(k_shard_rbase, dim3(1), dim3(1024), 0, c->stream, (const unsigned long long *)c->fnfp.p, ns,
                        ecap, sg.rbase, sg.sp, ds);
     EW_CHECK(hipEventRecord(c->evf0, c->stream));
+    c->evf_start = c->evf0;
     fr_launch_frames<true>(tsh, ntiles, a, sg, fr_cus(c), c->stream);
     EW_CHECK(hipEventRecord(c->evf1, c->stream));
     fr_launch_seam<true>(c, tsh, ntiles, a, sg, nullptr, nullptr);
