@@ -121,6 +121,7 @@ struct ewal_ctx {
   hipEvent_t evf0 = nullptr, evf1 = nullptr;   // around k_frames (the serial pipeline)
   hipEvent_t evf_start = nullptr;              // the frame pass's start: evf0, or evs1 when nothing ran between
   bool frames_timed = false;                   // evf0 / evf1 bracket this call's frame pass
+  bool spin = false;                           // ew_sync: spin on the stream instead of blocking
   std::map<uint32_t, DevTables> tables;
   std::map<uint32_t, std::unique_ptr<ewal::CrcTables>> host_tables;
   DevBuf encw, encs, lbstat, gagg, slow, mlist, pf, v, pwave, ux, tagg, tpx, wcnt, slots, cbase, ovf, cpos, clen, nxt, exc, E, rs, jl, vis, entry, on, rec_cand, rd, opf, ops, kk, kkrev, suf,
@@ -723,6 +724,20 @@ static int reset_small(ewal_ctx *c) {
 #ifndef EW_FR_EVF0
 #define EW_FR_EVF0 0
 #endif
+// The call's wait for its last kernel: a spin on the stream's completion
+// (c->spin) instead of the runtime's blocking wait, whose wake-up sits between
+// the device finishing and the host seeing the result.
+static hipError_t ew_sync(ewal_ctx *c) {
+  bool spin = c->spin;
+#ifdef EW_ABLATION_HOOKS
+  if (const char *e = std::getenv("EWAL_SPIN")) spin = std::atoi(e) != 0;   // tools/ only
+#endif
+  if (!spin) return hipStreamSynchronize(c->stream);
+  hipError_t e;
+  while ((e = hipStreamQuery(c->stream)) == hipErrorNotReady) {
+  }
+  return e;
+}
 static int set_times(ewal_ctx *c, ewal_result *o, uint32_t n = 1) {
   float dev = 0, str = 0, post = 0, fr = 0;
   EW_CHECK(hipEventElapsedTime(&dev, c->ev0, c->ev1));
@@ -916,7 +931,7 @@ static int frames_pass(ewal_ctx *c, DevTables *tb, const uint8_t *d_buf, uint64_
     // the call's end event rides behind the last kernel: when the regular
     // case held, the sync below is the call's only wait for the device
     EW_CHECK(hipEventRecord(c->ev1, c->stream));
-    EW_CHECK(hipStreamSynchronize(c->stream));
+    EW_CHECK(ew_sync(c));
     const Small *hs = c->h_small;
     if (ew_debug())
       std::fprintf(stderr, "ewal frames: pass %d tsh %d spec %u rare %u irr %u need %llu nmeta %u K %llu\n", pass, tsh,
@@ -1567,7 +1582,7 @@ static int frames_batch(ewal_ctx *c, DevTables *tb, const uint8_t *d_buf, uint64
     EW_CHECK(hipMemcpyAsync(out, c->bres.p, (size_t)ns * sizeof(ewal_result), hipMemcpyDeviceToHost, c->stream));
     EW_CHECK(hipMemcpyAsync(c->bent_first.data(), c->bef.p, (size_t)ns * 8, hipMemcpyDeviceToHost, c->stream));
     EW_CHECK(hipEventRecord(c->ev1, c->stream));
-    EW_CHECK(hipStreamSynchronize(c->stream));
+    EW_CHECK(ew_sync(c));
     const Small *hs = c->h_small;
     if (hs->errflag) return EWAL_E_TIMEOUT;
     c->last_k = hs->total;
