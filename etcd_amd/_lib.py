@@ -58,6 +58,8 @@ FLAG_METADATA_SPLIT = 2   # metadata_off / _len index the split bytes (ewal_copy
 FLAG_FAST_PATH = 4        # the fused frame pass decided this result (diagnostics)
 OPT_GENERAL_PATH = 1      # ewal_ctx_set_options: every ReadAll on the general path
 OPT_OVERLAP = 2           # ewal_ctx_set_options: the overlapped stream / frame pipeline (opt-in)
+OPT_VH_ON = 4             # ewal_ctx_set_options: the frame pass's 128-B prefixes forced on (default: record-dense WALs)
+OPT_VH_OFF = 8            # ... forced off
 RANGE_DEFER_FIRST = 1     # ewal_readall_range_device: frame 0's CRC check is the caller's
 
 CASTAGNOLI, IEEE, KOOPMAN = 0x82F63B78, 0xEDB88320, 0xEB31D82E

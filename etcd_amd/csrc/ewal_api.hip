@@ -121,7 +121,16 @@ struct ewal_ctx {
   hipEvent_t evf0 = nullptr, evf1 = nullptr;   // around k_frames (the serial pipeline)
   hipEvent_t evf_start = nullptr;              // the frame pass's start: evf0, or evs1 when nothing ran between
   bool frames_timed = false;                   // evf0 / evf1 bracket this call's frame pass
-  bool spin = false;                           // ew_sync: spin on the stream instead of blocking
+  bool spin = true;                            // ew_sync: spin on the stream instead of blocking (profiles/r05/
+                                               // host_gap_*.txt: the call's host time 21 -> 14 us on configs[0])
+  // record-dense WALs: the stream pass also stores vh[] (every super-piece's
+  // first 128-B half) and the frame pass takes its prefixes at 128-B
+  // granularity.  vh_opt: 0 auto (the ctx's previous single ReadAll had >= 4
+  // frames per 4 KiB unit: dense_hint), 1 on, -1 off (EWAL_OPT_VH_ON / _OFF)
+  int vh_opt = 0;
+  bool dense_hint = false;
+  uint32_t *vh_next = nullptr;                 // run_stream: the vh[] of this call's stream pass
+  DevBuf vhb;
   std::map<uint32_t, DevTables> tables;
   std::map<uint32_t, std::unique_ptr<ewal::CrcTables>> host_tables;
   DevBuf encw, encs, lbstat, gagg, slow, mlist, pf, v, pwave, ux, tagg, tpx, wcnt, slots, cbase, ovf, cpos, clen, nxt, exc, E, rs, jl, vis, entry, on, rec_cand, rd, opf, ops, kk, kkrev, suf,
@@ -359,6 +368,8 @@ static int run_stream(ewal_ctx *c, DevTables *tb, const uint8_t *d_buf, uint64_t
   a.small = ds;
   a.u_begin = 0;
   a.u_end = nunits;
+  a.vh = find_cand ? c->vh_next : nullptr;
+  c->vh_next = nullptr;
   c->ov_sa = a;
   if (!launch) return 0;   // the overlapped pipeline launches the stream pass in chunks (frames_pass)
   unsigned grid = (unsigned)std::min<uint64_t>((nunits + 2 * EW_WAVES - 1) / (2 * EW_WAVES), (uint64_t)c->num_cu);
@@ -708,6 +719,7 @@ static FrArgs fr_args(ewal_ctx *c, DevTables *tb, const uint8_t *d_buf, uint64_t
   a.t0 = 0;
   a.nrun = 0;
   a.tick = nullptr;
+  a.vh = nullptr;
   return a;
 }
 // the call's scratch as k_stream leaves it (a rerun of the frame pass, or the
@@ -814,6 +826,12 @@ static void ov_stream_chunk(ewal_ctx *c, uint32_t ub, uint32_t ue, int cus, hipS
 template <bool SEG>
 static void fr_launch_frames(int tsh, uint32_t nt, const FrArgs &a, const FrSeg &sg, int cus, hipStream_t st) {
   const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(grid_for(nt, FR_WAVES), (uint64_t)cus));
+  if (!SEG && a.vh) {   // record-dense: the 128-B prefixes
+    if (tsh == 8) hipLaunchKernelGGL((k_frames<false, 8, true>), dim3(grid), dim3(FR_THREADS), 0, st, a, sg);
+    else if (tsh == 6) hipLaunchKernelGGL((k_frames<false, 6, true>), dim3(grid), dim3(FR_THREADS), 0, st, a, sg);
+    else hipLaunchKernelGGL((k_frames<false, 4, true>), dim3(grid), dim3(FR_THREADS), 0, st, a, sg);
+    return;
+  }
   if (tsh == 8) hipLaunchKernelGGL((k_frames<SEG, 8>), dim3(grid), dim3(FR_THREADS), 0, st, a, sg);
   else if (tsh == 6) hipLaunchKernelGGL((k_frames<SEG, 6>), dim3(grid), dim3(FR_THREADS), 0, st, a, sg);
   else hipLaunchKernelGGL((k_frames<SEG, 4>), dim3(grid), dim3(FR_THREADS), 0, st, a, sg);
@@ -890,6 +908,7 @@ static int frames_pass(ewal_ctx *c, DevTables *tb, const uint8_t *d_buf, uint64_
     EW_CHECK(c->mlist.ensure((size_t)mcap * 8));
     if (pass) if (int rc = reset_small(c)) return rc;
     FrArgs a = fr_args(c, tb, d_buf, B, nunits, ntiles, ri, c->ents.as<ewal_entry>(), ecap, mcap);
+    a.vh = c->ov_sa.vh;   // the stream pass's vh[] when it stored one (record-dense WALs)
     if (rew) {
       clcap = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(clcap, ecap), 0xffffffffull);
       EW_CHECK(c->fown.ensure((size_t)ecap * 8));
@@ -1074,6 +1093,14 @@ static int readall_impl(ewal_ctx *c, const uint8_t *d_buf, uint64_t B, uint64_t 
     const uint32_t nunits_ov = (uint32_t)(B / EW_WAVE_BYTES + 1);
     const bool ov = !EW_XS && c->ov_opt && c->fused && B >= (512ull << 20) && fr_tsh(c, nunits_ov) == 8 &&
                     ov_ready(c);
+    // record-dense WALs (the ctx's previous ReadAll: >= 4 frames per 4 KiB
+    // unit, or EWAL_OPT_VH_ON): the stream pass also stores vh[] and the
+    // frame pass takes its prefixes from 128-B boundaries
+    const bool vh = c->fused && (c->vh_opt > 0 || (c->vh_opt == 0 && c->dense_hint));
+    if (vh) {
+      EW_CHECK(c->vhb.ensure(((size_t)B / EW_WAVE_BYTES + 1) * EW_VPU * 4));
+      c->vh_next = c->vhb.as<uint32_t>();
+    }
     rc = run_stream(c, tb, d_buf, B, 1, ccap, !c->fused, !ov);
     if (rc) return rc;
     if (c->defer_first && !ov) EW_CHECK(hipMemsetAsync(&ds->defer_first, 1, 1, c->stream));   // (Small is zeroed by k_stream)
@@ -1489,6 +1516,7 @@ static int readall_impl(ewal_ctx *c, const uint8_t *d_buf, uint64_t B, uint64_t 
   }
   if (fused_done_final) out->flags |= EWAL_FLAG_FAST_PATH;
   c->last_n = n;
+  if (B) c->dense_hint = n * EW_WAVE_BYTES >= 4 * B;   // >= 4 frames per 4 KiB unit: the next call stores vh[]
   c->rec_rebuild = n && !c->rd_valid;   // the fused pass decided: descriptors are rebuilt on demand
   c->rec_valid = true;
   if (!ev1_final) EW_CHECK(hipEventRecord(c->ev1, c->stream));
@@ -2106,9 +2134,11 @@ int ewal_ctx_set_stream(ewal_ctx *c, void *s) {
 }
 
 int ewal_ctx_set_options(ewal_ctx *c, uint32_t opts) {
-  if (!c || (opts & ~(EWAL_OPT_GENERAL_PATH | EWAL_OPT_OVERLAP))) return EWAL_E_INVAL;
+  const uint32_t known = EWAL_OPT_GENERAL_PATH | EWAL_OPT_OVERLAP | EWAL_OPT_VH_ON | EWAL_OPT_VH_OFF;
+  if (!c || (opts & ~known) || ((opts & EWAL_OPT_VH_ON) && (opts & EWAL_OPT_VH_OFF))) return EWAL_E_INVAL;
   c->fused = (opts & EWAL_OPT_GENERAL_PATH) ? 0 : 1;
   c->ov_opt = (opts & EWAL_OPT_OVERLAP) != 0;
+  c->vh_opt = (opts & EWAL_OPT_VH_ON) ? 1 : (opts & EWAL_OPT_VH_OFF) ? -1 : 0;
   return EWAL_OK;
 }
 

@@ -21,6 +21,8 @@ struct StreamArgs {
   Small *small;            // the call's device scratch, zeroed by k_stream's workgroup 0 (of the launch
                            // that starts at unit 0)
   uint32_t u_begin, u_end; // the units this launch covers (a chunk of the stream: u_begin even; all: 0, nunits)
+  uint32_t *vh;            // record-dense WALs (the frame pass's 128-B prefixes): the lin of every super-piece's
+                           // first 128-B half [nunits*16], else null
 };
 
 struct ScanArgs {

@@ -119,6 +119,7 @@ struct FrArgs {
   // of the stream whose stream pass has completed (the overlapped pipeline)
   uint32_t t0, nrun;
   uint32_t *tick;                  // this launch's tile counter (zeroed before it)
+  const uint32_t *vh;              // record-dense WALs: the first 128-B half's lin of every super-piece (k_stream), else null
 };
 struct FrSeg {
   uint32_t ns;
@@ -248,12 +249,15 @@ __device__ __noinline__ void fr_decode_slow(const uint8_t *__restrict__ buf, uin
 }
 
 // canon_finish (wal_kernels.hip) on the frame at p with P relative to the
-// tile: pw = P at p's unit start
+// tile: pw = P at p's unit start.  VH: the prefix from the nearest 128-B
+// boundary (vh[], prefix_load_near_vh), else the nearest 256-B one.
+template <bool VH>
 __device__ __forceinline__ bool fr_decode(const uint8_t *__restrict__ buf, uint64_t B, uint64_t p, uint32_t pw,
-                                          const uint32_t *__restrict__ v, const uint32_t *s_t16, const uint32_t *s_svp,
-                                          const uint32_t *s_inv, uint32_t *w, RecDesc &d, int64_t &L, uint32_t &Pfo,
+                                          const uint32_t *__restrict__ v, const uint32_t *__restrict__ vh,
+                                          const uint32_t *s_t16, const uint32_t *s_svp, const uint32_t *s_inv,
+                                          const uint32_t *s_n128, uint32_t *w, RecDesc &d, int64_t &L, uint32_t &Pfo,
                                           uint32_t &Pfd) {
-  CanonLoad<true> ld;
+  CanonLoad<VH ? 2 : 1> ld;
   const uint64_t p16 = p & ~15ull;
 #pragma unroll
   for (int k = 0; k < 5; ++k) {
@@ -267,9 +271,11 @@ __device__ __forceinline__ bool fr_decode(const uint8_t *__restrict__ buf, uint6
       ld.hq[k] = make_uint4(x[0], x[1], x[2], x[3]);
     }
   }
-  prefix_load_near_pw(p, B, pw, v, buf, ld.pin);
+  if constexpr (VH) prefix_load_near_vh(p, B, pw, v, vh, buf, ld.pin);
+  else prefix_load_near_pw(p, B, pw, v, buf, ld.pin);
   const bool slow = ld.pin.slow;
-  const bool ok = canon_finish<FR_THREADS, true>(buf, B, p, nullptr, v, s_t16, s_svp, w, d, L, Pfo, Pfd, slow, s_inv, ld);
+  const bool ok = canon_finish<FR_THREADS, VH ? 2 : 1>(buf, B, p, nullptr, v, s_t16, s_svp, w, d, L, Pfo, Pfd, slow,
+                                                       s_inv, ld, s_n128);
   if (slow) fr_decode_slow(buf, p, pw, v, s_t16, s_svp, d, Pfo, Pfd);
   return ok;
 }
@@ -371,7 +377,7 @@ struct FrAcc {
   uint32_t ash, pad;
 };
 
-template <bool SEG, int TSH>
+template <bool SEG, int TSH, bool VH = false>
 __global__ __launch_bounds__(FR_THREADS, 1) void k_frames(FrArgs a, FrSeg sg) {
 #ifdef FR_TIMING
   unsigned long long tacc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tlast = clock64();
@@ -631,7 +637,7 @@ __global__ __launch_bounds__(FR_THREADS, 1) void k_frames(FrArgs a, FrSeg sg) {
       d.type = 0; d.crc = 0; d.dlen = 0; d.doff = p + 8; d.f0 = d.f1 = d.f2 = 0; d.edoff = 0; d.edlen = 0;
       d.enil = 1; d.etype = 0; d.dnil = 1;
       if (isnew) {
-        ok = fr_decode(a.buf, a.B, p, pwu, a.v, s_t16, s_svp, s_inv, w, d, L, Pfo, Pfd);
+        ok = fr_decode<VH>(a.buf, a.B, p, pwu, a.v, a.vh, s_t16, s_svp, s_inv, s_nib + 7 * 128, w, d, L, Pfo, Pfd);
         if (!ok) { d.type = 0; d.dlen = 0; d.doff = p + 8; }
       }
       FR_T(3);

@@ -367,6 +367,15 @@ __device__ __forceinline__ void stream_units(const StreamArgs &a, const uint8_t 
     crc_pieces<NU>(s_slice, Lt, D, c);
   }
   const bool top = (lane & 3) == 3;
+  if (FIND && a.vh) {   // record-dense WALs: every super-piece's first 128-B half, S_64(c[4m]) ^ c[4m+1] (lane 4m+1)
+    const uint32_t *s64 = EW_TREE4 ? s_s64 + 2 * 1024 : s_s64;
+#pragma unroll
+    for (int i = 0; i < NU; ++i) {
+      const uint32_t o = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c[i], EW_DPP_ROW_SHR(1), 0xf, 0xf, false);
+      const uint32_t h = tab_apply(s64, o) ^ c[i];
+      if ((lane & 3) == 1) a.vh[(uint64_t)u[i] * EW_VPU + (lane >> 2)] = h;
+    }
+  }
 #if EW_TREE4
   // lin of every 256-B super-piece (lanes 4m .. 4m+3):
   //   S_192(c[4m]) ^ S_128(c[4m+1]) ^ S_64(c[4m+2]) ^ c[4m+3]
@@ -1416,22 +1425,18 @@ __device__ __forceinline__ void prefix_load_near(uint64_t x, uint64_t B, const u
 #define EW_FR_ABL 0   // timing-only ablations of the frame pass (tools/): 1 no Horner over v, 2 no prefix tail,
                       // 4 no S_dlen in the checks; results are wrong
 #endif
-__device__ __forceinline__ uint32_t prefix_finish_near(const PrefixNear &in, const uint32_t *t16, const uint32_t *svp,
-                                                       const uint32_t *inv) {
-  uint32_t acc = in.pw;
-  if (EW_FR_ABL & 2) return acc ^ in.vv[0].x ^ in.dd[0].y;
-#pragma unroll
-  for (int q = 0; q < EW_VPU / 4 && !(EW_FR_ABL & 1); ++q) {
-    if (4u * q + 0 < in.nk) acc = tab_apply(svp, acc) ^ in.vv[q].x;
-    if (4u * q + 1 < in.nk) acc = tab_apply(svp, acc) ^ in.vv[q].y;
-    if (4u * q + 2 < in.nk) acc = tab_apply(svp, acc) ^ in.vv[q].z;
-    if (4u * q + 3 < in.nk) acc = tab_apply(svp, acc) ^ in.vv[q].w;
-  }
-  if (!in.up) {   // forward over the n <= 128 bytes after x0
+// The prefix tail from the Horner result acc at the boundary the load chose
+// (prefix_load_near: x0 below x, or the next boundary x1 above it): forward
+// over the bytes [x0, x), or lin(stream[x, x1)) stepped back with the inverse
+// shifts.  NCH: the chunks the load holds.
+template <int NCH, class PN>
+__device__ __forceinline__ uint32_t prefix_near_tail(uint32_t acc, const PN &in, const uint32_t *t16,
+                                                     const uint32_t *inv) {
+  if (!in.up) {   // forward over the n bytes after x0
     const uint32_t nq = in.n >> 4;
     uint4 pc = in.dd[0];
 #pragma unroll
-    for (int q = 0; q < 9; ++q) {
+    for (int q = 0; q < NCH; ++q) {
       if ((uint32_t)q < nq) acc = step16(t16, acc, in.dd[q]);
       if (q && (uint32_t)q == nq) pc = in.dd[q];
     }
@@ -1458,7 +1463,7 @@ __device__ __forceinline__ uint32_t prefix_finish_near(const PrefixNear &in, con
   }
   const uint32_t nq = in.n >> 4;   // in.n is a multiple of 16 here
 #pragma unroll
-  for (int q = 1; q < 9; ++q)
+  for (int q = 1; q < NCH; ++q)
     if ((uint32_t)q < nq) c = step16(t16, c, in.dd[q]);
   uint32_t x = acc ^ c;
   const uint32_t m = in.n - lead;   // x1 - x, 1..127
@@ -1466,6 +1471,67 @@ __device__ __forceinline__ uint32_t prefix_finish_near(const PrefixNear &in, con
   for (int l = 0; l < 7; ++l)
     if ((m >> l) & 1) x = nib_apply(inv + l * 128, x);
   return x;
+}
+__device__ __forceinline__ uint32_t prefix_finish_near(const PrefixNear &in, const uint32_t *t16, const uint32_t *svp,
+                                                       const uint32_t *inv) {
+  uint32_t acc = in.pw;
+  if (EW_FR_ABL & 2) return acc ^ in.vv[0].x ^ in.dd[0].y;
+#pragma unroll
+  for (int q = 0; q < EW_VPU / 4 && !(EW_FR_ABL & 1); ++q) {
+    if (4u * q + 0 < in.nk) acc = tab_apply(svp, acc) ^ in.vv[q].x;
+    if (4u * q + 1 < in.nk) acc = tab_apply(svp, acc) ^ in.vv[q].y;
+    if (4u * q + 2 < in.nk) acc = tab_apply(svp, acc) ^ in.vv[q].z;
+    if (4u * q + 3 < in.nk) acc = tab_apply(svp, acc) ^ in.vv[q].w;
+  }
+  return prefix_near_tail<9>(acc, in, t16, inv);
+}
+
+// The same at 128-B granularity (the frame pass on record-dense WALs, round
+// 5): besides v[] the stream pass stored vh[], the lin of the FIRST 128-B
+// half of every super-piece, so P at a mid boundary is S_128(P(super-piece
+// start)) ^ vh -- the tail is at most 64 bytes forward or 64 stepped back
+// (half the bytes, 5 chunks of registers instead of 9).
+struct PrefixNearVH {
+  uint32_t pw, nk, n, up, lead, slow, mid, vhv;   // mid: the boundary is a super-piece's 128-B mid point
+  uint4 vv[EW_VPU / 4];
+  uint4 dd[5];
+};
+__device__ __forceinline__ void prefix_load_near_vh(uint64_t x, uint64_t B, uint32_t pw, const uint32_t *__restrict__ v,
+                                                    const uint32_t *__restrict__ vh, const uint8_t *__restrict__ buf,
+                                                    PrefixNearVH &in) {
+  const uint64_t w = x >> 12;
+  const uint64_t x0 = x & ~127ull;
+  const uint32_t tail = (uint32_t)(x - x0);
+  in.up = tail > 64 && x0 + 128 <= B;
+  in.slow = tail > 64 && !in.up;
+  const uint32_t rel = (uint32_t)((in.up ? x0 + 128 : x0) - (w << 12));   // the boundary in x's unit, 0..4096
+  in.nk = rel >> 8;
+  in.mid = (rel >> 7) & 1;
+  in.lead = (uint32_t)(x & 15);
+  const uint64_t base = in.up ? (x & ~15ull) : x0;
+  in.n = in.up ? (uint32_t)(x0 + 128 - base) : (in.slow ? 0u : tail);
+  const uint4 *vq = (const uint4 *)(v + w * EW_VPU);
+#pragma unroll
+  for (int q = 0; q < EW_VPU / 4; ++q) in.vv[q] = (4u * q < in.nk) ? vq[q] : make_uint4(0, 0, 0, 0);
+  in.vhv = in.mid ? vh[w * EW_VPU + in.nk] : 0u;
+  const uint4 *dq = (const uint4 *)(buf + base);
+#pragma unroll
+  for (int q = 0; q < 5; ++q) in.dd[q] = (16u * q < in.n) ? dq[q] : make_uint4(0, 0, 0, 0);
+  in.pw = pw;
+}
+__device__ __forceinline__ uint32_t prefix_finish_near_vh(const PrefixNearVH &in, const uint32_t *t16,
+                                                          const uint32_t *svp, const uint32_t *inv,
+                                                          const uint32_t *n128) {
+  uint32_t acc = in.pw;
+#pragma unroll
+  for (int q = 0; q < EW_VPU / 4; ++q) {
+    if (4u * q + 0 < in.nk) acc = tab_apply(svp, acc) ^ in.vv[q].x;
+    if (4u * q + 1 < in.nk) acc = tab_apply(svp, acc) ^ in.vv[q].y;
+    if (4u * q + 2 < in.nk) acc = tab_apply(svp, acc) ^ in.vv[q].z;
+    if (4u * q + 3 < in.nk) acc = tab_apply(svp, acc) ^ in.vv[q].w;
+  }
+  if (in.mid) acc = nib_apply(n128, acc) ^ in.vhv;
+  return prefix_near_tail<5>(acc, in, t16, inv);
 }
 
 // lin of the concatenation of every non-empty segment of bytes field fnum
@@ -1943,12 +2009,15 @@ struct NoOp {
 // The frame's loads (head + prefix operands) and the decode from them are
 // split so a caller can keep the next frame's loads in flight while it
 // decodes this one (canon_issue / canon_finish); decode_canon runs both.
-template <bool NEAR>
+// NEAR: 0 prefix_load (the general path), 1 prefix_load_near (the frame
+// pass), 2 prefix_load_near_vh (the frame pass at 128-B granularity)
+template <int NEAR>
 struct CanonLoad {
   uint4 hq[5];
-  typename std::conditional<NEAR, PrefixNear, PrefixIn>::type pin;
+  typename std::conditional<NEAR == 2, PrefixNearVH,
+                            typename std::conditional<NEAR == 1, PrefixNear, PrefixIn>::type>::type pin;
 };
-template <bool NEAR>
+template <int NEAR>
 __device__ __forceinline__ void canon_issue(const uint8_t *__restrict__ buf, uint64_t B, uint64_t p,
                                             const uint32_t *__restrict__ pwave, const uint32_t *__restrict__ v,
                                             CanonLoad<NEAR> &ld) {
@@ -1965,15 +2034,17 @@ __device__ __forceinline__ void canon_issue(const uint8_t *__restrict__ buf, uin
       ld.hq[k] = make_uint4(x[0], x[1], x[2], x[3]);
     }
   }
-  if constexpr (NEAR) prefix_load_near(p, B, pwave, v, buf, ld.pin);
+  static_assert(NEAR != 2, "the frame pass loads its own operands (fr_decode)");
+  if constexpr (NEAR == 1) prefix_load_near(p, B, pwave, v, buf, ld.pin);
   else prefix_load(p, pwave, v, buf, ld.pin);
 }
-template <int WS, bool NEAR>
+template <int WS, int NEAR>
 __device__ __forceinline__ bool canon_finish(const uint8_t *__restrict__ buf, uint64_t B, uint64_t p,
                                              const uint32_t *__restrict__ pwave, const uint32_t *__restrict__ v,
                                              const uint32_t *s_t4, const uint32_t *s_svp, uint32_t *w, RecDesc &d,
                                              int64_t &L, uint32_t &Pfo, uint32_t &Pfd, bool noprefix,
-                                             const uint32_t *s_inv, const CanonLoad<NEAR> &ld) {
+                                             const uint32_t *s_inv, const CanonLoad<NEAR> &ld,
+                                             const uint32_t *s_n128 = nullptr) {
   const uint64_t p16 = p & ~15ull;
   const auto &pin = ld.pin;
 #pragma unroll
@@ -2021,7 +2092,9 @@ __device__ __forceinline__ bool canon_finish(const uint8_t *__restrict__ buf, ui
   }
   // P at the frame start even when the frame is not canonical: the frame
   // before it takes it as its P(data end) (a batched shard's torn last frame)
-  if constexpr (NEAR)
+  if constexpr (NEAR == 2)   // (the frame pass: a slow position comes back as noprefix, fr_decode_slow)
+    Pfo = noprefix ? pin.pw : prefix_finish_near_vh(pin, s_t4, s_svp, s_inv, s_n128);
+  else if constexpr (NEAR == 1)
     Pfo = noprefix ? pin.pw
                    : (pin.slow ? prefix_at(p, pwave, v, buf, s_t4, s_svp) : prefix_finish_near(pin, s_t4, s_svp, s_inv));
   else Pfo = noprefix ? pin.pw : prefix_finish16(pin, s_t4, s_svp);
@@ -2037,7 +2110,7 @@ __device__ __forceinline__ bool canon_finish(const uint8_t *__restrict__ buf, ui
   }
   return true;
 }
-template <int WS, bool NEAR = false, class AfterIssue = NoOp>
+template <int WS, int NEAR = 0, class AfterIssue = NoOp>
 __device__ __forceinline__ bool decode_canon(const uint8_t *__restrict__ buf, uint64_t B, uint64_t p,
                                              const uint32_t *__restrict__ pwave, const uint32_t *__restrict__ v,
                                              const uint32_t *s_t4, const uint32_t *s_svp, uint32_t *w, RecDesc &d,

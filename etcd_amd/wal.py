@@ -91,12 +91,15 @@ class Context:
         except Exception:
             pass
 
-    def set_options(self, general_path=False, overlap=False):
+    def set_options(self, general_path=False, overlap=False, vh=None):
         """ewal_ctx_set_options: general_path=True makes every ReadAll take the
         general path (for cross-checking it against the fused pass);
-        overlap=True the opt-in overlapped stream / frame pipeline."""
+        overlap=True the opt-in overlapped stream / frame pipeline; vh=True /
+        False forces the frame pass's 128-B prefixes on / off (None: on for
+        record-dense WALs)."""
         check(lib.ewal_ctx_set_options(self._p, (L.OPT_GENERAL_PATH if general_path else 0) |
-                                       (L.OPT_OVERLAP if overlap else 0)))
+                                       (L.OPT_OVERLAP if overlap else 0) |
+                                       (0 if vh is None else (L.OPT_VH_ON if vh else L.OPT_VH_OFF))))
 
     def set_stream(self, hip_stream):
         """Run this ctx's work on a caller-owned hipStream_t (e.g. torch's)."""

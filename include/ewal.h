@@ -158,6 +158,14 @@ int ewal_ctx_reserve(ewal_ctx *ctx, uint64_t wal_bytes, uint32_t flags);
  * with this option owns two extra streams: destroy it before the process
  * exits. */
 #define EWAL_OPT_OVERLAP 2u
+/* Record-dense WALs (round 5): the stream pass also stores the lin of every
+ * 256-B super-piece's first 128-B half, and the frame pass takes every frame
+ * start's prefix from the nearest 128-B boundary instead of the nearest 256-B
+ * one (half the tail bytes).  By default a ctx turns it on when its previous
+ * single ReadAll had >= 4 frames per 4 KiB (average frame <= 1 KiB);
+ * EWAL_OPT_VH_ON / EWAL_OPT_VH_OFF force it either way (the same results). */
+#define EWAL_OPT_VH_ON 4u
+#define EWAL_OPT_VH_OFF 8u
 int ewal_ctx_set_options(ewal_ctx *ctx, uint32_t opts);
 const char *ewal_status_string(int status);
 /* Device time (ms) of the last pipeline call on this ctx (HIP events). */
