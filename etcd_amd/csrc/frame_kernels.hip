@@ -60,6 +60,7 @@ struct FrTile {
   uint32_t crc0, pfd0, pe0;   // the first frame's check operands (pe0: FRT_PE0)
   uint32_t seedz, pfdz;       // the last frame's (seedz: FRT_SEEDZ)
   uint32_t flags;
+  uint32_t peB;            // the stream's last tile (FRT_PEB): P at the stream end, tile-local
   uint64_t dlen0, dlenz;
   // entry ops
   uint32_t nops, seam;     // seam: the gap rule for the tile's first op is the seam pass's
@@ -76,6 +77,7 @@ struct FrTile {
 #define FRT_TORN0 16u      // batch: the first / last frame runs past its shard's end (a terminal, no frame)
 #define FRT_TORNZ 32u
 #define FRT_OKZ 64u        // the last frame decoded (canonical layout)
+#define FRT_PEB 128u       // peB holds P at the stream end (single WAL, its last tile)
 
 // Batch: per shard, positions in the batch buffer.
 struct ShardPos {
@@ -246,6 +248,16 @@ __device__ __noinline__ void fr_decode_slow(const uint8_t *__restrict__ buf, uin
   for (uint64_t n = d.doff - p; n; --n) delta = s_t16[delta & 0xff] ^ (delta >> 8);   // S_1, byte by byte
   Pfd ^= delta;
   Pfo = P;
+}
+
+// P at the stream end B from its unit's start (pw, tile-local): the stream's
+// last frame's P(data end), computed by the wave that ran the last tile
+// through the LDS tables (the seam pass would step up to 255 bytes through
+// global ones); out of line, once per call
+__device__ __noinline__ uint32_t fr_prefix_end(const uint8_t *__restrict__ buf, uint64_t B, uint32_t pw,
+                                               const uint32_t *__restrict__ v, const uint32_t *s_t16,
+                                               const uint32_t *s_svp) {
+  return prefix_at_pw(B, pw, v, buf, s_t16, s_svp);
 }
 
 // canon_finish (wal_kernels.hip) on the frame at p with P relative to the
@@ -963,6 +975,10 @@ __global__ __launch_bounds__(FR_THREADS, 1) void k_frames(FrArgs a, FrSeg sg) {
         T->last_state1 = tr.last_state1;
         T->meta0 = tr.meta0;
         atomicAdd(&ds->total, (unsigned long long)nfr);
+        if (!SEG && (uint64_t)u0 + TU >= a.nunits) {   // the stream's last tile
+          T->peB = fr_prefix_end(a.buf, a.B, spw[(uint32_t)((a.B >> 12) - u0)], a.v, s_t16, s_svp);
+          T->flags |= FRT_PEB;
+        }
       }
     }
     FR_T(7);
@@ -1298,7 +1314,8 @@ __global__ __launch_bounds__(256) void k_frames_seam(FrArgs a, FrSeg sg, ResultD
         else atomicMin(&sg.sp[shz].term, (T.sz << 8) | (uint32_t)tst);
       }
     }
-    if (!pe_ok && !farn && T.dlenz && e <= a.B) Pe = fr_pe_far(a, s_n, t, e, TU, TLOG);
+    if (!pe_ok && !farn && T.dlenz && e <= a.B)   // (the stream's end: from the frame pass when it kept it)
+      Pe = (!SEG && e == a.B && (T.flags & FRT_PEB)) ? T.peB : fr_pe_far(a, s_n, t, e, TU, TLOG);
     if (!tornz && !farn && seededz && (T.flags & FRT_OKZ)) {
       const bool defer = !SEG && T.pz == 0 && ds->defer_first;
       const int st = fr_check(s_n, a.g_shift, T.typez, T.crcz, seedz, T.pfdz, Pe, T.dlenz, defer);
