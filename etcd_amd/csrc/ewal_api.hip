@@ -40,6 +40,7 @@ namespace {
 struct DevTables {
   uint32_t *slice = nullptr;  // [16][256] slicing-by-16 (the first 4 tables: slicing-by-4)
   uint32_t *shift = nullptr;  // [48][4][256]
+  uint32_t *unib = nullptr;   // [16][8][16] nibble tables of S_{256 (15 - m)}, m = 0..15 (k_stream's unit lins)
 };
 
 // Grow-only device buffer owned by a ctx (freed by its destructor when the
@@ -228,6 +229,24 @@ static int get_tables(ewal_ctx *c, uint32_t poly, DevTables **out) {
   EW_CHECK(hipMalloc(&t.shift, ht->shift.size() * sizeof(uint32_t)));
   EW_CHECK(hipMemcpy(t.slice, ht->slice16, sizeof(ht->slice16), hipMemcpyHostToDevice));
   EW_CHECK(hipMemcpy(t.shift, ht->shift.data(), ht->shift.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+  {   // unib[m][k][d] = S_{256 (15 - m)}(d << 4k): the shift of super-piece m's lin to its unit's end
+    std::vector<uint32_t> un(16 * 128);
+    auto apply = [&](int lvl, uint32_t x) {
+      const uint32_t *tb = &ht->shift[(size_t)lvl * 1024];
+      return tb[x & 0xff] ^ tb[256 + ((x >> 8) & 0xff)] ^ tb[512 + ((x >> 16) & 0xff)] ^ tb[768 + (x >> 24)];
+    };
+    for (int m = 0; m < 16; ++m)
+      for (int k = 0; k < 8; ++k)
+        for (uint32_t d = 0; d < 16; ++d) {
+          uint32_t x = d << (4 * k);
+          const uint32_t n = 256u * (15u - (uint32_t)m);
+          for (int lvl = 0; lvl < 32; ++lvl)
+            if ((n >> lvl) & 1u) x = apply(lvl, x);
+          un[(size_t)m * 128 + k * 16 + d] = x;
+        }
+    EW_CHECK(hipMalloc(&t.unib, un.size() * sizeof(uint32_t)));
+    EW_CHECK(hipMemcpy(t.unib, un.data(), un.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+  }
   c->host_tables[poly] = std::move(ht);
   c->tables[poly] = t;
   *out = &c->tables[poly];
@@ -370,6 +389,8 @@ static int run_stream(ewal_ctx *c, DevTables *tb, const uint8_t *d_buf, uint64_t
   a.u_end = nunits;
   a.vh = find_cand ? c->vh_next : nullptr;
   c->vh_next = nullptr;
+  a.ulin = c->ux.as<uint32_t>();   // (find_cand, EW_ULIN: the unit lins, read by the frame pass's phase A)
+  a.g_unib = tb->unib;
   c->ov_sa = a;
   if (!launch) return 0;   // the overlapped pipeline launches the stream pass in chunks (frames_pass)
   unsigned grid = (unsigned)std::min<uint64_t>((nunits + 2 * EW_WAVES - 1) / (2 * EW_WAVES), (uint64_t)c->num_cu);
@@ -720,6 +741,7 @@ static FrArgs fr_args(ewal_ctx *c, DevTables *tb, const uint8_t *d_buf, uint64_t
   a.nrun = 0;
   a.tick = nullptr;
   a.vh = nullptr;
+  a.ulin = c->ux.as<uint32_t>();
   return a;
 }
 // the call's scratch as k_stream leaves it (a rerun of the frame pass, or the
@@ -2100,6 +2122,7 @@ void ewal_ctx_destroy(ewal_ctx *c) {
   for (auto &kv : c->tables) {
     (void)hipFree(kv.second.slice);
     (void)hipFree(kv.second.shift);
+    (void)hipFree(kv.second.unib);
   }
   if (c->h_small) (void)hipHostFree(c->h_small);
   if (c->h_res) (void)hipHostFree(c->h_res);

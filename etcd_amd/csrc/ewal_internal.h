@@ -23,6 +23,8 @@ struct StreamArgs {
   uint32_t u_begin, u_end; // the units this launch covers (a chunk of the stream: u_begin even; all: 0, nunits)
   uint32_t *vh;            // record-dense WALs (the frame pass's 128-B prefixes): the lin of every super-piece's
                            // first 128-B half [nunits*16], else null
+  uint32_t *ulin;          // find_cand (EW_ULIN): the lin of every 4 KiB unit [nunits] (the frame pass's phase A)
+  const uint32_t *g_unib;  // [16][8][16] nibble tables of S_{256 (15 - m)} for it
 };
 
 struct ScanArgs {

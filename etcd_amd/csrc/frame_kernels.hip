@@ -122,6 +122,7 @@ struct FrArgs {
   uint32_t t0, nrun;
   uint32_t *tick;                  // this launch's tile counter (zeroed before it)
   const uint32_t *vh;              // record-dense WALs: the first 128-B half's lin of every super-piece (k_stream), else null
+  const uint32_t *ulin;            // EW_ULIN: every unit's lin (k_stream)
 };
 struct FrSeg {
   uint32_t ns;
@@ -447,6 +448,17 @@ __global__ __launch_bounds__(FR_THREADS, 1) void k_frames(FrArgs a, FrSeg sg) {
     // ---- A: the tile's unit lins, P at every unit start (tile-local) ----
     uint32_t x[UPL];
     uint32_t pcs = 0, lcnt = 0;   // flagged pieces per unit of the lane (8 bits each), their sum
+#if EW_ULIN
+#pragma unroll
+    for (int j = 0; j < UPL; ++j) {   // the unit lins k_stream stored
+      const uint32_t u = u0 + UPL * lane + j;
+      const bool in = u < a.nunits && (NL == 64 || lane < NL);
+      const uint32_t c = in ? (uint32_t)__popcll(a.hmask[u].x) : 0u;
+      pcs |= c << (8 * j);
+      lcnt += c;
+      x[j] = in ? a.ulin[u] : 0u;
+    }
+#else
     {
       uint4 vq[UPL][4];
 #pragma unroll
@@ -475,6 +487,7 @@ __global__ __launch_bounds__(FR_THREADS, 1) void k_frames(FrArgs a, FrSeg sg) {
 #endif
         }
     }
+#endif
 #pragma unroll
     for (int j = 0; j < UPL; ++j)
       if (NL == 64 || lane < NL) ucnt[UPL * lane + j] = 0;

@@ -340,6 +340,11 @@ __device__ __forceinline__ void half_transpose(uint32_t (&D)[19]) {
 #ifndef EW_LOAD_HALF
 #define EW_LOAD_HALF 0   // A/B: half-used-line loads + one permlane32 stage (see k_stream)
 #endif
+#ifndef EW_ULIN
+#define EW_ULIN 0    // A/B: k_stream stores every 4 KiB unit's lin and the frame pass's phase A loads it -- the
+                     // phase A saves 18 us on configs[1], the stream pass loses 68 (+4 %, +16 % on configs[0]):
+                     // off (profiles/r05/ab_notes.txt)
+#endif
 #ifndef EW_TREE4
 #define EW_TREE4 1   // the super-piece lins in one table step per lane + two DPP xors (round 5)
 #endif
@@ -350,7 +355,7 @@ __device__ __forceinline__ void half_transpose(uint32_t (&D)[19]) {
 #endif
 template <int NU, bool FIND, bool SAFE = false>   // SAFE: every piece lies inside the stream (the pair loop)
 __device__ __forceinline__ void stream_units(const StreamArgs &a, const uint8_t *s_slice, const uint32_t *s_s64,
-                                             const uint32_t *s_s128, const uint32_t (&Lt)[4],
+                                             const uint32_t *s_s128, const uint32_t *s_unib, const uint32_t (&Lt)[4],
                                              const uint32_t (&u)[NU], const uint32_t (&D)[NU][19]) {
   const int lane = threadIdx.x & 63;
   const uint64_t B = a.B;
@@ -425,6 +430,21 @@ __device__ __forceinline__ void stream_units(const StreamArgs &a, const uint8_t 
     for (int i = 0; i < NU; ++i)
       if ((!(EW_XS & 4) || c[i] == 0x12345678u) && !vskip[i]) a.v[(uint64_t)u[i] * EW_VPU + (lane >> 2)] = c[i];
   }
+  if (FIND && EW_ULIN) {
+    // the unit's lin: super-piece m's (lane 4m+3) moved by the 256 (15 - m)
+    // bytes after it -- one nibble-table step through its own table -- and
+    // the 16 xored into lane 63 (row_shr 4, 8 inside the rows, then the
+    // row broadcasts)
+#pragma unroll
+    for (int i = 0; i < NU; ++i) {
+      uint32_t e = nib_apply(s_unib + (lane >> 2) * 128, top ? c[i] : 0u);
+      e ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)e, EW_DPP_ROW_SHR(4), 0xf, 0xf, false);
+      e ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)e, EW_DPP_ROW_SHR(8), 0xf, 0xf, false);
+      e ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)e, EW_DPP_ROW_BCAST15, 0xa, 0xf, false);
+      e ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)e, EW_DPP_ROW_BCAST31, 0xc, 0xf, false);
+      if (lane == 63) a.ulin[u[i]] = e;
+    }
+  }
   if (!FIND) return;
   if (EW_SPLIT_CAND && !(EW_XS & 8)) {   // the flagged pieces, for k_cand
 #pragma unroll
@@ -482,6 +502,7 @@ __device__ __forceinline__ void stream_units(const StreamArgs &a, const uint8_t 
 template <bool FIND>
 __global__ __launch_bounds__(EW_THREADS, 1) void k_stream(StreamArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t s_slice[EW_SLICE_DWORDS * 4];
+  __shared__ uint32_t s_unib[(FIND && EW_ULIN) ? 16 * 128 : 1];   // the unit step: S_{256 (15 - m)} nibble tables
 #if EW_TREE4
   __shared__ uint32_t s_s64[4096];   // the super-piece step: S_192, S_128, S_64, identity byte tables
   uint32_t *const s_s128 = nullptr;
@@ -555,7 +576,7 @@ __global__ __launch_bounds__(EW_THREADS, 1) void k_stream(StreamArgs a) {
     next3_fast(f3, T[0]);
     next3_fast(t3, T[1]);
     const uint32_t uu[2] = {2 * p, 2 * p + 1};
-    stream_units<2, FIND, true>(a, s_slice, s_s64, s_s128, Lt, uu, T);
+    stream_units<2, FIND, true>(a, s_slice, s_s64, s_s128, s_unib, Lt, uu, T);
   };
   const uint32_t npairs = PB + p0 < NP ? (NP - 1 - PB - p0) / W + 1 : 0u;
   auto pair_at = [&](uint32_t k) {   // clamped: a prefetch past the end reloads the last pair
@@ -568,6 +589,7 @@ __global__ __launch_bounds__(EW_THREADS, 1) void k_stream(StreamArgs a) {
     load_pair(pair_at(1), DB, nB);
   }
   stage_lds<EW_THREADS>((uint32_t *)s_slice, EW_SLICE_DWORDS, [&](int i) { return a.g_slice[slice_src(i)]; });
+  if (FIND && EW_ULIN) stage_lds<EW_THREADS>(s_unib, 16 * 128, [&](int i) { return a.g_unib[i]; });
 #if EW_TREE4
   stage_lds<EW_THREADS>(s_s64, 4096, [&](int i) {
     const int k = i >> 10, j = i & 1023;   // table k of lane class k; j = t * 256 + b: S(b << 8t)
@@ -601,7 +623,7 @@ __global__ __launch_bounds__(EW_THREADS, 1) void k_stream(StreamArgs a) {
     load_piece(a.buf, B, off, D1[0]);
     load_next3(a.buf, B, off, D1[0]);
     const uint32_t uu[1] = {u};
-    stream_units<1, FIND>(a, s_slice, s_s64, s_s128, Lt, uu, D1);
+    stream_units<1, FIND>(a, s_slice, s_s64, s_s128, s_unib, Lt, uu, D1);
   }
 }
 
