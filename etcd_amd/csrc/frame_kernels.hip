@@ -77,7 +77,7 @@ struct FrTile {
 #define FRT_TORN0 16u      // batch: the first / last frame runs past its shard's end (a terminal, no frame)
 #define FRT_TORNZ 32u
 #define FRT_OKZ 64u        // the last frame decoded (canonical layout)
-#define FRT_PEB 128u       // peB holds P at the stream end (single WAL, its last tile)
+#define FRT_PEB 128u       // peB holds P at the stream end (the stream's last tile)
 
 // Batch: per shard, positions in the batch buffer.
 struct ShardPos {
@@ -988,7 +988,7 @@ __global__ __launch_bounds__(FR_THREADS, 1) void k_frames(FrArgs a, FrSeg sg) {
         T->last_state1 = tr.last_state1;
         T->meta0 = tr.meta0;
         atomicAdd(&ds->total, (unsigned long long)nfr);
-        if (!SEG && (uint64_t)u0 + TU >= a.nunits) {   // the stream's last tile
+        if ((uint64_t)u0 + TU >= a.nunits) {   // the stream's (the batch's) last tile
           T->peB = fr_prefix_end(a.buf, a.B, spw[(uint32_t)((a.B >> 12) - u0)], a.v, s_t16, s_svp);
           T->flags |= FRT_PEB;
         }
@@ -1328,7 +1328,7 @@ __global__ __launch_bounds__(256) void k_frames_seam(FrArgs a, FrSeg sg, ResultD
       }
     }
     if (!pe_ok && !farn && T.dlenz && e <= a.B)   // (the stream's end: from the frame pass when it kept it)
-      Pe = (!SEG && e == a.B && (T.flags & FRT_PEB)) ? T.peB : fr_pe_far(a, s_n, t, e, TU, TLOG);
+      Pe = (e == a.B && (T.flags & FRT_PEB)) ? T.peB : fr_pe_far(a, s_n, t, e, TU, TLOG);
     if (!tornz && !farn && seededz && (T.flags & FRT_OKZ)) {
       const bool defer = !SEG && T.pz == 0 && ds->defer_first;
       const int st = fr_check(s_n, a.g_shift, T.typez, T.crcz, seedz, T.pfdz, Pe, T.dlenz, defer);

@@ -340,6 +340,9 @@ __device__ __forceinline__ void half_transpose(uint32_t (&D)[19]) {
 #ifndef EW_LOAD_HALF
 #define EW_LOAD_HALF 0   // A/B: half-used-line loads + one permlane32 stage (see k_stream)
 #endif
+#ifndef EW_V_NT
+#define EW_V_NT 0    // A/B: v[] / hmask stored nontemporally (fewer dirty L2 lines when the stream pass ends)
+#endif
 #ifndef EW_ULIN
 #define EW_ULIN 0    // A/B: k_stream stores every 4 KiB unit's lin and the frame pass's phase A loads it -- the
                      // phase A saves 18 us on configs[1], the stream pass loses 68 (+4 %, +16 % on configs[0]):
@@ -428,7 +431,10 @@ __device__ __forceinline__ void stream_units(const StreamArgs &a, const uint8_t 
   if (top) {
 #pragma unroll
     for (int i = 0; i < NU; ++i)
-      if ((!(EW_XS & 4) || c[i] == 0x12345678u) && !vskip[i]) a.v[(uint64_t)u[i] * EW_VPU + (lane >> 2)] = c[i];
+      if ((!(EW_XS & 4) || c[i] == 0x12345678u) && !vskip[i]) {
+        if (EW_V_NT) __builtin_nontemporal_store(c[i], a.v + (uint64_t)u[i] * EW_VPU + (lane >> 2));
+        else a.v[(uint64_t)u[i] * EW_VPU + (lane >> 2)] = c[i];
+      }
   }
   if (FIND && EW_ULIN) {
     // the unit's lin: super-piece m's (lane 4m+3) moved by the 256 (15 - m)
@@ -456,7 +462,14 @@ __device__ __forceinline__ void stream_units(const StreamArgs &a, const uint8_t 
         // the pieces flagged in their last dword group (bit 4 of each byte
         // of fm): only their candidates can need the 12 bytes after the piece
         const unsigned long long h3 = __ballot((fm[i] & 0x10101010u) != 0 && in);
-        if (lane == 0) *(ulonglong2 *)(a.hmask + 2 * (uint64_t)u[i]) = make_ulonglong2(hm, h3);
+        if (lane == 0) {
+          if (EW_V_NT) {
+            __builtin_nontemporal_store(hm, a.hmask + 2 * (uint64_t)u[i]);
+            __builtin_nontemporal_store(h3, a.hmask + 2 * (uint64_t)u[i] + 1);
+          } else {
+            *(ulonglong2 *)(a.hmask + 2 * (uint64_t)u[i]) = make_ulonglong2(hm, h3);
+          }
+        }
       } else if (lane == 0) {
         a.hmask[u[i]] = hm;
       }
