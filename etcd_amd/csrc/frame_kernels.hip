@@ -1344,14 +1344,14 @@ __global__ __launch_bounds__(256) void k_frames_seam(FrArgs a, FrSeg sg, ResultD
       uint64_t pidx = 0;
       uint32_t scanned = 0;
       int64_t u0 = (int64_t)t - 1;
-      if (hp && P_nops && (uint64_t)t * TB > lo_p) {   // the previous tile holds the predecessor op
+      if (hp && cp && P_nops && (uint64_t)t * TB > lo_p) {   // the previous tile holds the predecessor op
         has = !SEG || P_lastop >= lo_p;
         pidx = P_lastidx;
         u0 = -1;
       }
       for (int64_t u = u0; u >= 0 && (uint64_t)(u + 1) * TB > lo_p; --u) {
         if (++scanned > FR_SCAN) { farop = true; break; }
-        if (!a.trec[u].nops) continue;
+        if (!a.tcnt[u] || !a.trec[u].nops) continue;   // (a tile without frames has no op fields written)
         has = !SEG || a.trec[u].lastop_p >= lo_p;
         pidx = a.trec[u].last_index;
         break;

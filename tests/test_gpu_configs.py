@@ -334,3 +334,29 @@ def test_configs1_shaped_with_leader_changes(ctx):
             (o["n_records"], o["last_crc"], o["enti"])
         assert [(e.Index, e.Term, e.Data) for e in r.ents] == [(e["index"], e["term"], e["data"]) for e in o["ents"]]
         assert not (r.flags & L.FLAG_SHARD_FALLBACK)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("rewinds", [0, 20])
+def test_tiles_without_frames_after_dense_call(ctx, rewinds):
+    """Tiles that hold no frame start (entries of 64-160 KiB span whole tiles)
+    after a record-dense call on the same ctx left every tile's op fields set:
+    the seam pass's gap rule must skip the empty tiles by their frame count,
+    not by op fields the frame pass writes only for tiles with frames
+    (wal/wal.go:170-176; round 5: stale fields read as the predecessor op gave
+    a false index-gap panic)."""
+    dense = bytes(W.synth_wal(24 << 20, 32, 600, seed=77)[0])
+    li = []
+    big = bytes(W.synth_wal(24 << 20, 64 << 10, 160 << 10, seed=78, rewind_per_mille=rewinds, last_index=li)[0])
+    for b, check_n in ((dense, False), (big, True), (dense, False), (big, True)):
+        d = ctx.alloc(len(b) + 64)
+        try:
+            d.upload(b)
+            g = _readall(ctx, d, len(b), 1, memoryview(b))
+        finally:
+            d.free()
+        o = O.readall_digest(b, 1)
+        assert o["status"] == O.OK
+        if check_n:
+            assert o["n_ents"] == li[0]
+        _assert_result(ctx, g, o, b)
