@@ -360,3 +360,49 @@ def test_tiles_without_frames_after_dense_call(ctx, rewinds):
         if check_n:
             assert o["n_ents"] == li[0]
         _assert_result(ctx, g, o, b)
+
+
+@pytest.mark.gpu
+def test_ctx_reuse_across_shapes(ctx):
+    """One ctx through a mixed sequence of single and batched ReadAlls whose
+    shapes differ call to call (record-dense, entries spanning whole tiles,
+    leader changes, corrupt and torn WALs, a one-frame WAL): every per-call
+    device buffer a call reads must be one it wrote, so each result equals
+    the oracle's whatever the previous call left behind (wal/wal.go:164-216)."""
+    def shape(kind, seed):
+        if kind == "dense":
+            return bytes(W.synth_wal(6 << 20, 16, 400, seed=seed)[0])
+        if kind == "big":
+            return bytes(W.synth_wal(12 << 20, 64 << 10, 150 << 10, seed=seed, rewind_per_mille=30)[0])
+        if kind == "c1":
+            return bytes(W.synth_wal(20 << 20, 64, 65536, seed=seed, rewind_per_mille=10)[0])
+        if kind == "corrupt":
+            return bytes(W.synth_wal(5 << 20, 32, 3000, seed=seed, corrupt_record=1500)[0])
+        if kind == "torn":
+            b = bytes(W.synth_wal(4 << 20, 32, 5000, seed=seed)[0])
+            return b[:-(seed % 200 + 1)]
+        return bytes(W.synth_wal(1, 8, 8, seed=seed)[0])   # "one": the smallest WAL the generator writes
+    rng = random.Random(4242)
+    kinds = ["dense", "big", "c1", "corrupt", "torn", "one"]
+    for step in range(14):
+        if step % 3 == 2:   # a batch of three different shapes
+            ks = rng.sample(kinds, 3)
+            shards = [shape(k, 900 + 10 * step + i) for i, k in enumerate(ks)]
+            res = W.readall_batch_bytes(shards, [1] * 3, ctx, with_ents=True)
+            for sb, r, k in zip(shards, res, ks):
+                o = O.readall(sb, 1)
+                assert (r.status, r.fail_record, r.fail_offset) == (o["status"], o["fail_record"], o["fail_offset"]), k
+                if o["status"] == O.OK:
+                    assert (r.n_records, r.last_crc, r.enti) == (o["n_records"], o["last_crc"], o["enti"]), k
+                    assert [(e.Index, e.Term, e.Data) for e in r.ents] == \
+                        [(e["index"], e["term"], e["data"]) for e in o["ents"]], k
+            continue
+        k = kinds[rng.randrange(len(kinds))]
+        b = shape(k, 700 + step)
+        d = ctx.alloc(len(b) + 64)
+        try:
+            d.upload(b)
+            g = _readall(ctx, d, len(b), 1, memoryview(b))
+        finally:
+            d.free()
+        _assert_result(ctx, g, O.readall_digest(b, 1), b)
