@@ -115,3 +115,22 @@ def test_mutated_large_wals(ctx, seed):
     m = _mutate(rng, bytes(buf))
     o, g = assert_parity(ctx, m, rng.choice([1, 1, 100]), check_chain=seed % 3 == 0)   # its entries start at Index 1
     assert g["status"] != L.UNSUPPORTED_ENCODING
+
+
+def _large_case(seed):
+    """a multi-MiB WAL whose entries may span whole frame-pass tiles (up to
+    150 KiB), leader changes for some seeds, mutated for 60 % of the seeds"""
+    rng = random.Random(13000 + seed)
+    size = rng.choice([2, 6, 12]) << 20
+    hi = rng.choice([4096, 65536, 150 << 10])
+    buf, _ = W.synth_wal(size, rng.choice([16, 64, 2048]), hi, seed=100 + seed,
+                         rewind_per_mille=rng.choice([0, 10, 30]))
+    b = bytes(buf)
+    return (_mutate(rng, b) if rng.random() < 0.6 else b), rng.choice([1, 1, 50])
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_mutated_wals_with_tile_spanning_entries(ctx, seed):
+    m, ri = _large_case(seed)
+    o, g = assert_parity(ctx, m, ri, check_chain=seed % 4 == 0)
+    assert g["status"] != L.UNSUPPORTED_ENCODING

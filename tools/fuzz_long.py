@@ -1,0 +1,34 @@
+"""A longer GPU fuzz run than the suite's (run ON the GPU box): the suite's
+tile-spanning large-WAL case (tests/test_gpu_fuzz.py::_large_case) over the
+seeds [first, first + count), every result against the oracle, one ctx for all
+(stale per-call state shows up as a mismatch).  Prints one line per 20 seeds.
+Usage: python3 tools/fuzz_long.py FIRST COUNT"""
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "tests"))
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+
+from etcd_amd import wal as W          # noqa: E402
+from test_gpu_fuzz import _large_case  # noqa: E402
+from test_gpu_parity import assert_parity  # noqa: E402
+
+
+def main():
+    first, count = int(sys.argv[1]), int(sys.argv[2])
+    ctx = W.Context()
+    t0 = time.time()
+    statuses = {}
+    for s in range(first, first + count):
+        m, ri = _large_case(s)
+        o, g = assert_parity(ctx, m, ri, check_chain=s % 4 == 0)
+        statuses[o["status"]] = statuses.get(o["status"], 0) + 1
+        if (s - first + 1) % 20 == 0:
+            print("seeds %d..%d ok, %.0f s, statuses %s" % (first, s, time.time() - t0, sorted(statuses.items())),
+                  flush=True)
+    print("done: %d seeds, statuses %s" % (count, sorted(statuses.items())), flush=True)
+
+
+if __name__ == "__main__":
+    main()
