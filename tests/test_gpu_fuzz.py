@@ -134,3 +134,38 @@ def test_mutated_wals_with_tile_spanning_entries(ctx, seed):
     m, ri = _large_case(seed)
     o, g = assert_parity(ctx, m, ri, check_chain=seed % 4 == 0)
     assert g["status"] != L.UNSUPPORTED_ENCODING
+
+
+def _large_batch_case(seed):
+    """3-8 multi-MiB shards of the large case's kinds (tile-spanning entries,
+    leader changes, mutations) side by side in one batch"""
+    rng = random.Random(17000 + seed)
+    shards, ris = [], []
+    for i in range(rng.randrange(3, 9)):
+        buf, _ = W.synth_wal(rng.choice([1, 3, 5]) << 20, rng.choice([16, 64, 2048]),
+                             rng.choice([4096, 65536, 150 << 10]), seed=200 + 16 * seed + i,
+                             rewind_per_mille=rng.choice([0, 10, 30]))
+        b = bytes(buf)
+        shards.append(_mutate(rng, b) if rng.random() < 0.4 else b)
+        ris.append(rng.choice([1, 1, 50]))
+    return shards, ris
+
+
+def check_batch(ctx, shards, ris):
+    res = W.readall_batch_bytes(shards, ris, ctx)
+    for s, ri, r in zip(shards, ris, res):
+        o = O.readall(s, ri)
+        assert r.status == o["status"], (r.status, o["status"])
+        if o["status"] == O.OK:
+            assert (r.n_records, r.last_crc, r.enti, r.metadata) == \
+                (o["n_records"], o["last_crc"], o["enti"], o["metadata"])
+            assert [(x.Index, x.Term, x.Data) for x in r.ents] == \
+                   [(x["index"], x["term"], x["data"]) for x in o["ents"]]
+        elif o["status"] != O.ERR_INDEX_NOT_FOUND:
+            assert (r.fail_record, r.fail_offset) == (o["fail_record"], o["fail_offset"])
+    return res
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_mutated_batches_with_tile_spanning_entries(ctx, seed):
+    check_batch(ctx, *_large_batch_case(seed))

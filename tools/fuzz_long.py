@@ -1,8 +1,9 @@
 """A longer GPU fuzz run than the suite's (run ON the GPU box): the suite's
 tile-spanning large-WAL case (tests/test_gpu_fuzz.py::_large_case) over the
 seeds [first, first + count), every result against the oracle, one ctx for all
-(stale per-call state shows up as a mismatch).  Prints one line per 20 seeds.
-Usage: python3 tools/fuzz_long.py FIRST COUNT"""
+(stale per-call state shows up as a mismatch); with --batch the batched case
+(_large_batch_case, 3-8 such shards per batch).  Prints one line per 20 seeds.
+Usage: python3 tools/fuzz_long.py FIRST COUNT [--batch]"""
 import os
 import sys
 import time
@@ -11,7 +12,7 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
 
 from etcd_amd import wal as W          # noqa: E402
-from test_gpu_fuzz import _large_case  # noqa: E402
+from test_gpu_fuzz import _large_batch_case, _large_case, check_batch  # noqa: E402
 from test_gpu_parity import assert_parity  # noqa: E402
 
 
@@ -20,10 +21,15 @@ def main():
     ctx = W.Context()
     t0 = time.time()
     statuses = {}
+    batch = "--batch" in sys.argv[3:]
     for s in range(first, first + count):
-        m, ri = _large_case(s)
-        o, g = assert_parity(ctx, m, ri, check_chain=s % 4 == 0)
-        statuses[o["status"]] = statuses.get(o["status"], 0) + 1
+        if batch:
+            got = [r.status for r in check_batch(ctx, *_large_batch_case(s))]
+        else:
+            m, ri = _large_case(s)
+            got = [assert_parity(ctx, m, ri, check_chain=s % 4 == 0)[0]["status"]]
+        for st in got:
+            statuses[st] = statuses.get(st, 0) + 1
         if (s - first + 1) % 20 == 0:
             print("seeds %d..%d ok, %.0f s, statuses %s" % (first, s, time.time() - t0, sorted(statuses.items())),
                   flush=True)

@@ -7,4 +7,5 @@ mkdir -p "$out"
 timeout -k 10 600 python3 -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_fuzz.py -m gpu \
   > "$out/pytest_fuzz.txt" 2>&1
 timeout -k 10 600 python3 -u tools/fuzz_long.py 1000 ${2:-400} > "$out/fuzz_long.txt" 2>&1
+timeout -k 10 600 python3 -u tools/fuzz_long.py 5000 ${3:-100} --batch > "$out/fuzz_long_batch.txt" 2>&1
 echo done
