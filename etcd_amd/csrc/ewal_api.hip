@@ -137,6 +137,7 @@ struct ewal_ctx {
   DevBuf encw, encs, lbstat, gagg, slow, mlist, pf, v, pwave, ux, tagg, tpx, wcnt, slots, cbase, ovf, cpos, clen, nxt, exc, E, rs, jl, vis, entry, on, rec_cand, rd, opf, ops, kk, kkrev, suf,
       ents, recs, tmp, small, sdesc, snaps, hbuf_dev, xpos, walk, fpos, ulist, uitems, uarena, ftrec, fpl, fucb,
       fnfp, frbase, fsp, ftcb, fown, fcl, ftl, ftcnt;
+  DevBuf rents, rmlist, rulist;   // materialise_records' k_check outputs (never the ReadAll's own ents)
   HostBuf hsdesc;                  // esnap_verify_packed's per-file table (host-mapped)
   // esnap_verify_packed's residual decode (esnap_copy_field): the batch's
   // buffer, per file its residual slot (-1: none), per slot its segments
@@ -2046,15 +2047,18 @@ static int materialise_records(ewal_ctx *c) {
     EW_CHECK(hipMemsetAsync(c->lbstat.p, 0, c->lbstat.cap, c->stream));
     if (c->epoch == 0) c->epoch = 1;
   }
+  // k_check's ents / metadata / unknown-field lists go to scratch: the
+  // call's ents (ewal_copy_entries) are the frame pass's, with index
+  // rewinds already applied (wal/wal.go:173), and must survive this
   EW_CHECK(c->opf.ensure((size_t)nb * 4));
-  EW_CHECK(c->mlist.ensure((size_t)n * 4));
-  EW_CHECK(c->ents.ensure((size_t)n * sizeof(ewal_entry)));
-  EW_CHECK(c->ulist.ensure((size_t)n * sizeof(uint2)));
+  EW_CHECK(c->rmlist.ensure((size_t)n * 4));
+  EW_CHECK(c->rents.ensure((size_t)n * sizeof(ewal_entry)));
+  EW_CHECK(c->rulist.ensure((size_t)n * sizeof(uint2)));
   SegArgs useg{};
-  useg.ulist = c->ulist.as<uint2>();
+  useg.ulist = c->rulist.as<uint2>();
   hipLaunchKernelGGL(k_check<false>, dim3(nb), dim3(1024), 0, c->stream, tb->shift, c->rd.as<RecDesc>(), (uint32_t)n,
                      (const uint32_t *)pf, (const uint32_t *)(pf + n), c->last_ri, c->lbstat.as<unsigned long long>(),
-                     c->epoch, c->opf.as<uint32_t>(), c->ents.as<ewal_entry>(), c->mlist.as<uint32_t>(), ds, useg,
+                     c->epoch, c->opf.as<uint32_t>(), c->rents.as<ewal_entry>(), c->rmlist.as<uint32_t>(), ds, useg,
                      (const uint32_t *)nullptr);
   EW_CHECK(hipGetLastError());
   EW_CHECK(hipStreamSynchronize(c->stream));

@@ -406,3 +406,28 @@ def test_ctx_reuse_across_shapes(ctx):
         finally:
             d.free()
         _assert_result(ctx, g, O.readall_digest(b, 1), b)
+
+
+@pytest.mark.gpu
+def test_records_and_range_info_after_rewinding_readall_keep_ents(ctx):
+    """ewal_copy_records / ewal_copy_range_info after a frame-pass ReadAll
+    that met index rewinds rebuild the per-frame descriptors on demand; the
+    call's ents (rewinds applied, wal/wal.go:173) must be unchanged by that
+    (round 5: the rebuild's k_check overwrote them with the ops in order,
+    found by splitting such a WAL over two ctxs)."""
+    li = []
+    b = bytes(W.synth_wal(8 << 20, 64, 4096, seed=91, rewind_per_mille=30, last_index=li)[0])
+    o = O.readall_digest(b, 1)
+    assert o["status"] == O.OK and o["n_ents"] == li[0] < o["n_records"]
+    d = ctx.alloc(len(b) + 64)
+    try:
+        d.upload(b)
+        g = _readall(ctx, d, len(b), 1, memoryview(b))
+        assert g.flags & L.FLAG_FAST_PATH
+        _assert_result(ctx, g, o, b)
+        recs = W.records(ctx, g.n_records)
+        assert len(recs) == o["n_records"]
+        W.range_info(ctx, stream=b)
+        _assert_result(ctx, g, o, b)   # the ents again, after both
+    finally:
+        d.free()

@@ -204,3 +204,15 @@ def test_join_frame0_entry_decode_after_crc(ctx):
         rows.append(r)
         blobs.append(b)
     assert shard.join_rows(rows, blobs, 1)[:3] == want
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_multi_inside_file_tile_spanning_entries(ctxs, seed):
+    """the fuzz suite's multi-MiB case (entries spanning whole frame-pass
+    tiles, leader changes, mutations) split inside its one file over 2 and 3
+    ctxs: the joined ReadAll equals the oracle's"""
+    from test_gpu_fuzz import _large_case
+    buf, ri = _large_case(40 + seed)
+    for n in (2, 3):
+        g, _ = W.readall_multi(ctxs[:n], buf, ri)
+        _check_full(buf, ri, g, (seed, n))

@@ -2,8 +2,10 @@
 tile-spanning large-WAL case (tests/test_gpu_fuzz.py::_large_case) over the
 seeds [first, first + count), every result against the oracle, one ctx for all
 (stale per-call state shows up as a mismatch); with --batch the batched case
-(_large_batch_case, 3-8 such shards per batch).  Prints one line per 20 seeds.
-Usage: python3 tools/fuzz_long.py FIRST COUNT [--batch]"""
+(_large_batch_case, 3-8 such shards per batch); with --split the single case
+split inside its file over 2 and 3 ctxs (ewal_readall_multi, the C join).
+Prints one line per 20 seeds.
+Usage: python3 tools/fuzz_long.py FIRST COUNT [--batch | --split]"""
 import os
 import sys
 import time
@@ -13,6 +15,7 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."
 
 from etcd_amd import wal as W          # noqa: E402
 from test_gpu_fuzz import _large_batch_case, _large_case, check_batch  # noqa: E402
+from test_gpu_multi import _check_full  # noqa: E402
 from test_gpu_parity import assert_parity  # noqa: E402
 
 
@@ -22,9 +25,17 @@ def main():
     t0 = time.time()
     statuses = {}
     batch = "--batch" in sys.argv[3:]
+    split = [W.Context(0) for _ in range(3)] if "--split" in sys.argv[3:] else None
     for s in range(first, first + count):
         if batch:
             got = [r.status for r in check_batch(ctx, *_large_batch_case(s))]
+        elif split:
+            m, ri = _large_case(s)
+            got = []
+            for n in (2, 3):
+                g, _ = W.readall_multi(split[:n], m, ri)
+                _check_full(m, ri, g, (s, n))
+                got.append(g.status)
         else:
             m, ri = _large_case(s)
             got = [assert_parity(ctx, m, ri, check_chain=s % 4 == 0)[0]["status"]]
