@@ -1,8 +1,8 @@
 #!/bin/bash
-# Round-5 session 11: the final build's GPU suite, smoke, the default bench line
+# The final build's GPU suite, smoke, the default bench line
 # and the kernel stats of every workload.  Run ON the GPU box from the repo root.
 set -eo pipefail
-out=${1:-gpurun_out/s17}
+out=${1:-gpurun_out/final}
 mkdir -p "$out"
 export TMPDIR=/tmp
 timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread \

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round-5 session 3: kernel timelines of the overlapped pipeline (hooks build)
+# Kernel timelines of the overlapped pipeline (hooks build)
 # and the GPU suite on the product build.  Run ON the GPU box from the repo root.
 set -eo pipefail
 out=${1:-gpurun_out/s3}

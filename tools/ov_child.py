@@ -1,6 +1,6 @@
 """One process: an 8 GiB configs[1]-shaped WAL in HBM, 4 ReadAll calls (the
 hooks library's EWAL_OV / EWAL_OV_NOFR select the pipeline) -- the target of
-rocprofv3 --kernel-trace in tools/gpu_s3.sh."""
+rocprofv3 --kernel-trace in tools/gpu_overlap.sh."""
 import ctypes as C
 import os
 import sys
