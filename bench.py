@@ -1236,6 +1236,7 @@ def main():
         dist.init_process_group(a.dist_backend)
 
     c1 = dict(size=int(285e6), min_data=256, max_data=256, label="configs[0] WAL on the GPU")
+    failed = []   # sub-configs that raised (their parity / gate asserts included): the run exits non-zero
     if a.workload in ("wal", "c1"):
         if a.workload == "c1":
             out = run_wal(a, dist, rank, world, local, cpu_seconds=a.cpu_seconds, full=False, **c1)
@@ -1253,10 +1254,11 @@ def main():
                         r = run_wal(a, dist, rank, world, local, cpu_seconds=a.sub_cpu_seconds, full=False, **c1)
                     else:
                         r = SUBS[name](a, dist, rank, world, local, cpu_seconds=a.sub_cpu_seconds)
-                except Exception as ex:   # the headline line still prints; the failure is in it
+                except Exception as ex:   # the headline line still prints, the failure is in it, and rc != 0
                     import traceback
                     traceback.print_exc()
                     r = {"error": "%s: %s" % (type(ex).__name__, ex), "ms_per_step": None}
+                    failed.append(name)
                 r["wall_seconds"] = round(time.time() - t0, 2)
                 for key in ("higher_is_better", "scaling", "vs_baseline", "data", "n_gpus"):
                     r.pop(key, None)
@@ -1270,10 +1272,16 @@ def main():
     if rank == 0:
         import resource   # this rank's peak host memory (synthetic inputs, pinned snapshot pool): for N-rank nodes
         out["host_peak_rss_gib"] = round(resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / (1 << 20), 2)
+        if failed:
+            out["failed_configs"] = failed
         print(json.dumps(out), flush=True)
     if dist is not None:
         dist.destroy_process_group()
+    if failed:
+        print("bench: FAILED sub-configs: %s" % ",".join(failed), file=sys.stderr, flush=True)
+        return 1
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -16,6 +16,8 @@
 #include <cstring>
 #include <map>
 #include <memory>
+#include <mutex>
+#include <set>
 #include <vector>
 
 #include "crc_math.h"
@@ -130,6 +132,9 @@ struct ewal_ctx {
   // frames per 4 KiB unit: dense_hint), 1 on, -1 off (EWAL_OPT_VH_ON / _OFF)
   int vh_opt = 0;
   bool dense_hint = false;
+  // the batched ReadAll's own hint: its previous batch had >= EW_VH_BATCH_FPU
+  // frames per 4 KiB unit (configs[2]-shaped shards: 3.5)
+  bool dense_hint_batch = false;
   uint32_t *vh_next = nullptr;                 // run_stream: the vh[] of this call's stream pass
   DevBuf vhb;
   std::map<uint32_t, DevTables> tables;
@@ -762,8 +767,11 @@ static int reset_small(ewal_ctx *c) {
 // The call's wait for its last kernel: a spin on the stream's completion
 // (c->spin) instead of the runtime's blocking wait, whose wake-up sits between
 // the device finishing and the host seeing the result.
+// Only on the ctx's own stream: a caller-owned stream (ewal_ctx_set_stream,
+// e.g. torch's) may hold the caller's other work, which a spin would wait
+// out on a whole host core; there the runtime's blocking wait is used.
 static hipError_t ew_sync(ewal_ctx *c) {
-  bool spin = c->spin;
+  bool spin = c->spin && c->own_stream;
 #ifdef EW_ABLATION_HOOKS
   if (const char *e = std::getenv("EWAL_SPIN")) spin = std::atoi(e) != 0;   // tools/ only
 #endif
@@ -807,6 +815,51 @@ static int set_times(ewal_ctx *c, ewal_result *o, uint32_t n = 1) {
 // stream, then the seam pass.  A tile's frame pass reads only its own units'
 // v[] / hmask (frames reaching into the next tile go to the seam pass), so a
 // chunk needs nothing of the chunks after it.
+// A ctx whose masked streams are still alive when the process exits
+// (ewal_ctx_destroy never called) used to crash in __cxa_finalize: the HIP
+// runtime's own teardown destroyed the CU-masked streams after the profiler /
+// runtime state they depend on was gone (profiles/r05: tools/ov_child.py under
+// rocprofv3, SIGSEGV at exit after four correct calls).  The library now keeps
+// the ctxs that own such streams and destroys those streams from an atexit
+// handler registered when the first one is created -- after the HIP runtime's
+// initialisation, so it runs before the runtime's own teardown.  Callers should
+// still destroy every ctx before exit (include/ewal.h); this covers the ones
+// that do not (a Go process that exits with a live ctx).
+static std::mutex &ov_reg_mu() {
+  static std::mutex *m = new std::mutex();   // never destroyed: used from the atexit handler
+  return *m;
+}
+static std::set<ewal_ctx *> &ov_reg() {
+  static std::set<ewal_ctx *> *r = new std::set<ewal_ctx *>();
+  return *r;
+}
+static void ov_release_streams(ewal_ctx *c) {
+  for (hipStream_t &st : c->ov_s)
+    if (st) {
+      (void)hipStreamSynchronize(st);
+      (void)hipStreamDestroy(st);
+      st = nullptr;
+    }
+}
+static void ov_atexit() {
+  std::lock_guard<std::mutex> g(ov_reg_mu());
+  for (ewal_ctx *c : ov_reg()) {
+    (void)hipSetDevice(c->device);
+    ov_release_streams(c);
+    c->ov_state = -1;
+  }
+  ov_reg().clear();
+}
+static void ov_register(ewal_ctx *c) {
+  static std::once_flag once;
+  std::call_once(once, [] { std::atexit(ov_atexit); });
+  std::lock_guard<std::mutex> g(ov_reg_mu());
+  ov_reg().insert(c);
+}
+static void ov_unregister(ewal_ctx *c) {
+  std::lock_guard<std::mutex> g(ov_reg_mu());
+  ov_reg().erase(c);
+}
 static bool ov_ready(ewal_ctx *c) {
   if (c->ov_state) return c->ov_state > 0;
   c->ov_state = -1;
@@ -826,6 +879,7 @@ static bool ov_ready(ewal_ctx *c) {
   c->ov_cu[0] = n - nf;
   c->ov_cu[1] = nf;
   c->ov_state = 1;
+  ov_register(c);
   return true;
 }
 static hipError_t ov_events(ewal_ctx *c, size_t n) {
@@ -849,10 +903,10 @@ static void ov_stream_chunk(ewal_ctx *c, uint32_t ub, uint32_t ue, int cus, hipS
 template <bool SEG>
 static void fr_launch_frames(int tsh, uint32_t nt, const FrArgs &a, const FrSeg &sg, int cus, hipStream_t st) {
   const unsigned grid = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(grid_for(nt, FR_WAVES), (uint64_t)cus));
-  if (!SEG && a.vh) {   // record-dense: the 128-B prefixes
-    if (tsh == 8) hipLaunchKernelGGL((k_frames<false, 8, true>), dim3(grid), dim3(FR_THREADS), 0, st, a, sg);
-    else if (tsh == 6) hipLaunchKernelGGL((k_frames<false, 6, true>), dim3(grid), dim3(FR_THREADS), 0, st, a, sg);
-    else hipLaunchKernelGGL((k_frames<false, 4, true>), dim3(grid), dim3(FR_THREADS), 0, st, a, sg);
+  if (a.vh) {   // record-dense: the 128-B prefixes
+    if (tsh == 8) hipLaunchKernelGGL((k_frames<SEG, 8, true>), dim3(grid), dim3(FR_THREADS), 0, st, a, sg);
+    else if (tsh == 6) hipLaunchKernelGGL((k_frames<SEG, 6, true>), dim3(grid), dim3(FR_THREADS), 0, st, a, sg);
+    else hipLaunchKernelGGL((k_frames<SEG, 4, true>), dim3(grid), dim3(FR_THREADS), 0, st, a, sg);
     return;
   }
   if (tsh == 8) hipLaunchKernelGGL((k_frames<SEG, 8>), dim3(grid), dim3(FR_THREADS), 0, st, a, sg);
@@ -1580,6 +1634,11 @@ static hipError_t grow_keep(DevBuf &b, size_t need, size_t keep, hipStream_t st)
 // entry op k is bents[rbase[s] + k], rbase[s] = 4 x the flagged pieces of the
 // shards before s (an entry frame is >= 20 bytes: at most 4 start in a 64-B
 // piece); *have = the regions' total (shards replayed alone append after it).
+// frames per 4 KiB unit from which a batch's next stream pass stores vh[]
+// (the 128-B prefixes of the batch frame pass; round 6, profiles/r06/)
+#ifndef EW_VH_BATCH_FPU
+#define EW_VH_BATCH_FPU 2
+#endif
 static int frames_batch(ewal_ctx *c, DevTables *tb, const uint8_t *d_buf, uint64_t B, uint32_t ns,
                         const std::vector<uint64_t> &soff, const uint64_t *ris, ewal_result *out, bool *done,
                         uint64_t *have) {
@@ -1613,6 +1672,7 @@ static int frames_batch(ewal_ctx *c, DevTables *tb, const uint8_t *d_buf, uint64
     EW_CHECK(c->mlist.ensure((size_t)mcap * 8));
     if (pass) if (int rc = reset_small(c)) return rc;
     FrArgs a = fr_args(c, tb, d_buf, B, nunits, ntiles, 0, c->bents.as<ewal_entry>(), ecap, mcap);
+    a.vh = c->ov_sa.vh;   // the batch's stream pass stored vh[] (record-dense shards): the 128-B prefixes
     const unsigned ngrid = (unsigned)std::min<uint64_t>(ns, (uint64_t)std::max(1, c->num_cu) * 4);
     hipLaunchKernelGGL(k_shard_nfp, dim3(ngrid), dim3(256), 0, c->stream, a.hmask, nunits, sg.soff, ns,
                        c->fnfp.as<unsigned long long>());
@@ -1637,6 +1697,7 @@ static int frames_batch(ewal_ctx *c, DevTables *tb, const uint8_t *d_buf, uint64
     const Small *hs = c->h_small;
     if (hs->errflag) return EWAL_E_TIMEOUT;
     c->last_k = hs->total;
+    c->dense_hint_batch = hs->total * EW_WAVE_BYTES >= (uint64_t)EW_VH_BATCH_FPU * B;
     if (hs->spec_n) {
       if (int rc = set_times(c, out, ns)) return rc;
       for (uint32_t i = 0; i < ns; ++i) {
@@ -1829,6 +1890,14 @@ static int readall_batch_impl(ewal_ctx *c, const uint8_t *d_buf, uint32_t ns, co
     EW_CHECK(c->cpos.ensure(ccap * 8));
     uint64_t rdcap = std::min<uint64_t>(ccap, std::max<uint64_t>(c->last_k + c->last_k / 8 + 1024,
                                                                  B / 1024 + 1024));
+    // record-dense shards (the ctx's previous batch: >= EW_VH_BATCH_FPU frames
+    // per 4 KiB unit, or EWAL_OPT_VH_ON): the stream pass also stores vh[] and
+    // the batch's frame pass takes its prefixes from 128-B boundaries
+    const bool vh = c->fused && (c->vh_opt > 0 || (c->vh_opt == 0 && c->dense_hint_batch));
+    if (vh) {
+      EW_CHECK(c->vhb.ensure(((size_t)B / EW_WAVE_BYTES + 1) * EW_VPU * 4));
+      c->vh_next = c->vhb.as<uint32_t>();
+    }
     rc = run_stream(c, tb, d_buf, B, 1, ccap, !c->fused);
     if (rc) return rc;
 #if EW_XS
@@ -2137,11 +2206,8 @@ void ewal_ctx_destroy(ewal_ctx *c) {
   (void)hipEventDestroy(c->evf0);
   (void)hipEventDestroy(c->evf1);
   for (hipEvent_t e : c->ov_ev) (void)hipEventDestroy(e);
-  for (hipStream_t st : c->ov_s)
-    if (st) {
-      (void)hipStreamSynchronize(st);
-      (void)hipStreamDestroy(st);
-    }
+  ov_unregister(c);
+  ov_release_streams(c);
   if (c->own_stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }

@@ -164,10 +164,25 @@ extern "C" int ewal_split_verdict(const ewal_range_row *rows, uint64_t n, uint64
     return finish(EWAL_ERR_INDEX_NOT_FOUND, -1, before, -1, 0);
   }
   // a HardState with unknown fields from a range whose own ReadAll kept no
-  // side list (its status was not EWAL_OK): read from that range on joined
+  // side list (its status was not EWAL_OK: ErrIndexNotFound, a range with no
+  // entry op at or past its w.ri -- e.g. a last file of crc + metadata +
+  // HardState after a Cut).  Re-reading from that range on gives the same
+  // status again when it is the last range holding bytes, so the
+  // ranges are read joined from the last EARLIER range whose own ReadAll ended
+  // EWAL_OK (its entries carry the joined read's enti to its w.ri), else from
+  // range 0 (the whole ReadAll, whose verdict this one is).  Every such resplit
+  // moves strictly earlier, so the caller's re-reads end.
   if (out->state_range >= 0) {
     const ewal_range_row &r = rows[out->state_range];
-    if (r.info.state_unrec && r.status != EWAL_OK) return finish(EWAL_OK, -1, before, out->state_range, 0);
+    if (r.info.state_unrec && r.status != EWAL_OK) {
+      int32_t k = 0;
+      for (int32_t j = out->state_range - 1; j > 0; --j)
+        if (rows[j].info.n_bytes && rows[j].status == EWAL_OK) {
+          k = j;
+          break;
+        }
+      return finish(EWAL_OK, -1, before, k, 0);
+    }
   }
   out->n_ents = ewal_split_ents_layout(rows, n, ri_global, nullptr, nullptr);
   return finish(EWAL_OK, -1, before, -1, 0);
@@ -463,8 +478,12 @@ extern "C" int ewal_multi_plan_device(ewal_multi *m, const void *d_buf, uint64_t
   for (uint32_t r = 1; r < n_ctx; ++r) {
     th.emplace_back([&, r] {
       // a 16-B aligned frame-start candidate after r * len / n (the range's
-      // bytes then start on an aligned address: no copy); any candidate when
-      // the window holds no aligned one
+      // bytes then start on an aligned address: no copy: ewal_readall_device
+      // reads 16-B aligned buffers only).  A window of 64 MiB with no aligned
+      // candidate (entries that large) leaves range r EMPTY: its start is the
+      // next range's, so the previous range reads on through it -- visible to
+      // the caller as starts[r] == starts[r + 1] in the plan (unbalanced, never
+      // wrong).
       const uint64_t from = (uint64_t)((__uint128_t)len * r / n_ctx);
       const uint64_t wl = std::min<uint64_t>(len - from, 64ull << 20);
       if (!wl) return;

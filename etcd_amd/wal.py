@@ -337,6 +337,16 @@ def records(ctx: Context, n: int):
                  chained_crc=x.chained_crc) for x in arr[:k]]
 
 
+class NotFinal(RuntimeError):
+    """A joined multi-range ReadAll whose verdict is not final: ranges
+    `resplit`.. must be read joined (ewal_split_result.resplit), which the
+    caller does when its device-resident ranges are not one contiguous span."""
+
+    def __init__(self, resplit):
+        super().__init__("joined verdict not final: read ranges %d.. joined" % resplit)
+        self.resplit = resplit
+
+
 class Multi:
     """ewal_multi: (*WAL).ReadAll over ONE WAL split across the contexts
     `ctxs` of this process (distinct ctxs; they may share a device), one host
@@ -423,6 +433,10 @@ class Multi:
 
     def _result(self, out, view, with_ents) -> ReadAllResult:
         self.resplit = out.resplit
+        if out.resplit >= 0:
+            # not a final verdict: device-resident ranges k.. are not one contiguous
+            # device span, so the C driver handed the re-read back (ewal_multi_readall_device)
+            raise NotFinal(out.resplit)
         ok = out.status == L.OK
         md = None
         if ok and out.md_range >= 0:

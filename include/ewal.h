@@ -128,6 +128,12 @@ typedef struct ewal_record {
 
 /* ---- context ------------------------------------------------------------ */
 int ewal_ctx_create(int device, ewal_ctx **out);
+/* Releases every device resource of ctx.  Contract: destroy every ctx before
+ * the process exits (a Go caller: before main returns / os.Exit).  The
+ * library covers a ctx left alive with EWAL_OPT_OVERLAP: its two CU-masked
+ * streams are destroyed by an atexit handler the library registers when it
+ * creates them, before the HIP runtime's own teardown (round 6: such a ctx
+ * crashed in __cxa_finalize at exit). */
 void ewal_ctx_destroy(ewal_ctx *ctx);
 /* Run on a caller-owned hipStream_t (NULL = the ctx's own stream).  The
  * ctx's own stream is a blocking stream: it is ordered with the legacy
@@ -156,7 +162,7 @@ int ewal_ctx_reserve(ewal_ctx *ctx, uint64_t wal_bytes, uint32_t flags);
  * stream pass loses speed faster than the frame pass gains CUs, and masks
  * of more than 32 CUs on the frame side slowed the stream side 2.4x.  A ctx
  * with this option owns two extra streams: destroy it before the process
- * exits. */
+ * exits (a live one is cleaned up at exit, see ewal_ctx_destroy). */
 #define EWAL_OPT_OVERLAP 2u
 /* Record-dense WALs (round 5): the stream pass also stores the lin of every
  * 256-B super-piece's first 128-B half, and the frame pass takes every frame
@@ -427,7 +433,9 @@ int ewal_multi_readall_device(ewal_multi *m, const void *const *d_ranges, const 
  * read (the contexts on d_buf's device): starts[0..n_ctx] (range r opens at a
  * 16-B aligned frame-start candidate after r * len / n_ctx, found by
  * ewal_range_probe_aligned on ctx r) and each range's w.ri; then
- * d_ranges[r] = d_buf + starts[r] for ewal_multi_readall_device. */
+ * d_ranges[r] = d_buf + starts[r] for ewal_multi_readall_device.  A range
+ * whose 64 MiB probe window holds no aligned candidate is left empty
+ * (starts[r] == starts[r + 1]: the range before reads on through it). */
 int ewal_multi_plan_device(ewal_multi *m, const void *d_buf, uint64_t len, uint64_t ri, uint64_t *starts,
                            uint64_t *ris);
 /* After a final EWAL_OK: len(ents) entries joined in order (Data offsets into

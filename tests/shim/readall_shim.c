@@ -15,7 +15,11 @@
  * the HardState's XXX_unrecognized (raft.pb.go:273,699; fresh copies out of
  * the side list, as Go's Unmarshal appends them).
  *
- * Usage: readall_shim DIR INDEX      prints one JSON line: the sentinel, the
+ * Usage: readall_shim DIR INDEX [overlap|overlap-live]
+ *   overlap       the ctx runs with EWAL_OPT_OVERLAP (two CU-masked streams)
+ *   overlap-live  ... and the program exits WITHOUT ewal_ctx_destroy (the
+ *                 library's atexit teardown of the masked streams, ewal.h)
+ * prints one JSON line: the sentinel, the
  * result, a digest of ents (CRC-32C over each entry's (term, index, type,
  * nil, len, Data), the oracle's or_ents_digest format) and the time of each
  * step, and a digest of the XXX_unrecognized bytes (CRC-32C over (entry
@@ -124,6 +128,12 @@ int main(int argc, char **argv) {
            ewal_status_string(job.rc));
     return 0;
   }
+  const int overlap = argc > 3 && strncmp(argv[3], "overlap", 7) == 0;
+  const int keep_live = argc > 3 && strcmp(argv[3], "overlap-live") == 0;
+  if (overlap && ewal_ctx_set_options(ctx, EWAL_OPT_OVERLAP) != EWAL_OK) {
+    printf("{\"ok\": false, \"stage\": \"options\"}\n");
+    return 0;
+  }
   if (rc) {
     printf("{\"ok\": true, \"rc\": %d, \"sentinel\": \"%s\"}\n", rc, go_sentinel(rc));
     if (w) ewal_wal_close(w);
@@ -208,21 +218,22 @@ int main(int argc, char **argv) {
   const double t5 = now_ms();
   const uint32_t dg = ents_digest(ents, n);
   printf("{\"ok\": true, \"rc\": %d, \"sentinel\": \"%s\", \"status_string\": \"%s\", \"fail_record\": %lld, "
-         "\"n_records\": %lld, \"n_ents\": %lld, \"enti\": %llu, \"last_crc\": %u, \"has_state\": %d, "
+         "\"n_records\": %lld, \"n_ents\": %lld, \"flags\": %u, \"enti\": %llu, \"last_crc\": %u, \"has_state\": %d, "
          "\"state\": [%llu, %llu, %llu], \"metadata_len\": %lld, \"ents_digest\": %u, \"n_unrec\": %u, "
          "\"unrec_digest\": %u, \"wal_bytes\": %llu, "
          "\"ms\": {\"ctx_create\": %.3f, \"open_at_index\": %.3f, \"until_ctx_ready\": %.3f, \"reserve\": %.3f, "
-         "\"readall\": %.3f, \"materialise\": %.3f, \"total\": %.3f}, \"device_ms\": %.3f}\n",
+         "\"readall\": %.3f, \"materialise\": %.3f, \"total\": %.3f}, \"device_ms\": %.3f, \"frames_ms\": %.3f}\n",
          rc, go_sentinel(rc), ewal_status_string(rc), (long long)r.fail_record, (long long)r.n_records,
-         (long long)n, (unsigned long long)r.enti, (unsigned)r.last_crc, r.has_state,
+         (long long)n, (unsigned)r.flags, (unsigned long long)r.enti, (unsigned)r.last_crc, r.has_state,
          (unsigned long long)r.state_term, (unsigned long long)r.state_vote, (unsigned long long)r.state_commit,
          md ? (long long)md_len : -1LL, dg, (unsigned)r.n_unrec, udg, (unsigned long long)len, job.t1 - job.t0,
-         t_open - t0, t2 - t0, t3 - t2, t4 - t3, t5 - t4, t5 - t0, r.device_ms);
+         t_open - t0, t2 - t0, t3 - t2, t4 - t3, t5 - t4, t5 - t0, r.device_ms, r.frames_ms);
   for (int64_t i = 0; i < n; i++) free(ents[i].unrec);
   free(state_unrec);
   free(split);
   free(ents);
   ewal_wal_close(w);
-  ewal_ctx_destroy(ctx);
+  if (!keep_live) ewal_ctx_destroy(ctx);
+  fflush(stdout);
   return 0;
 }

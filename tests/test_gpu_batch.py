@@ -7,7 +7,8 @@ ents, XXX_unrecognized), whichever path each shard took: the batch's fused
 pass (one stream pass and one frame + check pass for the whole batch) or,
 for a shard that pass cannot decide (corrupt framing, an index
 rewind, unknown fields), its replay alone -- which must not take any other
-shard off the batch's path."""
+shard off the batch's path.  Every test runs with the automatic choice of
+the frame pass's prefix granularity and with the 128-B prefixes forced on."""
 import random
 import struct
 
@@ -19,6 +20,20 @@ from etcd_amd import wal as W
 from test_gpu_parity import build_wal
 
 pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(autouse=True, params=["auto", "vh"])
+def vh_mode(request, ctx):
+    """Every batch test twice: the ctx's automatic choice, and with the 128-B
+    prefixes forced on (EWAL_OPT_VH_ON: the batch's stream pass stores vh[]
+    and the batch frame pass k_frames<true, TSH, true> takes every frame
+    start's prefix from the nearest 128-B boundary; round 6)."""
+    if request.param == "vh":
+        ctx.set_options(vh=True)
+    try:
+        yield request.param
+    finally:
+        ctx.set_options()
 
 
 def check_batch(ctx, shards, ris, expect_fast=None, fallback=None):

@@ -91,6 +91,63 @@ def test_configs0_1m_x_256b(ctx):
         d.free()
 
 
+def test_configs1_full_size_against_oracle(ctx):
+    """configs[1] at its full size (8 GiB, mixed 64 B - 64 KiB entries, the
+    bench's WAL): the whole ReadAll result against the oracle's over the same
+    bytes -- clean: status, frames, lastCRC, enti, metadata, HardState and the
+    ents digest against the faithful restatement (or_readall), and every
+    entry descriptor (term, index, Data offset + length, type, nil flag)
+    against the optimised restatement (orf_readall, pinned to or_readall by
+    tests/test_cpu_baseline.py); with one flipped payload byte at frame
+    k = 0.73 N: status, fail_record and fail_offset against both.
+    Reference: wal/wal.go:164-216, wal/decoder.go:28-47."""
+    buf, n = W.synth_wal(8 << 30, 64, 65536, seed=2)
+    nb = len(buf)
+    d = ctx.alloc(nb + 64)
+    try:
+        d.upload_ptr(C.addressof((C.c_char * nb).from_buffer(buf)), nb)
+        hb = bytes(buf)
+        o = O.readall_digest(hb, 1)
+        assert o["status"] == O.OK and o["n_records"] == n
+        g = _readall(ctx, d, nb, 1, buf)
+        _assert_result(ctx, g, o, hb)
+        # every entry descriptor against the optimised restatement
+        raw = (C.c_char * nb).from_buffer(buf)
+        fr = O.FastResult()
+        st = O.lib.orf_readall(C.c_void_p(C.addressof(raw)), nb, 1, 16, C.byref(fr))
+        try:
+            assert st != O.IRREGULAR
+            assert (fr.status, fr.n_records, fr.last_crc, fr.enti, fr.n_ents) == \
+                (g.status, g.n_records, g.last_crc, g.enti, g.n_ents)
+            ne = int(fr.n_ents)
+            got = (L.EntryDesc * max(ne, 1))()
+            assert L.lib.ewal_copy_entries(ctx.handle, got, ne) == ne
+            want = np.frombuffer(C.string_at(fr.ents, ne * _ENT_DT.itemsize), dtype=_ENT_DT)
+            assert np.array_equal(np.frombuffer(got, dtype=_ENT_DT)[:ne], want)
+        finally:
+            O.lib.orf_result_free(C.byref(fr))
+        del raw
+        # one corrupt record at k = 0.73 N (the bench's), device and host alike
+        k = int(0.73 * n)
+        rec = W.records(ctx, n)[k]
+        p = rec["data_off"] + rec["data_len"] // 2
+        b = bytearray(d.download(1, p))
+        b[0] ^= 0x5A
+        d.upload(bytes(b), p)
+        buf[p] ^= 0x5A
+        del hb
+        hb = bytes(buf)
+        o2 = O.readall_digest(hb, 1)
+        assert o2["status"] == O.ERR_RECORD_CRC and o2["fail_record"] == k
+        g2 = _readall(ctx, d, nb, 1, buf)
+        _assert_result(ctx, g2, o2, hb)
+        assert g2.fail_offset == rec["offset"]
+        f2 = O.fast_readall_status(C.addressof((C.c_char * nb).from_buffer(buf)), nb, 1, 16)
+        assert f2[0] == O.ERR_RECORD_CRC and f2[2] == k
+    finally:
+        d.free()
+
+
 def test_configs2_512_shards_x_64mib(ctx):
     nsh, bad_shard, bad_rec = 512, 2749 % 512, 1000
     blob, lens, nrec = W.synth_shards(list(range(nsh)), 64 << 20, 128, 4096, corrupt={bad_shard: bad_rec})

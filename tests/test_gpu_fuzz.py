@@ -81,8 +81,17 @@ def test_mutated_wals(ctx, block):
     assert len(seen) >= 3   # the mutations reach several verdicts
 
 
+@pytest.mark.parametrize("vh", [None, True])
 @pytest.mark.parametrize("block", range(5))
-def test_mutated_batches(ctx, block):
+def test_mutated_batches(ctx, block, vh):
+    ctx.set_options(vh=vh)
+    try:
+        _mutated_batches(ctx, block)
+    finally:
+        ctx.set_options()
+
+
+def _mutated_batches(ctx, block):
     rng = random.Random(9100 + block)
     for _ in range(6):
         shards, ris = [], []
@@ -166,6 +175,11 @@ def check_batch(ctx, shards, ris):
     return res
 
 
+@pytest.mark.parametrize("vh", [None, True])
 @pytest.mark.parametrize("seed", range(4))
-def test_mutated_batches_with_tile_spanning_entries(ctx, seed):
-    check_batch(ctx, *_large_batch_case(seed))
+def test_mutated_batches_with_tile_spanning_entries(ctx, seed, vh):
+    ctx.set_options(vh=vh)
+    try:
+        check_batch(ctx, *_large_batch_case(seed))
+    finally:
+        ctx.set_options()

@@ -112,6 +112,35 @@ def _rich_wal(rng, n_ents, rewinds=False):
 
 
 @pytest.mark.parametrize("n", [2, 3])
+def test_multi_by_file_state_unrec_in_entryless_last_file(ctxs, n):
+    """ADVICE r05 (medium) on the GPU: by file, the last file holds only
+    crcType, metadata and a HardState with XXX_unrecognized (no entry op, so
+    its range's own ReadAll is ErrIndexNotFound and keeps no side list); the
+    driver's re-read must settle on the whole ReadAll's result -- the HardState
+    with its unknown bytes included (round 5: EWAL_E_INVAL after n + 1
+    resplits)."""
+    from test_split_join import _state_only_last_file
+    rng = random.Random(770 + n)
+    files = _state_only_last_file(rng, nfiles=12)
+    buf = b"".join(b for b, _ in files)
+    # whole files grouped so that the driver's byte shares put the entry-less
+    # last file alone in the last range: group r opens at the first file
+    # boundary at or past r * len / n (ewal_multi_readall's by-file split)
+    offs = [0]
+    for b, _ in files:
+        offs.append(offs[-1] + len(b))
+    cut = [0] + [next(i for i in range(len(files)) if offs[i] >= r * len(buf) / n) for r in range(1, n - 1)]
+    cut += [len(files) - 1, len(files)]
+    groups = [(offs[cut[j + 1]] - offs[cut[j]], files[cut[j]][1]) for j in range(len(cut) - 1)]
+    assert len(groups) == n + 0 and groups[-1][0] == len(files[-1][0])
+    for ri in (1, 2):
+        g, t = W.readall_multi(ctxs[:n], buf, ri, files=groups)
+        _check_full(buf, ri, g, ("state_unrec", n, ri))
+        assert g.state.XXX_unrecognized == bytes([0x20, 0x05])
+        assert t["resplits"] >= 1
+
+
+@pytest.mark.parametrize("n", [2, 3])
 def test_multi_full_result_rich(ctxs, n):
     """metadata, the last HardState (with XXX_unrecognized), ents with
     unknown fields and index rewinds, joined from 2 / 3 ranges inside a file"""
@@ -127,11 +156,16 @@ def test_multi_full_result_rich(ctxs, n):
 def test_multi_device_resident_1gib(ctxs, n):
     """configs[1]-shaped WAL (64 B - 64 KiB entries) of 1 GiB resident in HBM,
     split over n ctxs on device 0 at 16-B aligned frame starts (no copy):
-    the joined result equals the single-ctx ReadAll exactly -- verdict,
-    lastCRC, enti, metadata, HardState and every entry descriptor."""
+    the joined result equals the faithful oracle's ReadAll over the same bytes
+    (verdict, lastCRC, enti, metadata, HardState, the ents digest over every
+    entry's fields and Data) and the single-ctx ReadAll exactly (every entry
+    descriptor)."""
     import ctypes as C
     from etcd_amd import _lib as L
     buf, nrec = W.synth_wal(1 << 30, 64, 65536, seed=5)
+    hb = bytes(buf)
+    o = O.readall_digest(hb, 1)
+    assert o["status"] == O.OK and o["n_records"] == nrec
     d = ctxs[0].alloc(len(buf) + 64)
     d.upload_ptr(C.addressof((C.c_char * len(buf)).from_buffer(buf)), len(buf))
     try:
@@ -145,12 +179,16 @@ def test_multi_device_resident_1gib(ctxs, n):
             plan = m.plan_device(d, len(buf), 1)
             assert all(s % 16 == 0 for s in plan[0][:-1]) and len(set(plan[0])) == n + 1, plan
             g = m.readall_device(d, len(buf), 1, plan=plan)
+            assert (g.status, g.n_records, g.last_crc, g.enti) == (o["status"], o["n_records"], o["last_crc"], o["enti"])
+            assert g.metadata == o["metadata"]
+            assert (g.state.Term, g.state.Vote, g.state.Commit) == o["state"]
             assert (g.status, g.n_records, g.last_crc, g.enti) == (one.status, one.n_records, one.last_crc, one.enti)
             assert g.metadata == one.metadata and g.state == one.state
             assert m.timing()["resplits"] == 0
             a2 = (L.EntryDesc * max(1, nrec))()
             k2 = L.lib.ewal_multi_copy_entries(m._h, a2, nrec)
-            assert k1 == k2 == g.n_ents and (ne is None or ne == k1)
+            assert k1 == k2 == g.n_ents == o["n_ents"] and (ne is None or ne == k1)
+            assert O.ent_views_digest(hb, a2, k2) == o["ents_digest"]
             assert C.string_at(a1, k1 * C.sizeof(L.EntryDesc)) == C.string_at(a2, k2 * C.sizeof(L.EntryDesc))
             # and from host bytes (each range staged into its ctx's buffer)
             h = m.readall(buf, 1, with_ents=False)

@@ -161,3 +161,42 @@ def test_shim_damaged_directories(tmp_path):
         victim.write_bytes(_mutate(rng, victim.read_bytes()))
         for index in (0, rng.randrange(1, idx + 1)):
             check(d, index)
+
+
+def run_shim_mode(d, index, mode):
+    p = subprocess.run([SHIM, str(d), str(index), mode], capture_output=True, text=True, timeout=180)
+    return p
+
+
+@pytest.mark.gpu
+def test_shim_overlap_ctx_exits_cleanly(tmp_path):
+    """EWAL_OPT_OVERLAP through the C ABI (a WAL large enough for the frame
+    pass's 1 MiB tiles, >= 6 GiB on 256 CUs: the chunked, CU-masked pipeline
+    runs, so frames_ms is 0): the results are the oracle's, and the process
+    exits 0 both after ewal_ctx_destroy and with the ctx left alive (the
+    library's atexit teardown of its masked streams; round 5 saw a SIGSEGV in
+    __cxa_finalize for a live overlap ctx).  The WAL file lives in tmpfs."""
+    import shutil
+    import tempfile
+    base = "/dev/shm" if os.path.isdir("/dev/shm") else str(tmp_path)
+    d = tempfile.mkdtemp(prefix="ewal_ov_", dir=base)
+    try:
+        _overlap_modes(d)
+    finally:
+        shutil.rmtree(d, ignore_errors=True)
+
+
+def _overlap_modes(d):
+    buf, n = W.synth_wal((6 << 30) + (64 << 20), 64, 65536, seed=21)
+    with open(os.path.join(d, W.walName(0, 0)), "wb") as f:
+        f.write(memoryview(buf))
+    o = O.readall_digest(bytes(buf), 1)
+    del buf
+    for mode in ("overlap", "overlap-live"):
+        p = run_shim_mode(d, 1, mode)
+        assert p.returncode == 0, (mode, p.returncode, p.stderr[-2000:])
+        g = json.loads(p.stdout.strip().splitlines()[-1])
+        assert g["rc"] == o["status"] == O.OK, (mode, g)
+        assert (g["n_records"], g["n_ents"], g["enti"], g["last_crc"], g["ents_digest"]) == \
+            (o["n_records"], o["n_ents"], o["enti"], o["last_crc"], o["ents_digest"]), mode
+        assert g["frames_ms"] == 0.0, (mode, g)   # the overlapped pipeline ran (no single frame-pass launch)

@@ -86,3 +86,43 @@ def test_join_deferred_frame0_failure_classes():
     good = O.crc32_update(running, data)
     r1 = _deferred_row(O.PANIC_BOUNDS, 0, good, u0, len(data))
     assert shard.join_rows([r0[0], r1[0]], [r0[1], r1[1]], 1)[:3] == (O.PANIC_BOUNDS, n0, n0)
+
+
+def _state_only_last_file(rng, nfiles=3):
+    """wal.Create + Save + Cut, then a last file holding only crcType,
+    metadata and a HardState with unknown fields (Save(st, nil) after the
+    Cut): its name index is the next entry Index, so its own ReadAll (w.ri =
+    that index, no entry op) ends in ErrIndexNotFound and keeps no side list."""
+    files = [(bytes(b), i) for b, i in build_files(rng, nfiles)]
+    allb = b"".join(b for b, _ in files)
+    o = O.readall(allb, 0)
+    e = O.WalEncoder(o["last_crc"])
+    e.save_crc(o["last_crc"])
+    e.encode(1, b"metadata")
+    e.encode(3, O.hardstate_marshal(1, 1, o["enti"]) + bytes([0x20, 0x05]))
+    return files + [(e.getvalue(), o["enti"] + 1)]
+
+
+def test_join_state_unrec_in_entryless_last_file():
+    """the last range holding the HardState (with
+    XXX_unrecognized) has no entry op, so its own read is ErrIndexNotFound
+    and the join must read joined -- from an EARLIER range whose read ended
+    OK, so that the re-read settles (reading from the state range again gave
+    the same rows forever and EWAL_E_INVAL).  By file, w.ri >= 1, 2 and 3
+    ranges: the resolved verdict is the whole ReadAll's."""
+    rng = random.Random(41)
+    files = _state_only_last_file(rng)
+    allb = b"".join(b for b, _ in files)
+    for rig in (1, 3):
+        whole = O.readall(allb, rig)
+        assert whole["status"] == O.OK and whole["state"]["unrec"] == bytes([0x20, 0x05])
+        assert _resolved(files, len(files) - 1, rig) == _whole(allb, rig)
+        # three ranges: files [0, 1), [1, 3), [3]
+        parts = [(files[0][0], rig), (files[1][0] + files[2][0], max(rig, files[1][1])),
+                 (files[3][0], max(rig, files[3][1]))]
+        v = _join(parts, rig)
+        assert v[0] == O.OK and v[3] == 1, v   # the state range is 2: re-read from range 1 (its read ended OK)
+        assert _row(parts[2][0], parts[2][1])[0].status == O.ERR_INDEX_NOT_FOUND
+        joined = parts[:1] + [(parts[1][0] + parts[2][0], parts[1][1]), (b"", 0)]
+        v2 = _join(joined, rig)
+        assert v2[:3] == _whole(allb, rig) and v2[3] == -1, v2
