@@ -198,6 +198,14 @@ struct ewal_ctx {
   bool last_ok = false;
   bool scan_valid = false;   // cpos / pwave / cbase hold the current stream pass's candidates and prefixes
   bool fr_rew_hint = false;  // the last single ReadAll needed the frame pass's rewind mode
+  // the batched ReadAll's: the shards of the ctx's previous batch (same shard
+  // count and bytes) whose indexes went back run the next batch's frame pass in
+  // rewind mode (k_shard_hint) instead of a second pass over their tiles
+  std::vector<uint32_t> brew_hint;
+  uint32_t brew_ns = 0;
+  uint64_t brew_B = 0;
+  uint32_t brew_clcap = 1u << 20;
+  DevBuf fhint;
   uint64_t last_q = 0;       // where the last ReadAll's frame chain ended (decoder.decode's terminal)
   // the overlapped pipeline (single WAL): two streams on disjoint CU masks --
   // the stream pass's chunks on ov_s[0] (ov_cu[0] CUs), the frame pass's on
@@ -1667,22 +1675,45 @@ static int frames_batch(ewal_ctx *c, DevTables *tb, const uint8_t *d_buf, uint64
   sg.tcb = c->ftcb.as<uint32_t>();
   uint64_t ecap = std::max<uint64_t>(c->bents.cap / sizeof(ewal_entry), B / 256 + 1024);
   uint32_t mcap = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(c->mlist.cap / 8, (uint64_t)ns + 4096), 0xffffffffull);
+  // the shards the ctx's previous batch of this shape saw rewind: rewind mode in this pass
+  const bool hint = !c->brew_hint.empty() && c->brew_ns == ns && c->brew_B == B;
+  const uint32_t nhint = hint ? (uint32_t)c->brew_hint.size() : 0u;
+  if (hint) {
+    EW_CHECK(c->fhint.ensure((size_t)nhint * 4));
+    EW_CHECK(hipMemcpyAsync(c->fhint.p, c->brew_hint.data(), (size_t)nhint * 4, hipMemcpyHostToDevice, c->stream));
+  }
   for (int pass = 0; pass < 3; ++pass) {
     EW_CHECK(grow_keep(c->bents, (size_t)ecap * sizeof(ewal_entry), 0, c->stream));
     EW_CHECK(c->mlist.ensure((size_t)mcap * 8));
     if (pass) if (int rc = reset_small(c)) return rc;
     FrArgs a = fr_args(c, tb, d_buf, B, nunits, ntiles, 0, c->bents.as<ewal_entry>(), ecap, mcap);
     a.vh = c->ov_sa.vh;   // the batch's stream pass stored vh[] (record-dense shards): the 128-B prefixes
+    if (hint) {
+      EW_CHECK(c->fown.ensure((size_t)ecap * 8));
+      EW_CHECK(c->fcl.ensure((size_t)c->brew_clcap * 4));
+      a.rew = 1;
+      a.own = c->fown.as<unsigned long long>();
+      a.clist = c->fcl.as<uint32_t>();
+      a.ccap = c->brew_clcap;
+    }
     const unsigned ngrid = (unsigned)std::min<uint64_t>(ns, (uint64_t)std::max(1, c->num_cu) * 4);
     hipLaunchKernelGGL(k_shard_nfp, dim3(ngrid), dim3(256), 0, c->stream, a.hmask, nunits, sg.soff, ns,
                        c->fnfp.as<unsigned long long>());
     hipLaunchKernelGGL(k_shard_rbase, dim3(1), dim3(1024), 0, c->stream, (const unsigned long long *)c->fnfp.p, ns,
                        ecap, sg.rbase, sg.sp, ds);
+    if (hint)
+      hipLaunchKernelGGL(k_shard_hint, dim3(std::min<uint32_t>(nhint, 256)), dim3(256), 0, c->stream, sg.sp,
+                         (const uint32_t *)c->fhint.as<uint32_t>(), nhint, (const uint64_t *)sg.rbase, a.own,
+                         (const Small *)ds);
     EW_CHECK(hipEventRecord(c->evf0, c->stream));
     c->evf_start = c->evf0;
     fr_launch_frames<true>(tsh, ntiles, a, sg, fr_cus(c), c->stream);
     EW_CHECK(hipEventRecord(c->evf1, c->stream));
     fr_launch_seam<true>(c, tsh, ntiles, a, sg, nullptr, nullptr);
+    if (hint)   // the hinted shards' slots claimed twice: their last op's entry
+      hipLaunchKernelGGL(k_ents_fix, dim3((unsigned)std::max(1, c->num_cu) * 2), dim3(256), 0, c->stream, d_buf, B,
+                         (const unsigned long long *)a.own, (const uint32_t *)a.clist, a.ccap, (const Small *)ds,
+                         a.ents, (const uint64_t *)sg.soff, ns);
     c->frames_timed = true;
     hipLaunchKernelGGL(k_tile_scan, dim3(1), dim3(1024), 0, c->stream, (const uint32_t *)a.tcnt, ntiles, sg.tcb,
                        (const Small *)ds);
@@ -1717,7 +1748,11 @@ static int frames_batch(ewal_ctx *c, DevTables *tb, const uint8_t *d_buf, uint64
       mcap = hs->nmeta + hs->nmeta / 8 + 1024;
       again = true;
     }
-    if (!again || (hs->fc.rare & ~8u)) break;
+    if ((hs->fc.rare & 64u) && hint) {   // more slots claimed twice than the list holds: once more
+      c->brew_clcap = (uint32_t)std::min<uint64_t>((uint64_t)hs->fr_ncl + hs->fr_ncl / 8 + 1024, 0xffffffffull);
+      again = true;
+    }
+    if (!again || (hs->fc.rare & ~(8u | 64u))) break;
   }
   return 0;
 }
@@ -1927,10 +1962,16 @@ static int readall_batch_impl(ewal_ctx *c, const uint8_t *d_buf, uint32_t ns, co
       }
       if (done) {   // every shard decided but those the fused pass flagged: they are replayed alone
         std::vector<uint32_t> rews;
-        for (uint32_t i = 0; i < ns; ++i)
-          if ((out[i].flags & EW_SHARD_REW) && !(out[i].flags & EW_SHARD_BAD)) rews.push_back(i);
+        c->brew_hint.clear();   // the next batch of this shape: these shards in rewind mode
+        for (uint32_t i = 0; i < ns; ++i) {
+          if (out[i].flags & EW_SHARD_BAD) continue;
+          if (out[i].flags & EW_SHARD_REW) rews.push_back(i);
+          if (out[i].flags & (EW_SHARD_REW | EW_SHARD_REWIN)) c->brew_hint.push_back(i);
+        }
+        c->brew_ns = ns;
+        c->brew_B = B;
         if (!rews.empty() && (rc = frames_batch_rewind(c, tb, d_buf, B, ns, soff, rews, out, have))) return rc;
-        for (uint32_t i = 0; i < ns; ++i) out[i].flags &= ~EW_SHARD_REW;
+        for (uint32_t i = 0; i < ns; ++i) out[i].flags &= ~(EW_SHARD_REW | EW_SHARD_REWIN);
         std::vector<uint32_t> bad;
         for (uint32_t i = 0; i < ns; ++i)
           if (out[i].flags & EW_SHARD_BAD) bad.push_back(i);

@@ -103,6 +103,9 @@ struct ShardAgg {
 // ... of a batched shard whose entry indexes go back (leader changes): the
 // frame pass runs again over its tiles in rewind mode
 #define EW_SHARD_REW 0x20000000
+// ... whose index rewinds the batch's own frame pass already resolved (the
+// shard ran in rewind mode: a ctx's previous batch saw it rewind; round 6)
+#define EW_SHARD_REWIN 0x10000000
 
 struct SegArgs {
   uint2 *ulist;            // (frame, op index) of entry ops with XXX_unrecognized (both modes)

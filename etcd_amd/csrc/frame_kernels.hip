@@ -823,7 +823,8 @@ __global__ __launch_bounds__(FR_THREADS, 1) void k_frames(FrArgs a, FrSeg sg) {
           if (has) {
             // an index rewind: the rewind-mode pass (single WAL), the shard replayed alone (batch)
             if (k <= kq) {
-              if (!a.rew) { if (SEG) sg.sp[sh].rew = 1u; else rare |= 2u; }
+              if (SEG) sg.sp[sh].rew = (a.rew && sg.sp[sh].rmode) ? 2u : 1u;   // 2: its claims are in this pass
+              else if (!a.rew) rare |= 2u;
               else rews |= 1u;
             }
             gap = k > kq && k - kq > 1;
@@ -1364,11 +1365,9 @@ __global__ __launch_bounds__(256) void k_frames_seam(FrArgs a, FrSeg sg, ResultD
         if (has) {
           const uint64_t kq = pidx - ri;
           if (k <= kq) {
-            if (!a.rew) {
-              if (SEG) sg.sp[shf].rew = 1u; else atomicOr(&ds->fc.rare, 2u);
-            } else if (!SEG) {
-              atomicOr(&ds->fr_rews, 1u);
-            }
+            if (SEG) sg.sp[shf].rew = (a.rew && sg.sp[shf].rmode) ? 2u : 1u;   // 2: its claims are in the pass
+            else if (!a.rew) atomicOr(&ds->fc.rare, 2u);
+            else atomicOr(&ds->fr_rews, 1u);
           }
           gap = k > kq && k - kq > 1;
         } else {
@@ -1698,6 +1697,22 @@ __global__ void k_shard_reset(ShardPos *__restrict__ sp, const uint32_t *__restr
   sp[list[i]] = p;
 }
 
+// The shards a ctx's previous batch saw rewind (list[0..n)) run this batch's
+// frame pass in rewind mode: their ops claim their slots (FrArgs.own) and
+// k_ents_fix rewrites the slots claimed twice right after the pass -- no
+// second pass over their tiles.  After k_shard_rbase: rmode set, the shards'
+// own[] regions unclaimed (one workgroup per listed shard, grid-strided).
+__global__ __launch_bounds__(256) void k_shard_hint(ShardPos *__restrict__ sp, const uint32_t *__restrict__ list,
+                                                    uint32_t n, const uint64_t *__restrict__ rbase,
+                                                    unsigned long long *__restrict__ own, const Small *ds) {
+  if (ds->fr_capfail) return;
+  for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
+    const uint32_t s = list[i];
+    if (threadIdx.x == 0) sp[s].rmode = 1u;
+    for (uint64_t k = rbase[s] + threadIdx.x; k < rbase[s + 1]; k += blockDim.x) own[k] = 0ull;
+  }
+}
+
 // One workgroup: tcb[t] = candidates of the tiles before t.
 __global__ __launch_bounds__(1024) void k_tile_scan(const uint32_t *__restrict__ tcnt, uint32_t nt, uint32_t *__restrict__ tcb,
                                                     const Small *ds) {
@@ -1823,7 +1838,8 @@ __global__ __launch_bounds__(256) void k_result_batch_fr(FrArgs a, FrSeg sg, ewa
     }
   }
   o.flags = EWAL_FLAG_FAST_PATH;
-  if (A.rew) o.flags |= EW_SHARD_REW;                           // the rewind-mode pass over its tiles
+  if (A.rew == 1) o.flags |= EW_SHARD_REW;                      // the rewind-mode pass over its tiles
+  if (A.rew == 2) o.flags |= EW_SHARD_REWIN;                    // resolved in this pass (rmode: claims + k_ents_fix)
   if (A.bad || (se > so && !A.open)) o.flags = EW_SHARD_BAD;   // replayed alone by the host
   out[s] = o;
   ent_first[s] = ef;

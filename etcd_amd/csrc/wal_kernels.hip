@@ -348,6 +348,9 @@ __device__ __forceinline__ void half_transpose(uint32_t (&D)[19]) {
                      // phase A saves 18 us on configs[1], the stream pass loses 68 (+4 %, +16 % on configs[0]):
                      // off (profiles/r05/ab_notes.txt)
 #endif
+#ifndef EW_RUN
+#define EW_RUN 1   // A/B: consecutive pairs per wave run (1: pairs strided by the wave count)
+#endif
 #ifndef EW_TREE4
 #define EW_TREE4 1   // the super-piece lins in one table step per lane + two DPP xors (round 5)
 #endif
@@ -591,10 +594,23 @@ __global__ __launch_bounds__(EW_THREADS, 1) void k_stream(StreamArgs a) {
     const uint32_t uu[2] = {2 * p, 2 * p + 1};
     stream_units<2, FIND, true>(a, s_slice, s_s64, s_s128, s_unib, Lt, uu, T);
   };
+#if EW_RUN > 1
+  // A/B (EW_RUN = R): each wave takes runs of R consecutive pairs, the runs
+  // dealt round-robin over the waves (span W * R pairs), instead of single
+  // pairs strided by W
+  const uint32_t tot = NP > PB ? NP - PB : 0u, span = W * EW_RUN;
+  const uint32_t remr = tot % span, myr = p0 * EW_RUN;
+  const uint32_t npairs = (tot / span) * EW_RUN + (remr > myr ? std::min<uint32_t>(remr - myr, EW_RUN) : 0u);
+  auto pair_at = [&](uint32_t k) {
+    const uint32_t kk = k < npairs ? k : npairs - 1;
+    return __builtin_amdgcn_readfirstlane(PB + (kk / EW_RUN) * span + myr + kk % EW_RUN);
+  };
+#else
   const uint32_t npairs = PB + p0 < NP ? (NP - 1 - PB - p0) / W + 1 : 0u;
   auto pair_at = [&](uint32_t k) {   // clamped: a prefetch past the end reloads the last pair
     return __builtin_amdgcn_readfirstlane(PB + p0 + W * (k < npairs ? k : npairs - 1));
   };
+#endif
   uint32_t DA[2][19], DB[2][19], DC[2][19];
   ew_v3u nA, nB, nC;
   if (npairs) {   // the first two pairs are in flight while the tables are staged

@@ -238,3 +238,39 @@ def test_batch_edges_and_ctx_reuse(ctx):
     g2 = W.readall_bytes(one, 0, ctx)           # a single ReadAll after a larger batch
     assert g2.as_dict() == g.as_dict()
     check_batch(ctx, [one, b"", one], [0, 0, 3], expect_fast=True)
+
+
+def _rewind_wal(seed, n=40):
+    """a shard after leader changes: entry indexes go back (wal/wal.go:173)"""
+    rng = random.Random(seed)
+    e = O.WalEncoder(0)
+    e.save_crc(0)
+    e.encode(1, b"m")
+    idx = 1
+    for i in range(n):
+        if i % 9 == 8:
+            idx = max(1, idx - rng.randrange(1, 5))   # a new leader rewrites the last indexes
+        e.save_entry(0, 1 + i // 9, idx, rng.randbytes(rng.randrange(0, 300)))
+        idx += 1
+    return e.getvalue()
+
+
+def test_batch_rewind_hint_repeated_and_stale(ctx):
+    """Round 6: the shards whose indexes went back in a ctx's previous batch of
+    the same shape run the next batch's own frame pass in rewind mode (their
+    ops claim slots, k_ents_fix after the pass) instead of a second pass over
+    their tiles.  Repeated calls (the hint right), then the same shard sizes
+    permuted (the hint names shards that no longer rewind, and a rewinding
+    shard it does not name): every shard's result is the oracle's, none is
+    replayed alone."""
+    rng = random.Random(61)
+    base = [build_wal(rng, 30, 400, big_terms=False) for _ in range(5)]
+    rw1, rw2 = _rewind_wal(1), _rewind_wal(2)
+    shards = [base[0], rw1, base[1], base[2], rw2, base[3]]
+    for _ in range(3):
+        check_batch(ctx, shards, [1] * len(shards), fallback=set())
+    perm = [rw1, base[0], base[1], rw2, base[2], base[3]]   # same shard count, same total bytes
+    assert sum(map(len, perm)) == sum(map(len, shards))
+    for _ in range(2):
+        check_batch(ctx, perm, [1] * len(perm), fallback=set())
+    check_batch(ctx, shards, [1] * len(shards), fallback=set())
