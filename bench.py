@@ -227,8 +227,8 @@ def run_shards(a, dist, rank, world, local, cpu_seconds=None):
         assert rc == 0, rc
         last["r"] = c_out
         if dist is not None:   # one all-reduce of the batch's verdicts (etcd_amd/shard.py)
-            shard.combine_batch(dist, first, [(x.fail_record if x.status != L.OK else -1, x.n_records,
-                                               x.status != L.OK) for x in c_out], out=summary)
+            last["v"] = shard.combine_batch(dist, first, [(x.fail_record if x.status != L.OK else -1, x.n_records,
+                                                           x.status != L.OK) for x in c_out], out=summary)
 
     fr_ms = []
 
@@ -243,6 +243,28 @@ def run_shards(a, dist, rank, world, local, cpu_seconds=None):
     assert all((x.status, x.fail_record) == ((L.ERR_RECORD_CRC, 1000) if first + i == bad_shard else (L.OK, -1))
                for i, x in enumerate(c_out))
     frames = sum(nrec)
+    # the node's verdict: the all-reduced {MIN first-corrupt key, SUM frames, SUM failing shards} of the last
+    # step (N = 1: the same reduction over this rank's shards), and every rank's kernel times
+    if dist is not None:
+        key, vframes, vfail = last["v"]
+        kt = torch.tensor([r0.stream_ms, frames_ms, r0.device_ms, float(nb), float(frames)], dtype=torch.float64,
+                          device="cuda")
+        allk = [torch.zeros_like(kt) for _ in range(world)]
+        dist.all_gather(allk, kt)
+        per_rank = [dict(rank=i, stream_ms=round(float(x[0]), 4), frames_ms=round(float(x[1]), 4),
+                         pipeline_ms=round(float(x[2]), 4),
+                         roofline_frames=frames_roofline(int(x[4]), int(x[3]), float(x[1]), "shards"))
+                    for i, x in enumerate(allk)]
+    else:
+        key, vframes, vfail = shard.combine_batch_local(first, [(x.fail_record if x.status != L.OK else -1,
+                                                                 x.n_records, x.status != L.OK) for x in c_out])
+        per_rank = None
+    dk = shard.decode_key(key)
+    assert dk == (bad_shard, 1000) and vfail == 1, (dk, vfail)
+    verdict = {"first_corrupt": {"shard": dk[0], "frame": dk[1]}, "frames_verified": vframes,
+               "failing_shards": vfail,
+               "note": "all-reduced over the ranks (MIN first-corrupt key = shard << 40 | frame, SUM frames, "
+                       "SUM failing shards), the last timed step's"}
     # ---- torn5: five shards end in a torn frame -----------------------------
     torn = sorted({(nsh * j) // 5 + 7 for j in range(5)} - {bad_shard - first})[:5]
     tlens = [x - (1000 + 37 * i) if i in torn else x for i, x in enumerate(lens)]
@@ -312,8 +334,10 @@ def run_shards(a, dist, rank, world, local, cpu_seconds=None):
     rwms = timed(dist, a.steps, rstep) / a.steps * 1e3
     rew1pct = {"ms_per_step": round(rwms, 4), "vs_clean": round(rwms / ms, 4), "rewinding_shards": rws,
                "note": "the same batch with %d shards (1 %%) replaced by WALs after leader changes (1 %% of their "
-                       "entries rewrite the last 1-8 indexes, wal/wal.go:170-176): the batch's rewind-mode pass "
-                       "over those shards' tiles, no shard is replayed alone" % len(rws)}
+                       "entries rewrite the last 1-8 indexes, wal/wal.go:170-176): no shard is replayed alone; "
+                       "the ctx's previous batch of this shape saw those shards rewind, so the batch's own frame "
+                       "pass runs them in rewind mode (slot claims + k_ents_fix, no second pass; the first call "
+                       "of a shape reruns the claims over their tiles, k_rew_claim)" % len(rws)}
     del rmem
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
@@ -359,6 +383,8 @@ def run_shards(a, dist, rank, world, local, cpu_seconds=None):
         "pipeline_device_ms": round(r0.device_ms, 4),
         "post_stream_ms": round(r0.post_ms, 4),
         "roofline_frames": frames_roofline(frames, nb, frames_ms, "shards"),
+        "verdict": verdict,
+        "per_rank": per_rank,
         "torn5": torn5,
         "rew1pct": rew1pct,
         "cpu_baseline": cpu,

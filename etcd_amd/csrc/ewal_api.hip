@@ -1645,7 +1645,7 @@ static hipError_t grow_keep(DevBuf &b, size_t need, size_t keep, hipStream_t st)
 // frames per 4 KiB unit from which a batch's next stream pass stores vh[]
 // (the 128-B prefixes of the batch frame pass; round 6, profiles/r06/)
 #ifndef EW_VH_BATCH_FPU
-#define EW_VH_BATCH_FPU 2
+#define EW_VH_BATCH_FPU 3
 #endif
 static int frames_batch(ewal_ctx *c, DevTables *tb, const uint8_t *d_buf, uint64_t B, uint32_t ns,
                         const std::vector<uint64_t> &soff, const uint64_t *ris, ewal_result *out, bool *done,

@@ -54,12 +54,7 @@ def combine_batch(dist, first_shard: int, verdicts, device="cpu", out=None):
     n_records, failed) of shard first_shard + i.  Same reduction as
     `combine` -- MIN of the failing shards' keys, SUM of frames verified, SUM
     of failing shards -- over the whole batch, in the same one exchange."""
-    key, frames, nfail = NO_FAILURE, 0, 0
-    for i, (fr, n, failed) in enumerate(verdicts):
-        if failed:
-            key = min(key, failure_key(first_shard + i, fr))
-            nfail += 1
-        frames += fr if fr >= 0 else n
+    key, frames, nfail = combine_batch_local(first_shard, verdicts)
     t = out if out is not None else torch.zeros(3, dtype=torch.int64, device=device)
     t[0] = key
     t[1] = frames
@@ -67,6 +62,18 @@ def combine_batch(dist, first_shard: int, verdicts, device="cpu", out=None):
     dist.all_reduce(t[0:1], op=dist.ReduceOp.MIN)
     dist.all_reduce(t[1:3], op=dist.ReduceOp.SUM)
     return int(t[0].item()), int(t[1].item()), int(t[2].item())
+
+
+def combine_batch_local(first_shard: int, verdicts):
+    """combine_batch's reduction over one rank's verdicts alone (N = 1): no
+    exchange."""
+    key, frames, nfail = NO_FAILURE, 0, 0
+    for i, (fr, n, failed) in enumerate(verdicts):
+        if failed:
+            key = min(key, failure_key(first_shard + i, fr))
+            nfail += 1
+        frames += fr if fr >= 0 else n
+    return key, frames, nfail
 
 
 def combine_commit(dist, changed, commit_min, commit_max, out=None, device="cpu"):
