@@ -343,6 +343,9 @@ __device__ __forceinline__ void half_transpose(uint32_t (&D)[19]) {
 #ifndef EW_V_NT
 #define EW_V_NT 0    // A/B: v[] / hmask stored nontemporally (fewer dirty L2 lines when the stream pass ends)
 #endif
+#ifndef EW_V_SC1
+#define EW_V_SC1 0   // A/B: v[] / hmask stored with relaxed agent-scope atomic stores (sc1: the line leaves L2)
+#endif
 #ifndef EW_ULIN
 #define EW_ULIN 0    // A/B: k_stream stores every 4 KiB unit's lin and the frame pass's phase A loads it -- the
                      // phase A saves 18 us on configs[1], the stream pass loses 68 (+4 %, +16 % on configs[0]):
@@ -436,6 +439,9 @@ __device__ __forceinline__ void stream_units(const StreamArgs &a, const uint8_t 
     for (int i = 0; i < NU; ++i)
       if ((!(EW_XS & 4) || c[i] == 0x12345678u) && !vskip[i]) {
         if (EW_V_NT) __builtin_nontemporal_store(c[i], a.v + (uint64_t)u[i] * EW_VPU + (lane >> 2));
+        else if (EW_V_SC1)
+          __hip_atomic_store(a.v + (uint64_t)u[i] * EW_VPU + (lane >> 2), c[i], __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
         else a.v[(uint64_t)u[i] * EW_VPU + (lane >> 2)] = c[i];
       }
   }
