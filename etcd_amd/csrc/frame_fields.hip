@@ -14,6 +14,16 @@
 // read back only by the host's copy or the next call): configs[1]
 // post-stream -8 us; the batched path keeps plain stores (+1-2 % with
 // nontemporal ones, profiles/r02/ab_nt_ents.txt).
+// the same with relaxed agent-scope atomic stores (sc1: the lines leave L2; A/B EW_ENTS_SC1)
+__device__ __forceinline__ void store_entry_sc1(ewal_entry *dst, const ewal_entry &e) {
+  uint64_t *q = (uint64_t *)dst;
+  __hip_atomic_store(q, e.term, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(q + 1, e.index, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(q + 2, e.data_off, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(q + 3, e.data_len, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(q + 4, ((uint64_t)(uint32_t)e.data_nil << 32) | (uint32_t)e.type, __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
 __device__ __forceinline__ void store_entry_nt(ewal_entry *dst, const ewal_entry &e) {
   uint64_t *q = (uint64_t *)dst;
   __builtin_nontemporal_store(e.term, q);

@@ -44,6 +44,16 @@
 #ifndef FR_THREADS
 #define FR_THREADS 768
 #endif
+#ifndef EW_ENTS_SC1
+#define EW_ENTS_SC1 0      // A/B: the entry ops' ents slots stored sc1 (1: batch, 2: single WAL too)
+#endif
+#ifndef EW_FR_SC1
+#define EW_FR_SC1 0        // A/B: the per-unit pl / ucb stored sc1
+#endif
+__device__ __forceinline__ void fr_st32(uint32_t *p, uint32_t x) {
+  if (EW_FR_SC1) __hip_atomic_store(p, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else *p = x;
+}
 #define FR_WAVES (FR_THREADS / 64)
 #define FR_NIB 20          // S_{2^0} .. S_{2^19} as nibble tables
 #define FR_SCAN 4096       // tiles the seam pass scans for a tile's neighbouring frame
@@ -509,7 +519,7 @@ __global__ __launch_bounds__(FR_THREADS, 1) void k_frames(FrArgs a, FrSeg sg) {
         const uint32_t u = u0 + UPL * lane + j;
         if (NL == 64 || lane < NL) {
           spw[UPL * lane + j] = pwj;
-          if (u < a.nunits) a.pl[u] = pwj;
+          if (u < a.nunits) fr_st32(a.pl + u, pwj);
         }
       }
     }
@@ -836,14 +846,16 @@ __global__ __launch_bounds__(FR_THREADS, 1) void k_frames(FrArgs a, FrSeg sg) {
         if (SEG) {   // op k of the shard: its region's entry k
           const uint64_t rb = sg.rbase[sh], room = sg.rbase[sh + 1] - rb;
           if (k < room) {
-            a.ents[rb + k] = ewal_entry{d.f0, d.f1, d.edoff - S0, d.edlen, d.etype, (int32_t)d.enil};
+            if (EW_ENTS_SC1) store_entry_sc1(a.ents + rb + k, ewal_entry{d.f0, d.f1, d.edoff - S0, d.edlen, d.etype, (int32_t)d.enil});
+            else a.ents[rb + k] = ewal_entry{d.f0, d.f1, d.edoff - S0, d.edlen, d.etype, (int32_t)d.enil};
             if (a.rew && sg.sp[sh].rmode && atomicMax(&a.own[rb + k], (unsigned long long)(p + 1))) {   // a slot written twice
               const uint32_t ci = atomicAdd(&ds->fr_ncl, 1u);
               if (ci < a.ccap) a.clist[ci] = (uint32_t)(rb + k); else rare |= 64u;
             }
           }
         } else if (k < a.ecap) {
-          store_entry_nt(a.ents + k, ewal_entry{d.f0, d.f1, d.edoff, d.edlen, d.etype, (int32_t)d.enil});
+          if (EW_ENTS_SC1 >= 2) store_entry_sc1(a.ents + k, ewal_entry{d.f0, d.f1, d.edoff, d.edlen, d.etype, (int32_t)d.enil});
+          else store_entry_nt(a.ents + k, ewal_entry{d.f0, d.f1, d.edoff, d.edlen, d.etype, (int32_t)d.enil});
           if (a.rew && atomicMax(&a.own[k], (unsigned long long)(p + 1))) {   // a slot written twice
             const uint32_t ci = atomicAdd(&ds->fr_ncl, 1u);
             if (ci < a.ccap) a.clist[ci] = (uint32_t)k; else rare |= 64u;
@@ -959,7 +971,7 @@ __global__ __launch_bounds__(FR_THREADS, 1) void k_frames(FrArgs a, FrSeg sg) {
 #pragma unroll
       for (int j = 0; j < UPL; ++j) {
         const uint32_t u = u0 + UPL * lane + j;
-        if (u < a.nunits && (NL == 64 || lane < NL)) a.ucb[u] = run;
+        if (u < a.nunits && (NL == 64 || lane < NL)) fr_st32(a.ucb + u, run);
         run += c[j];
       }
     }

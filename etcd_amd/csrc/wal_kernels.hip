@@ -343,13 +343,38 @@ __device__ __forceinline__ void half_transpose(uint32_t (&D)[19]) {
 #ifndef EW_V_NT
 #define EW_V_NT 0    // A/B: v[] / hmask stored nontemporally (fewer dirty L2 lines when the stream pass ends)
 #endif
+// The stream pass's lin outputs (v[], vh[]) are stored with relaxed
+// agent-scope atomic stores (global_store ... sc1): the lines leave the XCD's
+// L2 as they are written instead of staying there dirty beside the stream's
+// nontemporal loads.  Round 6 A/B, one box, the rounds before the box's
+// clock state changed (profiles/r06/ab_stores_*_s4.txt): configs[1] k_stream
+// 1.627 -> 1.57 ms (-3.5 %, as fast as without the v[] stores at all: the
+// timing-only EW_XS=4 build, session s2), pipeline 1.957 -> 1.91 ms; 128 x 64
+// MiB shards pipeline 2.922 -> 2.879 ms; configs[0] 0.2949 -> 0.2927 ms.  The
+// hmask stores stay plain: as two 8-B sc1 stores by one lane (bit 4) they
+// gave the gain back.  (Round 2 measured plain vs nt only.)
+// (bits: 1 v[], 2 vh[], 4 hmask)
 #ifndef EW_V_SC1
-#define EW_V_SC1 0   // A/B: v[] / hmask stored with relaxed agent-scope atomic stores (sc1: the line leaves L2)
+#define EW_V_SC1 3
+#endif
+template <int BIT>
+__device__ __forceinline__ void st_out32(uint32_t *p, uint32_t x) {
+  if (EW_V_SC1 & BIT) __hip_atomic_store(p, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else *p = x;
+}
+__device__ __forceinline__ void st_out64(unsigned long long *p, unsigned long long x) {
+  __hip_atomic_store(p, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+#ifndef EW_HM_PAIR
+#define EW_HM_PAIR 0   // A/B: the pair loop's two hmask entries in one 2-lane store
 #endif
 #ifndef EW_ULIN
 #define EW_ULIN 0    // A/B: k_stream stores every 4 KiB unit's lin and the frame pass's phase A loads it -- the
                      // phase A saves 18 us on configs[1], the stream pass loses 68 (+4 %, +16 % on configs[0]):
                      // off (profiles/r05/ab_notes.txt)
+#endif
+#ifndef EW_STREAM_AUX
+#define EW_STREAM_AUX 2   // the stream pass's buffer-load cache policy: 2 = nontemporal (A/B: 0 = default policy)
 #endif
 #ifndef EW_RUN
 #define EW_RUN 1   // A/B: consecutive pairs per wave run (1: pairs strided by the wave count)
@@ -387,7 +412,7 @@ __device__ __forceinline__ void stream_units(const StreamArgs &a, const uint8_t 
     for (int i = 0; i < NU; ++i) {
       const uint32_t o = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c[i], EW_DPP_ROW_SHR(1), 0xf, 0xf, false);
       const uint32_t h = tab_apply(s64, o) ^ c[i];
-      if ((lane & 3) == 1) a.vh[(uint64_t)u[i] * EW_VPU + (lane >> 2)] = h;
+      if ((lane & 3) == 1) st_out32<2>(a.vh + (uint64_t)u[i] * EW_VPU + (lane >> 2), h);
     }
   }
 #if EW_TREE4
@@ -439,10 +464,7 @@ __device__ __forceinline__ void stream_units(const StreamArgs &a, const uint8_t 
     for (int i = 0; i < NU; ++i)
       if ((!(EW_XS & 4) || c[i] == 0x12345678u) && !vskip[i]) {
         if (EW_V_NT) __builtin_nontemporal_store(c[i], a.v + (uint64_t)u[i] * EW_VPU + (lane >> 2));
-        else if (EW_V_SC1)
-          __hip_atomic_store(a.v + (uint64_t)u[i] * EW_VPU + (lane >> 2), c[i], __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_AGENT);
-        else a.v[(uint64_t)u[i] * EW_VPU + (lane >> 2)] = c[i];
+        else st_out32<1>(a.v + (uint64_t)u[i] * EW_VPU + (lane >> 2), c[i]);
       }
   }
   if (FIND && EW_ULIN) {
@@ -462,6 +484,15 @@ __device__ __forceinline__ void stream_units(const StreamArgs &a, const uint8_t 
   }
   if (!FIND) return;
   if (EW_SPLIT_CAND && !(EW_XS & 8)) {   // the flagged pieces, for k_cand
+    if (EW_HM_PAIR && NU == 2 && SAFE && EW_CAND_TAILMASK && !EW_V_NT && !(EW_V_SC1 & 4)) {
+      // the pair's two 16-B mask pairs (units u[0], u[0] + 1: 32 contiguous
+      // bytes) in ONE store instruction, lanes 0 and 1
+      const unsigned long long hm0 = __ballot(fm[0] != 0), h30 = __ballot((fm[0] & 0x10101010u) != 0);
+      const unsigned long long hm1 = __ballot(fm[NU - 1] != 0), h31 = __ballot((fm[NU - 1] & 0x10101010u) != 0);
+      if (lane < 2)
+        *(ulonglong2 *)(a.hmask + 2 * ((uint64_t)u[0] + lane)) = lane ? make_ulonglong2(hm1, h31) : make_ulonglong2(hm0, h30);
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < NU; ++i) {
       const uint64_t off = (uint64_t)u[i] * EW_WAVE_BYTES + (uint64_t)lane * EW_PIECE;
@@ -476,7 +507,12 @@ __device__ __forceinline__ void stream_units(const StreamArgs &a, const uint8_t 
             __builtin_nontemporal_store(hm, a.hmask + 2 * (uint64_t)u[i]);
             __builtin_nontemporal_store(h3, a.hmask + 2 * (uint64_t)u[i] + 1);
           } else {
-            *(ulonglong2 *)(a.hmask + 2 * (uint64_t)u[i]) = make_ulonglong2(hm, h3);
+            if (EW_V_SC1 & 4) {
+              st_out64(a.hmask + 2 * (uint64_t)u[i], hm);
+              st_out64(a.hmask + 2 * (uint64_t)u[i] + 1, h3);
+            } else {
+              *(ulonglong2 *)(a.hmask + 2 * (uint64_t)u[i]) = make_ulonglong2(hm, h3);
+            }
           }
         }
       } else if (lane == 0) {
@@ -576,11 +612,11 @@ __global__ __launch_bounds__(EW_THREADS, 1) void k_stream(StreamArgs a) {
 #else
         const int off = EW_WAVE_BYTES * i + 1024 * r;
 #endif
-        const ew_v4u w = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)lo + off, 0, 2 /* nt */);
+        const ew_v4u w = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)lo + off, 0, EW_STREAM_AUX);
         T[i][4 * r] = w.x; T[i][4 * r + 1] = w.y; T[i][4 * r + 2] = w.z; T[i][4 * r + 3] = w.w;
       }
     }
-    t3 = __builtin_amdgcn_raw_buffer_load_b96(rs, o3, 0, 2);
+    t3 = __builtin_amdgcn_raw_buffer_load_b96(rs, o3, 0, EW_STREAM_AUX);
   };
   auto run_pair = [&](uint32_t p, uint32_t (&T)[2][19], const ew_v3u &t3) {
 #if EW_LOAD_HALF

@@ -1,6 +1,6 @@
 """Per-phase cycles of k_frames (a -DFR_TIMING build of the library, loaded
 through EWAL_LIB_PATH): the configs[1] WAL and configs[0]'s WAL on the GPU.
-Usage: EWAL_LIB_PATH=tools/libewal_tm.so python tools/fr_timing.py"""
+Usage: EWAL_LIB_PATH=tools/libewal_tm.so python tools/fr_timing.py [wal] [c1] [shards]"""
 import ctypes as C
 import os
 import sys
@@ -20,19 +20,32 @@ lib.ewal_dbg_fr_seam_maxsteps.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
 lib.ewal_dbg_fr_result_steps.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
 
 
-def one(label, size, lo, hi):
-    buf, n = W.synth_wal(size, lo, hi, seed=2)
+def one(label, size, lo, hi, nsh=0):
+    """nsh > 0: a configs[2]-shaped batch of nsh shards of `size` bytes each (one batched ReadAll)"""
+    if nsh:
+        buf, lens, nrec = W.synth_shards(list(range(nsh)), size, lo, hi)
+        n = sum(nrec)
+    else:
+        buf, n = W.synth_wal(size, lo, hi, seed=2)
+        lens = [len(buf)]
     ctx = W.Context(0)
     nb = len(buf)
     d = ctx.alloc(nb + 64)
     d.upload_ptr(C.addressof((C.c_char * nb).from_buffer(buf)), nb)
     rs = L.Result()
     mx = (C.c_ulonglong * (1024 * 8))()
+    ns = len(lens)
+    cl, cr, co = (C.c_uint64 * ns)(*lens), (C.c_uint64 * ns)(*([1] * ns)), (L.Result * ns)()
     for i in range(3):
         if i == 2:   # the per-block maxima accumulate: zeroed before the measured call
             lib.ewal_dbg_fr_seam_maxsteps(mx, 1024 * 8)
-        rc = lib.ewal_readall_device(ctx.handle, d.ptr, nb, 1, C.byref(rs))
-        assert rc == 0 and rs.flags & L.FLAG_FAST_PATH, (rc, rs.flags)
+        if nsh:
+            rc = lib.ewal_readall_batch_device(ctx.handle, d.ptr, ns, cl, cr, co)
+            rs = co[0]
+            assert rc == 0 and all(x.status == 0 and not (x.flags & L.FLAG_SHARD_FALLBACK) for x in co)
+        else:
+            rc = lib.ewal_readall_device(ctx.handle, d.ptr, nb, 1, C.byref(rs))
+            assert rc == 0 and rs.flags & L.FLAG_FAST_PATH, (rc, rs.flags)
     t = (C.c_ulonglong * (8192 * 8))()
     lib.ewal_dbg_fr_timing(t, 8192 * 8)
     sd = (C.c_ulonglong * (1024 * 4))()
@@ -87,5 +100,10 @@ def one(label, size, lo, hi):
     ctx.close()
 
 
-one("configs[1]", 8 << 30, 64, 65536)
-one("configs[0]", int(285e6), 256, 256)
+which = sys.argv[1:] or ["wal", "c1"]
+if "wal" in which:
+    one("configs[1]", 8 << 30, 64, 65536)
+if "c1" in which:
+    one("configs[0]", int(285e6), 256, 256)
+if "shards" in which:
+    one("configs[2] x128 shards", 64 << 20, 128, 4096, nsh=128)
