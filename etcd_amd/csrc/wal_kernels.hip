@@ -484,13 +484,19 @@ __device__ __forceinline__ void stream_units(const StreamArgs &a, const uint8_t 
   }
   if (!FIND) return;
   if (EW_SPLIT_CAND && !(EW_XS & 8)) {   // the flagged pieces, for k_cand
-    if (EW_HM_PAIR && NU == 2 && SAFE && EW_CAND_TAILMASK && !EW_V_NT && !(EW_V_SC1 & 4)) {
+    if (EW_HM_PAIR && NU == 2 && SAFE && EW_CAND_TAILMASK && !EW_V_NT) {
       // the pair's two 16-B mask pairs (units u[0], u[0] + 1: 32 contiguous
-      // bytes) in ONE store instruction, lanes 0 and 1
+      // bytes) in ONE store instruction: 1 -- lanes 0 and 1, 16 B each;
+      // 2 -- lanes 0..7, one dword each (sc1 when EW_V_SC1 & 4)
       const unsigned long long hm0 = __ballot(fm[0] != 0), h30 = __ballot((fm[0] & 0x10101010u) != 0);
       const unsigned long long hm1 = __ballot(fm[NU - 1] != 0), h31 = __ballot((fm[NU - 1] & 0x10101010u) != 0);
-      if (lane < 2)
-        *(ulonglong2 *)(a.hmask + 2 * ((uint64_t)u[0] + lane)) = lane ? make_ulonglong2(hm1, h31) : make_ulonglong2(hm0, h30);
+      if (EW_HM_PAIR == 1) {
+        if (lane < 2)
+          *(ulonglong2 *)(a.hmask + 2 * ((uint64_t)u[0] + lane)) = lane ? make_ulonglong2(hm1, h31) : make_ulonglong2(hm0, h30);
+      } else if (lane < 8) {
+        const unsigned long long q = lane < 2 ? hm0 : lane < 4 ? h30 : lane < 6 ? hm1 : h31;
+        st_out32<4>((uint32_t *)(a.hmask + 2 * (uint64_t)u[0]) + lane, (uint32_t)(q >> (32 * (lane & 1))));
+      }
       return;
     }
 #pragma unroll
