@@ -51,7 +51,10 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--snap-files", type=int, default=10000)
-    ap.add_argument("--pool-gib", type=float, default=24.0)
+    ap.add_argument("--pool-gib", type=float, default=None,
+                    help="snapstream's pinned host pool per rank (default 24 GiB at N=1, max(6, 48 / N) at N>1: "
+                         "the files are drawn from it at random, so its size does not move the PCIe-bound rate, and "
+                         "8 ranks x 24 GiB of pinned memory would be 192 GiB of the node's RAM)")
     ap.add_argument("--batch-gib", type=float, default=8.0)
     ap.add_argument("--workload", choices=["wal", "c1", "shards", "snap", "snapstream", "commit", "msg", "restart",
                                            "rewind"],
@@ -518,7 +521,8 @@ def run_snapstream(a, dist, rank, world, local, cpu_seconds=None):
     t = time.time()
     src = np.random.default_rng(4 + rank).integers(0, 256, size=(256 << 20) + 4096, dtype=np.uint8).tobytes()
     sizes, total = [], 0
-    budget = int(a.pool_gib * (1 << 30))
+    pool_gib = a.pool_gib if a.pool_gib is not None else (24.0 if world == 1 else max(6.0, 48.0 / world))
+    budget = int(pool_gib * (1 << 30))
     while total < budget:
         n = int(math.exp(rng.uniform(math.log(1 << 20), math.log(256 << 20))))
         sizes.append(n + 64)    # + the snappb / raftpb.Snapshot envelope (upper bound)
