@@ -134,3 +134,46 @@ def test_vh_options_validated(ctx):
     with pytest.raises(Exception):
         W.check(L.lib.ewal_ctx_set_options(ctx.handle, L.OPT_VH_ON | L.OPT_VH_OFF))
     ctx.set_options()
+
+
+def _batch_vs_oracle(ctx, shards, ris, vh):
+    ctx.set_options(vh=vh)
+    try:
+        res = W.readall_batch_bytes(shards, ris, ctx)
+    finally:
+        ctx.set_options()
+    for s, (b, ri, g) in enumerate(zip(shards, ris, res)):
+        o = O.readall(b, ri)
+        assert g.status == o["status"], (vh, s, g.status, o["status"])
+        if o["status"] == O.OK:
+            assert (g.n_records, g.last_crc, g.enti, g.metadata) == \
+                (o["n_records"], o["last_crc"], o["enti"], o["metadata"]), (vh, s)
+            assert [(x.Index, x.Term, x.Data) for x in g.ents] == \
+                   [(x["index"], x["term"], x["data"]) for x in o["ents"]], (vh, s)
+        elif o["status"] != O.ERR_INDEX_NOT_FOUND:
+            assert (g.fail_record, g.fail_offset) == (o["fail_record"], o["fail_offset"]), (vh, s)
+    return res
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_vh_batches_shapes_corrupt_torn_rewinds(ctx, seed):
+    """Round 6: the batch frame pass with the 128-B prefixes (k_frames<true,
+    TSH, true>; the batch's stream pass stores vh[]) -- record-dense shards of
+    several shapes, a corrupt record, a torn tail and a shard after leader
+    changes in one batch, with the option on, off and automatic (the second
+    automatic call takes it: the first batch was record-dense), every shard
+    against the oracle's ReadAll alone."""
+    rng = random.Random(9100 + seed)
+    shards, ris = [], []
+    for i in range(6):
+        lo, hi = rng.choice([(16, 300), (64, 1200), (128, 4096), (1, 200)])
+        buf, n = W.synth_wal(rng.choice([1, 2, 3]) << 20, lo, hi, seed=300 + 10 * seed + i,
+                             corrupt_record=rng.randrange(1, 500) if i == 2 else -1,
+                             rewind_per_mille=20 if i == 4 else 0)
+        b = bytes(buf)
+        if i == 3:
+            b = b[:-rng.randrange(1, 200)]   # a torn last frame
+        shards.append(b)
+        ris.append(1)
+    for vh in (True, False, None, None):
+        _batch_vs_oracle(ctx, shards, ris, vh)

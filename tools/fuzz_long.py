@@ -4,8 +4,13 @@ seeds [first, first + count), every result against the oracle, one ctx for all
 (stale per-call state shows up as a mismatch); with --batch the batched case
 (_large_batch_case, 3-8 such shards per batch); with --split the single case
 split inside its file over 2 and 3 ctxs (ewal_readall_multi, the C join).
+--repeat (with --batch): every batch twice in a row and then with its shards
+in reverse order (the same shard count and bytes): the second call runs the
+shards the first saw rewind in rewind mode inside the batch's own pass (the
+ctx's hint), the reversed one with a stale hint (round 6).  --vh: the 128-B
+prefixes forced on.
 Prints one line per 20 seeds.
-Usage: python3 tools/fuzz_long.py FIRST COUNT [--batch | --split]"""
+Usage: python3 tools/fuzz_long.py FIRST COUNT [--batch [--repeat] | --split] [--vh]"""
 import os
 import sys
 import time
@@ -25,10 +30,17 @@ def main():
     t0 = time.time()
     statuses = {}
     batch = "--batch" in sys.argv[3:]
+    repeat = "--repeat" in sys.argv[3:]
+    if "--vh" in sys.argv[3:]:
+        ctx.set_options(vh=True)
     split = [W.Context(0) for _ in range(3)] if "--split" in sys.argv[3:] else None
     for s in range(first, first + count):
         if batch:
-            got = [r.status for r in check_batch(ctx, *_large_batch_case(s))]
+            shards, ris = _large_batch_case(s)
+            got = [r.status for r in check_batch(ctx, shards, ris)]
+            if repeat:
+                got += [r.status for r in check_batch(ctx, shards, ris)]
+                got += [r.status for r in check_batch(ctx, shards[::-1], ris[::-1])]
         elif split:
             m, ri = _large_case(s)
             got = []
