@@ -411,11 +411,7 @@ __device__ __forceinline__ void stream_units(const StreamArgs &a, const uint8_t 
 #pragma unroll
     for (int i = 0; i < NU; ++i) {
       const uint32_t o = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c[i], EW_DPP_ROW_SHR(1), 0xf, 0xf, false);
-      // only lanes 4m+1 need the lookup: the others read entry 0 (one address,
-      // a broadcast) instead of 48 random addresses that share the 16 lanes'
-      // banks (round 6: the vh[] step's LDS conflicts, not its stores, were
-      // most of its +4-6 % on the stream pass)
-      const uint32_t h = tab_apply(s64, (lane & 3) == 1 ? o : 0u) ^ c[i];
+      const uint32_t h = tab_apply(s64, o) ^ c[i];
       if ((lane & 3) == 1) st_out32<2>(a.vh + (uint64_t)u[i] * EW_VPU + (lane >> 2), h);
     }
   }
