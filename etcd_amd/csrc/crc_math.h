@@ -18,7 +18,12 @@
 //                      (S_1 is x -> x * x^8 mod the polynomial, invertible
 //                      because the polynomial has a constant term), so that
 //                      P(x) = S_{b-x}^-1(P(b) ^ lin(stream[x, b))) reaches a
-//                      prefix from the NEXT boundary b
+//                      prefix from the NEXT boundary b;
+//                      then EW_TAIL_TABS nibble tables (128 words each) of
+//                      the shifts by -128..128 bytes in two factors, for the
+//                      frame pass's prefix tails (ew_tail_tab, tail_shift in
+//                      wal_kernels.hip): S_{16a} (a = 0..8), S_b (b = 0..15),
+//                      S_{16a}^-1, S_b^-1
 #pragma once
 #include <cstdint>
 #include <cstring>
@@ -27,6 +32,11 @@
 
 #define EW_SHIFT_LEVELS 48  // S_{2^m} for m < 48: lengths up to 256 TiB
 #define EW_INV_LEVELS 8     // S_{2^m}^-1 for m < 8 (inverse shifts up to 255 bytes), after the forward levels
+#define EW_TAIL_TABS 50     // nibble tables after the inverse levels (see above)
+#define EW_TAIL_OFF ((EW_SHIFT_LEVELS + EW_INV_LEVELS) * 1024)
+
+// The signed shift amount of tail table t: S_{16t}, S_{t-9}, S_{16(t-25)}^-1, S_{t-34}^-1
+inline int ew_tail_amount(int t) { return t < 9 ? 16 * t : t < 25 ? t - 9 : t < 34 ? -16 * (t - 25) : -(t - 34); }
 
 namespace ewal {
 
@@ -36,7 +46,7 @@ struct CrcTables {
   uint32_t slice16[16][256];    // slicing-by-16 (slice16[t] = slice[t] for t < 4): the device table
   std::vector<uint32_t> shift;  // EW_SHIFT_LEVELS * 4 * 256
 
-  explicit CrcTables(uint32_t p) : poly(p), shift((size_t)(EW_SHIFT_LEVELS + EW_INV_LEVELS) * 1024) {
+  explicit CrcTables(uint32_t p) : poly(p), shift((size_t)EW_TAIL_OFF + EW_TAIL_TABS * 128) {
     for (uint32_t i = 0; i < 256; i++) {
       uint32_t c = i;
       for (int j = 0; j < 8; j++) c = (c & 1) ? (c >> 1) ^ poly : (c >> 1);
@@ -72,6 +82,11 @@ struct CrcTables {
         for (uint32_t b = 0; b < 256; b++) tb[k * 256 + b] = matvec(m, b << (8 * k));
       for (int j = 0; j < 32; j++) sq[j] = matvec(m, m[j]);
       std::memcpy(m, sq, sizeof(m));
+    }
+    for (int t = 0; t < EW_TAIL_TABS; t++) {
+      const int a = ew_tail_amount(t);
+      for (int k = 0; k < 8; k++)
+        for (uint32_t d = 0; d < 16; d++) shift[(size_t)EW_TAIL_OFF + t * 128 + k * 16 + d] = shift_signed(a, d << (4 * k));
     }
   }
 
@@ -110,6 +125,13 @@ struct CrcTables {
   uint32_t shift_pow2(int lvl, uint32_t x) const {
     const uint32_t *tb = &shift[(size_t)lvl * 1024];
     return tb[x & 0xff] ^ tb[256 + ((x >> 8) & 0xff)] ^ tb[512 + ((x >> 16) & 0xff)] ^ tb[768 + (x >> 24)];
+  }
+  // S_n(x) for -256 < n < 2^48 (negative: the inverse levels)
+  uint32_t shift_signed(int64_t n, uint32_t x) const {
+    if (n >= 0) return shift_n((uint64_t)n, x);
+    for (int lvl = 0, u = (int)-n; u; lvl++, u >>= 1)
+      if (u & 1) x = shift_pow2(EW_SHIFT_LEVELS + lvl, x);
+    return x;
   }
   // S_n(x) for any n < 2^48.
   uint32_t shift_n(uint64_t n, uint32_t x) const {

@@ -226,7 +226,7 @@ __device__ __forceinline__ void prefix_load_near_pw(uint64_t x, uint64_t B, uint
   for (int q = 0; q < EW_VPU / 4; ++q) in.vv[q] = (4u * q < in.nk) ? vq[q] : make_uint4(0, 0, 0, 0);
   const uint4 *dq = (const uint4 *)(buf + base);
 #pragma unroll
-  for (int q = 0; q < 9; ++q) in.dd[q] = (16u * q < in.n) ? dq[q] : make_uint4(0, 0, 0, 0);
+  for (int q = 0; q < 8; ++q) in.dd[q] = (16u * q < in.n) ? dq[q] : make_uint4(0, 0, 0, 0);
   in.pw = pw;
 }
 // P(x) forward from its unit's start, pw = P there (rare paths)
@@ -412,7 +412,11 @@ __global__ __launch_bounds__(FR_THREADS, 1) void k_frames(FrArgs a, FrSeg sg) {
   __shared__ uint32_t s_t16[16 * 256];               // slicing-by-16
   __shared__ uint32_t s_svp[1024];                   // S_256 byte tables
   __shared__ uint32_t s_nib[FR_NIB * 128];           // S_{2^0} .. S_{2^19}, nibble tables
+#if EW_TAIL2
+  __shared__ uint32_t s_inv[EW_TAIL_TABS * 128];     // the prefix tails' shifts by -128..128 (tail_shift)
+#else
   __shared__ uint32_t s_inv[7 * 128];                // S_{2^0}^-1 .. S_{2^6}^-1
+#endif
   __shared__ uint32_t s_win[20 * FR_THREADS];        // frame heads, transposed
   __shared__ uint32_t s_ucnt[FR_WAVES][TU];          // candidates per unit of each wave's tile
   __shared__ uint32_t s_pw[FR_WAVES][TU];            // P at every unit start of each wave's tile (tile-local)
@@ -427,7 +431,11 @@ __global__ __launch_bounds__(FR_THREADS, 1) void k_frames(FrArgs a, FrSeg sg) {
   stage_lds<FR_THREADS>(s_t16, 16 * 256, [&](int i) { return a.g_slice[i]; });
   stage_lds<FR_THREADS>(s_svp, 1024, [&](int i) { return a.g_shift[EW_VLOG * 1024 + i]; });
   stage_lds<FR_THREADS>(s_nib, FR_NIB * 128, [&](int i) { return nib_src(a.g_shift, i); });
+#if EW_TAIL2
+  stage_lds<FR_THREADS>(s_inv, EW_TAIL_TABS * 128, [&](int i) { return a.g_shift[EW_TAIL_OFF + i]; });
+#else
   stage_lds<FR_THREADS>(s_inv, 7 * 128, [&](int i) { return nib_src(a.g_shift + EW_SHIFT_LEVELS * 1024, i); });
+#endif
   __syncthreads();   // the only barrier: every wave runs its own tiles from here on
   FR_T(0);
 #ifdef FR_TIMING

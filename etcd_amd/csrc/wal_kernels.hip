@@ -1497,7 +1497,7 @@ struct PrefixNear {
   uint32_t pw, nk, n, up, lead, slow;   // slow: x in the upper half of the stream's last, partial
                                         // super-piece (no next boundary): prefix_at instead
   uint4 vv[EW_VPU / 4];
-  uint4 dd[9];
+  uint4 dd[8];   // n <= 128 either way: tail <= 128 forward, x1 - (x & ~15) <= 128 back
 };
 __device__ __forceinline__ void prefix_load_near(uint64_t x, uint64_t B, const uint32_t *__restrict__ pwave,
                                                  const uint32_t *__restrict__ v, const uint8_t *__restrict__ buf,
@@ -1517,20 +1517,75 @@ __device__ __forceinline__ void prefix_load_near(uint64_t x, uint64_t B, const u
   for (int q = 0; q < EW_VPU / 4; ++q) in.vv[q] = (4u * q < in.nk) ? vq[q] : make_uint4(0, 0, 0, 0);
   const uint4 *dq = (const uint4 *)(buf + base);
 #pragma unroll
-  for (int q = 0; q < 9; ++q) in.dd[q] = (16u * q < in.n) ? dq[q] : make_uint4(0, 0, 0, 0);
+  for (int q = 0; q < 8; ++q) in.dd[q] = (16u * q < in.n) ? dq[q] : make_uint4(0, 0, 0, 0);
   in.pw = pwave[w];
 }
 #ifndef EW_FR_ABL
 #define EW_FR_ABL 0   // timing-only ablations of the frame pass (tools/): 1 no Horner over v, 2 no prefix tail,
                       // 4 no S_dlen in the checks; results are wrong
 #endif
+#ifndef EW_TAIL2
+#define EW_TAIL2 1   // 0: the round-5 tails (forward / backward branches, binary inverse steps)
+#endif
+// x shifted by s bytes, -128 <= s <= 128 (s < 0: the inverse), with the
+// EW_TAIL_TABS nibble tables (crc_math.h): two lookups rounds, a table base
+// per lane (lanes going forward and back share the code)
+__device__ __forceinline__ uint32_t tail_shift(const uint32_t *tt, bool neg, uint32_t u, uint32_t x) {
+  const uint32_t *t1 = tt + ((neg ? 34u : 9u) + (u & 15)) * 128;
+  const uint32_t *t2 = tt + ((neg ? 25u : 0u) + (u >> 4)) * 128;
+  return nib_apply(t2, nib_apply(t1, x));
+}
 // The prefix tail from the Horner result acc at the boundary the load chose
-// (prefix_load_near: x0 below x, or the next boundary x1 above it): forward
-// over the bytes [x0, x), or lin(stream[x, x1)) stepped back with the inverse
-// shifts.  NCH: the chunks the load holds.
+// (prefix_load_near: x0 below x, or the next boundary x1 above it).  NCH: the
+// chunks the load holds, BLK = 16 NCH bytes from its 16-B aligned base.
+//
+// EW_TAIL2 (round 6): one code path for both directions, off the Horner's
+// chain.  c = lin of the whole BLK-byte block with the bytes outside the tail
+// zeroed (chunk 0 below `lead` going back, the bytes from n on going forward;
+// whole chunks past n come zero from the load) -- NCH full slicing-by-16
+// steps from register 0, no per-byte steps, independent of acc.  Trailing
+// zeros shift a lin (lin(D || 0^k) = S_k(lin D)) and leading ones do not, so
+//   forward  [x0, x0 + n):  P(x) = S_n(acc) ^ S_{BLK-n}^-1(c)
+//   back     [x, x1):       P(x) = S_{x1-x}^-1(acc) ^ S_{BLK-lead}^-1(c)
+// (x1 - x = n - lead): two table shifts of acc after the Horner, where the
+// branches stepped up to 8 chunks + 6 words/bytes forward or 7 inverse
+// nibble rounds back -- and a wave holding lanes of both ran both.
 template <int NCH, class PN>
 __device__ __forceinline__ uint32_t prefix_near_tail(uint32_t acc, const PN &in, const uint32_t *t16,
                                                      const uint32_t *inv) {
+#if EW_TAIL2
+  constexpr uint32_t BLK = 16 * NCH;
+  const uint32_t lo = in.up ? in.lead : 0u;   // chunk 0's bytes below lo are not the tail's
+  const uint32_t r = in.n & 15, jp = in.n >> 4;   // going forward chunk jp holds r tail bytes
+  uint32_t ml[4], mh[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int kl = (int)lo - 4 * i, kh = (int)r - 4 * i;   // bytes of word i below lo / below n
+    ml[i] = kl <= 0 ? ~0u : kl >= 4 ? 0u : ~0u << (8 * kl);
+    mh[i] = kh >= 4 ? ~0u : kh <= 0 ? 0u : (1u << (8 * kh)) - 1u;
+  }
+  uint32_t c = 0;
+#pragma unroll
+  for (int q = 0; q < NCH; ++q) {
+    uint4 d = in.dd[q];
+    if (q == 0) {
+      d.x &= ml[0];
+      d.y &= ml[1];
+      d.z &= ml[2];
+      d.w &= ml[3];
+    }
+    const bool pq = (uint32_t)q == jp;
+    d.x &= pq ? mh[0] : ~0u;
+    d.y &= pq ? mh[1] : ~0u;
+    d.z &= pq ? mh[2] : ~0u;
+    d.w &= pq ? mh[3] : ~0u;
+    c = step16(t16, c, d);
+  }
+  const bool up = in.up;
+  const uint32_t ua = up ? in.n - in.lead : in.n;
+  const uint32_t uc = up ? BLK - in.lead : BLK - in.n;
+  return tail_shift(inv, up, ua, acc) ^ tail_shift(inv, true, uc, c);
+#else
   if (!in.up) {   // forward over the n bytes after x0
     const uint32_t nq = in.n >> 4;
     uint4 pc = in.dd[0];
@@ -1570,6 +1625,7 @@ __device__ __forceinline__ uint32_t prefix_near_tail(uint32_t acc, const PN &in,
   for (int l = 0; l < 7; ++l)
     if ((m >> l) & 1) x = nib_apply(inv + l * 128, x);
   return x;
+#endif
 }
 __device__ __forceinline__ uint32_t prefix_finish_near(const PrefixNear &in, const uint32_t *t16, const uint32_t *svp,
                                                        const uint32_t *inv) {
@@ -1582,18 +1638,18 @@ __device__ __forceinline__ uint32_t prefix_finish_near(const PrefixNear &in, con
     if (4u * q + 2 < in.nk) acc = tab_apply(svp, acc) ^ in.vv[q].z;
     if (4u * q + 3 < in.nk) acc = tab_apply(svp, acc) ^ in.vv[q].w;
   }
-  return prefix_near_tail<9>(acc, in, t16, inv);
+  return prefix_near_tail<8>(acc, in, t16, inv);
 }
 
 // The same at 128-B granularity (the frame pass on record-dense WALs, round
 // 5): besides v[] the stream pass stored vh[], the lin of the FIRST 128-B
 // half of every super-piece, so P at a mid boundary is S_128(P(super-piece
 // start)) ^ vh -- the tail is at most 64 bytes forward or 64 stepped back
-// (half the bytes, 5 chunks of registers instead of 9).
+// (half the bytes, 4 chunks of registers instead of 8).
 struct PrefixNearVH {
   uint32_t pw, nk, n, up, lead, slow, mid, vhv;   // mid: the boundary is a super-piece's 128-B mid point
   uint4 vv[EW_VPU / 4];
-  uint4 dd[5];
+  uint4 dd[4];   // n <= 64
 };
 __device__ __forceinline__ void prefix_load_near_vh(uint64_t x, uint64_t B, uint32_t pw, const uint32_t *__restrict__ v,
                                                     const uint32_t *__restrict__ vh, const uint8_t *__restrict__ buf,
@@ -1615,7 +1671,7 @@ __device__ __forceinline__ void prefix_load_near_vh(uint64_t x, uint64_t B, uint
   in.vhv = in.mid ? vh[w * EW_VPU + in.nk] : 0u;
   const uint4 *dq = (const uint4 *)(buf + base);
 #pragma unroll
-  for (int q = 0; q < 5; ++q) in.dd[q] = (16u * q < in.n) ? dq[q] : make_uint4(0, 0, 0, 0);
+  for (int q = 0; q < 4; ++q) in.dd[q] = (16u * q < in.n) ? dq[q] : make_uint4(0, 0, 0, 0);
   in.pw = pw;
 }
 __device__ __forceinline__ uint32_t prefix_finish_near_vh(const PrefixNearVH &in, const uint32_t *t16,
@@ -1630,7 +1686,7 @@ __device__ __forceinline__ uint32_t prefix_finish_near_vh(const PrefixNearVH &in
     if (4u * q + 3 < in.nk) acc = tab_apply(svp, acc) ^ in.vv[q].w;
   }
   if (in.mid) acc = nib_apply(n128, acc) ^ in.vhv;
-  return prefix_near_tail<5>(acc, in, t16, inv);
+  return prefix_near_tail<4>(acc, in, t16, inv);
 }
 
 // lin of the concatenation of every non-empty segment of bytes field fnum
