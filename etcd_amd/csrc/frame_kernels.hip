@@ -1432,6 +1432,9 @@ __global__ __launch_bounds__(256) void k_frames_seam(FrArgs a, FrSeg sg, ResultD
     if (nops) atomicAdd(&s_red[5], nops);
   }
   __syncthreads();
+#ifdef FR_TIMING
+  const unsigned long long t_fold = clock64();
+#endif
   if (threadIdx.x == 0) {
     if (s_red[0] != ~0ull) atomicMax(&ds->fc.fail_inv, ~s_red[0]);
     if (s_red[1] != ~0ull) atomicMax(&ds->fc.meta_inv, ~s_red[1]);
@@ -1439,7 +1442,9 @@ __global__ __launch_bounds__(256) void k_frames_seam(FrArgs a, FrSeg sg, ResultD
     if (s_red[3]) atomicMax(&ds->fr.ls, s_red[3]);
     if (s_red[4]) atomicMax(&ds->fr.lo, s_red[4]);
     if (s_red[5]) atomicAdd(&ds->fr.nops, s_red[5]);
+#ifndef FR_SEAM_NOFENCE   // (timing only: the fence's price; results may be stale without it)
     __threadfence();
+#endif
     s_last = atomicAdd(&ds->fc_done, 1u) == gridDim.x - 1;
   }
   __syncthreads();
@@ -1458,6 +1463,7 @@ __global__ __launch_bounds__(256) void k_frames_seam(FrArgs a, FrSeg sg, ResultD
     fr_sdbg[blockIdx.x * 4 + 3] = t_loop;
     fr_sdbg2[blockIdx.x * 8 + 5] = tq[0] - t_seam0;            // staging + the first barrier
     fr_sdbg2[blockIdx.x * 8 + 6] = tq[4] ? t_loop - tq[4] : 0ull;   // after thread 0's last tile: the block's wait + fold
+    fr_sdbg2[blockIdx.x * 8 + 7] = t_loop - t_fold;                 // the block's device atomics, fence, done count
   }
 #endif
 }
