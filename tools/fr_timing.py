@@ -63,7 +63,8 @@ def one(label, size, lo, hi, nsh=0):
         print("  seam thread 0 steps (cycles from the loop start, median over blocks): " +
               " ".join("%s=%d" % (nm, sorted(r[i] for r in rows)[len(rows) // 2])
                        for i, nm in ((1, "loads"), (2, "first"), (3, "last"), (4, "end"), (5, "staging"),
-                                     (6, "wait+fold"), (7, "atomics+fence"))))
+                                     (6, "wait+fold"), (7, "atomics+fence"))) +
+              "  (wait+fold includes this timing build's own 1024 same-line atomics per block)")
     lib.ewal_dbg_fr_seam_maxsteps(mx, 1024 * 8)
     rows = [list(mx[b * 8:(b + 1) * 8]) for b in range(1024) if any(mx[b * 8:(b + 1) * 8])]
     if rows:
