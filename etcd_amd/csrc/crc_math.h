@@ -21,9 +21,11 @@
 //                      prefix from the NEXT boundary b;
 //                      then EW_TAIL_TABS nibble tables (128 words each) of
 //                      the shifts by -128..128 bytes in two factors, for the
-//                      frame pass's prefix tails (ew_tail_tab, tail_shift in
+//                      frame pass's prefix tails (tail_shift in
 //                      wal_kernels.hip): S_{16a} (a = 0..8), S_b (b = 0..15),
-//                      S_{16a}^-1, S_b^-1
+//                      S_{16a}^-1, S_b^-1; then S_{16a} (a = 9..15) and
+//                      S_{256a} (a = 1..15), with which the checks take the
+//                      low 12 bits of S_dlen in three rounds (frame_kernels.hip)
 #pragma once
 #include <cstdint>
 #include <cstring>
@@ -32,11 +34,15 @@
 
 #define EW_SHIFT_LEVELS 48  // S_{2^m} for m < 48: lengths up to 256 TiB
 #define EW_INV_LEVELS 8     // S_{2^m}^-1 for m < 8 (inverse shifts up to 255 bytes), after the forward levels
-#define EW_TAIL_TABS 50     // nibble tables after the inverse levels (see above)
+#define EW_TAIL_TABS 72     // nibble tables after the inverse levels (see above); then S_{16a} (a = 9..15)
+                            // and S_{256a} (a = 1..15) for the checks' S_dlen
 #define EW_TAIL_OFF ((EW_SHIFT_LEVELS + EW_INV_LEVELS) * 1024)
 
-// The signed shift amount of tail table t: S_{16t}, S_{t-9}, S_{16(t-25)}^-1, S_{t-34}^-1
-inline int ew_tail_amount(int t) { return t < 9 ? 16 * t : t < 25 ? t - 9 : t < 34 ? -16 * (t - 25) : -(t - 34); }
+// The signed shift amount of tail table t: S_{16t}, S_{t-9}, S_{16(t-25)}^-1, S_{t-34}^-1, S_{16(t-41)},
+// S_{256(t-56)}
+inline int ew_tail_amount(int t) {
+  return t < 9 ? 16 * t : t < 25 ? t - 9 : t < 34 ? -16 * (t - 25) : t < 50 ? -(t - 34) : t < 57 ? 16 * (t - 41) : 256 * (t - 56);
+}
 
 namespace ewal {
 

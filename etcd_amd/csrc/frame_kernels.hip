@@ -41,6 +41,9 @@
 #ifndef FR_HORNER_NIB
 #define FR_HORNER_NIB 1    // phase A's Horner steps through the S_256 nibble tables (no bank conflicts)
 #endif
+#ifndef FR_DLEN2
+#define FR_DLEN2 1         // the checks' S_dlen: its low 12 bits in three table rounds
+#endif
 #ifndef FR_THREADS
 #define FR_THREADS 768
 #endif
@@ -780,7 +783,21 @@ __global__ __launch_bounds__(FR_THREADS, 1) void k_frames(FrArgs a, FrSeg sg) {
             if (d.dlen && !(EW_FR_ABL & 4)) {
               uint32_t xs = seed ^ 0xffffffffu ^ Pfd;
               uint64_t m = d.dlen;
-              for (int lvl = 0; m; ++lvl, m >>= 1)
+              int lvl = 0;
+#if FR_DLEN2
+              // the low 12 bits in three rounds through the tail tables (S_b,
+              // S_{16a}: tables 0..8 and 50..56, S_{256a}: 57..71), the rest
+              // bit by bit
+              {
+                const uint32_t lo4 = (uint32_t)m & 15u, a4 = (uint32_t)(m >> 4) & 15u, h4 = (uint32_t)(m >> 8) & 15u;
+                xs = nib_apply(s_inv + (9u + lo4) * 128, xs);
+                xs = nib_apply(s_inv + (a4 <= 8u ? a4 : 41u + a4) * 128, xs);
+                xs = nib_apply(s_inv + (h4 ? 56u + h4 : 0u) * 128, xs);
+                m >>= 12;
+                lvl = 12;
+              }
+#endif
+              for (; m; ++lvl, m >>= 1)
                 if (m & 1) xs = lvl < FR_NIB ? nib_apply(s_nib + lvl * 128, xs) : gshift_pow2(a.g_shift, lvl, xs);
               computed = xs ^ Pe ^ 0xffffffffu;
             }
