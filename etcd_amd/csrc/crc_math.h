@@ -25,7 +25,9 @@
 //                      wal_kernels.hip): S_{16a} (a = 0..8), S_b (b = 0..15),
 //                      S_{16a}^-1, S_b^-1; then S_{16a} (a = 9..15) and
 //                      S_{256a} (a = 1..15), with which the checks take the
-//                      low 12 bits of S_dlen in three rounds (frame_kernels.hip)
+//                      low 12 bits of S_dlen in three rounds (frame_kernels.hip);
+//                      then EW_DIG_TABS digit tables S_{d 16^p} for the seam
+//                      pass's shifts by n < 2^20 in <= 5 rounds (seam_shift)
 #pragma once
 #include <cstdint>
 #include <cstring>
@@ -37,6 +39,9 @@
 #define EW_TAIL_TABS 72     // nibble tables after the inverse levels (see above); then S_{16a} (a = 9..15)
                             // and S_{256a} (a = 1..15) for the checks' S_dlen
 #define EW_TAIL_OFF ((EW_SHIFT_LEVELS + EW_INV_LEVELS) * 1024)
+#define EW_DIG_POS 5        // then digit tables for the seam pass: S_{d 16^p}, p < EW_DIG_POS, d = 1..15
+#define EW_DIG_OFF (EW_TAIL_OFF + EW_TAIL_TABS * 128)
+#define EW_DIG_TABS (EW_DIG_POS * 15)
 
 // The signed shift amount of tail table t: S_{16t}, S_{t-9}, S_{16(t-25)}^-1, S_{t-34}^-1, S_{16(t-41)},
 // S_{256(t-56)}
@@ -52,7 +57,7 @@ struct CrcTables {
   uint32_t slice16[16][256];    // slicing-by-16 (slice16[t] = slice[t] for t < 4): the device table
   std::vector<uint32_t> shift;  // EW_SHIFT_LEVELS * 4 * 256
 
-  explicit CrcTables(uint32_t p) : poly(p), shift((size_t)EW_TAIL_OFF + EW_TAIL_TABS * 128) {
+  explicit CrcTables(uint32_t p) : poly(p), shift((size_t)EW_DIG_OFF + EW_DIG_TABS * 128) {
     for (uint32_t i = 0; i < 256; i++) {
       uint32_t c = i;
       for (int j = 0; j < 8; j++) c = (c & 1) ? (c >> 1) ^ poly : (c >> 1);
@@ -93,6 +98,11 @@ struct CrcTables {
       const int a = ew_tail_amount(t);
       for (int k = 0; k < 8; k++)
         for (uint32_t d = 0; d < 16; d++) shift[(size_t)EW_TAIL_OFF + t * 128 + k * 16 + d] = shift_signed(a, d << (4 * k));
+    }
+    for (int t = 0; t < EW_DIG_TABS; t++) {
+      const uint64_t n = (uint64_t)(t % 15 + 1) << (4 * (t / 15));
+      for (int k = 0; k < 8; k++)
+        for (uint32_t d = 0; d < 16; d++) shift[(size_t)EW_DIG_OFF + t * 128 + k * 16 + d] = shift_n(n, d << (4 * k));
     }
   }
 

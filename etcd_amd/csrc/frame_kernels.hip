@@ -1063,8 +1063,23 @@ __global__ __launch_bounds__(FR_THREADS, 1) void k_frames(FrArgs a, FrSeg sg) {
 // S_n from the seam pass's LDS nibble tables (S_{2^0} .. S_{2^23}), the
 // global byte tables above them
 #define SEAM_NIB 24
+#ifndef SEAM_DIG
+#define SEAM_DIG 1   // the seam pass's shifts by hex digits (<= 5 table rounds below 2^20) instead of bit by bit
+#endif
+// S_n(x): s_n holds S_{2^m} (m < SEAM_NIB), then (SEAM_DIG) the digit tables
+// S_{d 16^p} (crc_math.h EW_DIG_*), one round per nonzero hex digit below 2^20
+#define SEAM_LDS (SEAM_NIB * 128 + (SEAM_DIG ? EW_DIG_TABS * 128 : 0))
 __device__ __forceinline__ uint32_t seam_shift(const uint32_t *s_n, const uint32_t *g_shift, uint64_t n, uint32_t x) {
-  for (int m = 0; n; ++m, n >>= 1)
+  const uint32_t *s_dg = s_n + SEAM_NIB * 128;   // (the kernels' s_n arrays: SEAM_LDS words)
+  int m = 0;
+  if (SEAM_DIG) {
+    for (int p = 0; p < EW_DIG_POS && n; ++p, n >>= 4) {
+      const uint32_t d = (uint32_t)n & 15u;
+      if (d) x = nib_apply(s_dg + (p * 15 + d - 1) * 128, x);
+    }
+    m = 4 * EW_DIG_POS;
+  }
+  for (; n; ++m, n >>= 1)
     if (n & 1) x = m < SEAM_NIB ? nib_apply(s_n + m * 128, x) : gshift_pow2(g_shift, m, x);
   return x;
 }
@@ -1219,7 +1234,7 @@ __global__ __launch_bounds__(256) void k_frames_seam(FrArgs a, FrSeg sg, ResultD
   __shared__ RecDesc s_d[SEG ? 1 : 6];
   __shared__ unsigned long long s_ord;
   __shared__ ResultDev s_res[SEG ? 1 : 1];
-  __shared__ uint32_t s_n[SEAM_NIB * 128];  // S_{2^m} nibble tables, m < 24
+  __shared__ uint32_t s_n[SEAM_LDS];  // S_{2^m} nibble tables, m < 24, then the digit tables
   static_assert(TLOG < SEAM_NIB, "tile shifts from the LDS tables");
   Small *ds = a.ds;
   if (SEG && ds->fr_capfail) return;
@@ -1227,6 +1242,7 @@ __global__ __launch_bounds__(256) void k_frames_seam(FrArgs a, FrSeg sg, ResultD
   const unsigned long long t_seam0 = clock64();
 #endif
   stage_lds<256>(s_n, SEAM_NIB * 128, [&](int i) { return nib_src(a.g_shift, i); });
+  if (SEAM_DIG) stage_lds<256>(s_n + SEAM_NIB * 128, EW_DIG_TABS * 128, [&](int i) { return a.g_shift[EW_DIG_OFF + i]; });
   if (!SEG && threadIdx.x == 0) {
     s_red[0] = s_red[1] = ~0ull;
     s_red[2] = s_red[3] = s_red[4] = s_red[5] = 0;
@@ -1506,9 +1522,10 @@ __global__ __launch_bounds__(512) void k_range_info_fr(FrArgs a, uint32_t nmeta,
   constexpr uint32_t TU = 1u << TSH;
   __shared__ unsigned long long s_pos[RFR_N];
   __shared__ uint4 s_w[RFR_N][6];
-  __shared__ uint32_t s_n[SEAM_NIB * 128];
+  __shared__ uint32_t s_n[SEAM_LDS];
   const uint32_t tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   stage_lds<512>(s_n, SEAM_NIB * 128, [&](int i) { return nib_src(a.g_shift, i); });
+  if (SEAM_DIG) stage_lds<512>(s_n + SEAM_NIB * 128, EW_DIG_TABS * 128, [&](int i) { return a.g_shift[EW_DIG_OFF + i]; });
   if (tid == 0) {
     s_pos[0] = ~0ull;
     s_pos[1] = meta_inv ? ~meta_inv : ~0ull;

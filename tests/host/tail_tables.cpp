@@ -65,6 +65,18 @@ int main() {
     y = T.shift_n(m >> 12 << 12, y);
     if (y != T.shift_n(m, x)) bad++;
   }
+  // the seam pass's digit tables (seam_shift): one round per nonzero hex digit below 2^20, then powers of two
+  const uint32_t *dg = &T.shift[EW_DIG_OFF];
+  for (int i = 0; i < 100000; i++) {
+    uint64_t n = g() % (1u << 26);
+    const uint64_t n0 = n;
+    const uint32_t x = g();
+    uint32_t y = x;
+    for (int p = 0; p < EW_DIG_POS && n; ++p, n >>= 4)
+      if (n & 15) y = nib(dg + (p * 15 + (n & 15) - 1) * 128, y);
+    y = T.shift_n(n << (4 * EW_DIG_POS), y);
+    if (y != T.shift_n(n0, x)) bad++;
+  }
   std::printf(bad ? "bad %ld\n" : "ok\n", bad);
   return bad != 0;
 }
