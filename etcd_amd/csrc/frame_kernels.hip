@@ -44,6 +44,9 @@
 #ifndef FR_DLEN2
 #define FR_DLEN2 1         // the checks' S_dlen: its low 12 bits in three table rounds
 #endif
+#ifndef FR_COMPOSE_W
+#define FR_COMPOSE_W 1     // fr_result's record composed by a wave (thread 0 alone: ~6 K cycles)
+#endif
 #ifndef FR_THREADS
 #define FR_THREADS 768
 #endif
@@ -1184,6 +1187,37 @@ __device__ void fr_result(const FrArgs &a, ResultDev *o, Small *h, uint4 (*s_w)[
   // the result composed in LDS by thread 0, then written to host-mapped
   // memory by a whole wave (wide PCIe writes instead of one lane's stores)
   ResultDev &res = *s_res;
+#if FR_COMPOSE_W
+  // (the zeroing and the named frames' copies by the first wave, dword-wise;
+  // thread 0 then sets the scalar fields -- one wave's LDS ops stay in order)
+  if (tid < 64) {
+    static_assert(sizeof(RecDesc) % 4 == 0 && sizeof(RecDesc) / 4 <= 64, "a frame's copy in one wave step");
+    uint32_t *rw = (uint32_t *)&res;
+    for (uint32_t i = tid; i < sizeof(ResultDev) / 4; i += 64) rw[i] = 0u;
+    constexpr uint32_t NW = sizeof(RecDesc) / 4;
+    if (tid < NW) {
+      const uint32_t *sw = (const uint32_t *)s_d;
+      if (key != ~0ull) rw[offsetof(ResultDev, fail) / 4 + tid] = sw[0 * NW + tid];
+      if (le) rw[offsetof(ResultDev, lastent) / 4 + tid] = sw[1 * NW + tid];
+      if (ls) rw[offsetof(ResultDev, sd) / 4 + tid] = sw[2 * NW + tid];
+      if (fm != ~0ull) rw[offsetof(ResultDev, md) / 4 + tid] = sw[3 * NW + tid];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");   // (the dword stores before thread 0's fields)
+    __builtin_amdgcn_wave_barrier();
+  }
+  if (tid == 0) {
+    res.agg.first_fail = key != ~0ull ? *s_ord : ~0ull;
+    res.agg.last_entry = le ? 0 : -1;
+    res.agg.last_state = ls ? 0 : -1;
+    res.agg.first_meta = fm != ~0ull ? 0ull : ~0ull;
+    if (key != ~0ull) res.fail.st = (int32_t)(key & 0xff);
+    res.last.chained = ds->fc.last_chained;
+    res.nops = (uint32_t)ds->fr.nops;
+    res.klast = lo ? s_d[4].f1 - a.ri : 0;
+    res.errflag = ds->errflag;
+    ds->spec_n = (uint32_t)K;
+  }
+#else
   if (tid == 0) {
     memset(&res, 0, sizeof(res));
     res.agg.first_fail = key != ~0ull ? *s_ord : ~0ull;
@@ -1203,6 +1237,7 @@ __device__ void fr_result(const FrArgs &a, ResultDev *o, Small *h, uint4 (*s_w)[
     res.errflag = ds->errflag;
     ds->spec_n = (uint32_t)K;
   }
+#endif
   __threadfence_block();
   __syncthreads();
   FR_RT(4);
