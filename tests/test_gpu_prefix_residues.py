@@ -86,3 +86,19 @@ def test_last_frame_in_partial_last_block(ctx, dense_wal, blk, lo, hi):
     assert o["status"] == O.OK
     for vh in (True, False):
         _assert_result(ctx, _dev_readall(ctx, x, 1, vh), o, x)
+
+
+@pytest.mark.parametrize("seed", range(2))
+def test_records_over_one_mib(ctx, seed):
+    """Data longer than 2^20 bytes: the checks' S_dlen past the table rounds
+    and the seam pass's shifts past its hex-digit tables (frame_kernels.hip
+    seam_shift) take the powers-of-two remainder; clean and with one corrupt
+    record, against the oracle."""
+    buf, n = W.synth_wal(48 << 20, 1 << 20, 3 << 20, seed=880 + seed)
+    b = bytes(buf)
+    assert n >= 8
+    for x in (b, bytes(W.synth_wal(48 << 20, 1 << 20, 3 << 20, seed=880 + seed, corrupt_record=n // 2)[0])):
+        o = O.readall_digest(x, 1)
+        assert (o["status"] == O.OK) == (x is b)
+        for vh in (True, False):
+            _assert_result(ctx, _dev_readall(ctx, x, 1, vh), o, x)
